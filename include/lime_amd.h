@@ -1,0 +1,197 @@
+/*
+ * lime_amd.h -- C-ABI of the MI355X (gfx950) engine for LIME's genomic
+ * set-theory hot path: intersection, merge (union), subtract (difference)
+ * and complement over ReferenceRegion-keyed interval sets.
+ *
+ * Plain C types only (no HIP/torch types in signatures); every function
+ * returns an int status (LIME_OK = 0) and leaves a thread-local message in
+ * lime_last_error().  One HIP stream per context; contexts are independent,
+ * so concurrent calls from N executor threads each use their own context
+ * (SURVEY.md 8(b) "Threading").
+ *
+ * Reference interface each entry point replaces (paths under gman90/lime):
+ *   lime_set_create_host    ADAM loadBed(...).repartitionAndSort() +
+ *                           OverlapBasedSetTheory.prepare()'s sort
+ *                           (cli/Intersection.scala:42-48,
+ *                            OverlapBasedSetTheory.scala:45-86)
+ *   lime_intersect_count /  DistributedIntersection(left, right, partitionMap,
+ *   lime_intersect_fill_*     threshold).compute()  (Intersection.scala:45-69,
+ *                            SetTheory.scala:162-187)
+ *   lime_merge              DistributedMerge(rdd, partitionMap).compute()
+ *                            (Merge.scala:34-36, SetTheory.scala:202-282)
+ *   lime_subtract           DistributedSubtract(left, right, partitionMap,
+ *                            threshold).compute()  (Subtract.scala:78-116)
+ *   lime_complement         DistributedComplement(rdd, partitionMap,
+ *                            referenceNameBounds).compute()
+ *                            (Complement.scala:33-134)
+ *   lime_bed_read           ADAM sc.loadBed(path) (3rd-party; BED3-6 text)
+ *   lime_contig_rank        ReferenceRegion ordering by referenceName
+ *                            (java.lang.String.compareTo)
+ *
+ * Semantics are SURVEY.md Appendix A (strict half-open overlap, sort order
+ * (contig, start, end), zero-width gaps dropped in complement).  Strand is
+ * handled by the host layer (lime_amd.hpp / lime_amd python package), which
+ * partitions rows by strand before calling this ABI; the engine itself sees
+ * unstranded contigs.
+ */
+#ifndef LIME_AMD_H
+#define LIME_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIME_ABI_VERSION 1
+
+/* status codes */
+#define LIME_OK 0
+#define LIME_ERR_ARG 1      /* bad argument (null pointer, negative count, ...)          */
+#define LIME_ERR_RANGE 2    /* coordinate outside [0, 2^32) / contig length / span > 2^32 */
+#define LIME_ERR_DEVICE 3   /* HIP runtime error (or no device)                          */
+#define LIME_ERR_NOMEM 4    /* device or host allocation failed                          */
+#define LIME_ERR_CONTIG 5   /* contig id not in the space (NoSuchElementException)       */
+#define LIME_ERR_IO 6       /* file could not be read / parsed                           */
+#define LIME_ERR_OVERFLOW 7 /* an output count does not fit the engine's index types     */
+
+/* subtract modes */
+#define LIME_SUBTRACT_LIME 0 /* Subtract.scala:103-114 exactly (per-block remnants, Q5) */
+#define LIME_SUBTRACT_SET 1  /* a minus union(hits)                                     */
+
+typedef struct lime_ctx lime_ctx;       /* device + stream + memory pool            */
+typedef struct lime_space lime_space;   /* contigs (String order) and their lengths */
+typedef struct lime_set lime_set;       /* sorted, device-resident interval set     */
+typedef struct lime_pairs lime_pairs;   /* intersect plan: pair count + fill state  */
+typedef struct lime_result lime_result; /* merge / subtract / complement output     */
+typedef struct lime_bed lime_bed;       /* parsed BED file (host memory)            */
+typedef struct lime_bitset lime_bitset; /* bit-per-base set over a space            */
+
+/* One intersect output record: the intersection region in contig-local
+ * coordinates (contig = contig of left row a_row) and the two input rows. */
+typedef struct {
+    uint32_t start, end, a_row, b_row;
+} lime_pair;
+
+const char *lime_last_error(void);
+int lime_abi_version(void);
+
+/* ----------------------------------------------------------------- context */
+int lime_ctx_create(int device, lime_ctx **out);
+int lime_ctx_destroy(lime_ctx *ctx);
+/* Run subsequent work on a caller-owned hipStream_t (e.g. torch's current
+ * stream); NULL restores the context's own stream. */
+int lime_ctx_set_stream(lime_ctx *ctx, void *hip_stream);
+int lime_ctx_synchronize(lime_ctx *ctx);
+/* bytes currently held by the context's device pool */
+int64_t lime_ctx_pool_bytes(const lime_ctx *ctx);
+
+/* ------------------------------------------------------------------- space */
+/* Contig ids are 0..n-1 in the caller's order, which must be Java String
+ * order of the names for output order to match the reference (use
+ * lime_contig_rank).  Internally contig c occupies global coordinates
+ * [off[c], off[c] + len[c]] with off[c+1] = off[c] + len[c] + 1, so the total
+ * span sum(len + 1) must stay below 2^32 (hg19/hg38: ~3.1e9). */
+int lime_space_create(int32_t n_contigs, const int64_t *lengths, lime_space **out);
+int lime_space_destroy(lime_space *space);
+int32_t lime_space_contigs(const lime_space *space);
+int64_t lime_space_span(const lime_space *space);
+int64_t lime_space_offset(const lime_space *space, int32_t contig);
+
+/* --------------------------------------------------------------------- sets */
+/* Host arrays (JVM Long coordinates): upload, validate and sort on device.
+ * Rows keep their input index (0..n-1) as the payload handle. */
+int lime_set_create_host(lime_ctx *ctx, const lime_space *space, int64_t n, const int32_t *contig,
+                         const int64_t *start, const int64_t *end, lime_set **out);
+/* Device arrays (u32 contig-local coordinates) already resident in HBM:
+ * validated and sorted on the context's stream, inputs are not modified. */
+int lime_set_create_device(lime_ctx *ctx, const lime_space *space, int64_t n,
+                           const int32_t *d_contig, const uint32_t *d_start,
+                           const uint32_t *d_end, lime_set **out);
+int lime_set_destroy(lime_set *set);
+int64_t lime_set_size(const lime_set *set);
+/* Device pointers of the sorted set: global start, global end, input row. */
+int lime_set_device_arrays(const lime_set *set, const uint32_t **gstart, const uint32_t **gend,
+                           const uint32_t **row);
+/* Host copy of the sorted set in contig-local coordinates. */
+int lime_set_fill_host(const lime_set *set, int32_t *contig, int64_t *start, int64_t *end,
+                       int64_t *row);
+
+/* ---------------------------------------------------------------- intersect */
+/* Count pass: exact number of qualifying pairs (overlapsBy >= threshold). */
+int lime_intersect_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,
+                         lime_pairs **plan, int64_t *n_pairs);
+/* Fill pass: write pairs [first, first + count) of the plan's output order
+ * into a caller-owned DEVICE buffer (chunked emission for outputs larger
+ * than HBM).  Asynchronous on the context stream. */
+int lime_intersect_fill_device(lime_pairs *plan, int64_t first, int64_t count, lime_pair *d_out);
+/* Same into a caller-owned HOST buffer (synchronous). */
+int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lime_pair *out);
+/* Order-independent checksum (sum and xor of lime_pair_hash over every pair)
+ * computed on device without materialising the pairs. */
+int lime_intersect_checksum(lime_pairs *plan, uint64_t *sum, uint64_t *xr);
+int lime_pairs_destroy(lime_pairs *plan);
+
+/* ------------------------------------------------------------ merge et al. */
+int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs);
+int lime_subtract(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,
+                  int mode, lime_result **out, int64_t *n_regions);
+int lime_complement(lime_ctx *ctx, const lime_space *genome_space, const lime_set *a,
+                    lime_result **out, int64_t *n_regions);
+int64_t lime_result_size(const lime_result *res);
+/* Host copy of a result: regions in contig-local coordinates plus the
+ * left/right input rows (-1 where the reference has None / no payload). */
+int lime_result_fill_host(const lime_result *res, int32_t *contig, int64_t *start, int64_t *end,
+                          int64_t *a_row, int64_t *b_row);
+/* merge only: run index of every input row (the Iterable[T] grouping). */
+int lime_result_run_of_row(const lime_result *res, int64_t *run_of_row);
+int lime_result_device_arrays(const lime_result *res, const uint32_t **gstart,
+                              const uint32_t **gend);
+int lime_result_destroy(lime_result *res);
+
+/* ----------------------------------------------------- bit-per-base path */
+int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out);
+/* op: 0 = a, 1 = not a (within contigs), 2 = a and b, 3 = a and not b */
+int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bitset *b,
+                     lime_result **out, int64_t *n_runs);
+/* k-way AND of k bitsets, runs extracted */
+int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, lime_result **out,
+                         int64_t *n_runs);
+int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
+int lime_bitset_destroy(lime_bitset *bs);
+
+/* ------------------------------------------------------ synthetic inputs */
+/* Counter-based generators (splitmix64 keyed by (seed, row)) identical to
+ * lime_amd/synth.py, written to caller-owned device arrays. */
+int lime_synth_uniform(lime_ctx *ctx, const lime_space *space, int64_t n, uint64_t seed,
+                       uint32_t len_lo, uint32_t len_hi, int32_t *d_contig, uint32_t *d_start,
+                       uint32_t *d_end);
+int lime_synth_pileup(lime_ctx *ctx, const lime_space *space, int64_t n, uint64_t seed,
+                      int64_t n_centres, uint32_t sigma, uint32_t len_lo, uint32_t len_hi,
+                      int32_t *d_contig, uint32_t *d_start, uint32_t *d_end);
+
+/* ------------------------------------------------------ host-only helpers */
+/* rank_out[i] = position of names[i] in Java String order of the distinct
+ * names (UTF-16 code-unit order; equal to byte order for ASCII). */
+int lime_contig_rank(int32_t n, const char *const *names, int32_t *rank_out);
+int lime_bed_read(const char *path, lime_bed **out);
+int64_t lime_bed_rows(const lime_bed *bed);
+int32_t lime_bed_contigs(const lime_bed *bed);
+const char *lime_bed_contig_name(const lime_bed *bed, int32_t i);
+/* per-row arrays, valid until lime_bed_free; contig = index into the BED's
+ * own name table (first-seen order); strand: 0 '.', 1 '+', 2 '-', 3 '?' */
+const int32_t *lime_bed_contig_ids(const lime_bed *bed);
+const int64_t *lime_bed_starts(const lime_bed *bed);
+const int64_t *lime_bed_ends(const lime_bed *bed);
+const int8_t *lime_bed_strands(const lime_bed *bed);
+const char *lime_bed_name(const lime_bed *bed, int64_t row); /* 4th column or "" */
+void lime_bed_free(lime_bed *bed);
+/* genome file: "name<TAB>length" per line (cli/Complement.scala:43-44) */
+int lime_genome_read(const char *path, int32_t *n_out, char ***names_out, int64_t **lengths_out);
+void lime_genome_free(int32_t n, char **names, int64_t *lengths);
+uint64_t lime_pair_hash(uint32_t start, uint32_t end, uint32_t a_row, uint32_t b_row);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIME_AMD_H */

@@ -1,0 +1,187 @@
+// lime-submit -- command surface of bin/lime-submit + LimeMain over the
+// MI355X engine.  Usage (bin/lime-submit:7-23, LimeMain.scala:30-57):
+//
+//   lime-submit [<spark-args> --] <command> <args> [-version]
+//
+//   intersect A.bed B.bed       cli/Intersection.scala:99-112 (keys stranded)
+//   merge     A.bed             cli/Merge.scala:36-44
+//   complement A.bed genome.txt cli/Complement.scala:154-166 (prints regions)
+//   subtract  A.bed B.bed       DistributedSubtract (API-only in the reference)
+//   sort      A.bed             cli/Sort.scala:34-38 (device radix sort)
+//
+// Everything before "--" is accepted and ignored (there is no Spark).
+// Output is one region per line, tab-separated (chrom, start, end), followed
+// by the BED name fields of the contributing rows; the reference printed
+// Scala tuple toString()s of ADAM Features, which have no stable text form.
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "lime_amd.hpp"
+
+using namespace lime;
+
+namespace {
+
+struct Cmd {
+    const char *name, *desc;
+};
+const Cmd kCommands[] = {
+    {"complement", "Extract intervals not represented by an interval file."},
+    {"intersect", "Compute intersection of regions between two inputs"},
+    {"merge", "Merges the regions in a single input"},
+    {"subtract", "Remove regions of the second input from the first"},
+    {"sort", "Sorts the regions in a single input"},
+};
+
+void usage() {
+    printf("\nUsage: lime-submit [<spark-args> --] <lime-args> [-version]\n\n");
+    printf("Choose one of the following commands:\n\n");
+    for (auto &c : kCommands) printf("%20s : %s\n", c.name, c.desc);
+    printf("\n");
+}
+
+Strand strand_of(int8_t s) {
+    return s == 1 ? Strand::Forward : s == 2 ? Strand::Reverse : s == 3 ? Strand::Unknown
+                                                                        : Strand::Independent;
+}
+
+RDD<std::string> load_bed(const std::string &path, bool stranded) {
+    lime_bed *b = nullptr;
+    check(lime_bed_read(path.c_str(), &b));
+    int64_t n = lime_bed_rows(b);
+    const int32_t *c = lime_bed_contig_ids(b);
+    const int64_t *s = lime_bed_starts(b);
+    const int64_t *e = lime_bed_ends(b);
+    const int8_t *st = lime_bed_strands(b);
+    RDD<std::string> rdd;
+    rdd.reserve((size_t)n);
+    for (int64_t i = 0; i < n; ++i)
+        rdd.push_back({ReferenceRegion(lime_bed_contig_name(b, c[i]), s[i], e[i],
+                                       stranded ? strand_of(st[i]) : Strand::Independent),
+                       lime_bed_name(b, i)});
+    lime_bed_free(b);
+    return rdd;
+}
+
+void print_region(const ReferenceRegion &r) {
+    printf("%s\t%lld\t%lld", r.referenceName.c_str(), (long long)r.start, (long long)r.end);
+}
+
+int run(const std::vector<std::string> &args) {
+    const std::string &cmd = args[0];
+    auto need = [&](size_t k) {
+        if (args.size() < k + 1) throw Error(LIME_ERR_ARG, cmd + ": expected " + std::to_string(k) + " arguments");
+    };
+    if (cmd == "intersect") {
+        need(2);
+        auto out = DistributedIntersection<std::string, std::string>(load_bed(args[1], true),
+                                                                     load_bed(args[2], true))
+                       .compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\t%s\t%s\n", o.second.first.c_str(), o.second.second.c_str());
+        }
+    } else if (cmd == "subtract") {
+        need(2);
+        auto out = DistributedSubtract<std::string, std::string>(load_bed(args[1], true),
+                                                                 load_bed(args[2], true))
+                       .compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\t%s\t%s\n", o.second.first.c_str(),
+                   o.second.second ? o.second.second->c_str() : ".");
+        }
+    } else if (cmd == "merge") {
+        need(1);
+        auto out = DistributedMerge<std::string>(load_bed(args[1], true)).compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\t%zu\n", o.second.size());
+        }
+    } else if (cmd == "complement") {
+        need(2);
+        int32_t n = 0;
+        char **names = nullptr;
+        int64_t *lens = nullptr;
+        check(lime_genome_read(args[2].c_str(), &n, &names, &lens));
+        std::map<std::string, ReferenceRegion> bounds;
+        for (int32_t i = 0; i < n; ++i) bounds[names[i]] = ReferenceRegion(names[i], 0, lens[i]);
+        lime_genome_free(n, names, lens);
+        auto out = DistributedComplement<std::string>(load_bed(args[1], false), {}, bounds).compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\n");
+        }
+    } else if (cmd == "sort") {
+        need(1);
+        auto rdd = load_bed(args[1], true);
+        // a merge-free pass through the device sort: runs of a set keyed by
+        // its own rows give the canonical order
+        std::map<std::string, int64_t> ext;
+        for (auto &kv : rdd) ext[kv.first.referenceName] = std::max(ext[kv.first.referenceName], kv.first.end);
+        std::vector<std::string> nm;
+        std::vector<int64_t> ln;
+        for (auto &kv : ext) {
+            nm.push_back(kv.first);
+            ln.push_back(kv.second);
+        }
+        detail::Space sp(nm, ln);
+        std::vector<size_t> rows(rdd.size());
+        for (size_t i = 0; i < rows.size(); ++i) rows[i] = i;
+        detail::SetHandle A;
+        detail::upload(Engine::thread_default().ctx(), sp, rdd, rows, A);
+        std::vector<int32_t> c(rdd.size());
+        std::vector<int64_t> s(rdd.size()), e(rdd.size()), r(rdd.size());
+        check(lime_set_fill_host(A.h, c.data(), s.data(), e.data(), r.data()));
+        for (size_t i = 0; i < rdd.size(); ++i) {
+            print_region(rdd[r[i]].first);
+            printf("\t%s\n", rdd[r[i]].second.c_str());
+        }
+    } else {
+        usage();
+    }
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    std::vector<std::string> all(argv + 1, argv + argc), lime_args;
+    // bin/lime-submit:7-23: everything after the first "--" is for lime
+    auto dd = std::find(all.begin(), all.end(), std::string("--"));
+    if (dd != all.end())
+        lime_args.assign(dd + 1, all.end());
+    else
+        lime_args = all;
+    bool version = false;
+    std::vector<std::string> rest;
+    for (auto &a : lime_args) {
+        if (a == "-version")
+            version = true;
+        else
+            rest.push_back(a);
+    }
+    if (version) printf("Version 0\n");  // LimeMain.scala:20-22
+    if (rest.empty()) {
+        usage();
+        return 0;
+    }
+    bool known = false;
+    for (auto &c : kCommands) known |= rest[0] == c.name;
+    if (!known) {
+        usage();
+        return 0;
+    }
+    try {
+        return run(rest);
+    } catch (const NoSuchElement &e) {
+        fprintf(stderr, "java.util.NoSuchElementException: %s\n", e.what());
+        return 1;
+    } catch (const Error &e) {
+        fprintf(stderr, "lime-submit: %s (status %d)\n", e.what(), e.code);
+        return 1;
+    }
+}

@@ -1,0 +1,235 @@
+// bitset.hip -- bit-per-base set algebra over a coordinate space.
+//
+// North-star path for dense multi-way algebra (BASELINE configs C4/C5): one
+// bit per base of the global coordinate space (span = sum(len + 1) bits,
+// ~386 MB for hg38).  The pad base after every contig is never set, so runs
+// never cross a contig boundary.
+//   k_paint     merged runs -> bits: interior words stored whole, the two
+//               edge words OR-ed atomically (adjacent runs may share one)
+//   k_ev_count  per 4096-word tile: events (run starts + run ends) of
+//               op(words) where op = A | ~A | A&B | A&~B | AND of k sets
+//   k_ev_write  the same, writing events at scanned offsets: event 2r is the
+//               start and event 2r+1 the end of output run r
+// Semantics: base-level algebra; book-ended runs of
+// the operands coalesce in the output.
+#include "common.hpp"
+
+namespace lime {
+namespace {
+
+constexpr int BB = 256;
+constexpr int BW = 16;            // words per thread
+constexpr int BT = BB * BW;       // words per tile
+constexpr int MAXK = 16;
+
+__global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
+                                              const uint32_t *__restrict__ rge, int64_t nr,
+                                              uint64_t *__restrict__ words) {
+    const int64_t r = (int64_t)blockIdx.x * BB + threadIdx.x;
+    if (r >= nr) return;
+    const uint64_t s = rgs[r], e = rge[r];
+    if (e <= s) return;
+    const uint64_t w0 = s >> 6, w1 = (e - 1) >> 6;
+    for (uint64_t w = w0; w <= w1; ++w) {
+        const uint64_t lo = w == w0 ? (s & 63) : 0;
+        const uint64_t hi = w == w1 ? ((e - 1) & 63) : 63;
+        const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
+        if (m == ~0ull)
+            words[w] = m;
+        else
+            atomicOr((unsigned long long *)&words[w], (unsigned long long)m);
+    }
+}
+
+struct OpArgs {
+    const uint64_t *w[MAXK];
+    int k;
+    int op;  // 0 a, 1 not a, 2 a & b, 3 a & ~b, 4 and of k
+    int64_t n_words;
+    int64_t span;
+    const uint32_t *pad;  // pad bit position of every contig (sorted), nc entries
+    int32_t nc;
+};
+
+__device__ __forceinline__ uint64_t op_word(const OpArgs &a, int64_t w) {
+    if (w < 0 || w >= a.n_words) return 0;
+    uint64_t x;
+    switch (a.op) {
+        case 0: x = a.w[0][w]; break;
+        case 1: {
+            x = ~a.w[0][w];
+            // clear pad bits and bits beyond the span
+            const int64_t b0 = w * 64;
+            if (b0 + 64 > a.span) {
+                const int64_t keep = a.span - b0;
+                x &= keep <= 0 ? 0ull : (keep >= 64 ? ~0ull : ((1ull << keep) - 1));
+            }
+            int64_t c = dev::lower_bound(a.pad, 0, (int64_t)a.nc, (uint32_t)(b0 > 0xffffffffLL ? 0xffffffffLL : b0));
+            for (; c < a.nc && (int64_t)a.pad[c] < b0 + 64; ++c) x &= ~(1ull << (a.pad[c] - b0));
+            break;
+        }
+        case 2: x = a.w[0][w] & a.w[1][w]; break;
+        case 3: x = a.w[0][w] & ~a.w[1][w]; break;
+        default: {
+            x = ~0ull;
+            for (int i = 0; i < a.k; ++i) x &= a.w[i][w];
+            break;
+        }
+    }
+    return x;
+}
+
+__device__ __forceinline__ void events_of(uint64_t x, uint64_t prev, uint64_t &st, uint64_t &en) {
+    const uint64_t sh = (x << 1) | (prev >> 63);
+    st = x & ~sh;
+    en = ~x & sh;
+}
+
+__global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict__ tcnt) {
+    const int64_t w0 = (int64_t)blockIdx.x * BT;
+    uint32_t c = 0;
+#pragma unroll 4
+    for (int k = 0; k < BW; ++k) {
+        const int64_t w = w0 + k * BB + threadIdx.x;
+        if (w < a.n_words) {
+            uint64_t st, en;
+            events_of(op_word(a, w), op_word(a, w - 1), st, en);
+            c += __popcll(st) + __popcll(en);
+        }
+    }
+    c = dev::wave_reduce_sum(c);
+    __shared__ uint32_t ws[BB / 64];
+    if (dev::lane_id() == 0) ws[threadIdx.x / 64] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < BB / 64; ++i) t += ws[i];
+        tcnt[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__restrict__ toff,
+                                                 uint32_t *__restrict__ rgs,
+                                                 uint32_t *__restrict__ rge) {
+    __shared__ uint32_t scratch[BB / 64 + 1];
+    // blocked: thread t owns words w0 + t*BW .. + BW-1 (events in position order)
+    const int64_t w0 = (int64_t)blockIdx.x * BT + (int64_t)threadIdx.x * BW;
+    uint64_t prev = op_word(a, w0 - 1);
+    uint64_t xs[BW];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < BW; ++k) {
+        xs[k] = op_word(a, w0 + k);
+        uint64_t st, en;
+        events_of(xs[k], k ? xs[k - 1] : prev, st, en);
+        c += __popcll(st) + __popcll(en);
+    }
+    uint32_t tot;
+    uint32_t ev = toff[blockIdx.x] + dev::block_exclusive_sum<BB>(c, scratch, &tot);
+#pragma unroll
+    for (int k = 0; k < BW; ++k) {
+        uint64_t st, en;
+        events_of(xs[k], k ? xs[k - 1] : prev, st, en);
+        uint64_t all = st | en;
+        const uint32_t base = (uint32_t)((w0 + k) * 64);
+        while (all) {
+            const int b = __builtin_ctzll(all);
+            all &= all - 1;
+            const uint32_t p = base + (uint32_t)b;
+            if (ev & 1u)
+                rge[ev >> 1] = p;
+            else
+                rgs[ev >> 1] = p;
+            ++ev;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w, int64_t n,
+                                                 unsigned long long *out) {
+    uint64_t c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < n; i += (int64_t)gridDim.x * BB)
+        c += __popcll(w[i]);
+    c = dev::wave_reduce_sum(c);
+    if (dev::lane_id() == 0) atomicAdd(out, (unsigned long long)c);
+}
+
+}  // namespace
+
+int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
+
+int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
+    lime_result runs;
+    runs.ctx = ctx;
+    LIME_TRY(merge_runs(ctx, a, &runs, false));
+    const int64_t span = (int64_t)a->off[a->n_contigs];
+    bs->span = span;
+    bs->n_words = (span + 63) / 64;
+    LIME_TRY(alloc(ctx, &bs->words, (size_t)bs->n_words));
+    LIME_HIP(hipMemsetAsync(bs->words, 0, (size_t)bs->n_words * 8, S(ctx)));
+    if (runs.n > 0)
+        hipLaunchKernelGGL(k_paint, dim3(blocks_for(runs.n, BB)), dim3(BB), 0, S(ctx), runs.gs,
+                           runs.ge, runs.n, bs->words);
+    LIME_HIP(hipGetLastError());
+    release(ctx, runs.gs);
+    release(ctx, runs.ge);
+    return LIME_OK;
+}
+
+int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res) {
+    const lime_bitset *a = sets[0];
+    if (k > MAXK) return fail(LIME_ERR_ARG, "at most 16 bitsets per op");
+    OpArgs oa;
+    for (int i = 0; i < MAXK; ++i) oa.w[i] = i < k ? sets[i]->words : nullptr;
+    oa.k = k;
+    oa.op = op;
+    oa.n_words = a->n_words;
+    oa.span = a->span;
+    oa.nc = a->n_contigs;
+    // pad positions: off[c+1] - 1
+    std::vector<uint32_t> pad(a->n_contigs);
+    for (int c = 0; c < a->n_contigs; ++c) pad[c] = a->off[c + 1] - 1;
+    uint32_t *d_pad;
+    LIME_TRY(alloc(ctx, &d_pad, pad.size() + 1));
+    LIME_HIP(hipMemcpy(d_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
+    oa.pad = d_pad;
+    const int64_t nt = (a->n_words + BT - 1) / BT;
+    uint32_t *tcnt, *toff, *total;
+    LIME_TRY(alloc(ctx, &tcnt, (size_t)nt));
+    LIME_TRY(alloc(ctx, &toff, (size_t)nt));
+    LIME_TRY(alloc(ctx, &total, 1));
+    hipLaunchKernelGGL(k_ev_count, dim3((unsigned)nt), dim3(BB), 0, S(ctx), oa, tcnt);
+    LIME_HIP(hipGetLastError());
+    LIME_TRY(scan_exclusive_u32(ctx, tcnt, toff, nt, total));
+    uint32_t nev = 0;
+    LIME_TRY(read_back(ctx, &nev, total, sizeof(nev)));
+    if (nev & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
+    const int64_t nr = nev / 2;
+    LIME_TRY(alloc(ctx, &res->gs, (size_t)nr));
+    LIME_TRY(alloc(ctx, &res->ge, (size_t)nr));
+    hipLaunchKernelGGL(k_ev_write, dim3((unsigned)nt), dim3(BB), 0, S(ctx), oa,
+                       (const uint32_t *)toff, res->gs, res->ge);
+    LIME_HIP(hipGetLastError());
+    release(ctx, tcnt);
+    release(ctx, toff);
+    release(ctx, total);
+    release(ctx, d_pad);
+    res->n = nr;
+    return LIME_OK;
+}
+
+int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a) {
+    unsigned long long *d;
+    if (alloc(ctx, &d, 1)) return -1;
+    if (hipMemsetAsync(d, 0, 8, S(ctx)) != hipSuccess) return -1;
+    unsigned grid = blocks_for(a->n_words, BB);
+    if (grid > 8192) grid = 8192;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(k_popcount, dim3(grid), dim3(BB), 0, S(ctx), a->words, a->n_words, d);
+    unsigned long long h = 0;
+    if (read_back(ctx, &h, d, 8)) return -1;
+    release(ctx, d);
+    return (int64_t)h;
+}
+
+}  // namespace lime

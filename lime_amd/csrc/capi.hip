@@ -1,0 +1,648 @@
+// capi.hip -- the extern "C" boundary (include/lime_amd.h): contexts, the
+// coordinate space, set creation, operator entry points and host copies.
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace lime {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string &msg) { g_err = msg; }
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+void *Pool::get(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    auto it = free_blocks.find(bytes);
+    if (it != free_blocks.end()) {
+        void *p = it->second;
+        free_blocks.erase(it);
+        live[p] = bytes;
+        return p;
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        // give cached blocks back and retry once
+        for (auto &kv : free_blocks) hipFree(kv.second);
+        for (auto &kv : free_blocks) held -= (int64_t)kv.first;
+        free_blocks.clear();
+        (void)hipGetLastError();
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    }
+    held += (int64_t)bytes;
+    live[p] = bytes;
+    return p;
+}
+void Pool::put(void *p) {
+    auto it = live.find(p);
+    if (it == live.end()) return;
+    free_blocks.emplace(it->second, p);
+    live.erase(it);
+}
+void Pool::release_all() {
+    for (auto &kv : free_blocks) hipFree(kv.second);
+    for (auto &kv : live) hipFree(kv.first);
+    free_blocks.clear();
+    live.clear();
+    held = 0;
+}
+
+int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes) {
+    LIME_HIP(hipMemcpyAsync(c->pinned, dev, bytes, hipMemcpyDeviceToHost, S(c)));
+    LIME_HIP(hipStreamSynchronize(S(c)));
+    memcpy(host, c->pinned, bytes);
+    return LIME_OK;
+}
+
+// defined in the kernel translation units
+struct PairsPlan;
+int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold,
+                   PairsPlan **out);
+int intersect_fill(PairsPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
+int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr);
+void intersect_free(PairsPlan *pl);
+int64_t plan_total(const PairsPlan *pl);
+int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
+int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold, int mode,
+                 lime_result *res);
+int complement_run(lime_ctx *ctx, const lime_result *runs, const uint32_t *d_off,
+                   const uint32_t *d_len, int32_t nc, lime_result *res);
+int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
+int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
+int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
+int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t n, uint64_t seed, uint32_t lo,
+          uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig, uint32_t *d_start,
+          uint32_t *d_end);
+
+static int32_t contig_of(const std::vector<uint32_t> &off, int32_t nc, uint32_t g) {
+    // largest c in [0, nc) with off[c] <= g
+    auto it = std::upper_bound(off.begin(), off.begin() + nc, g);
+    return (int32_t)(it - off.begin()) - 1;
+}
+
+template <typename T>
+static int d2h(lime_ctx *ctx, std::vector<T> &v, const T *d, int64_t n) {
+    v.resize((size_t)n);
+    if (n == 0 || !d) return LIME_OK;
+    LIME_HIP(hipMemcpyAsync(v.data(), d, sizeof(T) * (size_t)n, hipMemcpyDeviceToHost, S(ctx)));
+    LIME_HIP(hipStreamSynchronize(S(ctx)));
+    return LIME_OK;
+}
+
+static int upload_space(lime_ctx *ctx, const lime_space *sp, uint32_t **d_off, uint32_t **d_len) {
+    LIME_TRY(alloc(ctx, d_off, (size_t)sp->n + 1));
+    std::vector<uint32_t> len32(sp->n + 1, 0);
+    for (int c = 0; c < sp->n; ++c) len32[c] = (uint32_t)sp->len[c];
+    LIME_HIP(hipMemcpyAsync(*d_off, sp->off.data(), 4 * ((size_t)sp->n + 1), hipMemcpyHostToDevice,
+                            S(ctx)));
+    if (d_len) {
+        LIME_TRY(alloc(ctx, d_len, (size_t)sp->n + 1));
+        LIME_HIP(hipMemcpyAsync(*d_len, len32.data(), 4 * ((size_t)sp->n + 1),
+                                hipMemcpyHostToDevice, S(ctx)));
+    }
+    LIME_HIP(hipStreamSynchronize(S(ctx)));
+    return LIME_OK;
+}
+
+static lime_set *new_set(lime_ctx *ctx, const lime_space *sp, int64_t n) {
+    lime_set *s = new lime_set();
+    s->ctx = ctx;
+    s->n = n;
+    s->n_contigs = sp->n;
+    s->off = sp->off;
+    s->len = sp->len;
+    return s;
+}
+
+static int create_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
+                              const int32_t *d_contig, const uint32_t *d_start,
+                              const uint32_t *d_end, lime_set **out) {
+    lime_set *s = new_set(ctx, sp, n);
+    uint32_t *d_len = nullptr;
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len);
+    if (rc == LIME_OK) rc = sort_set(ctx, s, d_contig, d_start, d_end, d_len);
+    release(ctx, d_len);
+    if (rc != LIME_OK) {
+        release(ctx, s->d_off);
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return LIME_OK;
+}
+
+static lime_result *new_result(lime_ctx *ctx, const lime_set *like) {
+    lime_result *r = new lime_result();
+    r->ctx = ctx;
+    r->off = like->off;
+    r->n_contigs = like->n_contigs;
+    return r;
+}
+
+// Java String.compareTo: lexicographic over UTF-16 code units.
+static std::vector<uint16_t> utf16(const char *s) {
+    std::vector<uint16_t> out;
+    const unsigned char *p = (const unsigned char *)s;
+    while (*p) {
+        uint32_t cp;
+        if (*p < 0x80) {
+            cp = *p++;
+        } else if ((*p >> 5) == 6 && p[1]) {
+            cp = ((p[0] & 0x1f) << 6) | (p[1] & 0x3f);
+            p += 2;
+        } else if ((*p >> 4) == 14 && p[1] && p[2]) {
+            cp = ((p[0] & 0x0f) << 12) | ((p[1] & 0x3f) << 6) | (p[2] & 0x3f);
+            p += 3;
+        } else if ((*p >> 3) == 30 && p[1] && p[2] && p[3]) {
+            cp = ((p[0] & 0x07) << 18) | ((p[1] & 0x3f) << 12) | ((p[2] & 0x3f) << 6) | (p[3] & 0x3f);
+            p += 4;
+        } else {
+            cp = *p++;  // invalid byte: keep as a code unit
+        }
+        if (cp >= 0x10000) {
+            cp -= 0x10000;
+            out.push_back((uint16_t)(0xD800 + (cp >> 10)));
+            out.push_back((uint16_t)(0xDC00 + (cp & 0x3ff)));
+        } else {
+            out.push_back((uint16_t)cp);
+        }
+    }
+    return out;
+}
+
+}  // namespace lime
+
+using namespace lime;
+
+extern "C" {
+
+const char *lime_last_error(void) { return g_err.c_str(); }
+int lime_abi_version(void) { return LIME_ABI_VERSION; }
+
+uint64_t lime_pair_hash(uint32_t start, uint32_t end, uint32_t a_row, uint32_t b_row) {
+    return dev::pair_hash(start, end, a_row, b_row);
+}
+
+int lime_ctx_create(int device, lime_ctx **out) {
+    if (!out) return fail(LIME_ERR_ARG, "out is null");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return fail(LIME_ERR_DEVICE, "no HIP device available");
+    }
+    if (device < 0 || device >= n) return fail(LIME_ERR_ARG, "device index out of range");
+    LIME_HIP(hipSetDevice(device));
+    lime_ctx *c = new lime_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault) != hipSuccess) {
+        delete c;
+        return fail(LIME_ERR_DEVICE, "stream / pinned buffer creation failed");
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return LIME_OK;
+}
+
+int lime_ctx_destroy(lime_ctx *ctx) {
+    if (!ctx) return LIME_OK;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    ctx->pool.release_all();
+    if (ctx->pinned) hipHostFree(ctx->pinned);
+    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return LIME_OK;
+}
+
+int lime_ctx_set_stream(lime_ctx *ctx, void *stream) {
+    if (!ctx) return fail(LIME_ERR_ARG, "ctx is null");
+    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    return LIME_OK;
+}
+
+int lime_ctx_synchronize(lime_ctx *ctx) {
+    if (!ctx) return fail(LIME_ERR_ARG, "ctx is null");
+    LIME_HIP(hipStreamSynchronize(ctx->stream));
+    return LIME_OK;
+}
+
+int64_t lime_ctx_pool_bytes(const lime_ctx *ctx) { return ctx ? ctx->pool.held : 0; }
+
+// ------------------------------------------------------------------- space
+int lime_space_create(int32_t n, const int64_t *lengths, lime_space **out) {
+    if (!out || n < 0 || (n > 0 && !lengths)) return fail(LIME_ERR_ARG, "bad space arguments");
+    lime_space *sp = new lime_space();
+    sp->n = n;
+    sp->len.assign(lengths, lengths + n);
+    sp->off.resize((size_t)n + 1);
+    int64_t o = 0;
+    for (int32_t c = 0; c < n; ++c) {
+        if (lengths[c] < 0) {
+            delete sp;
+            return fail(LIME_ERR_RANGE, "negative contig length");
+        }
+        sp->off[c] = (uint32_t)o;
+        o += lengths[c] + 1;
+        if (o > 0xffffffffLL) {
+            delete sp;
+            return fail(LIME_ERR_RANGE, "coordinate span sum(len + 1) exceeds 2^32");
+        }
+    }
+    sp->off[n] = (uint32_t)o;
+    sp->span = o;
+    *out = sp;
+    return LIME_OK;
+}
+int lime_space_destroy(lime_space *sp) {
+    delete sp;
+    return LIME_OK;
+}
+int32_t lime_space_contigs(const lime_space *sp) { return sp ? sp->n : 0; }
+int64_t lime_space_span(const lime_space *sp) { return sp ? sp->span : 0; }
+int64_t lime_space_offset(const lime_space *sp, int32_t c) {
+    return (sp && c >= 0 && c <= sp->n) ? (int64_t)sp->off[c] : -1;
+}
+
+// -------------------------------------------------------------------- sets
+int lime_set_create_host(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *contig,
+                         const int64_t *start, const int64_t *end, lime_set **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!contig || !start || !end)))
+        return fail(LIME_ERR_ARG, "bad set arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    std::vector<uint32_t> s32((size_t)n), e32((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        if (contig[i] < 0 || contig[i] >= sp->n)
+            return fail(LIME_ERR_CONTIG, "row " + std::to_string(i) + ": contig id not in space");
+        if (start[i] < 0 || end[i] < start[i])
+            return fail(LIME_ERR_RANGE, "row " + std::to_string(i) + ": invalid region");
+        if (end[i] > sp->len[contig[i]])
+            return fail(LIME_ERR_RANGE, "row " + std::to_string(i) + ": end beyond contig length");
+        s32[i] = (uint32_t)start[i];
+        e32[i] = (uint32_t)end[i];
+    }
+    int32_t *dc;
+    uint32_t *ds, *de;
+    LIME_TRY(alloc(ctx, &dc, (size_t)n));
+    LIME_TRY(alloc(ctx, &ds, (size_t)n));
+    LIME_TRY(alloc(ctx, &de, (size_t)n));
+    if (n > 0) {
+        LIME_HIP(hipMemcpyAsync(dc, contig, 4 * (size_t)n, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipMemcpyAsync(ds, s32.data(), 4 * (size_t)n, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipMemcpyAsync(de, e32.data(), 4 * (size_t)n, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipStreamSynchronize(S(ctx)));
+    }
+    int rc = create_from_device(ctx, sp, n, dc, ds, de, out);
+    release(ctx, dc);
+    release(ctx, ds);
+    release(ctx, de);
+    return rc;
+}
+
+int lime_set_create_device(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                           const uint32_t *d_start, const uint32_t *d_end, lime_set **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_contig || !d_start || !d_end)))
+        return fail(LIME_ERR_ARG, "bad set arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    return create_from_device(ctx, sp, n, d_contig, d_start, d_end, out);
+}
+
+int lime_set_destroy(lime_set *s) {
+    if (!s) return LIME_OK;
+    lime_ctx *ctx = s->ctx;
+    release(ctx, s->gs);
+    release(ctx, s->ge);
+    release(ctx, s->row);
+    release(ctx, s->d_off);
+    release(ctx, s->pmax);
+    delete s;
+    return LIME_OK;
+}
+
+int64_t lime_set_size(const lime_set *s) { return s ? s->n : -1; }
+
+int lime_set_device_arrays(const lime_set *s, const uint32_t **gs, const uint32_t **ge,
+                           const uint32_t **row) {
+    if (!s) return fail(LIME_ERR_ARG, "set is null");
+    if (gs) *gs = s->gs;
+    if (ge) *ge = s->ge;
+    if (row) *row = s->row;
+    return LIME_OK;
+}
+
+int lime_set_fill_host(const lime_set *s, int32_t *contig, int64_t *start, int64_t *end,
+                       int64_t *row) {
+    if (!s) return fail(LIME_ERR_ARG, "set is null");
+    lime_ctx *ctx = s->ctx;
+    std::vector<uint32_t> gs, ge, rw;
+    LIME_TRY(d2h(ctx, gs, (const uint32_t *)s->gs, s->n));
+    LIME_TRY(d2h(ctx, ge, (const uint32_t *)s->ge, s->n));
+    LIME_TRY(d2h(ctx, rw, (const uint32_t *)s->row, s->n));
+    for (int64_t i = 0; i < s->n; ++i) {
+        int32_t c = contig_of(s->off, s->n_contigs, gs[i]);
+        if (contig) contig[i] = c;
+        if (start) start[i] = (int64_t)gs[i] - s->off[c];
+        if (end) end[i] = (int64_t)ge[i] - s->off[c];
+        if (row) row[i] = rw[i];
+    }
+    return LIME_OK;
+}
+
+static bool same_space(const lime_set *a, const lime_set *b) {
+    return a->n_contigs == b->n_contigs && a->off == b->off;
+}
+
+// --------------------------------------------------------------- intersect
+struct lime_pairs {
+    PairsPlan *plan;
+    lime_ctx *ctx;
+};
+
+int lime_intersect_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,
+                         lime_pairs **plan, int64_t *n_pairs) {
+    if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad intersect arguments");
+    if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
+    hipSetDevice(ctx->device);
+    PairsPlan *pl = nullptr;
+    LIME_TRY(intersect_plan(ctx, a, b, threshold, &pl));
+    lime_pairs *p = new lime_pairs{pl, ctx};
+    *plan = p;
+    if (n_pairs) *n_pairs = plan_total(pl);
+    return LIME_OK;
+}
+
+int lime_intersect_fill_device(lime_pairs *plan, int64_t first, int64_t count, lime_pair *d_out) {
+    if (!plan || (count > 0 && !d_out)) return fail(LIME_ERR_ARG, "bad fill arguments");
+    hipSetDevice(plan->ctx->device);
+    return intersect_fill(plan->plan, first, count, d_out);
+}
+
+int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lime_pair *out) {
+    if (!plan || (count > 0 && !out)) return fail(LIME_ERR_ARG, "bad fill arguments");
+    lime_ctx *ctx = plan->ctx;
+    hipSetDevice(ctx->device);
+    const int64_t chunk = 1 << 24;
+    lime_pair *stage;
+    LIME_TRY(alloc(ctx, &stage, (size_t)std::min(chunk, std::max(count, (int64_t)1))));
+    for (int64_t f = 0; f < count; f += chunk) {
+        const int64_t c = std::min(chunk, count - f);
+        LIME_TRY(intersect_fill(plan->plan, first + f, c, stage));
+        LIME_HIP(hipMemcpyAsync(out + f, stage, sizeof(lime_pair) * (size_t)c,
+                                hipMemcpyDeviceToHost, S(ctx)));
+        LIME_HIP(hipStreamSynchronize(S(ctx)));
+    }
+    release(ctx, stage);
+    return LIME_OK;
+}
+
+int lime_intersect_checksum(lime_pairs *plan, uint64_t *sum, uint64_t *xr) {
+    if (!plan || !sum || !xr) return fail(LIME_ERR_ARG, "bad checksum arguments");
+    hipSetDevice(plan->ctx->device);
+    return intersect_checksum(plan->plan, sum, xr);
+}
+
+int lime_pairs_destroy(lime_pairs *plan) {
+    if (!plan) return LIME_OK;
+    intersect_free(plan->plan);
+    delete plan;
+    return LIME_OK;
+}
+
+// ----------------------------------------------------------------- results
+int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs) {
+    if (!ctx || !a || !out) return fail(LIME_ERR_ARG, "bad merge arguments");
+    hipSetDevice(ctx->device);
+    lime_result *r = new_result(ctx, a);
+    r->src = a;
+    int rc = merge_runs(ctx, a, r, true);
+    if (rc != LIME_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    if (n_runs) *n_runs = r->n;
+    return LIME_OK;
+}
+
+int lime_subtract(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold, int mode,
+                  lime_result **out, int64_t *n) {
+    if (!ctx || !a || !b || !out) return fail(LIME_ERR_ARG, "bad subtract arguments");
+    if (mode != LIME_SUBTRACT_LIME && mode != LIME_SUBTRACT_SET)
+        return fail(LIME_ERR_ARG, "unknown subtract mode");
+    if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
+    hipSetDevice(ctx->device);
+    lime_result *r = new_result(ctx, a);
+    int rc = subtract_run(ctx, a, b, threshold, mode, r);
+    if (rc != LIME_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    if (n) *n = r->n;
+    return LIME_OK;
+}
+
+int lime_complement(lime_ctx *ctx, const lime_space *genome, const lime_set *a, lime_result **out,
+                    int64_t *n) {
+    if (!ctx || !genome || !a || !out) return fail(LIME_ERR_ARG, "bad complement arguments");
+    if (genome->n != a->n_contigs || genome->off != a->off)
+        return fail(LIME_ERR_CONTIG, "set was not created in the genome's coordinate space");
+    hipSetDevice(ctx->device);
+    lime_result runs;
+    runs.ctx = ctx;
+    LIME_TRY(merge_runs(ctx, a, &runs, false));
+    uint32_t *d_len = nullptr;
+    uint32_t *d_off = nullptr;
+    LIME_TRY(upload_space(ctx, genome, &d_off, &d_len));
+    lime_result *r = new_result(ctx, a);
+    int rc = complement_run(ctx, &runs, d_off, d_len, genome->n, r);
+    release(ctx, runs.gs);
+    release(ctx, runs.ge);
+    release(ctx, d_off);
+    release(ctx, d_len);
+    if (rc != LIME_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    if (n) *n = r->n;
+    return LIME_OK;
+}
+
+int64_t lime_result_size(const lime_result *r) { return r ? r->n : -1; }
+
+int lime_result_fill_host(const lime_result *r, int32_t *contig, int64_t *start, int64_t *end,
+                          int64_t *a_row, int64_t *b_row) {
+    if (!r) return fail(LIME_ERR_ARG, "result is null");
+    lime_ctx *ctx = r->ctx;
+    hipSetDevice(ctx->device);
+    std::vector<uint32_t> gs, ge, ar, br;
+    LIME_TRY(d2h(ctx, gs, (const uint32_t *)r->gs, r->n));
+    LIME_TRY(d2h(ctx, ge, (const uint32_t *)r->ge, r->n));
+    if (a_row) LIME_TRY(d2h(ctx, ar, (const uint32_t *)r->a_row, r->a_row ? r->n : 0));
+    if (b_row) LIME_TRY(d2h(ctx, br, (const uint32_t *)r->b_row, r->b_row ? r->n : 0));
+    for (int64_t i = 0; i < r->n; ++i) {
+        int32_t c = contig_of(r->off, r->n_contigs, gs[i]);
+        if (contig) contig[i] = c;
+        if (start) start[i] = (int64_t)gs[i] - r->off[c];
+        if (end) end[i] = (int64_t)ge[i] - r->off[c];
+        if (a_row) a_row[i] = r->a_row ? (int64_t)ar[i] : -1;
+        if (b_row) b_row[i] = r->b_row ? (br[i] == 0xffffffffu ? -1 : (int64_t)br[i]) : -1;
+    }
+    return LIME_OK;
+}
+
+int lime_result_run_of_row(const lime_result *r, int64_t *run_of_row) {
+    if (!r || !run_of_row) return fail(LIME_ERR_ARG, "bad arguments");
+    if (!r->run_of_sorted || !r->src) return fail(LIME_ERR_ARG, "not a merge result");
+    lime_ctx *ctx = r->ctx;
+    std::vector<uint32_t> rid, row;
+    LIME_TRY(d2h(ctx, rid, (const uint32_t *)r->run_of_sorted, r->src->n));
+    LIME_TRY(d2h(ctx, row, (const uint32_t *)r->src->row, r->src->n));
+    for (int64_t i = 0; i < r->src->n; ++i) run_of_row[row[i]] = rid[i];
+    return LIME_OK;
+}
+
+int lime_result_device_arrays(const lime_result *r, const uint32_t **gs, const uint32_t **ge) {
+    if (!r) return fail(LIME_ERR_ARG, "result is null");
+    if (gs) *gs = r->gs;
+    if (ge) *ge = r->ge;
+    return LIME_OK;
+}
+
+int lime_result_destroy(lime_result *r) {
+    if (!r) return LIME_OK;
+    lime_ctx *ctx = r->ctx;
+    release(ctx, r->gs);
+    release(ctx, r->ge);
+    release(ctx, r->a_row);
+    release(ctx, r->b_row);
+    release(ctx, r->run_of_sorted);
+    delete r;
+    return LIME_OK;
+}
+
+// ------------------------------------------------------------------ bitset
+int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out) {
+    if (!ctx || !a || !out) return fail(LIME_ERR_ARG, "bad bitset arguments");
+    hipSetDevice(ctx->device);
+    lime_bitset *bs = new lime_bitset();
+    bs->ctx = ctx;
+    bs->n_contigs = a->n_contigs;
+    bs->off = a->off;
+    bs->len = a->len;
+    int rc = bitset_build(ctx, a, bs);
+    if (rc != LIME_OK) {
+        delete bs;
+        return rc;
+    }
+    *out = bs;
+    return LIME_OK;
+}
+
+static lime_result *bitset_result(lime_ctx *ctx, const lime_bitset *b) {
+    lime_result *r = new lime_result();
+    r->ctx = ctx;
+    r->off = b->off;
+    r->n_contigs = b->n_contigs;
+    return r;
+}
+
+int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bitset *b,
+                     lime_result **out, int64_t *n) {
+    if (!ctx || !a || !out || op < 0 || op > 3 || ((op == 2 || op == 3) && !b))
+        return fail(LIME_ERR_ARG, "bad bitset op arguments");
+    if (b && (b->off != a->off)) return fail(LIME_ERR_ARG, "bitsets over different spaces");
+    hipSetDevice(ctx->device);
+    const lime_bitset *sets[2] = {a, b};
+    lime_result *r = bitset_result(ctx, a);
+    int rc = bitset_runs(ctx, op, b ? 2 : 1, sets, r);
+    if (rc != LIME_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    if (n) *n = r->n;
+    return LIME_OK;
+}
+
+int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, lime_result **out,
+                         int64_t *n) {
+    if (!ctx || k < 1 || !sets || !out) return fail(LIME_ERR_ARG, "bad bitset and arguments");
+    for (int i = 1; i < k; ++i)
+        if (sets[i]->off != sets[0]->off) return fail(LIME_ERR_ARG, "bitsets over different spaces");
+    hipSetDevice(ctx->device);
+    lime_result *r = bitset_result(ctx, sets[0]);
+    int rc = bitset_runs(ctx, 4, k, sets, r);
+    if (rc != LIME_OK) {
+        delete r;
+        return rc;
+    }
+    *out = r;
+    if (n) *n = r->n;
+    return LIME_OK;
+}
+
+int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a) {
+    if (!ctx || !a) return -1;
+    hipSetDevice(ctx->device);
+    return bitset_popcount(ctx, a);
+}
+
+int lime_bitset_destroy(lime_bitset *bs) {
+    if (!bs) return LIME_OK;
+    release(bs->ctx, bs->words);
+    delete bs;
+    return LIME_OK;
+}
+
+// ------------------------------------------------------------------- synth
+int lime_synth_uniform(lime_ctx *ctx, const lime_space *sp, int64_t n, uint64_t seed,
+                       uint32_t lo, uint32_t hi, int32_t *d_contig, uint32_t *d_start,
+                       uint32_t *d_end) {
+    if (!ctx || !sp) return fail(LIME_ERR_ARG, "bad synth arguments");
+    hipSetDevice(ctx->device);
+    return synth(ctx, sp, 0, n, seed, lo, hi, 0, 0, d_contig, d_start, d_end);
+}
+
+int lime_synth_pileup(lime_ctx *ctx, const lime_space *sp, int64_t n, uint64_t seed,
+                      int64_t n_centres, uint32_t sigma, uint32_t lo, uint32_t hi,
+                      int32_t *d_contig, uint32_t *d_start, uint32_t *d_end) {
+    if (!ctx || !sp) return fail(LIME_ERR_ARG, "bad synth arguments");
+    hipSetDevice(ctx->device);
+    return synth(ctx, sp, 1, n, seed, lo, hi, n_centres, sigma, d_contig, d_start, d_end);
+}
+
+// ----------------------------------------------------------- host helpers
+int lime_contig_rank(int32_t n, const char *const *names, int32_t *rank_out) {
+    if (n < 0 || (n > 0 && (!names || !rank_out))) return fail(LIME_ERR_ARG, "bad rank arguments");
+    std::vector<std::vector<uint16_t>> u(n);
+    for (int32_t i = 0; i < n; ++i) {
+        if (!names[i]) return fail(LIME_ERR_ARG, "null contig name");
+        u[i] = utf16(names[i]);
+    }
+    std::vector<int32_t> idx(n);
+    for (int32_t i = 0; i < n; ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return u[x] < u[y]; });
+    int32_t rank = -1;
+    for (int32_t k = 0; k < n; ++k) {
+        if (k == 0 || u[idx[k]] != u[idx[k - 1]]) ++rank;
+        rank_out[idx[k]] = rank;
+    }
+    return LIME_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,308 @@
+// common.hpp -- internal types shared by the engine's translation units:
+// context (device, stream, caching pool), coordinate space, device sets and
+// results, error plumbing, and the wave/block primitives the kernels use.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lime_amd.h"
+
+namespace lime {
+
+// ------------------------------------------------------------------ errors
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define LIME_HIP(expr)                                                                          \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return ::lime::fail(LIME_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define LIME_TRY(expr)                \
+    do {                              \
+        int _s = (expr);              \
+        if (_s != LIME_OK) return _s; \
+    } while (0)
+
+// ------------------------------------------------------------- device pool
+// Grow-only caching allocator: blocks are recycled by exact (rounded) size so
+// that repeated operator calls of the same shape never hit hipMalloc.
+struct Pool {
+    std::multimap<size_t, void *> free_blocks;
+    std::map<void *, size_t> live;
+    int64_t held = 0;
+    void *get(size_t bytes);
+    void put(void *p);
+    void release_all();
+};
+
+}  // namespace lime
+
+struct lime_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    lime::Pool pool;
+    std::mutex mu;
+    // small pinned scratch for scalar read-backs
+    void *pinned = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+struct lime_space {
+    int32_t n = 0;
+    std::vector<int64_t> len;   // contig lengths
+    std::vector<uint32_t> off;  // n + 1 entries; off[c+1] = off[c] + len[c] + 1
+    int64_t span = 0;           // off[n]
+};
+
+// Device-resident sorted set: canonical order (gstart, zero-width first).
+struct lime_set {
+    lime_ctx *ctx = nullptr;
+    int64_t n = 0;
+    uint32_t *gs = nullptr;   // global start
+    uint32_t *ge = nullptr;   // global end
+    uint32_t *row = nullptr;  // input row
+    // device copy of the space offsets (n_contigs + 1)
+    uint32_t *d_off = nullptr;
+    int32_t n_contigs = 0;
+    std::vector<uint32_t> off;  // host copy
+    std::vector<int64_t> len;
+    // statistics gathered during creation
+    uint32_t min_width = 0, max_width = 0;
+    bool has_zero_width = false;
+    // lazily built: inclusive prefix max of ge (for subtract)
+    mutable uint32_t *pmax = nullptr;
+};
+
+struct lime_result {
+    lime_ctx *ctx = nullptr;
+    int64_t n = 0;
+    uint32_t *gs = nullptr;   // global start
+    uint32_t *ge = nullptr;   // global end
+    uint32_t *a_row = nullptr;  // may be null
+    uint32_t *b_row = nullptr;  // may be null (0xffffffff = None)
+    uint32_t *run_of_sorted = nullptr;  // merge only (per sorted input)
+    const lime_set *src = nullptr;      // merge only
+    uint32_t *d_off = nullptr;          // contig offsets used to localise
+    int32_t n_contigs = 0;
+    std::vector<uint32_t> off;
+};
+
+struct lime_bitset {
+    lime_ctx *ctx = nullptr;
+    uint64_t *words = nullptr;
+    int64_t n_words = 0;
+    int64_t span = 0;
+    uint32_t *d_off = nullptr;
+    int32_t n_contigs = 0;
+    std::vector<uint32_t> off;
+    std::vector<int64_t> len;
+};
+
+namespace lime {
+
+inline hipStream_t S(lime_ctx *c) { return c->stream; }
+
+template <typename T>
+inline int alloc(lime_ctx *c, T **p, size_t count) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 256;
+    void *v = c->pool.get(bytes);
+    if (!v) return fail(LIME_ERR_NOMEM, "device allocation of " + std::to_string(bytes) + " bytes failed");
+    *p = reinterpret_cast<T *>(v);
+    return LIME_OK;
+}
+template <typename T>
+inline void release(lime_ctx *c, T *&p) {
+    if (p) c->pool.put(reinterpret_cast<void *>(p));
+    p = nullptr;
+}
+
+// read a device scalar back to the host (synchronises the context stream)
+int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes);
+
+// grid helper
+inline unsigned blocks_for(int64_t n, int64_t per_block) {
+    return (unsigned)((n + per_block - 1) / per_block);
+}
+
+// ------------------------------------------------------ kernel entry points
+// (defined in the .hip translation units)
+int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32_t *d_start,
+             const uint32_t *d_end, const uint32_t *d_len);
+int scan_exclusive_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n,
+                       uint32_t *total_dev);
+int scan_exclusive_u64(lime_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n,
+                       uint64_t *total_dev);
+int build_prefix_max(lime_ctx *ctx, const lime_set *set);
+
+}  // namespace lime
+
+// ====================================================================== device
+// Wave (64-lane) and block primitives.  Block size is a multiple of 64.
+#ifdef __HIPCC__
+namespace lime {
+namespace dev {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    int l = __lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_inclusive_sum(T v) {
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        T o = __shfl_up(v, d, WAVE);
+        if (__lane_id() >= d) v += o;
+    }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_inclusive_max(T v) {
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        T o = __shfl_up(v, d, WAVE);
+        if (__lane_id() >= d) v = v > o ? v : o;
+    }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_reduce_sum(T v) {
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) v += __shfl_xor(v, d, WAVE);
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_reduce_max(T v) {
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) {
+        T o = __shfl_xor(v, d, WAVE);
+        v = v > o ? v : o;
+    }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_reduce_or(T v) {
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) v |= __shfl_xor(v, d, WAVE);
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_reduce_min(T v) {
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) {
+        T o = __shfl_xor(v, d, WAVE);
+        v = v < o ? v : o;
+    }
+    return v;
+}
+
+// Block-wide exclusive sum. `scratch` holds >= BLOCK/64 + 1 T's.  Returns the
+// exclusive prefix; *total receives the block total.  Contains barriers.
+template <int BLOCK, typename T>
+__device__ __forceinline__ T block_exclusive_sum(T v, T *scratch, T *total) {
+    constexpr int NW = BLOCK / WAVE;
+    const int w = threadIdx.x / WAVE;
+    T inc = wave_inclusive_sum(v);
+    if (__lane_id() == WAVE - 1) scratch[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T run = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            T t = scratch[i];
+            scratch[i] = run;
+            run += t;
+        }
+        scratch[NW] = run;
+    }
+    __syncthreads();
+    T res = scratch[w] + inc - v;
+    *total = scratch[NW];
+    __syncthreads();
+    return res;
+}
+
+// Block-wide exclusive max with identity `ident`.
+template <int BLOCK, typename T>
+__device__ __forceinline__ T block_exclusive_max(T v, T ident, T *scratch, T *total) {
+    constexpr int NW = BLOCK / WAVE;
+    const int w = threadIdx.x / WAVE;
+    T inc = wave_inclusive_max(v);
+    T exc = __shfl_up(inc, 1, WAVE);
+    if (__lane_id() == 0) exc = ident;
+    if (__lane_id() == WAVE - 1) scratch[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T run = ident;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            T t = scratch[i];
+            scratch[i] = run;
+            run = run > t ? run : t;
+        }
+        scratch[NW] = run;
+    }
+    __syncthreads();
+    T pre = scratch[w];
+    T res = pre > exc ? pre : exc;
+    *total = scratch[NW];
+    __syncthreads();
+    return res;
+}
+
+// first index in [lo, hi) with a[i] >= key (a sorted ascending)
+template <typename T, typename K>
+__device__ __forceinline__ int64_t lower_bound(const T *a, int64_t lo, int64_t hi, K key) {
+    while (lo < hi) {
+        int64_t mid = lo + ((hi - lo) >> 1);
+        if ((K)a[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+// first index in [lo, hi) with a[i] > key
+template <typename T, typename K>
+__device__ __forceinline__ int64_t upper_bound(const T *a, int64_t lo, int64_t hi, K key) {
+    while (lo < hi) {
+        int64_t mid = lo + ((hi - lo) >> 1);
+        if ((K)a[mid] <= key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// splitmix64 finaliser (shared with oracle/lime_oracle.c lo_pair_hash)
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t pair_hash(uint32_t s, uint32_t e, uint32_t a,
+                                                       uint32_t b) {
+    uint64_t x = ((uint64_t)s << 32) | e;
+    uint64_t y = ((uint64_t)a << 32) | b;
+    return mix64(x ^ mix64(y));
+}
+
+}  // namespace dev
+}  // namespace lime
+#endif

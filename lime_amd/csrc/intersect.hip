@@ -1,0 +1,537 @@
+// intersect.hip -- DistributedIntersection as a two-stream merge-path join.
+//
+// Reference: SetTheory.scala:175-187 sweeps each sorted left row against a
+// cache of right rows (advance/prune, OverlapBasedSetTheory.scala:21-38) and
+// Intersection.scala:58-69 emits ([max s, min e), (L, R)) for every cached R
+// with overlapsBy(L, R) >= threshold (strict half-open overlap).
+//
+// MI355X formulation.  A pair (a, b) overlaps strictly iff exactly one of
+//   stream 0:  b.s in [a.s, a.e)        (b starts inside a, ties to a)
+//   stream 1:  a.s in (b.s, b.e)        (a starts strictly inside b)
+// holds, so every owner row's partners are a CONTIGUOUS range of the other
+// sorted set, found by two lower_bounds:
+//   lo = lb(P.gs, o.gs + lo_off)       lo_off = 0 (stream 0) / 1 (stream 1)
+//   hi = lb(P.gs, o.ge - tp + 1)       tp = max(threshold, 1)
+// With a threshold t >= 1 the range already encodes "overlap >= t" on the
+// owner side; the partner must additionally have width >= t (a filter, only
+// evaluated when the partner set actually holds rows narrower than t).  For
+// t <= 0 the only false candidates are zero-width b at exactly a.s, which the
+// canonical order puts first in the range, so lo just skips them.
+//
+// Work is decomposed by OUTPUT, not by input: per-owner counts are scanned
+// into per-tile offsets and every fill workgroup writes exactly S consecutive
+// output records, so pile-ups cannot unbalance the grid.  Output records are
+// 16 B (start, end, a_row, b_row), written with 16-B non-temporal stores,
+// fully coalesced (lane i writes record base + i).
+//
+// Kernels:
+//   k_windows   one wave per owner tile (1024 owners): partner window
+//   k_count     lo / count per owner (LDS-staged window), tile totals
+//   scan (u64)  tile offsets
+//   k_fill      S-record blocks: owner = load-balanced search, partner = lo + rank
+//   k_fill_filtered  thread-per-owner fallback when a width filter applies
+#include "common.hpp"
+
+namespace lime {
+
+struct PairsPlan {
+    lime_ctx *ctx;
+    const lime_set *A, *B;
+    int64_t threshold;
+    int64_t tp;
+    bool filtered;
+    int64_t nt0, nt1;  // owner tiles of stream 0 (owners A) and 1 (owners B)
+    uint32_t *olo = nullptr, *ocnt = nullptr;  // per owner, stream 0 then stream 1
+    uint64_t *toff = nullptr;                  // per tile exclusive offsets
+    uint32_t *win = nullptr;                   // per tile partner window [lo, hi)
+    int64_t total = 0;
+};
+
+namespace {
+
+constexpr int IB = 256;
+constexpr int OPT = 4;               // owners per thread
+constexpr int OT = IB * OPT;         // owners per tile
+constexpr int WCAP = 4096;           // LDS window capacity (partner starts)
+constexpr int64_t SBLK = 131072;     // output records per fill workgroup
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct StreamArgs {
+    const uint32_t *ogs, *oge, *orow;  // owner set
+    const uint32_t *pgs, *pge, *prow;  // partner set
+    int64_t no, np;
+    uint32_t lo_off;  // 0 or 1
+    int zw_skip;      // skip zero-width partners at exactly o.gs
+    int64_t tile0;    // first global tile index of this stream
+    int64_t owner0;   // first global owner slot of this stream (olo/ocnt)
+};
+
+__device__ __forceinline__ void owner_keys(uint32_t og, uint32_t oe, uint32_t lo_off, int64_t tp,
+                                           int64_t &lo_key, int64_t &hi_key) {
+    lo_key = (int64_t)og + lo_off;
+    hi_key = (int64_t)oe - tp + 1;
+}
+
+__global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64_t ntiles,
+                                                uint32_t *__restrict__ win) {
+    const int64_t t = (int64_t)blockIdx.x * (IB / 64) + threadIdx.x / 64;
+    if (t >= ntiles) return;
+    const int lane = dev::lane_id();
+    const int64_t o0 = t * OT;
+    const int64_t o1 = min(o0 + OT, sa.no);
+    int64_t hmax = INT64_MIN;
+    for (int64_t j = o0 + lane; j < o1; j += 64) hmax = max(hmax, (int64_t)sa.oge[j] - tp + 1);
+    hmax = dev::wave_reduce_max(hmax);
+    const int64_t lkey = (int64_t)sa.ogs[o0] + sa.lo_off;
+    if (hmax < lkey) hmax = lkey;
+    if (lane == 0) win[2 * (sa.tile0 + t)] = (uint32_t)dev::lower_bound(sa.pgs, 0, sa.np, lkey);
+    if (lane == 1) win[2 * (sa.tile0 + t) + 1] = (uint32_t)dev::lower_bound(sa.pgs, 0, sa.np, hmax);
+}
+
+template <bool FILTER>
+__global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t threshold,
+                                              const uint32_t *__restrict__ win,
+                                              uint32_t *__restrict__ olo,
+                                              uint32_t *__restrict__ ocnt,
+                                              uint64_t *__restrict__ tcnt) {
+    __shared__ uint32_t wgs[WCAP];
+    __shared__ uint64_t red[IB / 64];
+    const int64_t t = blockIdx.x;
+    const int64_t o0 = t * OT;
+    const int64_t o1 = min(o0 + OT, sa.no);
+    const uint32_t wlo = win[2 * (sa.tile0 + t)], whi = win[2 * (sa.tile0 + t) + 1];
+    const int64_t wlen = (int64_t)whi - wlo;
+    const bool in_lds = wlen <= WCAP;
+    if (in_lds)
+        for (int64_t i = threadIdx.x; i < wlen; i += IB) wgs[i] = sa.pgs[wlo + i];
+    __syncthreads();
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+        const int64_t j = o0 + k * IB + threadIdx.x;
+        if (j >= o1) break;
+        const uint32_t og = sa.ogs[j], oe = sa.oge[j];
+        int64_t lk, hk;
+        owner_keys(og, oe, sa.lo_off, tp, lk, hk);
+        int64_t lo = wlo, hi = wlo;
+        if (hk > lk) {
+            if (in_lds) {
+                lo = wlo + dev::lower_bound(wgs, 0, wlen, lk);
+                hi = wlo + dev::lower_bound(wgs, lo - wlo, wlen, hk);
+            } else {
+                lo = dev::lower_bound(sa.pgs, (int64_t)wlo, (int64_t)whi, lk);
+                hi = dev::lower_bound(sa.pgs, lo, (int64_t)whi, hk);
+            }
+            if (sa.zw_skip)
+                while (lo < hi && sa.pgs[lo] == og && sa.pge[lo] == og) ++lo;
+        }
+        uint32_t c;
+        if (FILTER) {
+            c = 0;
+            for (int64_t p = lo; p < hi; ++p) c += (int64_t)(sa.pge[p] - sa.pgs[p]) >= threshold;
+        } else {
+            c = (uint32_t)(hi - lo);
+        }
+        olo[sa.owner0 + j] = (uint32_t)lo;
+        ocnt[sa.owner0 + j] = c;
+        sum += c;
+    }
+    sum = dev::wave_reduce_sum(sum);
+    if (dev::lane_id() == 0) red[threadIdx.x / 64] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int i = 0; i < IB / 64; ++i) s += red[i];
+        tcnt[sa.tile0 + t] = s;
+    }
+}
+
+__device__ __forceinline__ uint32_t contig_off(const uint32_t *__restrict__ off, int32_t nc,
+                                               uint32_t g) {
+    // largest c with off[c] <= g
+    int64_t c = dev::upper_bound(off, 0, (int64_t)nc, g) - 1;
+    return off[c < 0 ? 0 : c];
+}
+
+struct FillArgs {
+    StreamArgs s[2];
+    const uint32_t *olo, *ocnt;
+    const uint64_t *toff;
+    int64_t ntiles;
+    const uint32_t *off;
+    int32_t n_contigs;
+    int64_t first, count;  // output window [first, first + count)
+    u32x4 *out;            // out[0] is record `first`
+    uint64_t *cksum;       // [sum, xor] when checksumming instead of writing
+};
+
+template <bool CKSUM>
+__global__ __launch_bounds__(IB) void k_fill(FillArgs fa) {
+    __shared__ uint32_t s_off[OT + 1];
+    __shared__ uint32_t s_lo[OT], s_gs[OT], s_ge[OT], s_row[OT], s_seg[OT];
+    __shared__ uint32_t scratch[IB / 64 + 1];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_red[2][IB / 64];
+
+    const int64_t g0 = fa.first / SBLK;
+    const int64_t ob = max(fa.first, (g0 + blockIdx.x) * SBLK);
+    const int64_t oend = min(fa.first + fa.count, (g0 + blockIdx.x + 1) * SBLK);
+    if (ob >= oend) return;
+    if (threadIdx.x == 0) s_tile = dev::upper_bound(fa.toff, 0, fa.ntiles, (uint64_t)ob) - 1;
+    __syncthreads();
+    int64_t t = s_tile;
+    uint64_t hsum = 0, hxor = 0;
+    while (t < fa.ntiles && (int64_t)fa.toff[t] < oend) {
+        const int st = t < fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT ? 0 : 1;
+        const StreamArgs sa = st ? fa.s[1] : fa.s[0];
+        const int64_t lt = t - sa.tile0;
+        const int64_t o0 = lt * OT;
+        const int nown = (int)min((int64_t)OT, sa.no - o0);
+        const int64_t tbase = (int64_t)fa.toff[t];
+        // ---- stage the tile's owners (blocked: thread i owns owners i*OPT..)
+        uint32_t c[OPT];
+        uint32_t csum = 0;
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) {
+            const int q = threadIdx.x * OPT + k;
+            c[k] = q < nown ? fa.ocnt[sa.owner0 + o0 + q] : 0u;
+            csum += c[k];
+        }
+        uint32_t ttot;
+        uint32_t run = dev::block_exclusive_sum<IB>(csum, scratch, &ttot);
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) {
+            s_off[threadIdx.x * OPT + k] = run;
+            run += c[k];
+        }
+        if (threadIdx.x == 0) s_off[OT] = ttot;
+        const uint32_t seg_first = contig_off(fa.off, fa.n_contigs, sa.ogs[o0]);
+        const uint32_t seg_last = contig_off(fa.off, fa.n_contigs, sa.ogs[o0 + nown - 1]);
+        for (int q = threadIdx.x; q < nown; q += IB) {
+            const int64_t j = o0 + q;
+            s_lo[q] = fa.olo[sa.owner0 + j];
+            const uint32_t og = sa.ogs[j];
+            s_gs[q] = og;
+            s_ge[q] = sa.oge[j];
+            s_row[q] = sa.orow[j];
+            s_seg[q] = seg_first == seg_last ? seg_first : contig_off(fa.off, fa.n_contigs, og);
+        }
+        for (int q = nown + threadIdx.x; q < OT; q += IB) s_off[q] = ttot;  // padding owners
+        __syncthreads();
+        // ---- expand this tile's slice of the output window
+        const int64_t lb = max(ob - tbase, (int64_t)0);
+        const int64_t le = min(oend - tbase, (int64_t)ttot);
+        int64_t o = lb + threadIdx.x;
+        if (o < le) {
+            // owner of o: largest q with s_off[q] <= o
+            int q = (int)dev::upper_bound(s_off, 0, (int64_t)nown, (uint32_t)o) - 1;
+            for (; o < le; o += IB) {
+                while (s_off[q + 1] <= (uint32_t)o) ++q;
+                const uint32_t p = s_lo[q] + ((uint32_t)o - s_off[q]);
+                const uint32_t pg = sa.pgs[p], pe = sa.pge[p], pr = sa.prow[p];
+                const uint32_t og = s_gs[q], oe = s_ge[q], orow = s_row[q], sg = s_seg[q];
+                const uint32_t rs = (og > pg ? og : pg) - sg;
+                const uint32_t re = (oe < pe ? oe : pe) - sg;
+                const uint32_t ar = st == 0 ? orow : pr;
+                const uint32_t br = st == 0 ? pr : orow;
+                if (CKSUM) {
+                    uint64_t h = dev::pair_hash(rs, re, ar, br);
+                    hsum += h;
+                    hxor ^= h;
+                } else {
+                    u32x4 v = {rs, re, ar, br};
+                    __builtin_nontemporal_store(v, fa.out + (tbase + o - fa.first));
+                }
+            }
+        }
+        __syncthreads();
+        ++t;
+    }
+    if (CKSUM) {
+        hsum = dev::wave_reduce_sum(hsum);
+        uint64_t x = hxor;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
+        if (dev::lane_id() == 0) {
+            s_red[0][threadIdx.x / 64] = hsum;
+            s_red[1][threadIdx.x / 64] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t a = 0, b = 0;
+            for (int i = 0; i < IB / 64; ++i) {
+                a += s_red[0][i];
+                b ^= s_red[1][i];
+            }
+            atomicAdd((unsigned long long *)&fa.cksum[0], (unsigned long long)a);
+            atomicXor((unsigned long long *)&fa.cksum[1], (unsigned long long)b);
+        }
+    }
+}
+
+// Filtered fallback (threshold >= 1 with partners narrower than it): thread per
+// owner walks its candidate range and emits the qualifying ones in order.
+template <bool CKSUM>
+__global__ __launch_bounds__(IB) void k_fill_filtered(FillArgs fa, int64_t threshold) {
+    __shared__ uint32_t scratch[IB / 64 + 1];
+    __shared__ uint64_t s_red[2][IB / 64];
+    const int64_t t = blockIdx.x;
+    const int st = t < fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT ? 0 : 1;
+    const StreamArgs sa = st ? fa.s[1] : fa.s[0];
+    const int64_t lt = t - sa.tile0;
+    const int64_t o0 = lt * OT;
+    const int nown = (int)min((int64_t)OT, sa.no - o0);
+    const int64_t tbase = (int64_t)fa.toff[t];
+    uint32_t c[OPT];
+    uint32_t csum = 0;
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+        const int q = threadIdx.x * OPT + k;
+        c[k] = q < nown ? fa.ocnt[sa.owner0 + o0 + q] : 0u;
+        csum += c[k];
+    }
+    uint32_t ttot;
+    int64_t pos = tbase + dev::block_exclusive_sum<IB>(csum, scratch, &ttot);
+    uint64_t hsum = 0, hxor = 0;
+    const int64_t wend = fa.first + fa.count;
+    for (int k = 0; k < OPT; ++k) {
+        const int q = threadIdx.x * OPT + k;
+        if (q >= nown || c[k] == 0) continue;
+        if (pos + c[k] <= fa.first || pos >= wend) {
+            pos += c[k];
+            continue;
+        }
+        const int64_t j = o0 + q;
+        const uint32_t og = sa.ogs[j], oe = sa.oge[j], orow = sa.orow[j];
+        const uint32_t sg = contig_off(fa.off, fa.n_contigs, og);
+        uint32_t p = fa.olo[sa.owner0 + j];
+        uint32_t left = c[k];
+        for (; left > 0; ++p) {
+            const uint32_t pg = sa.pgs[p], pe = sa.pge[p];
+            if ((int64_t)(pe - pg) < threshold) continue;
+            --left;
+            if (pos >= fa.first && pos < wend) {
+                const uint32_t pr = sa.prow[p];
+                const uint32_t rs = (og > pg ? og : pg) - sg;
+                const uint32_t re = (oe < pe ? oe : pe) - sg;
+                const uint32_t ar = st == 0 ? orow : pr;
+                const uint32_t br = st == 0 ? pr : orow;
+                if (CKSUM) {
+                    uint64_t h = dev::pair_hash(rs, re, ar, br);
+                    hsum += h;
+                    hxor ^= h;
+                } else {
+                    u32x4 v = {rs, re, ar, br};
+                    fa.out[pos - fa.first] = v;
+                }
+            }
+            ++pos;
+        }
+    }
+    if (CKSUM) {
+        hsum = dev::wave_reduce_sum(hsum);
+        uint64_t x = hxor;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
+        if (dev::lane_id() == 0) {
+            s_red[0][threadIdx.x / 64] = hsum;
+            s_red[1][threadIdx.x / 64] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t a = 0, b = 0;
+            for (int i = 0; i < IB / 64; ++i) {
+                a += s_red[0][i];
+                b ^= s_red[1][i];
+            }
+            atomicAdd((unsigned long long *)&fa.cksum[0], (unsigned long long)a);
+            atomicXor((unsigned long long *)&fa.cksum[1], (unsigned long long)b);
+        }
+    }
+}
+
+StreamArgs stream_args(const lime_set *O, const lime_set *P, int st, int64_t threshold,
+                       int64_t tile0, int64_t owner0) {
+    StreamArgs s;
+    s.ogs = O->gs;
+    s.oge = O->ge;
+    s.orow = O->row;
+    s.pgs = P->gs;
+    s.pge = P->ge;
+    s.prow = P->row;
+    s.no = O->n;
+    s.np = P->n;
+    s.lo_off = st == 0 ? 0u : 1u;
+    s.zw_skip = (st == 0 && threshold <= 0 && P->has_zero_width) ? 1 : 0;
+    s.tile0 = tile0;
+    s.owner0 = owner0;
+    return s;
+}
+
+FillArgs fill_args(PairsPlan *pl) {
+    FillArgs fa;
+    fa.s[0] = stream_args(pl->A, pl->B, 0, pl->threshold, 0, 0);
+    fa.s[1] = stream_args(pl->B, pl->A, 1, pl->threshold, pl->nt0, pl->A->n);
+    fa.olo = pl->olo;
+    fa.ocnt = pl->ocnt;
+    fa.toff = pl->toff;
+    fa.ntiles = pl->nt0 + pl->nt1;
+    fa.off = pl->A->d_off;
+    fa.n_contigs = pl->A->n_contigs;
+    fa.first = 0;
+    fa.count = 0;
+    fa.out = nullptr;
+    fa.cksum = nullptr;
+    return fa;
+}
+
+int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_t *cksum) {
+    lime_ctx *ctx = pl->ctx;
+    if (count <= 0) return LIME_OK;
+    FillArgs fa = fill_args(pl);
+    fa.first = first;
+    fa.count = count;
+    fa.out = out;
+    fa.cksum = cksum;
+    if (pl->filtered) {
+        const unsigned grid = (unsigned)(pl->nt0 + pl->nt1);
+        if (cksum)
+            hipLaunchKernelGGL(k_fill_filtered<true>, dim3(grid), dim3(IB), 0, S(ctx), fa,
+                               pl->threshold);
+        else
+            hipLaunchKernelGGL(k_fill_filtered<false>, dim3(grid), dim3(IB), 0, S(ctx), fa,
+                               pl->threshold);
+    } else {
+        const int64_t g0 = first / SBLK;
+        const int64_t g1 = (first + count + SBLK - 1) / SBLK;
+        const int64_t grid = g1 - g0;
+        if (grid > 0x7fffffff) return fail(LIME_ERR_OVERFLOW, "fill window too large");
+        if (cksum)
+            hipLaunchKernelGGL(k_fill<true>, dim3((unsigned)grid), dim3(IB), 0, S(ctx), fa);
+        else
+            hipLaunchKernelGGL(k_fill<false>, dim3((unsigned)grid), dim3(IB), 0, S(ctx), fa);
+    }
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
+}  // namespace
+
+int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold,
+                   PairsPlan **out) {
+    PairsPlan *pl = new PairsPlan();
+    pl->ctx = ctx;
+    pl->A = A;
+    pl->B = B;
+    pl->threshold = threshold;
+    pl->tp = threshold > 1 ? threshold : 1;
+    pl->filtered = threshold >= 1 && (int64_t)std::min(A->min_width, B->min_width) < threshold &&
+                   A->n > 0 && B->n > 0;
+    pl->nt0 = (A->n + OT - 1) / OT;
+    pl->nt1 = (B->n + OT - 1) / OT;
+    const int64_t nt = pl->nt0 + pl->nt1;
+    int rc = LIME_OK;
+    uint64_t *tcnt = nullptr, *total = nullptr;
+    if ((rc = alloc(ctx, &pl->olo, (size_t)(A->n + B->n))) ||
+        (rc = alloc(ctx, &pl->ocnt, (size_t)(A->n + B->n))) ||
+        (rc = alloc(ctx, &pl->toff, (size_t)nt)) || (rc = alloc(ctx, &pl->win, (size_t)2 * nt)) ||
+        (rc = alloc(ctx, &tcnt, (size_t)nt)) || (rc = alloc(ctx, &total, 1))) {
+        delete pl;
+        return rc;
+    }
+    if (A->n > 0 && B->n > 0) {
+        for (int st = 0; st < 2; ++st) {
+            const lime_set *O = st == 0 ? A : B;
+            const lime_set *P = st == 0 ? B : A;
+            const int64_t ntl = st == 0 ? pl->nt0 : pl->nt1;
+            StreamArgs sa = stream_args(O, P, st, threshold, st == 0 ? 0 : pl->nt0,
+                                        st == 0 ? 0 : A->n);
+            hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa,
+                               pl->tp, ntl, pl->win);
+            if (pl->filtered)
+                hipLaunchKernelGGL(k_count<true>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
+                                   pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
+                                   tcnt);
+            else
+                hipLaunchKernelGGL(k_count<false>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
+                                   pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
+                                   tcnt);
+            LIME_HIP(hipGetLastError());
+        }
+    } else {
+        LIME_HIP(hipMemsetAsync(tcnt, 0, sizeof(uint64_t) * (size_t)(nt > 0 ? nt : 1), S(ctx)));
+        LIME_HIP(hipMemsetAsync(pl->ocnt, 0, sizeof(uint32_t) * (size_t)(A->n + B->n > 0 ? A->n + B->n : 1), S(ctx)));
+    }
+    LIME_TRY(scan_exclusive_u64(ctx, tcnt, pl->toff, nt, total));
+    uint64_t tot = 0;
+    LIME_TRY(read_back(ctx, &tot, total, sizeof(tot)));
+    release(ctx, tcnt);
+    release(ctx, total);
+    pl->total = (int64_t)tot;
+    *out = pl;
+    return LIME_OK;
+}
+
+// Candidate range [olo, olo + ocnt) of every owner row of O in P for stream
+// `st` (unfiltered), used by subtract (stream 0: b.s in [a.s, a.e - tp]).
+int owner_ranges(lime_ctx *ctx, const lime_set *O, const lime_set *P, int st, int64_t threshold,
+                 uint32_t *olo, uint32_t *ocnt) {
+    if (O->n == 0) return LIME_OK;
+    if (P->n == 0) {
+        LIME_HIP(hipMemsetAsync(olo, 0, sizeof(uint32_t) * (size_t)O->n, S(ctx)));
+        LIME_HIP(hipMemsetAsync(ocnt, 0, sizeof(uint32_t) * (size_t)O->n, S(ctx)));
+        return LIME_OK;
+    }
+    const int64_t tp = threshold > 1 ? threshold : 1;
+    const int64_t ntl = (O->n + OT - 1) / OT;
+    uint32_t *win;
+    uint64_t *tcnt;
+    LIME_TRY(alloc(ctx, &win, (size_t)2 * ntl));
+    LIME_TRY(alloc(ctx, &tcnt, (size_t)ntl));
+    StreamArgs sa = stream_args(O, P, st, threshold, 0, 0);
+    hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa, tp, ntl,
+                       win);
+    hipLaunchKernelGGL(k_count<false>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa, tp, threshold,
+                       (const uint32_t *)win, olo, ocnt, tcnt);
+    LIME_HIP(hipGetLastError());
+    release(ctx, win);
+    release(ctx, tcnt);
+    return LIME_OK;
+}
+
+int intersect_fill(PairsPlan *pl, int64_t first, int64_t count, lime_pair *d_out) {
+    if (first < 0 || count < 0 || first + count > pl->total)
+        return fail(LIME_ERR_ARG, "fill window outside [0, n_pairs)");
+    return launch_fill(pl, first, count, reinterpret_cast<u32x4 *>(d_out), nullptr);
+}
+
+int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr) {
+    lime_ctx *ctx = pl->ctx;
+    uint64_t *ck;
+    LIME_TRY(alloc(ctx, &ck, 2));
+    LIME_HIP(hipMemsetAsync(ck, 0, 16, S(ctx)));
+    // bound each launch to keep the grid size in range
+    const int64_t step = (int64_t)SBLK * 1048576;
+    for (int64_t f = 0; f < pl->total; f += step)
+        LIME_TRY(launch_fill(pl, f, std::min(step, pl->total - f), nullptr, ck));
+    uint64_t h[2];
+    LIME_TRY(read_back(ctx, h, ck, 16));
+    release(ctx, ck);
+    *sum = h[0];
+    *xr = h[1];
+    return LIME_OK;
+}
+
+int64_t plan_total(const PairsPlan *pl) { return pl->total; }
+
+void intersect_free(PairsPlan *pl) {
+    lime_ctx *ctx = pl->ctx;
+    release(ctx, pl->olo);
+    release(ctx, pl->ocnt);
+    release(ctx, pl->toff);
+    release(ctx, pl->win);
+    delete pl;
+}
+
+}  // namespace lime

@@ -1,0 +1,319 @@
+// sort.hip -- the partition-and-sort stage: device LSD radix sort of an
+// interval set into the canonical order (global start, zero-width first).
+//
+// Replaces ADAM repartitionAndSort() (cli/Intersection.scala:42-43,
+// cli/Merge.scala:37, cli/Complement.scala:42) and the right-side
+// repartitionAndSortWithinPartitions of OverlapBasedSetTheory.scala:81-82.
+//
+// Layout in HBM (SoA, 12 B per interval):
+//   gs[i]  = off[contig] + start   (u32 global start, the sort key)
+//   ge[i]  = off[contig] + end     (u32 global end)
+//   row[i] = input row             (payload handle for T / U)
+// Order: gs ascending; among equal gs, zero-width intervals first (the only
+// tie order that changes a fold result, see DESIGN.md "canonical order");
+// remaining ties keep input order (every pass is stable).
+//
+// Passes: an optional 1-bit pass on (ge > gs) when the set holds zero-width
+// intervals (LSD: least-significant digit first), then ceil(bits(max gs)/8)
+// 8-bit digit passes.  Each pass = per-tile digit histogram, one exclusive
+// scan over the digit-major count matrix, and a stable scatter that ranks
+// items with wave ballots, stages the tile in LDS in digit order and writes
+// each digit's run contiguously.
+#include "common.hpp"
+
+namespace lime {
+namespace {
+
+constexpr int RB = 256;
+constexpr int RITEMS = 16;
+constexpr int RTILE = RB * RITEMS;  // 4096 items per tile
+constexpr int RBINS = 256;
+constexpr int RWAVES = RB / 64;
+
+struct SetStats {
+    uint32_t err;        // bit0 contig out of range, bit1 end < start, bit2 end > contig length
+    uint32_t max_gs;
+    uint32_t min_width;
+    uint32_t max_width;
+    uint32_t has_zero;
+    uint32_t unsorted;
+};
+
+__global__ __launch_bounds__(256) void k_prep(const int32_t *__restrict__ contig,
+                                              const uint32_t *__restrict__ start,
+                                              const uint32_t *__restrict__ end,
+                                              const uint32_t *__restrict__ off,
+                                              const uint32_t *__restrict__ len, int32_t n_contigs,
+                                              int64_t n, uint32_t *__restrict__ gs,
+                                              uint32_t *__restrict__ ge, uint32_t *__restrict__ row,
+                                              SetStats *st) {
+    uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int32_t c = contig[i];
+        uint32_t s = start[i], e = end[i];
+        uint32_t g0 = 0, g1 = 0;
+        if (c < 0 || c >= n_contigs) {
+            err |= 1u;
+        } else {
+            if (e < s) err |= 2u;
+            if (e > len[c]) err |= 4u;
+            g0 = off[c] + s;
+            g1 = off[c] + e;
+        }
+        gs[i] = g0;
+        ge[i] = g1;
+        row[i] = (uint32_t)i;
+        mx = g0 > mx ? g0 : mx;
+        uint32_t w = g1 - g0;
+        mnw = w < mnw ? w : mnw;
+        mxw = w > mxw ? w : mxw;
+        zero |= (w == 0);
+        if (i > 0) {  // canonical-order check against the previous row
+            int32_t pc = contig[i - 1];
+            if (pc >= 0 && pc < n_contigs && c >= 0 && c < n_contigs) {
+                uint32_t p0 = off[pc] + start[i - 1], p1 = off[pc] + end[i - 1];
+                bool pnz = p1 > p0, nz = g1 > g0;
+                if (p0 > g0 || (p0 == g0 && pnz && !nz)) uns = 1;
+            }
+        }
+    }
+    err = dev::wave_reduce_or(err);
+    mx = dev::wave_reduce_max(mx);
+    mnw = dev::wave_reduce_min(mnw);
+    mxw = dev::wave_reduce_max(mxw);
+    zero = dev::wave_reduce_or(zero);
+    uns = dev::wave_reduce_or(uns);
+    if (dev::lane_id() == 0) {
+        if (err) atomicOr(&st->err, err);
+        atomicMax(&st->max_gs, mx);
+        atomicMin(&st->min_width, mnw);
+        atomicMax(&st->max_width, mxw);
+        if (zero) atomicOr(&st->has_zero, 1u);
+        if (uns) atomicOr(&st->unsorted, 1u);
+    }
+}
+
+// digit of an item: 8-bit digit of gs, or the zero-width bit (0 = zero width)
+template <bool NZ>
+__device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, int shift) {
+    if (NZ) return e > k ? 1u : 0u;
+    return (k >> shift) & (RBINS - 1);
+}
+
+// lanes of the wave holding the same digit (among `valid` lanes)
+template <bool NZ>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
+    uint64_t m = __ballot(valid);
+    if (NZ) {
+        uint64_t b = __ballot(d & 1u);
+        return m & ((d & 1u) ? b : ~b);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t bit = (d >> b) & 1u;
+        uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+template <bool NZ>
+__global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
+                                             const uint32_t *__restrict__ ge, int64_t n, int shift,
+                                             uint32_t *__restrict__ counts, uint32_t ntiles) {
+    __shared__ uint32_t hist[RWAVES][RBINS];
+    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t base = (int64_t)blockIdx.x * RTILE + w * (RTILE / RWAVES);
+#pragma unroll 4
+    for (int k = 0; k < RITEMS; ++k) {
+        int64_t i = base + k * 64 + lane;
+        bool valid = i < n;
+        uint32_t d = 0;
+        if (valid) d = digit_of<NZ>(key[i], NZ ? ge[i] : 0u, shift);
+        uint64_t m = match_digit<NZ>(d, valid);
+        if (valid && (m & dev::lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < RBINS; d += RB) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < RWAVES; ++ww) t += hist[ww][d];
+        counts[(int64_t)d * ntiles + blockIdx.x] = t;
+    }
+}
+
+template <bool NZ>
+__global__ __launch_bounds__(RB) void k_scatter(const uint32_t *__restrict__ key_in,
+                                                const uint32_t *__restrict__ ge_in,
+                                                const uint32_t *__restrict__ row_in, int64_t n,
+                                                int shift, const uint32_t *__restrict__ base_mat,
+                                                uint32_t ntiles, uint32_t *__restrict__ key_out,
+                                                uint32_t *__restrict__ ge_out,
+                                                uint32_t *__restrict__ row_out) {
+    __shared__ uint32_t cnt[RWAVES][RBINS];
+    __shared__ uint32_t dstart[RBINS];
+    __shared__ uint32_t gbase[RBINS];
+    __shared__ uint32_t scratch[RWAVES + 1];
+    __shared__ uint32_t sk[RTILE], se[RTILE], sr[RTILE];
+
+    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t tile0 = (int64_t)blockIdx.x * RTILE;
+    const int64_t base = tile0 + w * (RTILE / RWAVES);
+    uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS], pos[RITEMS], dg[RITEMS];
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k) {
+        int64_t i = base + k * 64 + lane;
+        bool valid = i < n;
+        vk[k] = valid ? key_in[i] : 0u;
+        ve[k] = valid ? ge_in[i] : 0u;
+        vr[k] = valid ? row_in[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k) {
+        int64_t i = base + k * 64 + lane;
+        bool valid = i < n;
+        uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
+        dg[k] = d;
+        uint64_t m = match_digit<NZ>(d, valid);
+        uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
+        uint32_t old = valid ? cnt[w][d] : 0u;
+        pos[k] = old + rank;
+        if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    // per digit: block offset of the digit, then per-wave offsets
+    {
+        const int d = threadIdx.x;  // RB == RBINS
+        uint32_t c[RWAVES];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int ww = 0; ww < RWAVES; ++ww) {
+            c[ww] = cnt[ww][d];
+            tot += c[ww];
+        }
+        uint32_t all;
+        uint32_t ds = dev::block_exclusive_sum<RB>(tot, scratch, &all);
+        dstart[d] = ds;
+        uint32_t run = ds;
+#pragma unroll
+        for (int ww = 0; ww < RWAVES; ++ww) {
+            cnt[ww][d] = run;
+            run += c[ww];
+        }
+        gbase[d] = base_mat[(int64_t)d * ntiles + blockIdx.x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k) {
+        int64_t i = base + k * 64 + lane;
+        if (i < n) {
+            uint32_t lp = cnt[w][dg[k]] + pos[k];
+            sk[lp] = vk[k];
+            se[lp] = ve[k];
+            sr[lp] = vr[k];
+        }
+    }
+    __syncthreads();
+    const int64_t rem = n - tile0;
+    const int count = rem < RTILE ? (int)rem : RTILE;
+    for (int j = threadIdx.x; j < count; j += RB) {
+        uint32_t k = sk[j], e = se[j];
+        uint32_t d = digit_of<NZ>(k, e, shift);
+        uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
+        key_out[g] = k;
+        ge_out[g] = e;
+        row_out[g] = sr[j];
+    }
+}
+
+int radix_pass(lime_ctx *ctx, bool nz, int shift, int64_t n, const uint32_t *k0, const uint32_t *e0,
+               const uint32_t *r0, uint32_t *k1, uint32_t *e1, uint32_t *r1, uint32_t *mat,
+               uint32_t ntiles) {
+    if (nz)
+        hipLaunchKernelGGL(k_hist<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift, mat,
+                           ntiles);
+    else
+        hipLaunchKernelGGL(k_hist<false>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift,
+                           mat, ntiles);
+    LIME_HIP(hipGetLastError());
+    LIME_TRY(scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr));
+    if (nz)
+        hipLaunchKernelGGL(k_scatter<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n,
+                           shift, (const uint32_t *)mat, ntiles, k1, e1, r1);
+    else
+        hipLaunchKernelGGL(k_scatter<false>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n,
+                           shift, (const uint32_t *)mat, ntiles, k1, e1, r1);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
+}  // namespace
+
+int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32_t *d_start,
+             const uint32_t *d_end, const uint32_t *d_len) {
+    const int64_t n = set->n;
+    uint32_t *k0, *e0, *r0;
+    LIME_TRY(alloc(ctx, &k0, (size_t)n));
+    LIME_TRY(alloc(ctx, &e0, (size_t)n));
+    LIME_TRY(alloc(ctx, &r0, (size_t)n));
+    SetStats *st;
+    LIME_TRY(alloc(ctx, &st, 1));
+    SetStats init = {0u, 0u, 0xffffffffu, 0u, 0u, 0u};
+    LIME_HIP(hipMemcpyAsync(st, &init, sizeof(init), hipMemcpyHostToDevice, S(ctx)));
+    if (n > 0) {
+        unsigned grid = blocks_for(n, 256);
+        if (grid > 8192) grid = 8192;
+        hipLaunchKernelGGL(k_prep, dim3(grid), dim3(256), 0, S(ctx), d_contig, d_start, d_end,
+                           (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0, e0, r0, st);
+        LIME_HIP(hipGetLastError());
+    }
+    SetStats h;
+    LIME_TRY(read_back(ctx, &h, st, sizeof(h)));
+    release(ctx, st);
+    if (h.err) {
+        release(ctx, k0);
+        release(ctx, e0);
+        release(ctx, r0);
+        if (h.err & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
+        if (h.err & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
+        return fail(LIME_ERR_RANGE, "interval end beyond its contig length");
+    }
+    set->min_width = n > 0 ? h.min_width : 0;
+    set->max_width = h.max_width;
+    set->has_zero_width = h.has_zero != 0;
+
+    if (n > 1 && h.unsorted) {
+        const uint32_t ntiles = (uint32_t)((n + RTILE - 1) / RTILE);
+        uint32_t *k1, *e1, *r1, *mat;
+        LIME_TRY(alloc(ctx, &k1, (size_t)n));
+        LIME_TRY(alloc(ctx, &e1, (size_t)n));
+        LIME_TRY(alloc(ctx, &r1, (size_t)n));
+        LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * ntiles));
+        int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
+        std::vector<std::pair<bool, int>> passes;
+        if (set->has_zero_width) passes.push_back({true, 0});
+        for (int sh = 0; sh < bits; sh += 8) passes.push_back({false, sh});
+        for (auto &p : passes) {
+            LIME_TRY(radix_pass(ctx, p.first, p.second, n, k0, e0, r0, k1, e1, r1, mat, ntiles));
+            std::swap(k0, k1);
+            std::swap(e0, e1);
+            std::swap(r0, r1);
+        }
+        release(ctx, k1);
+        release(ctx, e1);
+        release(ctx, r1);
+        release(ctx, mat);
+    }
+    set->gs = k0;
+    set->ge = e0;
+    set->row = r0;
+    return LIME_OK;
+}
+
+}  // namespace lime

@@ -1,0 +1,343 @@
+"""Pythonic handles over the C-ABI: Context, Space, IntervalSet, results.
+
+This is plumbing for tests, benchmarks and the multi-GPU driver; the
+operator mirror of lime-core lives in :mod:`lime_amd.set_theory`.
+All compute goes through liblime_amd.so (HIP, gfx950); nothing here falls
+back to the CPU.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import check, i32, i64, u64, vp
+
+P = C.POINTER
+
+PAIR_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4"), ("a_row", "<u4"), ("b_row", "<u4")])
+
+
+def _lib():
+    return _ffi.load()
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(P(ct))
+
+
+def java_string_order(names):
+    """Ranks of `names` in java.lang.String.compareTo order (via the C-ABI)."""
+    lib = _lib()
+    n = len(names)
+    arr = (C.c_char_p * max(n, 1))(*[s.encode() for s in names])
+    out = np.zeros(max(n, 1), dtype=np.int32)
+    check(lib.lime_contig_rank(n, arr, _ptr(out, i32)))
+    return out[:n]
+
+
+class Space:
+    """Contigs in Java String order with their lengths (the coordinate space)."""
+
+    def __init__(self, names, lengths):
+        names = list(names)
+        lengths = [int(x) for x in lengths]
+        if len(set(names)) != len(names):
+            raise ValueError("duplicate contig names")
+        rank = java_string_order(names) if names else np.zeros(0, np.int32)
+        order = np.argsort(rank, kind="stable")
+        self.names = [names[i] for i in order]
+        self.lengths = np.array([lengths[i] for i in order], dtype=np.int64)
+        self.index = {n: i for i, n in enumerate(self.names)}
+        lib = _lib()
+        h = vp()
+        check(lib.lime_space_create(len(self.names), _ptr(self.lengths, i64), C.byref(h)))
+        self._h = h
+        self.offsets = np.array(
+            [lib.lime_space_offset(h, c) for c in range(len(self.names) + 1)], dtype=np.int64)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def span(self):
+        return int(_lib().lime_space_span(self._h))
+
+    @classmethod
+    def from_genome_file(cls, path):
+        lib = _lib()
+        n = i32()
+        names = P(C.c_char_p)()
+        lens = P(i64)()
+        check(lib.lime_genome_read(path.encode(), C.byref(n), C.byref(names), C.byref(lens)))
+        try:
+            nm = [names[i].decode() for i in range(n.value)]
+            ln = [lens[i] for i in range(n.value)]
+        finally:
+            lib.lime_genome_free(n.value, names, lens)
+        return cls(nm, ln)
+
+    def contig_ids(self, names):
+        return np.array([self.index[n] for n in names], dtype=np.int32)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                _lib().lime_space_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class IntervalSet:
+    """A sorted, device-resident interval set (lime_set)."""
+
+    def __init__(self, ctx, handle, space):
+        self.ctx, self._h, self.space = ctx, handle, space
+
+    @property
+    def n(self):
+        return int(_lib().lime_set_size(self._h))
+
+    def device_arrays(self):
+        gs, ge, row = vp(), vp(), vp()
+        check(_lib().lime_set_device_arrays(self._h, C.byref(gs), C.byref(ge), C.byref(row)))
+        return gs.value, ge.value, row.value
+
+    def to_host(self):
+        n = self.n
+        out = {k: np.zeros(n, dtype=np.int64) for k in ("start", "end", "row")}
+        out["contig"] = np.zeros(n, dtype=np.int32)
+        check(_lib().lime_set_fill_host(self._h, _ptr(out["contig"], i32), _ptr(out["start"], i64),
+                                        _ptr(out["end"], i64), _ptr(out["row"], i64)))
+        return out
+
+    def close(self):
+        if self._h:
+            _lib().lime_set_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Result:
+    """merge / subtract / complement / bitset output (lime_result)."""
+
+    def __init__(self, ctx, handle, space):
+        self.ctx, self._h, self.space = ctx, handle, space
+
+    @property
+    def n(self):
+        return int(_lib().lime_result_size(self._h))
+
+    def to_host(self):
+        n = self.n
+        out = {k: np.zeros(n, dtype=np.int64) for k in ("start", "end", "a_row", "b_row")}
+        out["contig"] = np.zeros(n, dtype=np.int32)
+        check(_lib().lime_result_fill_host(self._h, _ptr(out["contig"], i32),
+                                           _ptr(out["start"], i64), _ptr(out["end"], i64),
+                                           _ptr(out["a_row"], i64), _ptr(out["b_row"], i64)))
+        return out
+
+    def run_of_row(self, n_rows):
+        out = np.zeros(n_rows, dtype=np.int64)
+        check(_lib().lime_result_run_of_row(self._h, _ptr(out, i64)))
+        return out
+
+    def device_arrays(self):
+        gs, ge = vp(), vp()
+        check(_lib().lime_result_device_arrays(self._h, C.byref(gs), C.byref(ge)))
+        return gs.value, ge.value
+
+    def close(self):
+        if self._h:
+            _lib().lime_result_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Pairs:
+    """Intersect plan: exact pair count plus chunked fill (lime_pairs)."""
+
+    def __init__(self, ctx, handle, n):
+        self.ctx, self._h, self.n = ctx, handle, n
+
+    def fill_host(self, first=0, count=None):
+        if count is None:
+            count = self.n - first
+        out = np.zeros(count, dtype=PAIR_DTYPE)
+        check(_lib().lime_intersect_fill_host(self._h, first, count, out.ctypes.data))
+        return out
+
+    def fill_device(self, first, count, d_out):
+        check(_lib().lime_intersect_fill_device(self._h, first, count, d_out))
+
+    def checksum(self):
+        s, x = u64(), u64()
+        check(_lib().lime_intersect_checksum(self._h, C.byref(s), C.byref(x)))
+        return s.value, x.value
+
+    def close(self):
+        if self._h:
+            _lib().lime_pairs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Bitset:
+    def __init__(self, ctx, handle, space):
+        self.ctx, self._h, self.space = ctx, handle, space
+
+    def popcount(self):
+        return int(_lib().lime_bitset_popcount(self.ctx.handle, self._h))
+
+    def close(self):
+        if self._h:
+            _lib().lime_bitset_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One device, one HIP stream, one memory pool (lime_ctx)."""
+
+    def __init__(self, device=0):
+        lib = _lib()
+        h = vp()
+        check(lib.lime_ctx_create(int(device), C.byref(h)))
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, hip_stream_ptr):
+        check(_lib().lime_ctx_set_stream(self._h, hip_stream_ptr))
+
+    def synchronize(self):
+        check(_lib().lime_ctx_synchronize(self._h))
+
+    def pool_bytes(self):
+        return int(_lib().lime_ctx_pool_bytes(self._h))
+
+    # ------------------------------------------------------------ sets
+    def set_from_host(self, space, contig, start, end):
+        contig = np.ascontiguousarray(contig, dtype=np.int32)
+        start = np.ascontiguousarray(start, dtype=np.int64)
+        end = np.ascontiguousarray(end, dtype=np.int64)
+        h = vp()
+        check(_lib().lime_set_create_host(self._h, space.handle, len(contig), _ptr(contig, i32),
+                                          _ptr(start, i64), _ptr(end, i64), C.byref(h)))
+        return IntervalSet(self, h, space)
+
+    def set_from_device(self, space, n, d_contig, d_start, d_end):
+        h = vp()
+        check(_lib().lime_set_create_device(self._h, space.handle, int(n), d_contig, d_start,
+                                            d_end, C.byref(h)))
+        return IntervalSet(self, h, space)
+
+    # ------------------------------------------------------------- ops
+    def intersect(self, a, b, threshold=0):
+        h, n = vp(), i64()
+        check(_lib().lime_intersect_count(self._h, a._h, b._h, int(threshold), C.byref(h),
+                                          C.byref(n)))
+        return Pairs(self, h, n.value)
+
+    def merge(self, a):
+        h, n = vp(), i64()
+        check(_lib().lime_merge(self._h, a._h, C.byref(h), C.byref(n)))
+        return Result(self, h, a.space)
+
+    def subtract(self, a, b, threshold=0, mode=_ffi.SUBTRACT_LIME):
+        h, n = vp(), i64()
+        check(_lib().lime_subtract(self._h, a._h, b._h, int(threshold), int(mode), C.byref(h),
+                                   C.byref(n)))
+        return Result(self, h, a.space)
+
+    def complement(self, genome_space, a):
+        h, n = vp(), i64()
+        check(_lib().lime_complement(self._h, genome_space.handle, a._h, C.byref(h), C.byref(n)))
+        return Result(self, h, a.space)
+
+    def bitset(self, a):
+        h = vp()
+        check(_lib().lime_bitset_from_set(self._h, a._h, C.byref(h)))
+        return Bitset(self, h, a.space)
+
+    def bitset_runs(self, op, a, b=None):
+        h, n = vp(), i64()
+        check(_lib().lime_bitset_runs(self._h, int(op), a._h, b._h if b is not None else None,
+                                      C.byref(h), C.byref(n)))
+        return Result(self, h, a.space)
+
+    def bitset_and(self, sets):
+        arr = (vp * len(sets))(*[s._h for s in sets])
+        h, n = vp(), i64()
+        check(_lib().lime_bitset_and_runs(self._h, len(sets), arr, C.byref(h), C.byref(n)))
+        return Result(self, h, sets[0].space)
+
+    # ----------------------------------------------------------- synth
+    def synth_uniform(self, space, n, seed, len_lo, len_hi, d_contig, d_start, d_end):
+        check(_lib().lime_synth_uniform(self._h, space.handle, int(n), int(seed), int(len_lo),
+                                        int(len_hi), d_contig, d_start, d_end))
+
+    def synth_pileup(self, space, n, seed, n_centres, sigma, len_lo, len_hi, d_contig, d_start,
+                     d_end):
+        check(_lib().lime_synth_pileup(self._h, space.handle, int(n), int(seed), int(n_centres),
+                                       int(sigma), int(len_lo), int(len_hi), d_contig, d_start,
+                                       d_end))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib().lime_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def read_bed(path):
+    """Parse a BED file with the engine's host reader -> dict of numpy arrays."""
+    lib = _lib()
+    h = vp()
+    check(lib.lime_bed_read(path.encode(), C.byref(h)))
+    try:
+        n = lib.lime_bed_rows(h)
+        nc = lib.lime_bed_contigs(h)
+        names = [lib.lime_bed_contig_name(h, i).decode() for i in range(nc)]
+        ids = np.ctypeslib.as_array(lib.lime_bed_contig_ids(h), shape=(n,)).copy() if n else \
+            np.zeros(0, np.int32)
+        s = np.ctypeslib.as_array(lib.lime_bed_starts(h), shape=(n,)).copy() if n else \
+            np.zeros(0, np.int64)
+        e = np.ctypeslib.as_array(lib.lime_bed_ends(h), shape=(n,)).copy() if n else \
+            np.zeros(0, np.int64)
+        st = np.ctypeslib.as_array(lib.lime_bed_strands(h), shape=(n,)).copy() if n else \
+            np.zeros(0, np.int8)
+        nm = [lib.lime_bed_name(h, i).decode() for i in range(n)]
+    finally:
+        lib.lime_bed_free(h)
+    return {"names": names, "contig": ids, "chrom": [names[i] for i in ids], "start": s,
+            "end": e, "strand": st, "name": nm}

@@ -1,0 +1,229 @@
+"""Host mirror of lime-core's operator API over the MI355X engine.
+
+Same class names, argument meaning and error behaviour as
+lime-core/src/main/scala/org/bdgenomics/lime/set_theory/:
+
+    DistributedIntersection(leftRdd, rightRdd, partitionMap, threshold=0).compute()
+        -> [(ReferenceRegion, (T, U))]             Intersection.scala:45-69
+    DistributedMerge(rddToCompute, partitionMap, threshold=0).compute()
+        -> [(ReferenceRegion, [T])]                Merge.scala:34-36
+    DistributedSubtract(leftRdd, rightRdd, partitionMap, threshold=0).compute()
+        -> [(ReferenceRegion, (T, U or None))]     Subtract.scala:78-116
+    DistributedComplement(rddToCompute, partitionMap, referenceNameBounds,
+                          threshold=0).compute()
+        -> [(ReferenceRegion, [])]                 Complement.scala:131-134
+
+An "RDD" here is any iterable of (ReferenceRegion, value) pairs held on the
+host.  `partitionMap` is accepted for signature parity and ignored: the
+engine is partition-free and its output equals the reference's single-
+partition (P = 1) execution, in the same emission order (SURVEY.md
+Appendix A).  Strand: rows are grouped by strand and each group runs through
+the engine separately, which is exactly ReferenceRegion.overlaps' strand
+equality; complement ignores strand (its gap regions carry none).
+"""
+from collections import namedtuple
+
+import numpy as np
+
+from . import _ffi
+from .engine import Context, Space
+
+STRANDS = ("INDEPENDENT", "FORWARD", "REVERSE", "UNKNOWN")
+_STRAND_CODE = {s: i for i, s in enumerate(STRANDS)}
+
+
+class ReferenceRegion(namedtuple("ReferenceRegion", "referenceName start end strand")):
+    """ADAM ReferenceRegion (0-based half-open), strand as a name."""
+    __slots__ = ()
+
+    def __new__(cls, referenceName, start, end, strand="INDEPENDENT"):
+        if start < 0 or end < start:
+            raise ValueError(f"invalid region {referenceName}:{start}-{end}")
+        return super().__new__(cls, referenceName, int(start), int(end), strand)
+
+    @classmethod
+    def unstranded(cls, name, start, end):
+        return cls(name, start, end, "INDEPENDENT")
+
+
+class NoSuchElementException(KeyError):
+    """Raised where the reference throws java.util.NoSuchElementException."""
+
+
+_CTX = None
+
+
+def default_context():
+    global _CTX
+    if _CTX is None:
+        _CTX = Context(0)
+    return _CTX
+
+
+def _rows(rdd):
+    rdd = list(rdd)
+    regions = [r for r, _ in rdd]
+    values = [v for _, v in rdd]
+    return regions, values
+
+
+def _space_for(*region_lists, bounds=None):
+    if bounds is not None:
+        return Space(list(bounds.keys()), [b.end for b in bounds.values()])
+    ext = {}
+    for regs in region_lists:
+        for r in regs:
+            ext[r.referenceName] = max(ext.get(r.referenceName, 0), r.end)
+    return Space(list(ext.keys()), list(ext.values()))
+
+
+def _arrays(space, regions, rows):
+    try:
+        c = np.array([space.index[regions[i].referenceName] for i in rows], dtype=np.int32)
+    except KeyError as e:
+        raise NoSuchElementException(f"key not found: {e.args[0]}") from None
+    s = np.array([regions[i].start for i in rows], dtype=np.int64)
+    e = np.array([regions[i].end for i in rows], dtype=np.int64)
+    return c, s, e
+
+
+def _strand_groups(regions):
+    groups = {}
+    for i, r in enumerate(regions):
+        groups.setdefault(r.strand, []).append(i)
+    return groups
+
+
+def _sorted_rank(regions):
+    """Rank of every row in RegionOrdering (name, start, end, strand), stable."""
+    keys = sorted(range(len(regions)), key=lambda i: (
+        _java_key(regions[i].referenceName), regions[i].start, regions[i].end,
+        _STRAND_CODE.get(regions[i].strand, 0), i))
+    rank = np.empty(len(regions), dtype=np.int64)
+    rank[keys] = np.arange(len(regions))
+    return rank
+
+
+def _java_key(name):
+    return name.encode("utf-16-be")
+
+
+class _Op:
+    def __init__(self, ctx=None):
+        self.ctx = ctx or default_context()
+
+
+class DistributedIntersection(_Op):
+    def __init__(self, leftRdd, rightRdd, partitionMap=None, threshold=0, ctx=None):
+        super().__init__(ctx)
+        self.left, self.right = list(leftRdd), list(rightRdd)
+        self.partitionMap, self.threshold = partitionMap, int(threshold)
+
+    def compute(self):
+        lr, lv = _rows(self.left)
+        rr, rv = _rows(self.right)
+        space = _space_for(lr, rr)
+        lg, rg = _strand_groups(lr), _strand_groups(rr)
+        out = []
+        for strand, lrows in lg.items():
+            rrows = rg.get(strand)
+            if not rrows:
+                continue
+            A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
+            B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
+            plan = self.ctx.intersect(A, B, self.threshold)
+            pairs = plan.fill_host()
+            for p in pairs:
+                a = lrows[p["a_row"]]
+                b = rrows[p["b_row"]]
+                out.append((a, b, int(p["start"]), int(p["end"])))
+            plan.close()
+            A.close()
+            B.close()
+        # reference emission order (P = 1): left in sorted order, then cache
+        # (= sorted right) order -- SetTheory.scala:181-186
+        lrank, rrank = _sorted_rank(lr), _sorted_rank(rr)
+        out.sort(key=lambda t: (lrank[t[0]], rrank[t[1]]))
+        return [(ReferenceRegion(lr[a].referenceName, s, e, lr[a].strand), (lv[a], rv[b]))
+                for a, b, s, e in out]
+
+
+class DistributedSubtract(_Op):
+    def __init__(self, leftRdd, rightRdd, partitionMap=None, threshold=0, ctx=None,
+                 mode=_ffi.SUBTRACT_LIME):
+        super().__init__(ctx)
+        self.left, self.right = list(leftRdd), list(rightRdd)
+        self.partitionMap, self.threshold, self.mode = partitionMap, int(threshold), mode
+
+    def compute(self):
+        lr, lv = _rows(self.left)
+        rr, rv = _rows(self.right)
+        space = _space_for(lr, rr)
+        lg, rg = _strand_groups(lr), _strand_groups(rr)
+        out = []
+        for strand, lrows in lg.items():
+            rrows = rg.get(strand, [])
+            A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
+            B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
+            res = self.ctx.subtract(A, B, self.threshold, self.mode).to_host()
+            for k in range(len(res["start"])):
+                a = lrows[res["a_row"][k]]
+                b = rrows[res["b_row"][k]] if res["b_row"][k] >= 0 else None
+                out.append((a, k, b, int(res["start"][k]), int(res["end"][k])))
+        lrank = _sorted_rank(lr)
+        out.sort(key=lambda t: (lrank[t[0]], t[1]))  # device order within a left row
+        return [(ReferenceRegion(lr[a].referenceName, s, e, lr[a].strand),
+                 (lv[a], rv[b] if b is not None else None)) for a, _, b, s, e in out]
+
+
+class DistributedMerge(_Op):
+    def __init__(self, rddToCompute, partitionMap=None, threshold=0, ctx=None):
+        super().__init__(ctx)
+        self.rdd = list(rddToCompute)
+        self.partitionMap, self.threshold = partitionMap, int(threshold)
+
+    def _runs(self):
+        regs, vals = _rows(self.rdd)
+        space = _space_for(regs)
+        runs = []
+        for strand, rows in _strand_groups(regs).items():
+            A = self.ctx.set_from_host(space, *_arrays(space, regs, rows))
+            res = self.ctx.merge(A)
+            h = res.to_host()
+            rid = res.run_of_row(len(rows))
+            members = [[] for _ in range(len(h["start"]))]
+            # Iterable[T] in fold order = sorted order of the member rows
+            rank = _sorted_rank([regs[r] for r in rows])
+            for local in np.argsort(rank, kind="stable"):
+                members[rid[local]].append(vals[rows[local]])
+            for k in range(len(h["start"])):
+                runs.append((ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
+                                             int(h["end"][k]), strand), members[k]))
+        runs.sort(key=lambda t: (_java_key(t[0].referenceName), t[0].start, t[0].end,
+                                 _STRAND_CODE.get(t[0].strand, 0)))
+        return runs
+
+    def compute(self):
+        return self._runs()
+
+
+class DistributedComplement(_Op):
+    def __init__(self, rddToCompute, partitionMap=None, referenceNameBounds=None, threshold=0,
+                 ctx=None):
+        super().__init__(ctx)
+        if referenceNameBounds is None:
+            raise ValueError("referenceNameBounds is required")
+        self.rdd = list(rddToCompute)
+        self.partitionMap, self.bounds, self.threshold = partitionMap, referenceNameBounds, \
+            int(threshold)
+
+    def compute(self):
+        regs, _ = _rows(self.rdd)
+        space = _space_for(bounds=self.bounds)
+        for r in regs:
+            if r.referenceName not in space.index:
+                raise NoSuchElementException(f"key not found: {r.referenceName}")
+        A = self.ctx.set_from_host(space, *_arrays(space, regs, range(len(regs))))
+        h = self.ctx.complement(space, A).to_host()
+        return [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
+                                 int(h["end"][k])), []) for k in range(len(h["start"]))]

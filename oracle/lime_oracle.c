@@ -1,0 +1,394 @@
+/*
+ * lime_oracle.c -- CPU restatement of LIME's per-partition set-theory
+ * algorithms.  TEST INFRASTRUCTURE ONLY: this file is the parity checker for
+ * the HIP engine (tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg).  It is never linked into, loaded by, or called from the product path
+ * (lime_amd/liblime_amd.so).
+ *
+ * What it restates (all paths relative to /root/reference):
+ *   - region order + predicates: ADAM 0.23 ReferenceRegion (3rd-party, not
+ *     vendored; restated from its call sites):
+ *       compareTo at OverlapBasedSetTheory.scala:23,37
+ *       covers(o)  = same name && a.end > o.start && a.start < o.end (strand-blind)
+ *       overlaps(o)= covers(o) && same strand
+ *       overlapsBy = min(end) - max(start) if overlaps, else None
+ *   - sweep-line join: SetTheory.scala:131-187 (pruneCache :131-141 incl. the
+ *     Q8 "index <= 0 -> trim nothing" quirk, advanceCache :150-155,
+ *     makeIterator :175-187) with OverlapBasedSetTheory.scala:21-38 predicates.
+ *   - intersection: Intersection.scala:19-24 (primitive), :37-42 (condition,
+ *     uses the *field* threshold), :58-69 (processHits).
+ *   - subtract: Subtract.scala:19-24 (condition), :53-75 (subtract), :91-116
+ *     (processHits: filter, reverse-order fold into blocks, per-block
+ *     remnants -- quirk Q5).  Mode LO_SUB_SET additionally restates the
+ *     set-difference definition of SURVEY.md Appendix A.3.
+ *   - merge: SetTheory.scala:208-225 (localCompute fold; condition/primitive
+ *     called without threshold -> 0, quirk Q6), Merge.scala:8-31.
+ *   - complement: Complement.scala:11-128 as pinned by ComplementSuite.scala
+ *     (canonical P=1-independent form): gaps of
+ *     merge(A) per genome contig in String order, zero-width gaps dropped,
+ *     contigs without data emitted whole.
+ *
+ * Every op runs the reference's algorithm as a single partition (P = 1); the
+ * partition-count artefacts Q1/Q2 of SURVEY.md Appendix B are deliberately not
+ * reproduced (they make Spark's own output P-dependent).
+ *
+ * Output arrays use the two-call protocol: each op returns the exact output
+ * count and writes min(count, cap) records, so callers ask with cap = 0 first.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+    int32_t contig; /* rank of the contig name in Java String order */
+    int64_t start;
+    int64_t end;
+    int8_t strand; /* 0 = unstranded / independent */
+    int64_t row;   /* original input row: the payload T / U */
+} lo_region;
+
+/* ------------------------------------------------------------------ order */
+
+/* RegionOrdering: (referenceName, start, end, strand); ties by input row so
+ * that equal regions keep input order (Spark's sort is stable per partition). */
+static int lo_cmp(const lo_region *a, const lo_region *b) {
+    if (a->contig != b->contig) return a->contig < b->contig ? -1 : 1;
+    if (a->start != b->start) return a->start < b->start ? -1 : 1;
+    if (a->end != b->end) return a->end < b->end ? -1 : 1;
+    if (a->strand != b->strand) return a->strand < b->strand ? -1 : 1;
+    return 0;
+}
+static int lo_qsort_cmp(const void *x, const void *y) {
+    const lo_region *a = (const lo_region *)x, *b = (const lo_region *)y;
+    int c = lo_cmp(a, b);
+    if (c) return c;
+    return a->row < b->row ? -1 : (a->row > b->row ? 1 : 0);
+}
+
+static int lo_covers(const lo_region *a, const lo_region *o) {
+    return a->contig == o->contig && a->end > o->start && a->start < o->end;
+}
+static int lo_overlaps(const lo_region *a, const lo_region *o) {
+    return lo_covers(a, o) && a->strand == o->strand;
+}
+/* overlapsBy(o).exists(_ >= t) */
+static int lo_overlaps_by_at_least(const lo_region *a, const lo_region *o, int64_t t) {
+    if (!lo_overlaps(a, o)) return 0;
+    int64_t e = a->end < o->end ? a->end : o->end;
+    int64_t s = a->start > o->start ? a->start : o->start;
+    return e - s >= t;
+}
+
+static lo_region *lo_load(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e,
+                          const int8_t *strand) {
+    lo_region *r = (lo_region *)malloc(sizeof(lo_region) * (size_t)(n > 0 ? n : 1));
+    for (int64_t i = 0; i < n; ++i) {
+        r[i].contig = c[i];
+        r[i].start = s[i];
+        r[i].end = e[i];
+        r[i].strand = strand ? strand[i] : 0;
+        r[i].row = i;
+    }
+    qsort(r, (size_t)n, sizeof(lo_region), lo_qsort_cmp);
+    return r;
+}
+
+/* ------------------------------------------------------- output buffering */
+
+typedef struct {
+    int64_t count, cap;
+    int32_t *contig;
+    int64_t *start, *end, *lrow, *rrow;
+} lo_out;
+
+static void lo_emit(lo_out *o, int32_t c, int64_t s, int64_t e, int64_t lr, int64_t rr) {
+    if (o->count < o->cap) {
+        int64_t k = o->count;
+        if (o->contig) o->contig[k] = c;
+        if (o->start) o->start[k] = s;
+        if (o->end) o->end[k] = e;
+        if (o->lrow) o->lrow[k] = lr;
+        if (o->rrow) o->rrow[k] = rr;
+    }
+    o->count++;
+}
+
+/* ----------------------------------------------------- sweep-line machinery */
+
+/* The right-side cache: SetTheory.scala:83 ListBuffer, append at the tail
+ * (advanceCache) and trimStart at the head (pruneCache). */
+typedef struct {
+    const lo_region **v;
+    int64_t head, tail, cap;
+} lo_cache;
+
+static void cache_push(lo_cache *c, const lo_region *r) {
+    if (c->tail == c->cap) {
+        if (c->head > 0) { /* compact */
+            memmove(c->v, c->v + c->head, sizeof(*c->v) * (size_t)(c->tail - c->head));
+            c->tail -= c->head;
+            c->head = 0;
+        }
+        if (c->tail == c->cap) {
+            c->cap = c->cap ? c->cap * 2 : 64;
+            c->v = (const lo_region **)realloc(c->v, sizeof(*c->v) * (size_t)c->cap);
+        }
+    }
+    c->v[c->tail++] = r;
+}
+
+/* OverlapBasedSetTheory.scala:21-24: cached < to && !cached.covers(to) */
+static int prune_cond(const lo_region *cached, const lo_region *to) {
+    return lo_cmp(cached, to) < 0 && !lo_covers(cached, to);
+}
+/* OverlapBasedSetTheory.scala:35-38: cand <= until || cand.covers(until) */
+static int advance_cond(const lo_region *cand, const lo_region *until) {
+    return lo_cmp(cand, until) <= 0 || lo_covers(cand, until);
+}
+
+/* SetTheory.scala:131-141.  indexWhere(!prune) == -1 (everything prunable)
+ * maps to 0, i.e. nothing is trimmed (quirk Q8, performance only). */
+static void prune_cache(lo_cache *c, const lo_region *to) {
+    int64_t index = -1;
+    for (int64_t i = c->head; i < c->tail; ++i)
+        if (!prune_cond(c->v[i], to)) { index = i - c->head; break; }
+    if (index > 0) c->head += index;
+}
+
+/* SetTheory.scala:150-155 */
+static void advance_cache(lo_cache *c, const lo_region *right, int64_t nr, int64_t *rpos,
+                          const lo_region *until) {
+    while (*rpos < nr && advance_cond(&right[*rpos], until)) cache_push(c, &right[(*rpos)++]);
+}
+
+/* ------------------------------------------------------------- intersect */
+
+/* Intersection.scala:58-69 processHits: every cached R with
+ * overlapsBy(L, R) >= threshold, in cache order, emits
+ * (L.intersection(R), (L.value, R.value)). */
+int64_t lo_intersect(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
+                     const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
+                     const int64_t *re, const int8_t *rstr, int64_t threshold, int64_t cap,
+                     int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow, int64_t *orrow) {
+    lo_region *L = lo_load(nl, lc, ls, le, lstr);
+    lo_region *R = lo_load(nr, rc, rs, re, rstr);
+    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+    lo_cache cache = {0};
+    int64_t rpos = 0;
+    for (int64_t i = 0; i < nl; ++i) { /* SetTheory.scala:181-186 */
+        const lo_region *cur = &L[i];
+        advance_cache(&cache, R, nr, &rpos, cur);
+        prune_cache(&cache, cur);
+        for (int64_t k = cache.head; k < cache.tail; ++k) {
+            const lo_region *r = cache.v[k];
+            if (lo_overlaps_by_at_least(cur, r, threshold)) {
+                int64_t s = cur->start > r->start ? cur->start : r->start;
+                int64_t e = cur->end < r->end ? cur->end : r->end;
+                lo_emit(&out, cur->contig, s, e, cur->row, r->row);
+            }
+        }
+    }
+    free(cache.v);
+    free(L);
+    free(R);
+    return out.count;
+}
+
+/* -------------------------------------------------------------- subtract */
+
+#define LO_SUB_LIME 0 /* Subtract.scala:103-114 exactly: per-block remnants (Q5) */
+#define LO_SUB_SET 1  /* a \ union(hits): SURVEY.md Appendix A.3 'set' mode */
+
+typedef struct {
+    int64_t start, end, rrow;
+} lo_block;
+
+int64_t lo_subtract(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
+                    const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
+                    const int64_t *re, const int8_t *rstr, int64_t threshold, int mode,
+                    int64_t cap, int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow,
+                    int64_t *orrow) {
+    lo_region *L = lo_load(nl, lc, ls, le, lstr);
+    lo_region *R = lo_load(nr, rc, rs, re, rstr);
+    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+    lo_cache cache = {0};
+    int64_t rpos = 0;
+    lo_block *blocks = NULL;
+    int64_t bcap = 0;
+    for (int64_t i = 0; i < nl; ++i) {
+        const lo_region *cur = &L[i];
+        advance_cache(&cache, R, nr, &rpos, cur);
+        prune_cache(&cache, cur);
+        /* Subtract.scala:95-98: filteredCache */
+        int64_t nb = 0;
+        int first = 1;
+        for (int64_t k = cache.head; k < cache.tail; ++k) {
+            const lo_region *r = cache.v[k];
+            if (!lo_overlaps_by_at_least(cur, r, threshold)) continue;
+            /* :103-108 fold: foldLeft(List(filteredCache.head)) over the WHOLE
+             * filtered cache, so the head is visited twice: a no-op hull for a
+             * non-empty head, a duplicated block for a zero-width one.
+             * b.head overlaps a -> hull, keep head's value; otherwise start a
+             * new block.  (The fold's List is built in reverse; we keep blocks
+             * in forward order and emit reversed.) */
+            if (first) {
+                first = 0;
+                if (nb == bcap) {
+                    bcap = bcap ? bcap * 2 : 16;
+                    blocks = (lo_block *)realloc(blocks, sizeof(lo_block) * (size_t)bcap);
+                }
+                blocks[0].start = r->start;
+                blocks[0].end = r->end;
+                blocks[0].rrow = r->row;
+                nb = 1;
+            }
+            if (nb > 0) {
+                lo_block *h = &blocks[nb - 1];
+                lo_region hr = {cur->contig, h->start, h->end, r->strand, 0};
+                if (lo_overlaps(&hr, r)) {
+                    if (r->start < h->start) h->start = r->start;
+                    if (r->end > h->end) h->end = r->end;
+                    continue;
+                }
+            }
+            if (nb == bcap) {
+                bcap = bcap ? bcap * 2 : 16;
+                blocks = (lo_block *)realloc(blocks, sizeof(lo_block) * (size_t)bcap);
+            }
+            blocks[nb].start = r->start;
+            blocks[nb].end = r->end;
+            blocks[nb].rrow = r->row;
+            nb++;
+        }
+        if (nb == 0) { /* :100-101 (L, (v, None)) */
+            lo_emit(&out, cur->contig, cur->start, cur->end, cur->row, -1);
+            continue;
+        }
+        if (mode == LO_SUB_LIME) {
+            /* :109-114 over the reversed block list; subtract() :53-75 */
+            for (int64_t b = nb - 1; b >= 0; --b) {
+                if (blocks[b].start > cur->start)
+                    lo_emit(&out, cur->contig, cur->start, blocks[b].start, cur->row, blocks[b].rrow);
+                if (cur->end > blocks[b].end)
+                    lo_emit(&out, cur->contig, blocks[b].end, cur->end, cur->row, blocks[b].rrow);
+            }
+        } else {
+            /* a \ (B_0 u ... u B_{nb-1}); blocks are disjoint, sorted */
+            int64_t pos = cur->start;
+            for (int64_t b = 0; b < nb; ++b) {
+                if (blocks[b].start > pos)
+                    lo_emit(&out, cur->contig, pos, blocks[b].start, cur->row, blocks[b].rrow);
+                if (blocks[b].end > pos) pos = blocks[b].end;
+            }
+            if (cur->end > pos) lo_emit(&out, cur->contig, pos, cur->end, cur->row, blocks[nb - 1].rrow);
+        }
+    }
+    free(blocks);
+    free(cache.v);
+    free(L);
+    free(R);
+    return out.count;
+}
+
+/* ----------------------------------------------------------------- merge */
+
+/* SetTheory.scala:208-225 localCompute with Merge.scala condition/primitive:
+ * fold over the sorted partition keeping the running hull at the list head;
+ * condition(head, next) = head.overlaps(next) (threshold not passed -> 0);
+ * primitive = hull.  run_of_row[row] receives the index of the run the input
+ * row was folded into (the Iterable[T] grouping). */
+int64_t lo_merge(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e,
+                 const int8_t *strand, int64_t cap, int32_t *oc, int64_t *os, int64_t *oe,
+                 int8_t *ostrand, int64_t *run_of_row) {
+    lo_region *A = lo_load(n, c, s, e, strand);
+    int64_t count = 0;
+    lo_region head;
+    for (int64_t i = 0; i < n; ++i) {
+        const lo_region *a = &A[i];
+        if (i > 0 && lo_overlaps(&head, a)) {
+            if (a->start < head.start) head.start = a->start;
+            if (a->end > head.end) head.end = a->end;
+        } else {
+            if (i > 0) {
+                if (count - 1 < cap) {
+                    if (oc) oc[count - 1] = head.contig;
+                    if (os) os[count - 1] = head.start;
+                    if (oe) oe[count - 1] = head.end;
+                    if (ostrand) ostrand[count - 1] = head.strand;
+                }
+            }
+            head = *a;
+            count++;
+        }
+        if (run_of_row) run_of_row[a->row] = count - 1;
+    }
+    if (count > 0 && count - 1 < cap) {
+        if (oc) oc[count - 1] = head.contig;
+        if (os) os[count - 1] = head.start;
+        if (oe) oe[count - 1] = head.end;
+        if (ostrand) ostrand[count - 1] = head.strand;
+    }
+    free(A);
+    return count;
+}
+
+/* ------------------------------------------------------------ complement */
+
+/* Complement.scala:59-128 getComplement + :33-50 postProcess, in the
+ * partition-count-independent form pinned by ComplementSuite.scala:19-114
+ * (SURVEY.md Appendix A.3): contigs in String order (= contig rank order);
+ * for a contig with merged runs r_0..r_k emit [0, r_0.s), [r_i.e, r_{i+1}.s),
+ * [r_k.e, len); a contig without data emits [0, len); zero-width gaps (quirk
+ * Q4) are dropped.  Strand is ignored (the gap regions carry none).
+ * Returns -1 if a data contig is outside [0, n_genome) (the reference throws
+ * NoSuchElementException from referenceNameBounds(name), :106,118). */
+int64_t lo_complement(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e,
+                      int32_t n_genome, const int64_t *genome_len, int64_t cap, int32_t *oc,
+                      int64_t *os, int64_t *oe) {
+    for (int64_t i = 0; i < n; ++i)
+        if (c[i] < 0 || c[i] >= n_genome) return -1;
+    lo_region *A = lo_load(n, c, s, e, NULL);
+    lo_out out = {0, cap, oc, os, oe, NULL, NULL};
+    int64_t i = 0;
+    for (int32_t g = 0; g < n_genome; ++g) {
+        int64_t pos = 0;
+        int have = 0;
+        lo_region head;
+        while (i < n && A[i].contig == g) {
+            const lo_region *a = &A[i++];
+            if (have && lo_overlaps(&head, a)) {
+                if (a->end > head.end) head.end = a->end;
+                continue;
+            }
+            if (have) { /* close the previous run: gap before the new one */
+                if (head.start > pos) lo_emit(&out, g, pos, head.start, -1, -1);
+                if (head.end > pos) pos = head.end;
+            }
+            head = *a;
+            have = 1;
+        }
+        if (have) {
+            if (head.start > pos) lo_emit(&out, g, pos, head.start, -1, -1);
+            if (head.end > pos) pos = head.end;
+        }
+        if (genome_len[g] > pos) lo_emit(&out, g, pos, genome_len[g], -1, -1);
+    }
+    free(A);
+    return out.count;
+}
+
+/* ---------------------------------------------------- order-free checksum */
+
+/* splitmix64 finaliser: the order-independent checksum of SURVEY.md 8(d)
+ * (sum and xor of mix64 over each output tuple), shared with the engine's
+ * verification kernels so full-size runs can be compared without sorting. */
+static uint64_t lo_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+uint64_t lo_pair_hash(uint32_t start, uint32_t end, uint32_t a, uint32_t b) {
+    uint64_t x = ((uint64_t)start << 32) | end;
+    uint64_t y = ((uint64_t)a << 32) | b;
+    return lo_mix64(x ^ lo_mix64(y));
+}

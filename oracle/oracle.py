@@ -1,0 +1,148 @@
+"""ctypes wrapper of oracle/lime_oracle.c -- TEST INFRASTRUCTURE ONLY.
+
+The C file restates LIME's per-partition algorithms line by line (see its
+header for the file:line map into /root/reference).  Parity pin: the
+reference's own golden vectors (IntersectionSuite, SubtractSuite,
+MergeSuite, ComplementSuite), checked in tests/test_oracle.py.
+This module is imported only by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(_HERE, "lime_oracle.c")
+LIB = os.path.join(_HERE, "build", "liblime_oracle.so")
+
+P = C.POINTER
+i32, i64, i8 = C.c_int32, C.c_int64, C.c_int8
+_lib = None
+
+SUB_LIME, SUB_SET = 0, 1
+
+
+def build():
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c99", "-o", LIB, SRC])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB)
+        pair_args = [i64, P(i32), P(i64), P(i64), P(i8), i64, P(i32), P(i64), P(i64), P(i8), i64]
+        L.lo_intersect.restype = i64
+        L.lo_intersect.argtypes = pair_args + [i64, P(i32), P(i64), P(i64), P(i64), P(i64)]
+        L.lo_subtract.restype = i64
+        L.lo_subtract.argtypes = pair_args + [C.c_int, i64, P(i32), P(i64), P(i64), P(i64),
+                                              P(i64)]
+        L.lo_merge.restype = i64
+        L.lo_merge.argtypes = [i64, P(i32), P(i64), P(i64), P(i8), i64, P(i32), P(i64), P(i64),
+                               P(i8), P(i64)]
+        L.lo_complement.restype = i64
+        L.lo_complement.argtypes = [i64, P(i32), P(i64), P(i64), i32, P(i64), i64, P(i32),
+                                    P(i64), P(i64)]
+        L.lo_pair_hash.restype = C.c_uint64
+        L.lo_pair_hash.argtypes = [C.c_uint32] * 4
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(P(t))
+
+
+def _in(contig, start, end, strand=None):
+    c = np.ascontiguousarray(contig, dtype=np.int32)
+    s = np.ascontiguousarray(start, dtype=np.int64)
+    e = np.ascontiguousarray(end, dtype=np.int64)
+    st = None if strand is None else np.ascontiguousarray(strand, dtype=np.int8)
+    return len(c), c, s, e, st
+
+
+def _out(n):
+    return (np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.int64),
+            np.zeros(n, np.int64), np.zeros(n, np.int64))
+
+
+def _result(arrs):
+    c, s, e, l, r = arrs
+    return {"contig": c, "start": s, "end": e, "a_row": l, "b_row": r}
+
+
+def intersect(a, b, threshold=0):
+    """a, b: (contig, start, end[, strand]) arrays.  Returns dict of arrays in
+    the reference's emission order (left sorted order, then cache order)."""
+    L = lib()
+    na, ac, as_, ae, ast = _in(*a)
+    nb, bc, bs, be, bst = _in(*b)
+    args = [na, _p(ac, i32), _p(as_, i64), _p(ae, i64), _p(ast, i8), nb, _p(bc, i32),
+            _p(bs, i64), _p(be, i64), _p(bst, i8), int(threshold)]
+    n = L.lo_intersect(*args, 0, None, None, None, None, None)
+    o = _out(n)
+    L.lo_intersect(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))])
+    return _result(o)
+
+
+def subtract(a, b, threshold=0, mode=SUB_LIME):
+    L = lib()
+    na, ac, as_, ae, ast = _in(*a)
+    nb, bc, bs, be, bst = _in(*b)
+    args = [na, _p(ac, i32), _p(as_, i64), _p(ae, i64), _p(ast, i8), nb, _p(bc, i32),
+            _p(bs, i64), _p(be, i64), _p(bst, i8), int(threshold), int(mode)]
+    n = L.lo_subtract(*args, 0, None, None, None, None, None)
+    o = _out(n)
+    L.lo_subtract(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))])
+    return _result(o)
+
+
+def merge(a):
+    L = lib()
+    n, c, s, e, st = _in(*a)
+    k = L.lo_merge(n, _p(c, i32), _p(s, i64), _p(e, i64), _p(st, i8), 0, None, None, None,
+                   None, None)
+    oc, os_, oe = np.zeros(k, np.int32), np.zeros(k, np.int64), np.zeros(k, np.int64)
+    ost = np.zeros(k, np.int8)
+    rid = np.zeros(n, np.int64)
+    L.lo_merge(n, _p(c, i32), _p(s, i64), _p(e, i64), _p(st, i8), k, _p(oc, i32),
+               _p(os_, i64), _p(oe, i64), _p(ost, i8), _p(rid, i64))
+    return {"contig": oc, "start": os_, "end": oe, "strand": ost, "run_of_row": rid}
+
+
+def complement(a, genome_lengths):
+    L = lib()
+    n, c, s, e, _ = _in(*a)
+    g = np.ascontiguousarray(genome_lengths, dtype=np.int64)
+    k = L.lo_complement(n, _p(c, i32), _p(s, i64), _p(e, i64), len(g), _p(g, i64), 0, None,
+                        None, None)
+    if k < 0:
+        raise KeyError("contig not in genome")
+    oc, os_, oe = np.zeros(k, np.int32), np.zeros(k, np.int64), np.zeros(k, np.int64)
+    L.lo_complement(n, _p(c, i32), _p(s, i64), _p(e, i64), len(g), _p(g, i64), k, _p(oc, i32),
+                    _p(os_, i64), _p(oe, i64))
+    return {"contig": oc, "start": os_, "end": oe}
+
+
+def pair_hash(start, end, a, b):
+    return lib().lo_pair_hash(int(start), int(end), int(a), int(b))
+
+
+def checksum_pairs(res):
+    """Order-independent (sum, xor) of mix64 hashes of (start, end, a_row, b_row)."""
+    from lime_amd.synth import mix64  # same finaliser as the C oracle
+    s = np.asarray(res["start"], dtype=np.uint64)
+    e = np.asarray(res["end"], dtype=np.uint64)
+    a = np.asarray(res["a_row"], dtype=np.uint64)
+    b = np.asarray(res["b_row"], dtype=np.uint64)
+    x = (s << np.uint64(32)) | e
+    y = (a << np.uint64(32)) | b
+    h = mix64(x ^ mix64(y))
+    with np.errstate(over="ignore"):
+        tot = int(np.sum(h, dtype=np.uint64))
+    xr = int(np.bitwise_xor.reduce(h)) if len(h) else 0
+    return tot, xr

@@ -1,0 +1,308 @@
+"""Parity of the HIP engine (through the C-ABI) with the CPU oracle and the
+reference's golden vectors.  Integer work: every comparison is bit-exact,
+as sorted lists."""
+import os
+
+import numpy as np
+import pytest
+
+from lime_amd import LimeError, Space, SUBTRACT_LIME, SUBTRACT_SET, synth
+from lime_amd.set_theory import (DistributedComplement, DistributedIntersection,
+                                 DistributedMerge, DistributedSubtract, NoSuchElementException,
+                                 ReferenceRegion)
+from oracle import oracle
+from tests.util import (GOLDEN, as_sorted_tuples, expected, random_sets, read_bed_py,
+                        read_genome_py)
+
+pytestmark = pytest.mark.gpu
+
+
+def keyed(name):
+    chrom, s, e, nm = read_bed_py(os.path.join(GOLDEN, name))
+    return [(ReferenceRegion.unstranded(c, a, b), n) for c, a, b, n in zip(chrom, s, e, nm)]
+
+
+def rr(triples):
+    return [ReferenceRegion(c, s, e) for c, s, e in triples]
+
+
+# ------------------------------------------------- the reference's own suites
+def test_intersection_suite(ctx):
+    # IntersectionSuite.scala:8-26 (full 7-pair truth; the suite's zip pins 5)
+    out = DistributedIntersection(keyed("intersect_with_overlap_00.bed"),
+                                  keyed("intersect_with_overlap_01.bed"), None, ctx=ctx).compute()
+    regs = [r for r, _ in out]
+    assert regs[:5] == rr(expected()["intersection_prefix"])
+    assert regs == rr(expected()["intersection_full"])
+    assert out[0][1] == ("CpG:_30", "CpG:_116")
+
+
+def test_subtract_suite(ctx):
+    # SubtractSuite.scala:8-40
+    out = DistributedSubtract(keyed("intersect_with_overlap_00.bed"),
+                              keyed("intersect_with_overlap_01.bed"), None, ctx=ctx).compute()
+    assert [r for r, _ in out] == rr(expected()["subtract"])
+    assert sum(v[1] is None for _, v in out) == 17
+
+
+def test_merge_suite(ctx):
+    # MergeSuite.scala:12-19
+    out = DistributedMerge(keyed("cpg_20merge.bed"), None, ctx=ctx).compute()
+    assert len(out) == expected()["merge_count"]
+    assert out[0][0] == ReferenceRegion("chr1", 28735, 30000)
+    assert len(out[0][1]) == 20
+
+
+def test_complement_suite(ctx):
+    # ComplementSuite.scala:8-115
+    names, lens = read_genome_py(os.path.join(GOLDEN, "genome.txt"))
+    bounds = {n: ReferenceRegion(n, 0, l) for n, l in zip(names, lens)}
+    out = DistributedComplement(keyed("cpg_20merge.bed"), None, bounds, ctx=ctx).compute()
+    assert [r for r, _ in out] == rr(expected()["complement"])
+
+
+def test_complement_missing_contig_raises(ctx):
+    bounds = {"chr2": ReferenceRegion("chr2", 0, 100)}
+    with pytest.raises(NoSuchElementException):
+        DistributedComplement(keyed("cpg_20merge.bed"), None, bounds, ctx=ctx).compute()
+
+
+def test_stranded_intersection(ctx):
+    # ReferenceRegion.overlaps requires equal strands (the CLI keys stranded)
+    L = [(ReferenceRegion("chr1", 0, 100, "FORWARD"), "a"),
+         (ReferenceRegion("chr1", 0, 100, "REVERSE"), "b")]
+    R = [(ReferenceRegion("chr1", 50, 60, "FORWARD"), "x")]
+    out = DistributedIntersection(L, R, None, ctx=ctx).compute()
+    assert out == [(ReferenceRegion("chr1", 50, 60, "FORWARD"), ("a", "x"))]
+
+
+# ----------------------------------------------------- randomised parity
+NAMES = [f"c{i:02d}" for i in range(4)]
+
+
+def space_for(n_contigs, contig_len):
+    return Space(NAMES[:n_contigs], [contig_len] * n_contigs)
+
+
+def engine_pairs(ctx, sp, A, B, t):
+    a = ctx.set_from_host(sp, *A)
+    b = ctx.set_from_host(sp, *B)
+    plan = ctx.intersect(a, b, t)
+    p = plan.fill_host()
+    # contig of a pair = contig of its left row
+    return {"contig": A[0][p["a_row"]], "start": p["start"], "end": p["end"],
+            "a_row": p["a_row"], "b_row": p["b_row"]}, plan
+
+
+CASES = [(1, 0, 0.0, 0.0), (2, 0, 0.1, 0.1), (3, 25, 0.0, 0.0), (4, -3, 0.2, 0.1),
+         (5, 1, 0.1, 0.0), (6, 120, 0.05, 0.2), (7, 0, 0.0, 0.3)]
+
+
+@pytest.mark.parametrize("seed,t,zero,book", CASES)
+def test_intersect_parity(ctx, seed, t, zero, book):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 3000, 2500, n_contigs=3, contig_len=30000, max_len=400,
+                       zero_frac=zero, dup_frac=0.05, book_frac=book)
+    sp = space_for(3, 30000)
+    got, plan = engine_pairs(ctx, sp, A, B, t)
+    exp = oracle.intersect(A, B, t)
+    assert plan.n == len(exp["start"])
+    assert as_sorted_tuples(got) == as_sorted_tuples(exp)
+    # device checksum kernel == checksum of the materialised pairs == oracle
+    assert plan.checksum() == oracle.checksum_pairs(got) == oracle.checksum_pairs(exp)
+
+
+@pytest.mark.parametrize("seed,zero,book", [(11, 0.0, 0.0), (12, 0.1, 0.1), (13, 0.3, 0.3)])
+def test_merge_parity(ctx, seed, zero, book):
+    rng = np.random.default_rng(seed)
+    A, _ = random_sets(rng, 20000, 1, n_contigs=4, contig_len=60000, max_len=300,
+                       zero_frac=zero, dup_frac=0.1, book_frac=book)
+    sp = space_for(4, 60000)
+    a = ctx.set_from_host(sp, *A)
+    res = ctx.merge(a)
+    h = res.to_host()
+    exp = oracle.merge(A)
+    assert list(h["contig"]) == list(exp["contig"])
+    assert list(h["start"]) == list(exp["start"]) and list(h["end"]) == list(exp["end"])
+    assert (res.run_of_row(len(A[0])) == exp["run_of_row"]).all()
+
+
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+@pytest.mark.parametrize("seed,t,zero", [(21, 0, 0.0), (22, 0, 0.1), (23, 30, 0.05),
+                                         (24, 1, 0.1), (25, -2, 0.0)])
+def test_subtract_parity(ctx, mode, seed, t, zero):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 4000, 3000, n_contigs=3, contig_len=40000, max_len=500,
+                       zero_frac=zero, dup_frac=0.05, book_frac=0.1)
+    sp = space_for(3, 40000)
+    res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t, mode).to_host()
+    exp = oracle.subtract(A, B, t, mode)
+    # exact emission order too (left sorted order, blocks reversed in lime mode)
+    for k in ("contig", "start", "end", "a_row", "b_row"):
+        assert list(res[k]) == list(exp[k]), k
+
+
+@pytest.mark.parametrize("seed,zero", [(31, 0.0), (32, 0.1)])
+def test_complement_parity(ctx, seed, zero):
+    rng = np.random.default_rng(seed)
+    A, _ = random_sets(rng, 5000, 1, n_contigs=3, contig_len=50000, max_len=400,
+                       zero_frac=zero, book_frac=0.1)
+    lens = [50000, 50000, 50000, 777]  # last contig has no data
+    sp = Space(NAMES, lens)
+    res = ctx.complement(sp, ctx.set_from_host(sp, *A)).to_host()
+    exp = oracle.complement(A, lens)
+    for k in ("contig", "start", "end"):
+        assert list(res[k]) == list(exp[k]), k
+
+
+def test_sorted_set_order(ctx):
+    rng = np.random.default_rng(41)
+    A, _ = random_sets(rng, 50000, 1, n_contigs=4, contig_len=100000, zero_frac=0.1,
+                       dup_frac=0.1)
+    sp = space_for(4, 100000)
+    h = ctx.set_from_host(sp, *A).to_host()
+    assert sorted(h["row"]) == list(range(50000))
+    c, s, e = A[0][h["row"]], A[1][h["row"]], A[2][h["row"]]
+    assert (c == h["contig"]).all() and (s == h["start"]).all() and (e == h["end"]).all()
+    key = list(zip(c, s, e > s, h["row"]))
+    assert key == sorted(key)  # (contig, start, zero-width first), stable
+
+
+def test_empty_and_errors(ctx):
+    sp = space_for(2, 1000)
+    z = (np.zeros(0, np.int32), np.zeros(0, np.int64), np.zeros(0, np.int64))
+    one = (np.array([1], np.int32), np.array([5]), np.array([9]))
+    e = ctx.set_from_host(sp, *z)
+    o = ctx.set_from_host(sp, *one)
+    assert ctx.intersect(e, o).n == 0 and ctx.intersect(o, e).n == 0
+    assert ctx.merge(e).n == 0
+    r = ctx.subtract(o, e).to_host()
+    assert list(r["start"]) == [5] and list(r["b_row"]) == [-1]
+    assert ctx.subtract(e, o).n == 0
+    assert ctx.complement(sp, e).n == 2
+    with pytest.raises(LimeError) as ei:
+        ctx.set_from_host(sp, np.array([2], np.int32), np.array([0]), np.array([1]))
+    assert ei.value.code == 5
+    with pytest.raises(LimeError) as ei:
+        ctx.set_from_host(sp, np.array([0], np.int32), np.array([0]), np.array([1001]))
+    assert ei.value.code == 2
+
+
+def test_device_synth_matches_numpy(ctx):
+    import torch
+    sp = Space(list(synth.HG38.keys()), list(synth.HG38.values()))
+    n = 200000
+    c = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.empty(n, dtype=torch.int32, device="cuda")
+    e = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.synth_uniform(sp, n, 0xA, 50, 5000, c.data_ptr(), s.data_ptr(), e.data_ptr())
+    ctx.synchronize()
+    ec, es, ee = synth.uniform(sp.lengths, n, 0xA, 50, 5000)
+    assert (c.cpu().numpy() == ec).all()
+    assert (s.cpu().numpy().view(np.uint32) == es).all()
+    assert (e.cpu().numpy().view(np.uint32) == ee).all()
+    ctx.synth_pileup(sp, n, 0xC, 5000, 150, 150, 600, c.data_ptr(), s.data_ptr(), e.data_ptr())
+    ctx.synchronize()
+    pc, ps, pe = synth.pileup(sp.lengths, n, 0xC, 5000, 150, 150, 600)
+    assert (c.cpu().numpy() == pc).all() and (s.cpu().numpy().view(np.uint32) == ps).all()
+
+
+def _device_set(ctx, sp, n, seed, lo, hi):
+    import torch
+    c = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.empty(n, dtype=torch.int32, device="cuda")
+    e = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.synth_uniform(sp, n, seed, lo, hi, c.data_ptr(), s.data_ptr(), e.data_ptr())
+    return ctx.set_from_device(sp, n, c.data_ptr(), s.data_ptr(), e.data_ptr())
+
+
+def test_scaled_c2_parity(ctx):
+    # C2's distribution on a 1/400 genome: same depth (~82 per set), so the
+    # same pairs per row; small enough for the oracle
+    lens = [x // 400 for x in synth.HG38.values()]
+    sp = Space(list(synth.HG38.keys()), lens)
+    n = 250_000
+    A = synth.uniform(sp.lengths, n, 0xA, 50, 5000)
+    B = synth.uniform(sp.lengths, n, 0xB, 50, 5000)
+    a = _device_set(ctx, sp, n, 0xA, 50, 5000)
+    b = _device_set(ctx, sp, n, 0xB, 50, 5000)
+    plan = ctx.intersect(a, b)
+    exp = oracle.intersect(A, B)
+    assert plan.n == len(exp["start"])
+    assert plan.checksum() == oracle.checksum_pairs(exp)
+    # chunked device fill (odd chunk size) reproduces the checksum
+    import torch
+    from lime_amd import PAIR_DTYPE
+    step = 10_000_019
+    tot, xr = 0, 0
+    buf = torch.empty((step, 4), dtype=torch.int32, device="cuda")
+    for f in range(0, plan.n, step):
+        k = min(step, plan.n - f)
+        plan.fill_device(f, k, buf.data_ptr())
+        ctx.synchronize()
+        p = buf[:k].cpu().numpy().view(np.uint32).reshape(-1).view(PAIR_DTYPE)
+        s_, x_ = oracle.checksum_pairs(p)
+        tot = (tot + s_) % 2**64
+        xr ^= x_
+    assert (tot, xr) == plan.checksum()
+    mres = ctx.merge(a).to_host()
+    mexp = oracle.merge(A)
+    assert (mres["start"] == mexp["start"]).all() and (mres["end"] == mexp["end"]).all()
+
+
+def test_full_size_c2_count_property(ctx):
+    # BASELINE C2 at full size (2 x 1e8): the pair count must equal an
+    # independent formula, #overlaps(a) = #{b.s < a.e} - #{b.e <= a.s},
+    # evaluated per contig with numpy searchsorted
+    sp = Space(list(synth.HG38.keys()), list(synth.HG38.values()))
+    n = 100_000_000
+    a = _device_set(ctx, sp, n, 0xA, 50, 5000)
+    b = _device_set(ctx, sp, n, 0xB, 50, 5000)
+    plan = ctx.intersect(a, b)
+    A = synth.uniform(sp.lengths, n, 0xA, 50, 5000)
+    B = synth.uniform(sp.lengths, n, 0xB, 50, 5000)
+    total = 0
+    for c in range(len(sp.lengths)):
+        ma, mb = A[0] == c, B[0] == c
+        bs, be = np.sort(B[1][mb]), np.sort(B[2][mb])
+        total += int(np.searchsorted(bs, A[2][ma], "left").sum() -
+                     np.searchsorted(be, A[1][ma], "right").sum())
+    assert plan.n == total
+    assert 1.5e10 < plan.n < 1.75e10  # E[pairs] ~ 1.63e10
+
+
+def test_bitset_paths(ctx):
+    rng = np.random.default_rng(51)
+    A, B = random_sets(rng, 20000, 20000, n_contigs=3, contig_len=200000, max_len=300)
+    sp = space_for(3, 200000)
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    ba, bb = ctx.bitset(a), ctx.bitset(b)
+    cov_a = sum(e - s for e, s in zip(oracle.merge(A)["end"], oracle.merge(A)["start"]))
+    assert ba.popcount() == cov_a
+
+    def coalesce(res):
+        out = []
+        for c, s, e in zip(res["contig"], res["start"], res["end"]):
+            if out and out[-1][0] == c and out[-1][2] == s:
+                out[-1][2] = e
+            else:
+                out.append([int(c), int(s), int(e)])
+        return out
+    # complement (bitset NOT) == interval complement after coalescing (A.4)
+    lens = [200000] * 3
+    got = ctx.bitset_runs(1, ba).to_host()
+    exp = oracle.complement(A, lens)
+    assert coalesce(got) == coalesce(exp)
+    # difference: base-level merge(A) \ merge(B) == set-mode subtract of merged runs
+    got = coalesce(ctx.bitset_runs(3, ba, bb).to_host())
+    ma, mb = oracle.merge(A), oracle.merge(B)
+    exp = oracle.subtract((ma["contig"], ma["start"], ma["end"]),
+                          (mb["contig"], mb["start"], mb["end"]), 0, oracle.SUB_SET)
+    assert got == coalesce(exp)
+    # 2-way AND == merged intersection of merged operands
+    got = coalesce(ctx.bitset_and([ba, bb]).to_host())
+    ix = oracle.intersect((ma["contig"], ma["start"], ma["end"]),
+                          (mb["contig"], mb["start"], mb["end"]))
+    order = np.lexsort((ix["start"], ix["contig"]))
+    exp = coalesce({k: ix[k][order] for k in ("contig", "start", "end")})
+    assert got == exp

@@ -1,0 +1,231 @@
+"""Pin the CPU oracle (oracle/lime_oracle.c) before trusting it:
+  1. against every golden vector the reference's hot-path suites hold
+     (IntersectionSuite, SubtractSuite, MergeSuite, ComplementSuite), on the
+     verbatim fixture files;
+  2. against brute-force restatements of Appendix A on seeded inputs.
+CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.util import (GOLDEN, expected, java_key, random_sets, ranked, read_bed_py,
+                        read_genome_py)
+
+
+def load(name, rank):
+    chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, name))
+    return np.array([rank[c] for c in chrom], np.int32), s, e
+
+
+def regions(res, names):
+    return [[names[c], int(s), int(e)] for c, s, e in zip(res["contig"], res["start"],
+                                                           res["end"])]
+
+
+@pytest.fixture(scope="module")
+def io():
+    a, _, _, _ = read_bed_py(os.path.join(GOLDEN, "intersect_with_overlap_00.bed"))
+    b, _, _, _ = read_bed_py(os.path.join(GOLDEN, "intersect_with_overlap_01.bed"))
+    rank = ranked(a + b)
+    names = sorted(rank, key=rank.get)
+    return load("intersect_with_overlap_00.bed", rank), load("intersect_with_overlap_01.bed",
+                                                             rank), names
+
+
+def test_intersection_suite(io):
+    # IntersectionSuite.scala:17-25 zips the output with 5 regions; the true
+    # result has 7 (two exact-duplicate matches missing from the array, Q10).
+    A, B, names = io
+    got = regions(oracle.intersect(A, B), names)
+    exp = expected()
+    assert got[:5] == exp["intersection_prefix"]
+    assert got == exp["intersection_full"]
+
+
+def test_subtract_suite(io):
+    # SubtractSuite.scala:20-39: exact 18 regions, in order
+    A, B, names = io
+    got = oracle.subtract(A, B)
+    assert regions(got, names) == expected()["subtract"]
+    # every left row that meets no right row comes back whole with None
+    assert (got["b_row"] == -1).sum() == 17
+    # lime and set modes agree whenever a left row meets <= 1 block
+    assert regions(oracle.subtract(A, B, mode=oracle.SUB_SET), names) == expected()["subtract"]
+
+
+def test_merge_suite():
+    chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, "cpg_20merge.bed"))
+    rank = ranked(chrom)
+    res = oracle.merge((np.array([rank[c] for c in chrom], np.int32), s, e))
+    assert len(res["start"]) == expected()["merge_count"]  # MergeSuite.scala:18
+    assert (int(res["start"][0]), int(res["end"][0])) == (28735, 30000)
+    assert (res["run_of_row"] == 0).all()
+
+
+def test_complement_suite():
+    gnames, glens = read_genome_py(os.path.join(GOLDEN, "genome.txt"))
+    order = sorted(range(len(gnames)), key=lambda i: java_key(gnames[i]))
+    names = [gnames[i] for i in order]
+    lens = [glens[i] for i in order]
+    rank = {n: i for i, n in enumerate(names)}
+    chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, "cpg_20merge.bed"))
+    res = oracle.complement((np.array([rank[c] for c in chrom], np.int32), s, e), lens)
+    assert regions(res, names) == expected()["complement"]  # ComplementSuite.scala:19-114
+
+
+def test_complement_unknown_contig():
+    with pytest.raises(KeyError):
+        oracle.complement((np.array([3], np.int32), np.array([0]), np.array([5])), [10, 10])
+
+
+# ------------------------------------------------------------ brute force
+def brute_pairs(A, B, t):
+    out = []
+    for i in range(len(A[0])):
+        for j in range(len(B[0])):
+            if A[0][i] != B[0][j]:
+                continue
+            a0, a1, b0, b1 = A[1][i], A[2][i], B[1][j], B[2][j]
+            if not (a1 > b0 and a0 < b1):
+                continue
+            ov = min(a1, b1) - max(a0, b0)
+            if ov >= t:
+                out.append((int(A[0][i]), max(a0, b0), min(a1, b1), i, j))
+    return sorted(out)
+
+
+def tuples(res):
+    return sorted(zip(res["contig"].tolist(), res["start"].tolist(), res["end"].tolist(),
+                      res["a_row"].tolist(), res["b_row"].tolist()))
+
+
+@pytest.mark.parametrize("seed,t,zero", [(1, 0, 0.0), (2, 0, 0.1), (3, 25, 0.0), (4, -3, 0.2),
+                                         (5, 1, 0.1), (6, 120, 0.05)])
+def test_intersect_vs_brute(seed, t, zero):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 300, 250, n_contigs=2, contig_len=6000, zero_frac=zero,
+                       dup_frac=0.05, book_frac=0.1)
+    assert tuples(oracle.intersect(A, B, t)) == brute_pairs(A, B, t)
+
+
+def merge_components(A):
+    """strict-overlap connected components (non-zero-width input)"""
+    n = len(A[0])
+    parent = list(range(n))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+    for i in range(n):
+        for j in range(i + 1, n):
+            if A[0][i] == A[0][j] and A[2][i] > A[1][j] and A[1][i] < A[2][j]:
+                parent[find(i)] = find(j)
+    comp = {}
+    for i in range(n):
+        r = find(i)
+        c, s, e = comp.get(r, (int(A[0][i]), 10**18, -1))
+        comp[r] = (c, min(s, int(A[1][i])), max(e, int(A[2][i])))
+    return sorted(comp.values())
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_merge_vs_components(seed):
+    rng = np.random.default_rng(seed)
+    A, _ = random_sets(rng, 400, 1, n_contigs=3, contig_len=8000, book_frac=0.2)
+    res = oracle.merge(A)
+    got = sorted(zip(res["contig"].tolist(), res["start"].tolist(), res["end"].tolist()))
+    assert got == merge_components(A)
+
+
+def base_sets(intervals):
+    cov = {}
+    for c, s, e in intervals:
+        cov.setdefault(c, set()).update(range(s, e))
+    return cov
+
+
+def runs_of(bases):
+    out = []
+    for c in sorted(bases):
+        xs = sorted(bases[c])
+        i = 0
+        while i < len(xs):
+            j = i
+            while j + 1 < len(xs) and xs[j + 1] == xs[j] + 1:
+                j += 1
+            out.append((c, xs[i], xs[j] + 1))
+            i = j + 1
+    return out
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_complement_vs_bases(seed):
+    rng = np.random.default_rng(seed)
+    lens = [3000, 2500, 0, 4000]
+    A, _ = random_sets(rng, 120, 1, n_contigs=2, contig_len=2500, max_len=200)
+    cov = base_sets(zip(A[0].tolist(), A[1].tolist(), A[2].tolist()))
+    comp = {c: set(range(lens[c])) - cov.get(c, set()) for c in range(len(lens))}
+    res = oracle.complement(A, lens)
+    got = sorted(zip(res["contig"].tolist(), res["start"].tolist(), res["end"].tolist()))
+    assert got == runs_of(comp)
+
+
+@pytest.mark.parametrize("seed,t", [(31, 0), (32, 10), (33, 1)])
+def test_subtract_set_mode_vs_bases(seed, t):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 150, 150, n_contigs=2, contig_len=3000, max_len=250)
+    res = oracle.subtract(A, B, t, mode=oracle.SUB_SET)
+    got = {}
+    for k in range(len(res["start"])):
+        got.setdefault(int(res["a_row"][k]), []).append((int(res["start"][k]),
+                                                          int(res["end"][k])))
+    for i in range(len(A[0])):
+        a0, a1 = int(A[1][i]), int(A[2][i])
+        keep = set(range(a0, a1))
+        for j in range(len(B[0])):
+            if B[0][j] != A[0][i]:
+                continue
+            b0, b1 = int(B[1][j]), int(B[2][j])
+            if a1 > b0 and a0 < b1 and min(a1, b1) - max(a0, b0) >= t:
+                keep -= set(range(b0, b1))
+        exp = [(c0, c1) for _, c0, c1 in runs_of({0: keep})]
+        if keep == set(range(a0, a1)):
+            exp = [(a0, a1)]
+        assert got.get(i, []) == exp, i
+
+
+def test_subtract_lime_multiblock_quirk():
+    # Q5: a left row meeting two disjoint blocks gets remnants per block, in
+    # reverse block order (Subtract.scala:103-114)
+    A = (np.array([0], np.int32), np.array([0]), np.array([100]))
+    B = (np.array([0, 0], np.int32), np.array([10, 50]), np.array([20, 60]))
+    res = oracle.subtract(A, B)
+    got = list(zip(res["start"].tolist(), res["end"].tolist(), res["b_row"].tolist()))
+    assert got == [(0, 50, 1), (60, 100, 1), (0, 10, 0), (20, 100, 0)]
+    res = oracle.subtract(A, B, mode=oracle.SUB_SET)
+    assert list(zip(res["start"].tolist(), res["end"].tolist())) == [(0, 10), (20, 50),
+                                                                      (60, 100)]
+
+
+def test_zero_width_edges():
+    # zero-width rows: merge keeps them apart from book-ended neighbours and
+    # the zero-width subtract head is folded twice (duplicate block)
+    A = (np.array([0, 0, 0], np.int32), np.array([5, 5, 7]), np.array([5, 10, 7]))
+    res = oracle.merge(A)
+    got = list(zip(res["start"].tolist(), res["end"].tolist()))
+    assert got == [(5, 5), (5, 10)]
+    L = (np.array([0], np.int32), np.array([0]), np.array([10]))
+    R = (np.array([0], np.int32), np.array([4]), np.array([4]))
+    res = oracle.subtract(L, R)
+    assert list(zip(res["start"].tolist(), res["end"].tolist())) == [(0, 4), (4, 10), (0, 4),
+                                                                      (4, 10)]
+    # intersect: zero-width b strictly inside a hits (overlapsBy == 0 >= 0);
+    # at a.start it does not (strict overlap)
+    R2 = (np.array([0, 0], np.int32), np.array([0, 4]), np.array([0, 4]))
+    res = oracle.intersect(L, R2)
+    assert list(zip(res["start"].tolist(), res["end"].tolist(), res["b_row"].tolist())) == \
+        [(4, 4, 1)]

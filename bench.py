@@ -110,7 +110,10 @@ def main():
     from lime_amd import synth
 
     ctx = lime_amd.Context(dev.index)
-    stream = torch.cuda.current_stream(dev)
+    # one non-default stream shared by torch and the engine: the HIP events
+    # below are recorded on the stream the kernels are launched on
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     space = lime_amd.Space(list(synth.HG38.keys()), list(synth.HG38.values()))
     n = args.n

@@ -106,6 +106,15 @@ def load(path=LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch-ROCm bundles its own HIP runtime with the same soname
+    # (libamdhip64.so.7).  Loading torch first makes this library bind to that
+    # already-loaded runtime, so the process holds ONE HIP runtime and device
+    # pointers / streams are shared with torch; loading ours first would make
+    # torch pull in a second runtime that no longer sees the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build the HIP engine first (make, or "

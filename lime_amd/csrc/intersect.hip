@@ -84,7 +84,10 @@ __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64
     for (int64_t j = o0 + lane; j < o1; j += 64) hmax = max(hmax, (int64_t)sa.oge[j] - tp + 1);
     hmax = dev::wave_reduce_max(hmax);
     const int64_t lkey = (int64_t)sa.ogs[o0] + sa.lo_off;
-    if (hmax < lkey) hmax = lkey;
+    // every owner's lo = lb(P, o.gs + lo_off) must lie inside the window too
+    // (subtract walks back from it even when the owner's range is empty)
+    const int64_t lkey_last = (int64_t)sa.ogs[o1 - 1] + sa.lo_off;
+    if (hmax < lkey_last) hmax = lkey_last;
     if (lane == 0) win[2 * (sa.tile0 + t)] = (uint32_t)dev::lower_bound(sa.pgs, 0, sa.np, lkey);
     if (lane == 1) win[2 * (sa.tile0 + t) + 1] = (uint32_t)dev::lower_bound(sa.pgs, 0, sa.np, hmax);
 }
@@ -114,17 +117,19 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
         const uint32_t og = sa.ogs[j], oe = sa.oge[j];
         int64_t lk, hk;
         owner_keys(og, oe, sa.lo_off, tp, lk, hk);
-        int64_t lo = wlo, hi = wlo;
-        if (hk > lk) {
-            if (in_lds) {
-                lo = wlo + dev::lower_bound(wgs, 0, wlen, lk);
-                hi = wlo + dev::lower_bound(wgs, lo - wlo, wlen, hk);
-            } else {
-                lo = dev::lower_bound(sa.pgs, (int64_t)wlo, (int64_t)whi, lk);
-                hi = dev::lower_bound(sa.pgs, lo, (int64_t)whi, hk);
-            }
-            if (sa.zw_skip)
-                while (lo < hi && sa.pgs[lo] == og && sa.pge[lo] == og) ++lo;
+        // lo = lb(P, o.gs + lo_off) always (subtract's spanning walk starts
+        // below it); the range [lo, hi) is empty when hk <= lk
+        int64_t lo, hi;
+        if (in_lds) {
+            lo = wlo + dev::lower_bound(wgs, 0, wlen, lk);
+            hi = hk > lk ? wlo + dev::lower_bound(wgs, lo - wlo, wlen, hk) : lo;
+        } else {
+            lo = dev::lower_bound(sa.pgs, (int64_t)wlo, (int64_t)whi, lk);
+            hi = hk > lk ? dev::lower_bound(sa.pgs, lo, (int64_t)whi, hk) : lo;
+        }
+        if (sa.zw_skip) {
+            while (lo < whi && sa.pgs[lo] == og && sa.pge[lo] == og) ++lo;
+            if (hi < lo) hi = lo;
         }
         uint32_t c;
         if (FILTER) {

@@ -87,9 +87,12 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         const int64_t hi1 = lo1 + sa.ocnt[i];
         const uint32_t thr = t <= 0 ? as : (uint32_t)((int64_t)as + t - 1);
         const int64_t j0 = first_spanning(sa.bpmax, lo1, thr);
-        // fold state
-        uint32_t bs = 0, be = 0, bh = 0;  // current block + head row
-        uint64_t cum = 0;                  // remnants of finished blocks (lime mode, write order)
+        // fold state.  The block's value is its head = first hit in the
+        // reference's (start, end, row) order; the device order only ties
+        // starts by (zero-width first, row), so among same-start non-empty
+        // hits the head is re-picked as the min (end, row).
+        uint32_t bs = 0, be = 0, bh = 0, bhe = 0;  // block, head row, head end
+        uint64_t cum = 0;  // remnants of finished blocks (lime mode, write order)
         uint32_t setpos = as;
         for (int64_t j = j0; j < hi1; ++j) {
             const uint32_t gs = sa.bgs[j], ge = sa.bge[j];
@@ -99,15 +102,20 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             else
                 hit = t >= 1 ? (int64_t)(ge - gs) >= t : true;
             if (!hit) continue;
-            int visits = any ? 1 : 2;  // the head is folded against itself once
-            if (!any) {
-                any = true;
+            const uint32_t row = sa.brow[j];
+            if (!any) {  // foldLeft(List(filteredCache.head)): the head seeds the
+                any = true;  // list and is then folded against itself once
                 bs = gs;
                 be = ge;
-                bh = sa.brow[j];
+                bh = row;
+                bhe = ge;
             }
-            for (int v = 0; v < visits; ++v) {
+            {
                 if (be > gs && bs < ge) {  // block.overlaps(b): hull
+                    if (gs == bs && bhe > bs && (ge < bhe || (ge == bhe && row < bh))) {
+                        bh = row;
+                        bhe = ge;
+                    }
                     bs = gs < bs ? gs : bs;
                     be = ge > be ? ge : be;
                 } else {
@@ -129,7 +137,8 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                     }
                     bs = gs;
                     be = ge;
-                    bh = sa.brow[j];
+                    bh = row;
+                    bhe = ge;
                 }
             }
         }

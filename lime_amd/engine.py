@@ -113,9 +113,9 @@ class IntervalSet:
         return out
 
     def close(self):
-        if self._h:
+        if self._h and self.ctx.handle:  # a closed context already freed its pool
             _lib().lime_set_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -127,8 +127,9 @@ class IntervalSet:
 class Result:
     """merge / subtract / complement / bitset output (lime_result)."""
 
-    def __init__(self, ctx, handle, space):
-        self.ctx, self._h, self.space = ctx, handle, space
+    def __init__(self, ctx, handle, space, keep=()):
+        # `keep`: the inputs whose device arrays this handle still reads
+        self.ctx, self._h, self.space, self._keep = ctx, handle, space, keep
 
     @property
     def n(self):
@@ -154,9 +155,9 @@ class Result:
         return gs.value, ge.value
 
     def close(self):
-        if self._h:
+        if self._h and self.ctx.handle:  # a closed context already freed its pool
             _lib().lime_result_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -168,8 +169,9 @@ class Result:
 class Pairs:
     """Intersect plan: exact pair count plus chunked fill (lime_pairs)."""
 
-    def __init__(self, ctx, handle, n):
-        self.ctx, self._h, self.n = ctx, handle, n
+    def __init__(self, ctx, handle, n, keep=()):
+        # the plan reads A's and B's device arrays: keep both alive
+        self.ctx, self._h, self.n, self._keep = ctx, handle, n, keep
 
     def fill_host(self, first=0, count=None):
         if count is None:
@@ -187,9 +189,9 @@ class Pairs:
         return s.value, x.value
 
     def close(self):
-        if self._h:
+        if self._h and self.ctx.handle:  # a closed context already freed its pool
             _lib().lime_pairs_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -199,16 +201,17 @@ class Pairs:
 
 
 class Bitset:
-    def __init__(self, ctx, handle, space):
-        self.ctx, self._h, self.space = ctx, handle, space
+    def __init__(self, ctx, handle, space, keep=()):
+        # `keep`: the inputs whose device arrays this handle still reads
+        self.ctx, self._h, self.space, self._keep = ctx, handle, space, keep
 
     def popcount(self):
         return int(_lib().lime_bitset_popcount(self.ctx.handle, self._h))
 
     def close(self):
-        if self._h:
+        if self._h and self.ctx.handle:  # a closed context already freed its pool
             _lib().lime_bitset_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -261,23 +264,23 @@ class Context:
         h, n = vp(), i64()
         check(_lib().lime_intersect_count(self._h, a._h, b._h, int(threshold), C.byref(h),
                                           C.byref(n)))
-        return Pairs(self, h, n.value)
+        return Pairs(self, h, n.value, keep=(a, b))
 
     def merge(self, a):
         h, n = vp(), i64()
         check(_lib().lime_merge(self._h, a._h, C.byref(h), C.byref(n)))
-        return Result(self, h, a.space)
+        return Result(self, h, a.space, keep=(a,))
 
     def subtract(self, a, b, threshold=0, mode=_ffi.SUBTRACT_LIME):
         h, n = vp(), i64()
         check(_lib().lime_subtract(self._h, a._h, b._h, int(threshold), int(mode), C.byref(h),
                                    C.byref(n)))
-        return Result(self, h, a.space)
+        return Result(self, h, a.space, keep=(a, b))
 
     def complement(self, genome_space, a):
         h, n = vp(), i64()
         check(_lib().lime_complement(self._h, genome_space.handle, a._h, C.byref(h), C.byref(n)))
-        return Result(self, h, a.space)
+        return Result(self, h, a.space, keep=(a,))
 
     def bitset(self, a):
         h = vp()
@@ -288,7 +291,7 @@ class Context:
         h, n = vp(), i64()
         check(_lib().lime_bitset_runs(self._h, int(op), a._h, b._h if b is not None else None,
                                       C.byref(h), C.byref(n)))
-        return Result(self, h, a.space)
+        return Result(self, h, a.space, keep=(a, b))
 
     def bitset_and(self, sets):
         arr = (vp * len(sets))(*[s._h for s in sets])

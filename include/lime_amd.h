@@ -121,6 +121,14 @@ int lime_set_fill_host(const lime_set *set, int32_t *contig, int64_t *start, int
 /* Count pass: exact number of qualifying pairs (overlapsBy >= threshold). */
 int lime_intersect_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,
                          lime_pairs **plan, int64_t *n_pairs);
+/* Same with ownership for a coordinate shard that carries its right
+ * neighbours' boundary rows ("halo") after its own: only the first a_owned
+ * rows of a and b_owned rows of b own output pairs (a pair is owned by the
+ * row whose start is the smaller, ties to a); the halo rows act as partners
+ * only, so shard outputs are disjoint.  -1 = all rows. */
+int lime_intersect_count_owned(lime_ctx *ctx, const lime_set *a, const lime_set *b,
+                               int64_t threshold, int64_t a_owned, int64_t b_owned,
+                               lime_pairs **plan, int64_t *n_pairs);
 /* Fill pass: write pairs [first, first + count) of the plan's output order
  * into a caller-owned DEVICE buffer (chunked emission for outputs larger
  * than HBM).  Asynchronous on the context stream. */

@@ -40,6 +40,7 @@ struct PairsPlan {
     int64_t threshold;
     int64_t tp;
     bool filtered;
+    int64_t a_own, b_own;  // owner rows (prefix) of A and B
     int64_t nt0, nt1;  // owner tiles of stream 0 (owners A) and 1 (owners B)
     uint32_t *olo = nullptr, *ocnt = nullptr;  // per owner, stream 0 then stream 1
     uint64_t *toff = nullptr;                  // per tile exclusive offsets
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(IB) void k_fill_filtered(FillArgs fa, int64_t thres
 }
 
 StreamArgs stream_args(const lime_set *O, const lime_set *P, int st, int64_t threshold,
-                       int64_t tile0, int64_t owner0) {
+                       int64_t tile0, int64_t owner0, int64_t n_own = -1) {
     StreamArgs s;
     s.ogs = O->gs;
     s.oge = O->ge;
@@ -365,7 +366,7 @@ StreamArgs stream_args(const lime_set *O, const lime_set *P, int st, int64_t thr
     s.pgs = P->gs;
     s.pge = P->ge;
     s.prow = P->row;
-    s.no = O->n;
+    s.no = n_own >= 0 ? n_own : O->n;  // owners: the first n_own rows (halo rows own nothing)
     s.np = P->n;
     s.lo_off = st == 0 ? 0u : 1u;
     s.zw_skip = (st == 0 && threshold <= 0 && P->has_zero_width) ? 1 : 0;
@@ -376,8 +377,8 @@ StreamArgs stream_args(const lime_set *O, const lime_set *P, int st, int64_t thr
 
 FillArgs fill_args(PairsPlan *pl) {
     FillArgs fa;
-    fa.s[0] = stream_args(pl->A, pl->B, 0, pl->threshold, 0, 0);
-    fa.s[1] = stream_args(pl->B, pl->A, 1, pl->threshold, pl->nt0, pl->A->n);
+    fa.s[0] = stream_args(pl->A, pl->B, 0, pl->threshold, 0, 0, pl->a_own);
+    fa.s[1] = stream_args(pl->B, pl->A, 1, pl->threshold, pl->nt0, pl->a_own, pl->b_own);
     fa.olo = pl->olo;
     fa.ocnt = pl->ocnt;
     fa.toff = pl->toff;
@@ -423,23 +424,30 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
 
 }  // namespace
 
+// Owners are the first a_own rows of A (stream 0) and b_own rows of B
+// (stream 1); the remaining rows are a halo (partners only), used when a
+// coordinate shard carries its right neighbours' boundary rows.
 int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold,
-                   PairsPlan **out) {
+                   int64_t a_own, int64_t b_own, PairsPlan **out) {
+    if (a_own < 0 || a_own > A->n) a_own = A->n;
+    if (b_own < 0 || b_own > B->n) b_own = B->n;
     PairsPlan *pl = new PairsPlan();
     pl->ctx = ctx;
     pl->A = A;
     pl->B = B;
+    pl->a_own = a_own;
+    pl->b_own = b_own;
     pl->threshold = threshold;
     pl->tp = threshold > 1 ? threshold : 1;
     pl->filtered = threshold >= 1 && (int64_t)std::min(A->min_width, B->min_width) < threshold &&
                    A->n > 0 && B->n > 0;
-    pl->nt0 = (A->n + OT - 1) / OT;
-    pl->nt1 = (B->n + OT - 1) / OT;
+    pl->nt0 = (a_own + OT - 1) / OT;
+    pl->nt1 = (b_own + OT - 1) / OT;
     const int64_t nt = pl->nt0 + pl->nt1;
     int rc = LIME_OK;
     uint64_t *tcnt = nullptr, *total = nullptr;
-    if ((rc = alloc(ctx, &pl->olo, (size_t)(A->n + B->n))) ||
-        (rc = alloc(ctx, &pl->ocnt, (size_t)(A->n + B->n))) ||
+    if ((rc = alloc(ctx, &pl->olo, (size_t)(a_own + b_own))) ||
+        (rc = alloc(ctx, &pl->ocnt, (size_t)(a_own + b_own))) ||
         (rc = alloc(ctx, &pl->toff, (size_t)nt)) || (rc = alloc(ctx, &pl->win, (size_t)2 * nt)) ||
         (rc = alloc(ctx, &tcnt, (size_t)nt)) || (rc = alloc(ctx, &total, 1))) {
         delete pl;
@@ -451,7 +459,8 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
             const lime_set *P = st == 0 ? B : A;
             const int64_t ntl = st == 0 ? pl->nt0 : pl->nt1;
             StreamArgs sa = stream_args(O, P, st, threshold, st == 0 ? 0 : pl->nt0,
-                                        st == 0 ? 0 : A->n);
+                                        st == 0 ? 0 : a_own, st == 0 ? a_own : b_own);
+            if (ntl == 0) continue;
             hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa,
                                pl->tp, ntl, pl->win);
             if (pl->filtered)
@@ -466,7 +475,9 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
         }
     } else {
         LIME_HIP(hipMemsetAsync(tcnt, 0, sizeof(uint64_t) * (size_t)(nt > 0 ? nt : 1), S(ctx)));
-        LIME_HIP(hipMemsetAsync(pl->ocnt, 0, sizeof(uint32_t) * (size_t)(A->n + B->n > 0 ? A->n + B->n : 1), S(ctx)));
+        LIME_HIP(hipMemsetAsync(pl->ocnt, 0,
+                                sizeof(uint32_t) * (size_t)(a_own + b_own > 0 ? a_own + b_own : 1),
+                                S(ctx)));
     }
     LIME_TRY(scan_exclusive_u64(ctx, tcnt, pl->toff, nt, total));
     uint64_t tot = 0;

@@ -1,0 +1,165 @@
+"""Multi-GPU range sharding over torch.distributed.
+
+One process per GPU; the global coordinate space is cut into contiguous
+ranges [split[r], split[r+1]) and shard r OWNS every row whose start falls
+in its range.  The steps below only move rows and small boundary records;
+all interval compute stays in the engine (lime_amd.engine) on each GPU.
+
+  route_rows      unsorted input -> owner shards: one all_to_all of counts,
+                  one all_to_all of (start, end, row) -- the equivalent of
+                  the Spark shuffle of OverlapBasedSetTheory.scala:81-82
+  right_halo      pairwise ops: a row owns the pairs whose partner starts
+                  inside it, so shard r needs the rows of later shards that
+                  start before max(end) of its own rows (the replication of
+                  OverlapBasedSetTheory.scala:75-80, bounded by the longest
+                  interval); one all_gather of shard bounds + one all_to_all
+  merge_carry     merge / complement: each shard merges locally, then ONE
+                  all_gather of every shard's leading runs and last end lets
+                  every shard drop the runs that continue an earlier shard's
+                  run and extend its own last run -- replacing the log2(P)
+                  rounds of SetTheory.scala:236-282 (and shard-count invariant,
+                  which the reference is not: quirks Q1/Q2)
+
+The functions work on int64 torch tensors on any device, so the same code
+runs over RCCL (backend "nccl") on MI355X and over gloo on the CPU in tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+def _ws(group):
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def even_splits(span, world):
+    """Equal-width coordinate ranges (int boundaries, last = span)."""
+    return [span * r // world for r in range(world)] + [span]
+
+
+def sample_splits(gs, span, world, group=None, samples=1024):
+    """Count-balanced splitters from an all_gather of local start samples."""
+    w, _ = _ws(group)
+    n = gs.numel()
+    if n:
+        idx = torch.linspace(0, n - 1, samples, device=gs.device).long()
+        s = torch.sort(gs)[0][idx]
+    else:
+        s = torch.full((samples,), -1, dtype=torch.int64, device=gs.device)
+    out = [torch.empty_like(s) for _ in range(w)]
+    dist.all_gather(out, s, group=group)
+    allv = torch.sort(torch.cat(out))[0]
+    allv = allv[allv >= 0]
+    if allv.numel() == 0:
+        return even_splits(span, world)
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(allv[(allv.numel() * r) // world].item()))
+    cuts.append(int(span))
+    for r in range(1, len(cuts)):  # monotone
+        cuts[r] = max(cuts[r], cuts[r - 1])
+    return cuts
+
+
+def _alltoallv(send, counts, group):
+    """Variable all_to_all of a 2-D int64 tensor [rows, k]; counts[q] rows to q."""
+    w, _ = _ws(group)
+    dev = send.device
+    sc = torch.tensor(counts, dtype=torch.int64, device=dev)
+    rc = torch.empty(w, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcounts = rc.tolist()
+    recv = torch.empty((sum(rcounts), send.shape[1]), dtype=send.dtype, device=dev)
+    dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
+                           input_split_sizes=list(counts), group=group)
+    return recv, rcounts
+
+
+def route_rows(gs, ge, row, splits, group=None):
+    """Send every row to the shard owning its start; returns (gs, ge, row)."""
+    w, _ = _ws(group)
+    bounds = torch.tensor(splits[1:-1], dtype=torch.int64, device=gs.device)
+    owner = torch.bucketize(gs, bounds, right=True)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=w).tolist()
+    send = torch.stack([gs[order], ge[order], row[order]], dim=1)
+    recv, _ = _alltoallv(send, counts, group)
+    return recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous()
+
+
+def right_halo(sets, group=None):
+    """sets: list of (gs, ge, row) int64 tensors of THIS shard, each sorted by
+    gs.  Returns, per set, the rows of later shards that start before this
+    shard's max end over all sets (sorted, concatenated in shard order) --
+    exactly the partners an owned row can have outside the shard."""
+    w, me = _ws(group)
+    dev = sets[0][0].device
+    my_end = max([int(s[1].max().item()) if s[1].numel() else -1 for s in sets])
+    ends = torch.empty(w, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(ends, torch.tensor([my_end], dtype=torch.int64, device=dev),
+                                group=group)
+    ends = ends.tolist()
+    out = []
+    for gs, ge, row in sets:
+        # rows of mine that earlier shards r < me need: gs < ends[r]
+        counts = []
+        for r in range(w):
+            if r < me and ends[r] >= 0:
+                counts.append(int(torch.searchsorted(gs, torch.tensor(ends[r], device=dev)).item()))
+            else:
+                counts.append(0)
+        send = torch.cat([torch.stack([gs[:c], ge[:c], row[:c]], dim=1) for c in counts]) \
+            if sum(counts) else torch.empty((0, 3), dtype=torch.int64, device=dev)
+        recv, _ = _alltoallv(send, counts, group)
+        out.append((recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous()))
+    return out
+
+
+def merge_carry(run_gs, run_ge, group=None, k=256):
+    """Cross-shard fix-up of locally merged runs (sorted, disjoint per shard).
+
+    Returns (drop, new_last_end): this shard must drop its first `drop` runs
+    (they continue a run that starts on an earlier shard) and, if
+    new_last_end is not None, set the end of its last remaining run to it.
+    One all_gather of (n_runs, last_end, first k runs) per call; k doubles
+    and the gather repeats only if a shard's k leading runs are all absorbed.
+    """
+    w, me = _ws(group)
+    dev = run_gs.device
+    while True:
+        n = run_gs.numel()
+        kk = min(k, n)
+        head = torch.full((2 * k + 2,), -1, dtype=torch.int64, device=dev)
+        head[0] = n
+        head[1] = int(run_ge[-1].item()) if n else -1
+        if kk:
+            head[2:2 + kk] = run_gs[:kk]
+            head[2 + k:2 + k + kk] = run_ge[:kk]
+        allh = torch.empty(w * (2 * k + 2), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allh, head, group=group)
+        allh = allh.view(w, 2 * k + 2).cpu().tolist()
+        # sequential carry over shards (host, tiny)
+        carry = -1           # running max end of the open run
+        owner = -1           # shard holding the open run's start
+        drops = [0] * w
+        ext = {}             # owner shard -> extended end of its last run
+        again = False
+        for r in range(w):
+            nr, last_end = allh[r][0], allh[r][1]
+            starts = allh[r][2:2 + k]
+            ends_ = allh[r][2 + k:2 + 2 * k]
+            i = 0
+            while i < min(nr, k) and carry > starts[i]:
+                carry = max(carry, ends_[i])
+                i += 1
+            if i == k and nr > k:
+                again = True
+                break
+            drops[r] = i
+            if i > 0 and owner >= 0:
+                ext[owner] = max(ext.get(owner, -1), carry)
+            if nr > i:  # shard r now holds the open run
+                owner = r
+                carry = max(carry, last_end)
+        if not again:
+            return drops[me], ext.get(me)
+        k *= 2

@@ -260,10 +260,11 @@ class Context:
         return IntervalSet(self, h, space)
 
     # ------------------------------------------------------------- ops
-    def intersect(self, a, b, threshold=0):
+    def intersect(self, a, b, threshold=0, a_owned=-1, b_owned=-1):
         h, n = vp(), i64()
-        check(_lib().lime_intersect_count(self._h, a._h, b._h, int(threshold), C.byref(h),
-                                          C.byref(n)))
+        check(_lib().lime_intersect_count_owned(self._h, a._h, b._h, int(threshold),
+                                                int(a_owned), int(b_owned), C.byref(h),
+                                                C.byref(n)))
         return Pairs(self, h, n.value, keep=(a, b))
 
     def merge(self, a):

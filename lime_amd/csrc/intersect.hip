@@ -74,6 +74,30 @@ __device__ __forceinline__ void owner_keys(uint32_t og, uint32_t oe, uint32_t lo
     hi_key = (int64_t)oe - tp + 1;
 }
 
+// 65-ary search by one wave: every step probes 64 evenly spaced rows at once
+// and keeps the gap the key falls in, so a lower_bound over 1e8 rows takes
+// 5 dependent memory round trips instead of 27.  Wave-uniform result.
+__device__ __forceinline__ int64_t wave_lower_bound(const uint32_t *__restrict__ a, int64_t n,
+                                                    int64_t key) {
+    int64_t lo = 0, hi = n;  // answer in [lo, hi]
+    const int lane = dev::lane_id();
+    while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 64) / 65;  // probes lo + step*(l+1) - 1, l < 64
+        const int64_t idx = lo + step * (lane + 1) - 1;
+        const bool less = idx < hi && (int64_t)a[idx] < key;
+        const uint64_t m = __ballot(less);
+        const int c = __popcll(m);  // probes below key (a prefix, a is sorted)
+        const int64_t nlo = c == 0 ? lo : lo + step * c;
+        const int64_t nhi = c == 64 ? hi : min(hi, lo + step * (c + 1) - 1);
+        lo = nlo;
+        hi = nhi;
+    }
+    // final: at most 64 candidates [lo, hi)
+    const int64_t idx = lo + lane;
+    const bool less = idx < hi && (int64_t)a[idx] < key;
+    return lo + __popcll(__ballot(less));
+}
+
 __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64_t ntiles,
                                                 uint32_t *__restrict__ win) {
     const int64_t t = (int64_t)blockIdx.x * (IB / 64) + threadIdx.x / 64;
@@ -89,8 +113,12 @@ __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64
     // (subtract walks back from it even when the owner's range is empty)
     const int64_t lkey_last = (int64_t)sa.ogs[o1 - 1] + sa.lo_off;
     if (hmax < lkey_last) hmax = lkey_last;
-    if (lane == 0) win[2 * (sa.tile0 + t)] = (uint32_t)dev::lower_bound(sa.pgs, 0, sa.np, lkey);
-    if (lane == 1) win[2 * (sa.tile0 + t) + 1] = (uint32_t)dev::lower_bound(sa.pgs, 0, sa.np, hmax);
+    const int64_t lo = wave_lower_bound(sa.pgs, sa.np, lkey);
+    const int64_t hi = wave_lower_bound(sa.pgs, sa.np, hmax);
+    if (lane == 0) {
+        win[2 * (sa.tile0 + t)] = (uint32_t)lo;
+        win[2 * (sa.tile0 + t) + 1] = (uint32_t)hi;
+    }
 }
 
 template <bool FILTER>
@@ -164,6 +192,7 @@ struct FillArgs {
     StreamArgs s[2];
     const uint32_t *olo, *ocnt;
     const uint64_t *toff;
+    const uint32_t *win;   // per tile partner window [lo, hi)
     int64_t ntiles;
     const uint32_t *off;
     int32_t n_contigs;
@@ -172,13 +201,29 @@ struct FillArgs {
     uint64_t *cksum;       // [sum, xor] when checksumming instead of writing
 };
 
+constexpr int FB = 512;           // fill workgroup: 8 waves
+constexpr int FW = FB / 64;
+constexpr int FOPT = OT / FB;     // owners per thread when staging a tile
+constexpr int PCAP = 2048;        // LDS partner window (16 B records)
+
+// One workgroup writes the SBLK consecutive output records of its slice of
+// the output index space.  Per owner tile it touches it stages, in LDS,
+//   s_lo_off[q] = (lo_q, off_q)   partner range start, exclusive output offset
+//   s_own[q]    = (gs, ge, row, contig offset) of the owner
+//   s_par[i]    = (gs, ge, row) of partner wlo + i   (the tile's window)
+// then splits its output range into one contiguous chunk per wave; lane l of
+// a wave handles outputs base + l + 64 k, so an owner switch happens about
+// once per 82/64 iterations (C2) and is a single LDS compare, and every
+// iteration is 1 b64 + 2 b128 LDS reads and ONE 16-B store per lane, the
+// wave's 64 stores forming one contiguous 1-KiB segment.
 template <bool CKSUM>
-__global__ __launch_bounds__(IB) void k_fill(FillArgs fa) {
-    __shared__ uint32_t s_off[OT + 1];
-    __shared__ uint32_t s_lo[OT], s_gs[OT], s_ge[OT], s_row[OT], s_seg[OT];
-    __shared__ uint32_t scratch[IB / 64 + 1];
+__global__ __launch_bounds__(FB) void k_fill(FillArgs fa) {
+    __shared__ uint2 s_lo_off[OT + 1];
+    __shared__ u32x4 s_own[OT];
+    __shared__ u32x4 s_par[PCAP];
+    __shared__ uint32_t scratch[FW + 1];
     __shared__ int64_t s_tile;
-    __shared__ uint64_t s_red[2][IB / 64];
+    __shared__ uint64_t s_red[2][FW];
 
     const int64_t g0 = fa.first / SBLK;
     const int64_t ob = max(fa.first, (g0 + blockIdx.x) * SBLK);
@@ -186,68 +231,90 @@ __global__ __launch_bounds__(IB) void k_fill(FillArgs fa) {
     if (ob >= oend) return;
     if (threadIdx.x == 0) s_tile = dev::upper_bound(fa.toff, 0, fa.ntiles, (uint64_t)ob) - 1;
     __syncthreads();
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
     int64_t t = s_tile;
     uint64_t hsum = 0, hxor = 0;
     while (t < fa.ntiles && (int64_t)fa.toff[t] < oend) {
         const int st = t < fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT ? 0 : 1;
         const StreamArgs sa = st ? fa.s[1] : fa.s[0];
-        const int64_t lt = t - sa.tile0;
-        const int64_t o0 = lt * OT;
+        const int64_t o0 = (t - sa.tile0) * OT;
         const int nown = (int)min((int64_t)OT, sa.no - o0);
         const int64_t tbase = (int64_t)fa.toff[t];
-        // ---- stage the tile's owners (blocked: thread i owns owners i*OPT..)
-        uint32_t c[OPT];
+        // ---- owners: counts -> exclusive offsets (blocked, FOPT per thread)
+        uint32_t c[FOPT];
         uint32_t csum = 0;
 #pragma unroll
-        for (int k = 0; k < OPT; ++k) {
-            const int q = threadIdx.x * OPT + k;
+        for (int k = 0; k < FOPT; ++k) {
+            const int q = threadIdx.x * FOPT + k;
             c[k] = q < nown ? fa.ocnt[sa.owner0 + o0 + q] : 0u;
             csum += c[k];
         }
         uint32_t ttot;
-        uint32_t run = dev::block_exclusive_sum<IB>(csum, scratch, &ttot);
-#pragma unroll
-        for (int k = 0; k < OPT; ++k) {
-            s_off[threadIdx.x * OPT + k] = run;
-            run += c[k];
-        }
-        if (threadIdx.x == 0) s_off[OT] = ttot;
+        uint32_t run = dev::block_exclusive_sum<FB>(csum, scratch, &ttot);
         const uint32_t seg_first = contig_off(fa.off, fa.n_contigs, sa.ogs[o0]);
         const uint32_t seg_last = contig_off(fa.off, fa.n_contigs, sa.ogs[o0 + nown - 1]);
-        for (int q = threadIdx.x; q < nown; q += IB) {
-            const int64_t j = o0 + q;
-            s_lo[q] = fa.olo[sa.owner0 + j];
-            const uint32_t og = sa.ogs[j];
-            s_gs[q] = og;
-            s_ge[q] = sa.oge[j];
-            s_row[q] = sa.orow[j];
-            s_seg[q] = seg_first == seg_last ? seg_first : contig_off(fa.off, fa.n_contigs, og);
+#pragma unroll
+        for (int k = 0; k < FOPT; ++k) {
+            const int q = threadIdx.x * FOPT + k;
+            uint32_t lo = 0;
+            if (q < nown) {
+                const int64_t j = o0 + q;
+                lo = fa.olo[sa.owner0 + j];
+                const uint32_t og = sa.ogs[j];
+                const uint32_t sg =
+                    seg_first == seg_last ? seg_first : contig_off(fa.off, fa.n_contigs, og);
+                s_own[q] = u32x4{og, sa.oge[j], sa.orow[j], sg};
+            }
+            s_lo_off[q] = make_uint2(lo, run);
+            run += c[k];
         }
-        for (int q = nown + threadIdx.x; q < OT; q += IB) s_off[q] = ttot;  // padding owners
+        if (threadIdx.x == 0) s_lo_off[OT] = make_uint2(0u, ttot);
+        // ---- partner window
+        const uint32_t wlo = fa.win[2 * t], whi = fa.win[2 * t + 1];
+        const bool par_lds = (int64_t)whi - wlo <= PCAP;
+        if (par_lds)
+            for (int i = threadIdx.x; i < (int)(whi - wlo); i += FB)
+                s_par[i] = u32x4{sa.pgs[wlo + i], sa.pge[wlo + i], sa.prow[wlo + i], 0u};
         __syncthreads();
-        // ---- expand this tile's slice of the output window
+        // ---- this tile's slice of the output window, one chunk per wave
         const int64_t lb = max(ob - tbase, (int64_t)0);
         const int64_t le = min(oend - tbase, (int64_t)ttot);
-        int64_t o = lb + threadIdx.x;
-        if (o < le) {
-            // owner of o: largest q with s_off[q] <= o
-            int q = (int)dev::upper_bound(s_off, 0, (int64_t)nown, (uint32_t)o) - 1;
-            for (; o < le; o += IB) {
-                while (s_off[q + 1] <= (uint32_t)o) ++q;
-                const uint32_t p = s_lo[q] + ((uint32_t)o - s_off[q]);
-                const uint32_t pg = sa.pgs[p], pe = sa.pge[p], pr = sa.prow[p];
-                const uint32_t og = s_gs[q], oe = s_ge[q], orow = s_row[q], sg = s_seg[q];
-                const uint32_t rs = (og > pg ? og : pg) - sg;
-                const uint32_t re = (oe < pe ? oe : pe) - sg;
-                const uint32_t ar = st == 0 ? orow : pr;
-                const uint32_t br = st == 0 ? pr : orow;
+        const int64_t per = ((le - lb + FW - 1) / FW + 63) & ~(int64_t)63;
+        const int64_t wb = lb + w * per;
+        const int64_t we = min(le, wb + per);
+        int64_t o = wb + lane;
+        if (wb < we) {
+            // owner of the wave's first output (largest q with off_q <= o)
+            int lo_q = 0, hi_q = nown;
+            const uint32_t key = (uint32_t)min(o, we - 1);
+            while (lo_q < hi_q) {
+                int mid = (lo_q + hi_q) >> 1;
+                if (s_lo_off[mid].y <= key)
+                    lo_q = mid + 1;
+                else
+                    hi_q = mid;
+            }
+            int q = lo_q - 1;
+            for (; o < we; o += 64) {
+                while (s_lo_off[q + 1].y <= (uint32_t)o) ++q;
+                const uint2 lof = s_lo_off[q];
+                const uint32_t p = lof.x + ((uint32_t)o - lof.y);
+                const u32x4 ow = s_own[q];
+                u32x4 pa;
+                if (par_lds)
+                    pa = s_par[p - wlo];
+                else
+                    pa = u32x4{sa.pgs[p], sa.pge[p], sa.prow[p], 0u};
+                const uint32_t rs = (ow.x > pa.x ? ow.x : pa.x) - ow.w;
+                const uint32_t re = (ow.y < pa.y ? ow.y : pa.y) - ow.w;
+                const uint32_t ar = st == 0 ? ow.z : pa.z;
+                const uint32_t br = st == 0 ? pa.z : ow.z;
                 if (CKSUM) {
                     uint64_t h = dev::pair_hash(rs, re, ar, br);
                     hsum += h;
                     hxor ^= h;
                 } else {
-                    u32x4 v = {rs, re, ar, br};
-                    __builtin_nontemporal_store(v, fa.out + (tbase + o - fa.first));
+                    fa.out[tbase + o - fa.first] = u32x4{rs, re, ar, br};
                 }
             }
         }
@@ -259,14 +326,14 @@ __global__ __launch_bounds__(IB) void k_fill(FillArgs fa) {
         uint64_t x = hxor;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
-        if (dev::lane_id() == 0) {
-            s_red[0][threadIdx.x / 64] = hsum;
-            s_red[1][threadIdx.x / 64] = x;
+        if (lane == 0) {
+            s_red[0][w] = hsum;
+            s_red[1][w] = x;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
             uint64_t a = 0, b = 0;
-            for (int i = 0; i < IB / 64; ++i) {
+            for (int i = 0; i < FW; ++i) {
                 a += s_red[0][i];
                 b ^= s_red[1][i];
             }
@@ -382,6 +449,7 @@ FillArgs fill_args(PairsPlan *pl) {
     fa.olo = pl->olo;
     fa.ocnt = pl->ocnt;
     fa.toff = pl->toff;
+    fa.win = pl->win;
     fa.ntiles = pl->nt0 + pl->nt1;
     fa.off = pl->A->d_off;
     fa.n_contigs = pl->A->n_contigs;
@@ -414,9 +482,9 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
         const int64_t grid = g1 - g0;
         if (grid > 0x7fffffff) return fail(LIME_ERR_OVERFLOW, "fill window too large");
         if (cksum)
-            hipLaunchKernelGGL(k_fill<true>, dim3((unsigned)grid), dim3(IB), 0, S(ctx), fa);
+            hipLaunchKernelGGL(k_fill<true>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa);
         else
-            hipLaunchKernelGGL(k_fill<false>, dim3((unsigned)grid), dim3(IB), 0, S(ctx), fa);
+            hipLaunchKernelGGL(k_fill<false>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa);
     }
     LIME_HIP(hipGetLastError());
     return LIME_OK;

@@ -15,20 +15,23 @@
 //
 // Passes: an optional 1-bit pass on (ge > gs) when the set holds zero-width
 // intervals (LSD: least-significant digit first), then ceil(bits(max gs)/8)
-// 8-bit digit passes.  Each pass = per-tile digit histogram, one exclusive
-// scan over the digit-major count matrix, and a stable scatter that ranks
-// items with wave ballots, stages the tile in LDS in digit order and writes
-// each digit's run contiguously.
+// 8-bit digit passes.  A pass = per-tile digit histogram, one exclusive scan
+// over the digit-major count matrix, and a stable scatter that ranks items
+// with wave ballots, stages the 8192-row tile in LDS in digit order and
+// writes each digit's run contiguously (32 rows = 128 B per array and digit
+// on average: whole L2 lines).  The first histogram is fused into the prep
+// kernel that builds gs / ge / row from the caller's (contig, start, end).
 #include "common.hpp"
 
 namespace lime {
 namespace {
 
-constexpr int RB = 256;
-constexpr int RITEMS = 16;
-constexpr int RTILE = RB * RITEMS;  // 4096 items per tile
+constexpr int RB = 1024;
+constexpr int RITEMS = 8;
+constexpr int RTILE = RB * RITEMS;  // 8192 items per tile
 constexpr int RBINS = 256;
-constexpr int RWAVES = RB / 64;
+constexpr int RWAVES = RB / 64;     // 16
+constexpr int WITEMS = RTILE / RWAVES;  // 512 consecutive rows per wave
 
 struct SetStats {
     uint32_t err;        // bit0 contig out of range, bit1 end < start, bit2 end > contig length
@@ -37,62 +40,8 @@ struct SetStats {
     uint32_t max_width;
     uint32_t has_zero;
     uint32_t unsorted;
+    uint32_t pad[2];
 };
-
-__global__ __launch_bounds__(256) void k_prep(const int32_t *__restrict__ contig,
-                                              const uint32_t *__restrict__ start,
-                                              const uint32_t *__restrict__ end,
-                                              const uint32_t *__restrict__ off,
-                                              const uint32_t *__restrict__ len, int32_t n_contigs,
-                                              int64_t n, uint32_t *__restrict__ gs,
-                                              uint32_t *__restrict__ ge, uint32_t *__restrict__ row,
-                                              SetStats *st) {
-    uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int32_t c = contig[i];
-        uint32_t s = start[i], e = end[i];
-        uint32_t g0 = 0, g1 = 0;
-        if (c < 0 || c >= n_contigs) {
-            err |= 1u;
-        } else {
-            if (e < s) err |= 2u;
-            if (e > len[c]) err |= 4u;
-            g0 = off[c] + s;
-            g1 = off[c] + e;
-        }
-        gs[i] = g0;
-        ge[i] = g1;
-        row[i] = (uint32_t)i;
-        mx = g0 > mx ? g0 : mx;
-        uint32_t w = g1 - g0;
-        mnw = w < mnw ? w : mnw;
-        mxw = w > mxw ? w : mxw;
-        zero |= (w == 0);
-        if (i > 0) {  // canonical-order check against the previous row
-            int32_t pc = contig[i - 1];
-            if (pc >= 0 && pc < n_contigs && c >= 0 && c < n_contigs) {
-                uint32_t p0 = off[pc] + start[i - 1], p1 = off[pc] + end[i - 1];
-                bool pnz = p1 > p0, nz = g1 > g0;
-                if (p0 > g0 || (p0 == g0 && pnz && !nz)) uns = 1;
-            }
-        }
-    }
-    err = dev::wave_reduce_or(err);
-    mx = dev::wave_reduce_max(mx);
-    mnw = dev::wave_reduce_min(mnw);
-    mxw = dev::wave_reduce_max(mxw);
-    zero = dev::wave_reduce_or(zero);
-    uns = dev::wave_reduce_or(uns);
-    if (dev::lane_id() == 0) {
-        if (err) atomicOr(&st->err, err);
-        atomicMax(&st->max_gs, mx);
-        atomicMin(&st->min_width, mnw);
-        atomicMax(&st->max_width, mxw);
-        if (zero) atomicOr(&st->has_zero, 1u);
-        if (uns) atomicOr(&st->unsorted, 1u);
-    }
-}
 
 // digit of an item: 8-bit digit of gs, or the zero-width bit (0 = zero width)
 template <bool NZ>
@@ -118,31 +67,163 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return m;
 }
 
+// per-wave digit histogram of this wave's rows into hist[w][*]
 template <bool NZ>
-__global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
-                                             const uint32_t *__restrict__ ge, int64_t n, int shift,
-                                             uint32_t *__restrict__ counts, uint32_t ntiles) {
-    __shared__ uint32_t hist[RWAVES][RBINS];
-    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
-    __syncthreads();
-    const int w = threadIdx.x / 64, lane = dev::lane_id();
-    const int64_t base = (int64_t)blockIdx.x * RTILE + w * (RTILE / RWAVES);
-#pragma unroll 4
+__device__ __forceinline__ void wave_hist(uint32_t (*hist)[RBINS], int w, const uint32_t *vk,
+                                          const uint32_t *ve, const bool *valid, int shift) {
+#pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        int64_t i = base + k * 64 + lane;
-        bool valid = i < n;
-        uint32_t d = 0;
-        if (valid) d = digit_of<NZ>(key[i], NZ ? ge[i] : 0u, shift);
-        uint64_t m = match_digit<NZ>(d, valid);
-        if (valid && (m & dev::lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
+        uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
+        uint64_t m = match_digit<NZ>(d, valid[k]);
+        if (valid[k] && (m & dev::lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
     }
-    __syncthreads();
+}
+
+__device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *counts,
+                                           uint32_t ntiles) {
     for (int d = threadIdx.x; d < RBINS; d += RB) {
         uint32_t t = 0;
 #pragma unroll
         for (int ww = 0; ww < RWAVES; ++ww) t += hist[ww][d];
         counts[(int64_t)d * ntiles + blockIdx.x] = t;
     }
+}
+
+// Build gs / ge / row from (contig, start, end), validate, gather statistics
+// (per-tile partials, reduced by k_stats) and the digit-0 histogram.
+__global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
+                                             const uint32_t *__restrict__ start,
+                                             const uint32_t *__restrict__ end,
+                                             const uint32_t *__restrict__ off,
+                                             const uint32_t *__restrict__ len, int32_t n_contigs,
+                                             int64_t n, uint32_t *__restrict__ gs,
+                                             uint32_t *__restrict__ ge, uint32_t *__restrict__ row,
+                                             SetStats *__restrict__ part,
+                                             uint32_t *__restrict__ counts, uint32_t ntiles) {
+    __shared__ uint32_t hist[RWAVES][RBINS];
+    __shared__ SetStats ws[RWAVES];
+    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
+    uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
+    uint32_t vk[RITEMS], ve[RITEMS];
+    bool valid[RITEMS];
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k) {
+        const int64_t i = base + k * 64 + lane;
+        valid[k] = i < n;
+        uint32_t g0 = 0, g1 = 0;
+        if (valid[k]) {
+            const int32_t c = contig[i];
+            const uint32_t s = start[i], e = end[i];
+            if (c < 0 || c >= n_contigs) {
+                err |= 1u;
+            } else {
+                if (e < s) err |= 2u;
+                if (e > len[c]) err |= 4u;
+                g0 = off[c] + s;
+                g1 = off[c] + e;
+            }
+            gs[i] = g0;
+            ge[i] = g1;
+            row[i] = (uint32_t)i;
+            mx = g0 > mx ? g0 : mx;
+            const uint32_t wd = g1 - g0;
+            mnw = wd < mnw ? wd : mnw;
+            mxw = wd > mxw ? wd : mxw;
+            zero |= (wd == 0);
+            if (i > 0) {  // canonical-order check against the previous row
+                const int32_t pc = contig[i - 1];
+                if (pc >= 0 && pc < n_contigs && c >= 0 && c < n_contigs) {
+                    const uint32_t p0 = off[pc] + start[i - 1], p1 = off[pc] + end[i - 1];
+                    if (p0 > g0 || (p0 == g0 && p1 > p0 && g1 == g0)) uns = 1;
+                }
+            }
+        }
+        vk[k] = g0;
+        ve[k] = g1;
+    }
+    __syncthreads();
+    wave_hist<false>(hist, w, vk, ve, valid, 0);
+    err = dev::wave_reduce_or(err);
+    mx = dev::wave_reduce_max(mx);
+    mnw = dev::wave_reduce_min(mnw);
+    mxw = dev::wave_reduce_max(mxw);
+    zero = dev::wave_reduce_or(zero);
+    uns = dev::wave_reduce_or(uns);
+    if (lane == 0) ws[w] = SetStats{err, mx, mnw, mxw, zero, uns, {0, 0}};
+    __syncthreads();
+    flush_hist(hist, counts, ntiles);
+    if (threadIdx.x == 0) {
+        SetStats s = ws[0];
+        for (int i = 1; i < RWAVES; ++i) {
+            s.err |= ws[i].err;
+            s.max_gs = max(s.max_gs, ws[i].max_gs);
+            s.min_width = min(s.min_width, ws[i].min_width);
+            s.max_width = max(s.max_width, ws[i].max_width);
+            s.has_zero |= ws[i].has_zero;
+            s.unsorted |= ws[i].unsorted;
+        }
+        part[blockIdx.x] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_stats(const SetStats *__restrict__ part, int64_t m,
+                                               SetStats *out) {
+    uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
+    for (int64_t i = threadIdx.x; i < m; i += 256) {
+        const SetStats s = part[i];
+        err |= s.err;
+        mx = max(mx, s.max_gs);
+        mnw = min(mnw, s.min_width);
+        mxw = max(mxw, s.max_width);
+        zero |= s.has_zero;
+        uns |= s.unsorted;
+    }
+    __shared__ SetStats ws[4];
+    err = dev::wave_reduce_or(err);
+    mx = dev::wave_reduce_max(mx);
+    mnw = dev::wave_reduce_min(mnw);
+    mxw = dev::wave_reduce_max(mxw);
+    zero = dev::wave_reduce_or(zero);
+    uns = dev::wave_reduce_or(uns);
+    if (dev::lane_id() == 0) ws[threadIdx.x / 64] = SetStats{err, mx, mnw, mxw, zero, uns, {0, 0}};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SetStats s = ws[0];
+        for (int i = 1; i < 4; ++i) {
+            s.err |= ws[i].err;
+            s.max_gs = max(s.max_gs, ws[i].max_gs);
+            s.min_width = min(s.min_width, ws[i].min_width);
+            s.max_width = max(s.max_width, ws[i].max_width);
+            s.has_zero |= ws[i].has_zero;
+            s.unsorted |= ws[i].unsorted;
+        }
+        *out = s;
+    }
+}
+
+template <bool NZ>
+__global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
+                                             const uint32_t *__restrict__ ge, int64_t n, int shift,
+                                             uint32_t *__restrict__ counts, uint32_t ntiles) {
+    __shared__ uint32_t hist[RWAVES][RBINS];
+    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
+    uint32_t vk[RITEMS], ve[RITEMS];
+    bool valid[RITEMS];
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k) {
+        const int64_t i = base + k * 64 + lane;
+        valid[k] = i < n;
+        vk[k] = valid[k] ? key[i] : 0u;
+        ve[k] = (NZ && valid[k]) ? ge[i] : 0u;
+    }
+    __syncthreads();
+    wave_hist<NZ>(hist, w, vk, ve, valid, shift);
+    __syncthreads();
+    flush_hist(hist, counts, ntiles);
 }
 
 template <bool NZ>
@@ -160,60 +241,58 @@ __global__ __launch_bounds__(RB) void k_scatter(const uint32_t *__restrict__ key
     __shared__ uint32_t sk[RTILE], se[RTILE], sr[RTILE];
 
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
-    __syncthreads();
 
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t tile0 = (int64_t)blockIdx.x * RTILE;
-    const int64_t base = tile0 + w * (RTILE / RWAVES);
+    const int64_t base = tile0 + w * WITEMS;
     uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS], pos[RITEMS], dg[RITEMS];
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        int64_t i = base + k * 64 + lane;
-        bool valid = i < n;
+        const int64_t i = base + k * 64 + lane;
+        const bool valid = i < n;
         vk[k] = valid ? key_in[i] : 0u;
         ve[k] = valid ? ge_in[i] : 0u;
         vr[k] = valid ? row_in[i] : 0u;
     }
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        int64_t i = base + k * 64 + lane;
-        bool valid = i < n;
-        uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
+        const int64_t i = base + k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
         dg[k] = d;
-        uint64_t m = match_digit<NZ>(d, valid);
-        uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
-        uint32_t old = valid ? cnt[w][d] : 0u;
+        const uint64_t m = match_digit<NZ>(d, valid);
+        const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
+        const uint32_t old = valid ? cnt[w][d] : 0u;
         pos[k] = old + rank;
         if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(m);
     }
     __syncthreads();
     // per digit: block offset of the digit, then per-wave offsets
     {
-        const int d = threadIdx.x;  // RB == RBINS
-        uint32_t c[RWAVES];
+        const int d = threadIdx.x;
         uint32_t tot = 0;
-#pragma unroll
-        for (int ww = 0; ww < RWAVES; ++ww) {
-            c[ww] = cnt[ww][d];
-            tot += c[ww];
-        }
+        if (d < RBINS)
+            for (int ww = 0; ww < RWAVES; ++ww) tot += cnt[ww][d];
         uint32_t all;
-        uint32_t ds = dev::block_exclusive_sum<RB>(tot, scratch, &all);
-        dstart[d] = ds;
-        uint32_t run = ds;
-#pragma unroll
-        for (int ww = 0; ww < RWAVES; ++ww) {
-            cnt[ww][d] = run;
-            run += c[ww];
+        const uint32_t ds = dev::block_exclusive_sum<RB>(tot, scratch, &all);
+        if (d < RBINS) {
+            dstart[d] = ds;
+            uint32_t run = ds;
+            for (int ww = 0; ww < RWAVES; ++ww) {
+                const uint32_t c = cnt[ww][d];
+                cnt[ww][d] = run;
+                run += c;
+            }
+            gbase[d] = base_mat[(int64_t)d * ntiles + blockIdx.x];
         }
-        gbase[d] = base_mat[(int64_t)d * ntiles + blockIdx.x];
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        int64_t i = base + k * 64 + lane;
+        const int64_t i = base + k * 64 + lane;
         if (i < n) {
-            uint32_t lp = cnt[w][dg[k]] + pos[k];
+            const uint32_t lp = cnt[w][dg[k]] + pos[k];
             sk[lp] = vk[k];
             se[lp] = ve[k];
             sr[lp] = vr[k];
@@ -223,25 +302,27 @@ __global__ __launch_bounds__(RB) void k_scatter(const uint32_t *__restrict__ key
     const int64_t rem = n - tile0;
     const int count = rem < RTILE ? (int)rem : RTILE;
     for (int j = threadIdx.x; j < count; j += RB) {
-        uint32_t k = sk[j], e = se[j];
-        uint32_t d = digit_of<NZ>(k, e, shift);
-        uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
+        const uint32_t k = sk[j], e = se[j];
+        const uint32_t d = digit_of<NZ>(k, e, shift);
+        const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
         key_out[g] = k;
         ge_out[g] = e;
         row_out[g] = sr[j];
     }
 }
 
-int radix_pass(lime_ctx *ctx, bool nz, int shift, int64_t n, const uint32_t *k0, const uint32_t *e0,
-               const uint32_t *r0, uint32_t *k1, uint32_t *e1, uint32_t *r1, uint32_t *mat,
-               uint32_t ntiles) {
-    if (nz)
-        hipLaunchKernelGGL(k_hist<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift, mat,
-                           ntiles);
-    else
-        hipLaunchKernelGGL(k_hist<false>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift,
-                           mat, ntiles);
-    LIME_HIP(hipGetLastError());
+int radix_pass(lime_ctx *ctx, bool nz, int shift, bool have_hist, int64_t n, const uint32_t *k0,
+               const uint32_t *e0, const uint32_t *r0, uint32_t *k1, uint32_t *e1, uint32_t *r1,
+               uint32_t *mat, uint32_t ntiles) {
+    if (!have_hist) {
+        if (nz)
+            hipLaunchKernelGGL(k_hist<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift,
+                               mat, ntiles);
+        else
+            hipLaunchKernelGGL(k_hist<false>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift,
+                               mat, ntiles);
+        LIME_HIP(hipGetLastError());
+    }
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr));
     if (nz)
         hipLaunchKernelGGL(k_scatter<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n,
@@ -258,28 +339,32 @@ int radix_pass(lime_ctx *ctx, bool nz, int shift, int64_t n, const uint32_t *k0,
 int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32_t *d_start,
              const uint32_t *d_end, const uint32_t *d_len) {
     const int64_t n = set->n;
-    uint32_t *k0, *e0, *r0;
+    const uint32_t ntiles = (uint32_t)((n + RTILE - 1) / RTILE);
+    uint32_t *k0, *e0, *r0, *mat;
+    SetStats *part, *st;
     LIME_TRY(alloc(ctx, &k0, (size_t)n));
     LIME_TRY(alloc(ctx, &e0, (size_t)n));
     LIME_TRY(alloc(ctx, &r0, (size_t)n));
-    SetStats *st;
+    LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * (ntiles ? ntiles : 1)));
+    LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &st, 1));
-    SetStats init = {0u, 0u, 0xffffffffu, 0u, 0u, 0u};
-    LIME_HIP(hipMemcpyAsync(st, &init, sizeof(init), hipMemcpyHostToDevice, S(ctx)));
+    SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
     if (n > 0) {
-        unsigned grid = blocks_for(n, 256);
-        if (grid > 8192) grid = 8192;
-        hipLaunchKernelGGL(k_prep, dim3(grid), dim3(256), 0, S(ctx), d_contig, d_start, d_end,
-                           (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0, e0, r0, st);
+        hipLaunchKernelGGL(k_prep, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start, d_end,
+                           (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0, e0, r0,
+                           part, mat, ntiles);
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
+                           (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());
+        LIME_TRY(read_back(ctx, &h, st, sizeof(h)));
     }
-    SetStats h;
-    LIME_TRY(read_back(ctx, &h, st, sizeof(h)));
+    release(ctx, part);
     release(ctx, st);
     if (h.err) {
         release(ctx, k0);
         release(ctx, e0);
         release(ctx, r0);
+        release(ctx, mat);
         if (h.err & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
         if (h.err & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
         return fail(LIME_ERR_RANGE, "interval end beyond its contig length");
@@ -289,18 +374,20 @@ int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32
     set->has_zero_width = h.has_zero != 0;
 
     if (n > 1 && h.unsorted) {
-        const uint32_t ntiles = (uint32_t)((n + RTILE - 1) / RTILE);
-        uint32_t *k1, *e1, *r1, *mat;
+        uint32_t *k1, *e1, *r1;
         LIME_TRY(alloc(ctx, &k1, (size_t)n));
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
         LIME_TRY(alloc(ctx, &r1, (size_t)n));
-        LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * ntiles));
-        int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
+        const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
         std::vector<std::pair<bool, int>> passes;
         if (set->has_zero_width) passes.push_back({true, 0});
         for (int sh = 0; sh < bits; sh += 8) passes.push_back({false, sh});
+        // k_prep already histogrammed digit 0 of the prep layout
+        bool have = !set->has_zero_width;
         for (auto &p : passes) {
-            LIME_TRY(radix_pass(ctx, p.first, p.second, n, k0, e0, r0, k1, e1, r1, mat, ntiles));
+            LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, k1, e1, r1, mat,
+                                ntiles));
+            have = false;
             std::swap(k0, k1);
             std::swap(e0, e1);
             std::swap(r0, r1);
@@ -308,8 +395,8 @@ int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32
         release(ctx, k1);
         release(ctx, e1);
         release(ctx, r1);
-        release(ctx, mat);
     }
+    release(ctx, mat);
     set->gs = k0;
     set->ge = e0;
     set->row = r0;

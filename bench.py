@@ -136,20 +136,38 @@ def main():
         e.record(stream)
         return e
 
+    def fill_all(plan, halos=None):
+        for f in range(0, plan.n, args.chunk):
+            k = min(args.chunk, plan.n - f)
+            e0 = ev()
+            plan.fill_device(f, k, buf.data_ptr())
+            fills.append((e0, ev(), k, plan.n))
+
+    shard = None
+    if world > 1:
+        from lime_amd.sharded import ShardStep
+        # rank r owns the r-th copy of the genome on one virtual coordinate
+        # line: offset r * span; boundary exchange + merge carry over RCCL
+        shard = ShardStep(ctx, space, offset=rank * space.span, comm_device=dev)
+
     def step(phases=None):
         t = [ev()] if phases is not None else None
         A = ctx.set_from_device(space, n, *(x.data_ptr() for x in A_in))
         B = ctx.set_from_device(space, n, *(x.data_ptr() for x in B_in))
         if t is not None:
             t.append(ev())
+        if shard is not None:
+            out = shard.run(A, B, on_pairs=fill_all)
+            for h in (out["merge_a"], out["merge_b"], A, B):
+                h.close()
+            if t is not None:
+                t += [ev(), ev(), ev()]
+                phases.append(t)
+            return out["pairs"], out["runs_a"] + out["runs_b"]
         plan = ctx.intersect(A, B)
         if t is not None:
             t.append(ev())
-        for f in range(0, plan.n, args.chunk):
-            k = min(args.chunk, plan.n - f)
-            e0 = ev()
-            plan.fill_device(f, k, buf.data_ptr())
-            fills.append((e0, ev(), k, plan.n))
+        fill_all(plan)
         if t is not None:
             t.append(ev())
         ma, mb = ctx.merge(A), ctx.merge(B)
@@ -191,8 +209,13 @@ def main():
     avg_b = sum(fill_bytes) / len(fill_bytes)
     achieved = avg_b / (avg_ms * 1e-3) / 1e9
     p = phases[-1]
-    breakdown = {"sort_ms": p[0].elapsed_time(p[1]), "count_ms": p[1].elapsed_time(p[2]),
-                 "fill_ms": p[2].elapsed_time(p[3]), "merge_ms": p[3].elapsed_time(p[4])}
+    if world > 1:
+        breakdown = {"sort_ms": p[0].elapsed_time(p[1]),
+                     "merge_halo_intersect_fill_carry_ms": p[1].elapsed_time(p[2]),
+                     "fill_ms": sum(fill_ms[-(-npairs // args.chunk):])}
+    else:
+        breakdown = {"sort_ms": p[0].elapsed_time(p[1]), "count_ms": p[1].elapsed_time(p[2]),
+                     "fill_ms": p[2].elapsed_time(p[3]), "merge_ms": p[3].elapsed_time(p[4])}
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "fill_pmc.json")

@@ -108,8 +108,20 @@ int lime_set_create_host(lime_ctx *ctx, const lime_space *space, int64_t n, cons
 int lime_set_create_device(lime_ctx *ctx, const lime_space *space, int64_t n,
                            const int32_t *d_contig, const uint32_t *d_start,
                            const uint32_t *d_end, lime_set **out);
+/* Device arrays already in the space's GLOBAL coordinates (gstart, gend) with
+ * caller-chosen row ids -- e.g. a coordinate shard's own sorted rows followed
+ * by its halo.  Validated (gend >= gstart, inside the span) and sorted only if
+ * not already in canonical order. */
+int lime_set_create_global(lime_ctx *ctx, const lime_space *space, int64_t n,
+                           const uint32_t *d_gstart, const uint32_t *d_gend,
+                           const uint32_t *d_row, lime_set **out);
 int lime_set_destroy(lime_set *set);
 int64_t lime_set_size(const lime_set *set);
+/* first sorted row with gstart >= gkey (-1 on error) */
+int64_t lime_set_lower_bound(const lime_set *set, uint32_t gkey);
+/* device-to-device copy of sorted rows [first, first + count) */
+int lime_set_copy_rows_device(const lime_set *set, int64_t first, int64_t count, uint32_t *d_gstart,
+                              uint32_t *d_gend, uint32_t *d_row);
 /* Device pointers of the sorted set: global start, global end, input row. */
 int lime_set_device_arrays(const lime_set *set, const uint32_t **gstart, const uint32_t **gend,
                            const uint32_t **row);
@@ -155,6 +167,9 @@ int lime_result_fill_host(const lime_result *res, int32_t *contig, int64_t *star
 int lime_result_run_of_row(const lime_result *res, int64_t *run_of_row);
 int lime_result_device_arrays(const lime_result *res, const uint32_t **gstart,
                               const uint32_t **gend);
+/* host copy of regions [first, first + count) in global coordinates */
+int lime_result_copy_range(const lime_result *res, int64_t first, int64_t count, uint32_t *gstart,
+                           uint32_t *gend);
 int lime_result_destroy(lime_result *res);
 
 /* ----------------------------------------------------- bit-per-base path */

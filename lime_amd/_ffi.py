@@ -58,8 +58,12 @@ SIGNATURES = {
     "lime_space_offset": (i64, [vp, i32]),
     "lime_set_create_host": (C.c_int, [vp, vp, i64, P(i32), P(i64), P(i64), pp]),
     "lime_set_create_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
+    "lime_set_create_global": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_set_destroy": (C.c_int, [vp]),
     "lime_set_size": (i64, [vp]),
+    "lime_set_lower_bound": (i64, [vp, u32]),
+    "lime_set_copy_rows_device": (C.c_int, [vp, i64, i64, vp, vp, vp]),
+    "lime_result_copy_range": (C.c_int, [vp, i64, i64, P(u32), P(u32)]),
     "lime_set_device_arrays": (C.c_int, [vp, pp, pp, pp]),
     "lime_set_fill_host": (C.c_int, [vp, P(i32), P(i64), P(i64), P(i64)]),
     "lime_intersect_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),

@@ -85,6 +85,13 @@ int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t n, uint64_t see
           uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig, uint32_t *d_start,
           uint32_t *d_end);
 
+int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const uint32_t *d_ge,
+                    const uint32_t *d_row, const uint32_t *d_len);
+
+__global__ void k_set_lower_bound(const uint32_t *gs, int64_t n, uint32_t key, int64_t *out) {
+    if (threadIdx.x == 0) *out = dev::lower_bound(gs, 0, n, key);
+}
+
 static int32_t contig_of(const std::vector<uint32_t> &off, int32_t nc, uint32_t g) {
     // largest c in [0, nc) with off[c] <= g
     auto it = std::upper_bound(off.begin(), off.begin() + nc, g);
@@ -340,6 +347,68 @@ int lime_set_device_arrays(const lime_set *s, const uint32_t **gs, const uint32_
     if (gs) *gs = s->gs;
     if (ge) *ge = s->ge;
     if (row) *row = s->row;
+    return LIME_OK;
+}
+
+int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const uint32_t *d_gs,
+                           const uint32_t *d_ge, const uint32_t *d_row, lime_set **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_gs || !d_ge || !d_row)))
+        return fail(LIME_ERR_ARG, "bad set arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    lime_set *s = new_set(ctx, sp, n);
+    uint32_t *d_len = nullptr;
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len);
+    if (rc == LIME_OK) rc = sort_set_global(ctx, s, d_gs, d_ge, d_row, d_len);
+    release(ctx, d_len);
+    if (rc != LIME_OK) {
+        release(ctx, s->d_off);
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return LIME_OK;
+}
+
+int64_t lime_set_lower_bound(const lime_set *s, uint32_t gkey) {
+    if (!s) return fail(LIME_ERR_ARG, "set is null"), -1;
+    lime_ctx *ctx = s->ctx;
+    hipSetDevice(ctx->device);
+    int64_t *d;
+    if (alloc(ctx, &d, 1)) return -1;
+    hipLaunchKernelGGL(k_set_lower_bound, dim3(1), dim3(64), 0, S(ctx), (const uint32_t *)s->gs,
+                       s->n, gkey, d);
+    int64_t h = -1;
+    if (hipGetLastError() != hipSuccess || read_back(ctx, &h, d, 8)) h = -1;
+    release(ctx, d);
+    return h;
+}
+
+int lime_set_copy_rows_device(const lime_set *s, int64_t first, int64_t count, uint32_t *d_gs,
+                              uint32_t *d_ge, uint32_t *d_row) {
+    if (!s || first < 0 || count < 0 || first + count > s->n)
+        return fail(LIME_ERR_ARG, "row range outside the set");
+    lime_ctx *ctx = s->ctx;
+    hipSetDevice(ctx->device);
+    if (count == 0) return LIME_OK;
+    const size_t b = 4 * (size_t)count;
+    if (d_gs) LIME_HIP(hipMemcpyAsync(d_gs, s->gs + first, b, hipMemcpyDeviceToDevice, S(ctx)));
+    if (d_ge) LIME_HIP(hipMemcpyAsync(d_ge, s->ge + first, b, hipMemcpyDeviceToDevice, S(ctx)));
+    if (d_row) LIME_HIP(hipMemcpyAsync(d_row, s->row + first, b, hipMemcpyDeviceToDevice, S(ctx)));
+    return LIME_OK;
+}
+
+int lime_result_copy_range(const lime_result *r, int64_t first, int64_t count, uint32_t *gs,
+                           uint32_t *ge) {
+    if (!r || first < 0 || count < 0 || first + count > r->n)
+        return fail(LIME_ERR_ARG, "range outside the result");
+    lime_ctx *ctx = r->ctx;
+    hipSetDevice(ctx->device);
+    if (count == 0) return LIME_OK;
+    const size_t b = 4 * (size_t)count;
+    if (gs) LIME_HIP(hipMemcpyAsync(gs, r->gs + first, b, hipMemcpyDeviceToHost, S(ctx)));
+    if (ge) LIME_HIP(hipMemcpyAsync(ge, r->ge + first, b, hipMemcpyDeviceToHost, S(ctx)));
+    LIME_HIP(hipStreamSynchronize(S(ctx)));
     return LIME_OK;
 }
 

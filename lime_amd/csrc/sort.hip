@@ -91,6 +91,10 @@ __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *co
 
 // Build gs / ge / row from (contig, start, end), validate, gather statistics
 // (per-tile partials, reduced by k_stats) and the digit-0 histogram.
+// GLOBAL: the input is already (gs, ge, row) in global coordinates (rows of
+// sets of this space, e.g. a shard's own rows + its halo); `contig` / `start`
+// / `end` then carry gs / ge / row and only order and span are validated.
+template <bool GLOBAL>
 __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              const uint32_t *__restrict__ start,
                                              const uint32_t *__restrict__ end,
@@ -108,6 +112,36 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
     uint32_t vk[RITEMS], ve[RITEMS];
     bool valid[RITEMS];
+    if (GLOBAL) {
+        const uint32_t *igs = reinterpret_cast<const uint32_t *>(contig);
+        const uint32_t span = off[n_contigs];
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) {
+            const int64_t i = base + k * 64 + lane;
+            valid[k] = i < n;
+            uint32_t g0 = 0, g1 = 0;
+            if (valid[k]) {
+                g0 = igs[i];
+                g1 = start[i];
+                if (g1 < g0) err |= 2u;
+                if (g1 >= span) err |= 4u;
+                gs[i] = g0;
+                ge[i] = g1;
+                row[i] = end[i];
+                mx = g0 > mx ? g0 : mx;
+                const uint32_t wd = g1 - g0;
+                mnw = wd < mnw ? wd : mnw;
+                mxw = wd > mxw ? wd : mxw;
+                zero |= (wd == 0);
+                if (i > 0) {
+                    const uint32_t p0 = igs[i - 1], p1 = start[i - 1];
+                    if (p0 > g0 || (p0 == g0 && p1 > p0 && g1 == g0)) uns = 1;
+                }
+            }
+            vk[k] = g0;
+            ve[k] = g1;
+        }
+    } else {
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
         const int64_t i = base + k * 64 + lane;
@@ -142,6 +176,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
         }
         vk[k] = g0;
         ve[k] = g1;
+    }
     }
     __syncthreads();
     wave_hist<false>(hist, w, vk, ve, valid, 0);
@@ -336,8 +371,22 @@ int radix_pass(lime_ctx *ctx, bool nz, int shift, bool have_hist, int64_t n, con
 
 }  // namespace
 
+int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
+                  const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_len);
+
 int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32_t *d_start,
              const uint32_t *d_end, const uint32_t *d_len) {
+    return sort_set_impl(ctx, set, false, d_contig, d_start, d_end, d_len);
+}
+
+int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const uint32_t *d_ge,
+                    const uint32_t *d_row, const uint32_t *d_len) {
+    return sort_set_impl(ctx, set, true, reinterpret_cast<const int32_t *>(d_gs), d_ge, d_row,
+                         d_len);
+}
+
+int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
+                  const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_len) {
     const int64_t n = set->n;
     const uint32_t ntiles = (uint32_t)((n + RTILE - 1) / RTILE);
     uint32_t *k0, *e0, *r0, *mat;
@@ -350,9 +399,14 @@ int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32
     LIME_TRY(alloc(ctx, &st, 1));
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
     if (n > 0) {
-        hipLaunchKernelGGL(k_prep, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start, d_end,
-                           (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0, e0, r0,
-                           part, mat, ntiles);
+        if (global)
+            hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start,
+                               d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0,
+                               e0, r0, part, mat, ntiles);
+        else
+            hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
+                               d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                               set->n_contigs, n, k0, e0, r0, part, mat, ntiles);
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());

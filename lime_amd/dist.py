@@ -114,26 +114,43 @@ def right_halo(sets, group=None):
     return out
 
 
-def merge_carry(run_gs, run_ge, group=None, k=256):
+class TensorRuns:
+    """Runs held as int64 tensors (global coordinates)."""
+
+    def __init__(self, run_gs, run_ge):
+        self.gs, self.ge = run_gs, run_ge
+        self.n = run_gs.numel()
+        self.last_end = int(run_ge[-1].item()) if self.n else -1
+
+    def head(self, k):
+        return self.gs[:k].tolist(), self.ge[:k].tolist()
+
+
+def merge_carry(run_gs, run_ge=None, group=None, k=256, device=None):
     """Cross-shard fix-up of locally merged runs (sorted, disjoint per shard).
 
+    `run_gs` is either an int64 tensor of run starts (with `run_ge`) or any
+    object with `.n`, `.last_end` and `.head(k) -> (starts, ends)`.
     Returns (drop, new_last_end): this shard must drop its first `drop` runs
     (they continue a run that starts on an earlier shard) and, if
     new_last_end is not None, set the end of its last remaining run to it.
     One all_gather of (n_runs, last_end, first k runs) per call; k doubles
     and the gather repeats only if a shard's k leading runs are all absorbed.
     """
+    runs = TensorRuns(run_gs, run_ge) if run_ge is not None else run_gs
     w, me = _ws(group)
-    dev = run_gs.device
+    dev = device if device is not None else (run_gs.device if run_ge is not None else "cpu")
     while True:
-        n = run_gs.numel()
+        n = runs.n
         kk = min(k, n)
-        head = torch.full((2 * k + 2,), -1, dtype=torch.int64, device=dev)
-        head[0] = n
-        head[1] = int(run_ge[-1].item()) if n else -1
+        h = [-1] * (2 * k + 2)
+        h[0] = n
+        h[1] = runs.last_end if n else -1
         if kk:
-            head[2:2 + kk] = run_gs[:kk]
-            head[2 + k:2 + k + kk] = run_ge[:kk]
+            hs, he = runs.head(kk)
+            h[2:2 + kk] = hs
+            h[2 + k:2 + k + kk] = he
+        head = torch.tensor(h, dtype=torch.int64, device=dev)
         allh = torch.empty(w * (2 * k + 2), dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allh, head, group=group)
         allh = allh.view(w, 2 * k + 2).cpu().tolist()

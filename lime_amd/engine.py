@@ -104,6 +104,17 @@ class IntervalSet:
         check(_lib().lime_set_device_arrays(self._h, C.byref(gs), C.byref(ge), C.byref(row)))
         return gs.value, ge.value, row.value
 
+    def lower_bound(self, gkey):
+        """first sorted row with global start >= gkey"""
+        r = _lib().lime_set_lower_bound(self._h, int(gkey))
+        if r < 0:
+            check(_ffi.LIME_ERR_ARG if r == -1 else int(r))
+        return int(r)
+
+    def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
+        check(_lib().lime_set_copy_rows_device(self._h, int(first), int(count), d_gs, d_ge,
+                                               d_row))
+
     def to_host(self):
         n = self.n
         out = {k: np.zeros(n, dtype=np.int64) for k in ("start", "end", "row")}
@@ -153,6 +164,15 @@ class Result:
         gs, ge = vp(), vp()
         check(_lib().lime_result_device_arrays(self._h, C.byref(gs), C.byref(ge)))
         return gs.value, ge.value
+
+    def copy_range(self, first, count):
+        """host copy of regions [first, first+count) in GLOBAL coordinates"""
+        gs = np.zeros(count, dtype=np.uint32)
+        ge = np.zeros(count, dtype=np.uint32)
+        check(_lib().lime_result_copy_range(self._h, int(first), int(count),
+                                            gs.ctypes.data_as(P(C.c_uint32)),
+                                            ge.ctypes.data_as(P(C.c_uint32))))
+        return gs, ge
 
     def close(self):
         if self._h and self.ctx.handle:  # a closed context already freed its pool
@@ -257,6 +277,13 @@ class Context:
         h = vp()
         check(_lib().lime_set_create_device(self._h, space.handle, int(n), d_contig, d_start,
                                             d_end, C.byref(h)))
+        return IntervalSet(self, h, space)
+
+    def set_from_global(self, space, n, d_gs, d_ge, d_row):
+        """rows already in the space's global coordinates (u32 device arrays)"""
+        h = vp()
+        check(_lib().lime_set_create_global(self._h, space.handle, int(n), d_gs, d_ge, d_row,
+                                            C.byref(h)))
         return IntervalSet(self, h, space)
 
     # ------------------------------------------------------------- ops

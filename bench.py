@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--n", type=int, default=100_000_000, help="rows per set (C2: 1e8)")
     p.add_argument("--chunk", type=int, default=1 << 31, help="pairs per output chunk")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-scale", type=int, default=100,
                    help="CPU sample: C2 density on hg38/scale with n/scale rows")
     return p.parse_args()
@@ -99,12 +100,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; --dist-backend gloo lets several ranks share one GPU
+    # (rehearsal of the multi-GPU path on a 1-GPU box, boundary records on CPU)
+    gpu = local % max(torch.cuda.device_count(), 1)
+    dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(dev)
+    comm_dev = dev
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+            comm_dev = torch.device("cpu")
 
     import lime_amd
     from lime_amd import synth
@@ -148,7 +155,7 @@ def main():
         from lime_amd.sharded import ShardStep
         # rank r owns the r-th copy of the genome on one virtual coordinate
         # line: offset r * span; boundary exchange + merge carry over RCCL
-        shard = ShardStep(ctx, space, offset=rank * space.span, comm_device=dev)
+        shard = ShardStep(ctx, space, offset=rank * space.span, comm_device=comm_dev)
 
     def step(phases=None):
         t = [ev()] if phases is not None else None
@@ -194,7 +201,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = dt / args.steps * 1e3

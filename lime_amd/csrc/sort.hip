@@ -26,8 +26,8 @@
 namespace lime {
 namespace {
 
-constexpr int RB = 1024;
-constexpr int RITEMS = 8;
+constexpr int RB = 512;
+constexpr int RITEMS = 16;
 constexpr int RTILE = RB * RITEMS;  // 8192 items per tile
 constexpr int RBINS = 256;
 constexpr int RWAVES = RB / 64;     // 16
@@ -262,7 +262,8 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
 }
 
 template <bool NZ>
-__global__ __launch_bounds__(RB) void k_scatter(const uint32_t *__restrict__ key_in,
+// 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
+__global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
                                                 const uint32_t *__restrict__ ge_in,
                                                 const uint32_t *__restrict__ row_in, int64_t n,
                                                 int shift, const uint32_t *__restrict__ base_mat,
@@ -273,33 +274,36 @@ __global__ __launch_bounds__(RB) void k_scatter(const uint32_t *__restrict__ key
     __shared__ uint32_t dstart[RBINS];
     __shared__ uint32_t gbase[RBINS];
     __shared__ uint32_t scratch[RWAVES + 1];
-    __shared__ uint32_t sk[RTILE], se[RTILE], sr[RTILE];
+    __shared__ uint32_t sk[RTILE], se[RTILE], sr[NZ ? RTILE : 1];
 
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
 
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t tile0 = (int64_t)blockIdx.x * RTILE;
     const int64_t base = tile0 + w * WITEMS;
-    uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS], pos[RITEMS], dg[RITEMS];
+    // pd[k] = (position among the wave's rows of its digit) << 8 | digit;
+    // packed to keep the kernel within 128 VGPRs (2 workgroups per CU)
+    uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS], pd[RITEMS];
+    // 32-bit offsets from per-wave base pointers keep address math scalar
+    const int lim = (int)min((int64_t)WITEMS, n - base);  // valid rows of this wave
+    const uint32_t *kin = key_in + base, *ein = ge_in + base, *rin = row_in + base;
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        const int64_t i = base + k * 64 + lane;
-        const bool valid = i < n;
-        vk[k] = valid ? key_in[i] : 0u;
-        ve[k] = valid ? ge_in[i] : 0u;
-        vr[k] = valid ? row_in[i] : 0u;
+        const int o = k * 64 + lane;
+        const bool valid = o < lim;
+        vk[k] = valid ? kin[o] : 0u;
+        ve[k] = valid ? ein[o] : 0u;
+        vr[k] = valid ? rin[o] : 0u;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        const int64_t i = base + k * 64 + lane;
-        const bool valid = i < n;
+        const bool valid = k * 64 + lane < lim;
         const uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
-        dg[k] = d;
         const uint64_t m = match_digit<NZ>(d, valid);
         const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
         const uint32_t old = valid ? cnt[w][d] : 0u;
-        pos[k] = old + rank;
+        pd[k] = ((old + rank) << 8) | d;
         if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(m);
     }
     __syncthreads();
@@ -323,26 +327,58 @@ __global__ __launch_bounds__(RB) void k_scatter(const uint32_t *__restrict__ key
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < RITEMS; ++k) {
-        const int64_t i = base + k * 64 + lane;
-        if (i < n) {
-            const uint32_t lp = cnt[w][dg[k]] + pos[k];
-            sk[lp] = vk[k];
-            se[lp] = ve[k];
-            sr[lp] = vr[k];
-        }
-    }
-    __syncthreads();
     const int64_t rem = n - tile0;
     const int count = rem < RTILE ? (int)rem : RTILE;
+    uint32_t *lp = pd;  // local position within the tile, in place
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        lp[k] = k * 64 + lane < lim ? cnt[w][pd[k] & 0xffu] + (pd[k] >> 8) : 0xffffffffu;
+    if (NZ) {  // digit needs (key, end): stage all three arrays at once
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k)
+            if (lp[k] != 0xffffffffu) {
+                sk[lp[k]] = vk[k];
+                se[lp[k]] = ve[k];
+                sr[lp[k]] = vr[k];
+            }
+        __syncthreads();
+        for (int j = threadIdx.x; j < count; j += RB) {
+            const uint32_t k = sk[j], e = se[j];
+            const uint32_t g = gbase[digit_of<NZ>(k, e, shift)] + (uint32_t)j -
+                               dstart[digit_of<NZ>(k, e, shift)];
+            key_out[g] = k;
+            ge_out[g] = e;
+            row_out[g] = sr[j];
+        }
+        return;
+    }
+    // keys first (they carry the digit), then ends, then rows through one
+    // shared buffer: 64 KiB of staging instead of 96, two workgroups per CU
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (lp[k] != 0xffffffffu) sk[lp[k]] = vk[k];
+    __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t k = sk[j], e = se[j];
-        const uint32_t d = digit_of<NZ>(k, e, shift);
-        const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
-        key_out[g] = k;
-        ge_out[g] = e;
-        row_out[g] = sr[j];
+        const uint32_t k = sk[j];
+        const uint32_t d = digit_of<NZ>(k, 0u, shift);
+        key_out[gbase[d] + (uint32_t)j - dstart[d]] = k;
+    }
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (lp[k] != 0xffffffffu) se[lp[k]] = ve[k];
+    __syncthreads();
+    for (int j = threadIdx.x; j < count; j += RB) {
+        const uint32_t d = digit_of<NZ>(sk[j], 0u, shift);
+        ge_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (lp[k] != 0xffffffffu) se[lp[k]] = vr[k];
+    __syncthreads();
+    for (int j = threadIdx.x; j < count; j += RB) {
+        const uint32_t d = digit_of<NZ>(sk[j], 0u, shift);
+        row_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
     }
 }
 

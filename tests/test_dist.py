@@ -45,7 +45,8 @@ def _owned_pairs(a, b):
 def _worker(rank, world, port, q, splits_mode):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
     try:
         from oracle import oracle
         span, n = 200_000, 3000

@@ -35,7 +35,9 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from datetime import timedelta
+    # a failing rank must not leave its peers blocked in a collective
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
     try:
         import lime_amd
         from lime_amd import dist as ld
@@ -60,8 +62,9 @@ def _worker(rank, world, port, q):
             ha, hb = halos
             for x in p:
                 a, b = int(x["a_row"]), int(x["b_row"])
-                ga = ia[a] if a < len(ia) else own_a[int(ha[a - len(ia)][2])][int(ha[a - len(ia)][3])]
-                gb = ib[b] if b < len(ib) else own_b[int(hb[b - len(ib)][2])][int(hb[b - len(ib)][3])]
+                # halo rows: (gs, ge, source row, source rank)
+                ga = ia[a] if a < len(ia) else own_a[int(ha[a - len(ia)][3])][int(ha[a - len(ia)][2])]
+                gb = ib[b] if b < len(ib) else own_b[int(hb[b - len(ib)][3])][int(hb[b - len(ib)][2])]
                 got.append((int(ga), int(gb), int(x["start"]), int(x["end"])))
         # own rows: srcs as seen by other ranks are (rank, local row) -> own_x[rank][row]
         step = ShardStep(ctx, sp, offset=0, comm_device=torch.device("cpu"))
@@ -78,6 +81,10 @@ def _worker(rank, world, port, q):
             runs.append(list(zip(ct, st, en)))
         q.put((rank, got, runs, out["halo"]))
         ctx.close()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, "error", traceback.format_exc(), None))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -91,9 +98,12 @@ def test_sharded_engine_matches_single_shard(world):
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda t: t[0])
     for p in ps:
-        p.join(timeout=120)
+        p.join(timeout=60)
+    errs = [r[2] for r in res if r[1] == "error"]
+    assert not errs, errs[0]
+    for p in ps:
         assert p.exitcode == 0
     A, B = _rows()
     exp = oracle.intersect(A, B)

@@ -36,7 +36,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--n", type=int, default=100_000_000, help="rows per set (C2: 1e8)")
+    p.add_argument("--rows", type=int, default=100_000_000, help="rows per set (C2: 1e8)")
     p.add_argument("--chunk", type=int, default=1 << 31, help="pairs per output chunk")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -123,7 +123,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     space = lime_amd.Space(list(synth.HG38.keys()), list(synth.HG38.values()))
-    n = args.n
+    n = args.rows
     seed_a, seed_b = 0xA + 0x100 * rank, 0xB + 0x100 * rank
 
     def gen(seed):

@@ -136,6 +136,17 @@ int run(const std::vector<std::string> &args) {
         std::vector<int32_t> c(rdd.size());
         std::vector<int64_t> s(rdd.size()), e(rdd.size()), r(rdd.size());
         check(lime_set_fill_host(A.h, c.data(), s.data(), e.data(), r.data()));
+        // the device order ties equal starts by (zero-width first, input row);
+        // RegionOrdering ties by end: re-order each (tiny) equal-start group
+        for (size_t i = 0; i < rdd.size();) {
+            size_t j = i + 1;
+            while (j < rdd.size() && c[j] == c[i] && s[j] == s[i]) ++j;
+            if (j - i > 1)
+                std::stable_sort(r.begin() + i, r.begin() + j, [&](int64_t x, int64_t y) {
+                    return rdd[x].first.end < rdd[y].first.end;
+                });
+            i = j;
+        }
         for (size_t i = 0; i < rdd.size(); ++i) {
             print_region(rdd[r[i]].first);
             printf("\t%s\n", rdd[r[i]].second.c_str());

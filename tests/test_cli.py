@@ -1,0 +1,65 @@
+"""bin/lime-submit: the command surface of bin/lime-submit + LimeMain
+(LimeMain.scala:30-57), backed by the C++ operator mirror (include/lime_amd.hpp)."""
+import os
+import subprocess
+
+import pytest
+
+from tests.util import GOLDEN, expected
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "bin", "lime-submit")
+
+
+def run(*args):
+    return subprocess.run([CLI, *args], capture_output=True, text=True, timeout=120)
+
+
+def g(name):
+    return os.path.join(GOLDEN, name)
+
+
+def test_usage_and_version():
+    r = run()
+    assert r.returncode == 0 and "Choose one of the following commands" in r.stdout
+    for cmd in ("complement", "intersect", "merge", "subtract", "sort"):
+        assert cmd in r.stdout
+    r = run("-version")
+    assert r.returncode == 0 and r.stdout.startswith("Version 0")
+    # spark args before "--" are accepted and ignored (bin/lime-submit:7-23)
+    r = run("--master", "local[4]", "--", "-version")
+    assert r.returncode == 0 and "Version 0" in r.stdout
+    r = run("nonsense")
+    assert "Choose one of the following commands" in r.stdout
+
+
+def test_no_device_fails_loudly():
+    r = run("intersect", g("intersect_with_overlap_00.bed"), g("intersect_with_overlap_01.bed"))
+    if r.returncode == 0:
+        pytest.skip("device present")
+    assert r.returncode == 1 and "status 3" in r.stderr
+
+
+def lines(r):
+    assert r.returncode == 0, r.stderr
+    return [l.split("\t") for l in r.stdout.strip().split("\n") if l]
+
+
+@pytest.mark.gpu
+def test_cli_intersect_subtract_merge_complement_sort():
+    ex = expected()
+    out = lines(run("--", "intersect", g("intersect_with_overlap_00.bed"),
+                    g("intersect_with_overlap_01.bed")))
+    assert [[c, int(s), int(e)] for c, s, e, *_ in out] == ex["intersection_full"]
+    assert out[0][3:] == ["CpG:_30", "CpG:_116"]
+    out = lines(run("subtract", g("intersect_with_overlap_00.bed"),
+                    g("intersect_with_overlap_01.bed")))
+    assert [[c, int(s), int(e)] for c, s, e, *_ in out] == ex["subtract"]
+    out = lines(run("merge", g("cpg_20merge.bed")))
+    assert out == [["chr1", "28735", "30000", "20"]]
+    out = lines(run("complement", g("cpg_20merge.bed"), g("genome.txt")))
+    assert [[c, int(s), int(e)] for c, s, e in out] == ex["complement"]
+    out = lines(run("sort", g("cpg.bed")))
+    assert len(out) == 28691
+    key = [(c.encode("utf-16-be"), int(s), int(e)) for c, s, e, _ in out]
+    assert key == sorted(key)

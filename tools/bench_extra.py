@@ -1,0 +1,172 @@
+"""Supplementary benchmark lines for BASELINE.json configs C3, C4 and C5
+(bench.py measures the headline config C2).  Single GPU; one JSON line each.
+
+  C3  merge of 5e8 ChIP-seq-like pile-ups (2e6 centres, N(0,150) offsets,
+      len U[150,600], seeds 0xC / 0xD): sort + merge with run ids.
+      unit: intervals/s
+  C4  difference + complement against hg38 via the bit-per-base path:
+      A, B = 1e7 rows, len U[50,500], seeds 0xD / 0xE: sort A, B -> bitsets
+      -> complement(merge(A)) runs (NOT) and merge(A) minus merge(B) runs
+      (AND-NOT).  unit: bases/s (G/t); intervals/s also reported
+  C5  8-way intersection over 1e9 rows (8 x 1.25e8, len U[10,40], seeds
+      0x50..0x57): sort each set -> bitsets -> 8-way AND runs.  On one GPU
+      (the whole genome); unit: intervals/s
+
+Inputs are generated on the device (counter-based RNG) outside the timed
+region; every step starts from unsorted rows in HBM.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM = 8000.0
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--workload", choices=["c3", "c4", "c5"], required=True)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scale", type=float, default=1.0, help="row-count scale (testing)")
+    a = p.parse_args()
+
+    import torch
+    import lime_amd
+    from lime_amd import synth
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ctx = lime_amd.Context(0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    space = lime_amd.Space(list(synth.HG38.keys()), list(synth.HG38.values()))
+    G = int(sum(synth.HG38.values()))
+
+    def ev():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def gen(n, seed, lo, hi, pile=None):
+        c = torch.empty(n, dtype=torch.int32, device=dev)
+        s = torch.empty(n, dtype=torch.int32, device=dev)
+        e = torch.empty(n, dtype=torch.int32, device=dev)
+        if pile:
+            ctx.synth_pileup(space, n, seed, pile[0], pile[1], lo, hi, c.data_ptr(), s.data_ptr(),
+                             e.data_ptr())
+        else:
+            ctx.synth_uniform(space, n, seed, lo, hi, c.data_ptr(), s.data_ptr(), e.data_ptr())
+        return n, c, s, e
+
+    def mkset(x):
+        n, c, s, e = x
+        return ctx.set_from_device(space, n, c.data_ptr(), s.data_ptr(), e.data_ptr())
+
+    if a.workload == "c3":
+        inp = gen(int(5e8 * a.scale), 0xC, 150, 600, pile=(2_000_000, 150))
+        n = inp[0]
+
+        def step(rec):
+            t0 = ev()
+            S = mkset(inp)
+            t1 = ev()
+            m = ctx.merge(S)
+            t2 = ev()
+            rec.append((t0, t1, t2, m.n))
+            m.close()
+            S.close()
+        units, unit = n, "intervals/s"
+        desc = f"C3: sort + merge (run ids) of {n} pile-up intervals (2e6 centres, N(0,150), " \
+               "len U[150,600])"
+
+        def roof(rec):
+            t0, t1, t2, runs = rec[-1]
+            ms = t1.elapsed_time(t2)
+            b = 12 * n + 8 * runs  # read gs+ge, write run id per row, write runs
+            return {"sort_ms": t0.elapsed_time(t1), "merge_ms": ms, "runs": runs}, \
+                {"kernel": "merge (k_tile_max, k_runs_count, k_runs_write)", "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+    elif a.workload == "c4":
+        ia = gen(int(1e7 * a.scale), 0xD, 50, 500)
+        ib = gen(int(1e7 * a.scale), 0xE, 50, 500)
+
+        def step(rec):
+            t0 = ev()
+            A, B = mkset(ia), mkset(ib)
+            t1 = ev()
+            ba, bb = ctx.bitset(A), ctx.bitset(B)
+            t2 = ev()
+            comp = ctx.bitset_runs(1, ba)
+            diff = ctx.bitset_runs(3, ba, bb)
+            t3 = ev()
+            rec.append((t0, t1, t2, t3, comp.n, diff.n))
+            for h in (comp, diff, ba, bb, A, B):
+                h.close()
+        units, unit = G, "bases/s"
+        desc = "C4: complement(merge(A)) and merge(A) \\ merge(B) on the hg38 bitset " \
+               "(A, B = 1e7 rows, len U[50,500])"
+
+        def roof(rec):
+            t0, t1, t2, t3, nc, nd = rec[-1]
+            ms = t2.elapsed_time(t3)
+            W = (space.span + 63) // 64 * 8
+            b = 2 * W + 2 * 2 * W + 8 * (nc + nd)  # NOT: 2 passes x 1 operand; ANDN: 2 x 2
+            return {"sort_ms": t0.elapsed_time(t1), "bitset_build_ms": t1.elapsed_time(t2),
+                    "extract_ms": ms, "complement_runs": nc, "difference_runs": nd}, \
+                {"kernel": "bitset extraction (k_ev_count, k_ev_write)", "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+    else:
+        k = 8
+        per = int(1.25e8 * a.scale)
+        ins = [gen(per, 0x50 + i, 10, 40) for i in range(k)]
+
+        def step(rec):
+            t0 = ev()
+            sets = [mkset(x) for x in ins]
+            t1 = ev()
+            bits = [ctx.bitset(s) for s in sets]
+            t2 = ev()
+            r = ctx.bitset_and(bits)
+            t3 = ev()
+            rec.append((t0, t1, t2, t3, r.n))
+            for h in [r] + bits + sets:
+                h.close()
+        units, unit = k * per, "intervals/s"
+        desc = f"C5: {k}-way intersection, {k} x {per} rows (len U[10,40]) on 1 GPU, bitset AND"
+
+        def roof(rec):
+            t0, t1, t2, t3, nr = rec[-1]
+            ms = t2.elapsed_time(t3)
+            W = (space.span + 63) // 64 * 8
+            b = 2 * k * W + 8 * nr
+            return {"sort_ms": t0.elapsed_time(t1), "bitset_build_ms": t1.elapsed_time(t2),
+                    "and_extract_ms": ms, "runs": nr}, \
+                {"kernel": "8-way AND + extraction (k_ev_count, k_ev_write)", "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+
+    torch.cuda.synchronize(dev)
+    rec = []
+    for _ in range(a.warmup):
+        step(rec)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        step(rec)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t) / a.steps
+    br, rf = roof(rec)
+    rf["peak"], rf["unit"] = HBM, "GB/s"
+    rf["frac"] = rf["achieved"] / HBM
+    print(json.dumps({"workload": a.workload, "config": desc, "value": units / dt, "unit": unit,
+                      "ms_per_step": dt * 1e3, "steps": a.steps, "breakdown_ms": br,
+                      "roofline": rf}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,11 @@ LIB      = lime_amd/liblime_amd.so
 ORACLE   = oracle/build/liblime_oracle.so
 CLI      = bin/lime-submit
 
-all: $(LIB) $(ORACLE) $(CLI)
+all: $(LIB) $(ORACLE) $(CLI) bin/bw_probe
+
+bin/bw_probe: tools/bw_probe.hip
+	@mkdir -p bin
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -Wno-unused-result -o $@ $<
 
 $(OBJDIR)/%.o: $(SRC)/%.hip $(SRC)/common.hpp include/lime_amd.h
 	@mkdir -p $(OBJDIR)

@@ -4,10 +4,13 @@
 // bit per base of the global coordinate space (span = sum(len + 1) bits,
 // ~386 MB for hg38).  The pad base after every contig is never set, so runs
 // never cross a contig boundary.
-//   k_paint     merged runs -> bits: interior words stored whole, the two
-//               edge words OR-ed atomically (adjacent runs may share one)
+//   k_paint     merged runs -> bits, one 4096-word (32 KiB) tile per
+//               workgroup: the tile's runs (two binary searches) are OR-ed
+//               into an LDS image, which is then stored once, coalesced --
+//               every word written exactly once, no memset, no global atomics
 //   k_ev_count  per 4096-word tile: events (run starts + run ends) of
-//               op(words) where op = A | ~A | A&B | A&~B | AND of k sets
+//               op(words) where op = A | ~A | A&B | A&~B | AND of k sets;
+//               operands are combined while loading (coalesced) into LDS
 //   k_ev_write  the same, writing events at scanned offsets: event 2r is the
 //               start and event 2r+1 the end of output run r
 // Semantics: base-level algebra; book-ended runs of
@@ -21,24 +24,37 @@ constexpr int BB = 256;
 constexpr int BW = 16;            // words per thread
 constexpr int BT = BB * BW;       // words per tile
 constexpr int MAXK = 16;
+constexpr int MAXPAD = 64;        // contig pads per tile handled in LDS
 
 __global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
                                               const uint32_t *__restrict__ rge, int64_t nr,
-                                              uint64_t *__restrict__ words) {
-    const int64_t r = (int64_t)blockIdx.x * BB + threadIdx.x;
-    if (r >= nr) return;
-    const uint64_t s = rgs[r], e = rge[r];
-    if (e <= s) return;
-    const uint64_t w0 = s >> 6, w1 = (e - 1) >> 6;
-    for (uint64_t w = w0; w <= w1; ++w) {
-        const uint64_t lo = w == w0 ? (s & 63) : 0;
-        const uint64_t hi = w == w1 ? ((e - 1) & 63) : 63;
-        const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
-        if (m == ~0ull)
-            words[w] = m;
-        else
-            atomicOr((unsigned long long *)&words[w], (unsigned long long)m);
+                                              uint64_t *__restrict__ words, int64_t n_words) {
+    __shared__ unsigned long long img[BT];
+    __shared__ int64_t s_r[2];
+    const int64_t w0 = (int64_t)blockIdx.x * BT;
+    const uint64_t blo = (uint64_t)w0 * 64, bhi = blo + (uint64_t)BT * 64;
+    for (int i = threadIdx.x; i < BT; i += BB) img[i] = 0ull;
+    if (threadIdx.x == 0) s_r[0] = dev::upper_bound(rge, 0, nr, blo);   // first end > blo
+    if (threadIdx.x == 64) s_r[1] = dev::lower_bound(rgs, 0, nr, bhi);  // first start >= bhi
+    __syncthreads();
+    for (int64_t r = s_r[0] + threadIdx.x; r < s_r[1]; r += BB) {
+        const uint64_t s = max((uint64_t)rgs[r], blo) - blo;
+        const uint64_t e = min((uint64_t)rge[r], bhi) - blo;
+        if (e <= s) continue;
+        const uint64_t a = s >> 6, b = (e - 1) >> 6;
+        for (uint64_t w = a; w <= b; ++w) {
+            const uint64_t lo = w == a ? (s & 63) : 0;
+            const uint64_t hi = w == b ? ((e - 1) & 63) : 63;
+            const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
+            if (m == ~0ull)
+                img[w] = m;  // interior word: only this run covers it
+            else
+                atomicOr(&img[w], (unsigned long long)m);
+        }
     }
+    __syncthreads();
+    const int cnt = (int)min((int64_t)BT, n_words - w0);
+    for (int i = threadIdx.x; i < cnt; i += BB) words[w0 + i] = img[i];
 }
 
 struct OpArgs {
@@ -51,32 +67,18 @@ struct OpArgs {
     int32_t nc;
 };
 
-__device__ __forceinline__ uint64_t op_word(const OpArgs &a, int64_t w) {
-    if (w < 0 || w >= a.n_words) return 0;
-    uint64_t x;
+__device__ __forceinline__ uint64_t op_raw(const OpArgs &a, int64_t w) {
     switch (a.op) {
-        case 0: x = a.w[0][w]; break;
-        case 1: {
-            x = ~a.w[0][w];
-            // clear pad bits and bits beyond the span
-            const int64_t b0 = w * 64;
-            if (b0 + 64 > a.span) {
-                const int64_t keep = a.span - b0;
-                x &= keep <= 0 ? 0ull : (keep >= 64 ? ~0ull : ((1ull << keep) - 1));
-            }
-            int64_t c = dev::lower_bound(a.pad, 0, (int64_t)a.nc, (uint32_t)(b0 > 0xffffffffLL ? 0xffffffffLL : b0));
-            for (; c < a.nc && (int64_t)a.pad[c] < b0 + 64; ++c) x &= ~(1ull << (a.pad[c] - b0));
-            break;
-        }
-        case 2: x = a.w[0][w] & a.w[1][w]; break;
-        case 3: x = a.w[0][w] & ~a.w[1][w]; break;
+        case 0: return a.w[0][w];
+        case 1: return ~a.w[0][w];
+        case 2: return a.w[0][w] & a.w[1][w];
+        case 3: return a.w[0][w] & ~a.w[1][w];
         default: {
-            x = ~0ull;
+            uint64_t x = ~0ull;
             for (int i = 0; i < a.k; ++i) x &= a.w[i][w];
-            break;
+            return x;
         }
     }
-    return x;
 }
 
 __device__ __forceinline__ void events_of(uint64_t x, uint64_t prev, uint64_t &st, uint64_t &en) {
@@ -85,20 +87,54 @@ __device__ __forceinline__ void events_of(uint64_t x, uint64_t prev, uint64_t &s
     en = ~x & sh;
 }
 
-__global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict__ tcnt) {
-    const int64_t w0 = (int64_t)blockIdx.x * BT;
-    uint32_t c = 0;
-#pragma unroll 4
-    for (int k = 0; k < BW; ++k) {
-        const int64_t w = w0 + k * BB + threadIdx.x;
-        if (w < a.n_words) {
-            uint64_t st, en;
-            events_of(op_word(a, w), op_word(a, w - 1), st, en);
-            c += __popcll(st) + __popcll(en);
+// Stage op(words) of tile [w0, w0 + BT) plus the word before it into LDS
+// (img[0] = word w0 - 1).  NOT clears pad bits and bits beyond the span.
+__device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned long long *img,
+                                           uint32_t *s_pad, int *s_npad) {
+    if (a.op == 1 && threadIdx.x == 0) {
+        const int64_t lo = (w0 > 0 ? w0 - 1 : 0) * 64, hi = (w0 + BT) * 64;
+        int64_t c = dev::lower_bound(a.pad, 0, (int64_t)a.nc, (uint32_t)min(lo, (int64_t)0xffffffff));
+        int np = 0;
+        for (; c < a.nc && (int64_t)a.pad[c] < hi && np < MAXPAD; ++c) s_pad[np++] = a.pad[c];
+        *s_npad = np;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= BT; i += BB) {
+        const int64_t w = w0 - 1 + i;
+        uint64_t x = 0;
+        if (w >= 0 && w < a.n_words) {
+            x = op_raw(a, w);
+            if (a.op == 1) {
+                const int64_t b0 = w * 64;
+                if (b0 + 64 > a.span) {
+                    const int64_t keep = a.span - b0;
+                    x &= keep <= 0 ? 0ull : (keep >= 64 ? ~0ull : ((1ull << keep) - 1));
+                }
+                for (int p = 0; p < *s_npad; ++p) {
+                    const int64_t d = (int64_t)s_pad[p] - b0;
+                    if (d >= 0 && d < 64) x &= ~(1ull << d);
+                }
+            }
         }
+        img[i] = x;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict__ tcnt) {
+    __shared__ unsigned long long img[BT + 1];
+    __shared__ uint32_t s_pad[MAXPAD];
+    __shared__ int s_npad;
+    __shared__ uint32_t ws[BB / 64];
+    const int64_t w0 = (int64_t)blockIdx.x * BT;
+    stage_tile(a, w0, img, s_pad, &s_npad);
+    uint32_t c = 0;
+    for (int i = threadIdx.x; i < BT; i += BB) {
+        uint64_t st, en;
+        events_of(img[i + 1], img[i], st, en);
+        c += __popcll(st) + __popcll(en);
     }
     c = dev::wave_reduce_sum(c);
-    __shared__ uint32_t ws[BB / 64];
     if (dev::lane_id() == 0) ws[threadIdx.x / 64] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -111,17 +147,19 @@ __global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict_
 __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__restrict__ toff,
                                                  uint32_t *__restrict__ rgs,
                                                  uint32_t *__restrict__ rge) {
+    __shared__ unsigned long long img[BT + 1];
+    __shared__ uint32_t s_pad[MAXPAD];
+    __shared__ int s_npad;
     __shared__ uint32_t scratch[BB / 64 + 1];
-    // blocked: thread t owns words w0 + t*BW .. + BW-1 (events in position order)
-    const int64_t w0 = (int64_t)blockIdx.x * BT + (int64_t)threadIdx.x * BW;
-    uint64_t prev = op_word(a, w0 - 1);
-    uint64_t xs[BW];
+    const int64_t w0 = (int64_t)blockIdx.x * BT;
+    stage_tile(a, w0, img, s_pad, &s_npad);
+    // blocked: thread t owns tile words t*BW .. t*BW + BW - 1 (position order)
+    const int q0 = threadIdx.x * BW;
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
-        xs[k] = op_word(a, w0 + k);
         uint64_t st, en;
-        events_of(xs[k], k ? xs[k - 1] : prev, st, en);
+        events_of(img[q0 + k + 1], img[q0 + k], st, en);
         c += __popcll(st) + __popcll(en);
     }
     uint32_t tot;
@@ -129,9 +167,9 @@ __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__res
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
         uint64_t st, en;
-        events_of(xs[k], k ? xs[k - 1] : prev, st, en);
+        events_of(img[q0 + k + 1], img[q0 + k], st, en);
         uint64_t all = st | en;
-        const uint32_t base = (uint32_t)((w0 + k) * 64);
+        const uint32_t base = (uint32_t)((w0 + q0 + k) * 64);
         while (all) {
             const int b = __builtin_ctzll(all);
             all &= all - 1;
@@ -166,10 +204,10 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     bs->span = span;
     bs->n_words = (span + 63) / 64;
     LIME_TRY(alloc(ctx, &bs->words, (size_t)bs->n_words));
-    LIME_HIP(hipMemsetAsync(bs->words, 0, (size_t)bs->n_words * 8, S(ctx)));
-    if (runs.n > 0)
-        hipLaunchKernelGGL(k_paint, dim3(blocks_for(runs.n, BB)), dim3(BB), 0, S(ctx), runs.gs,
-                           runs.ge, runs.n, bs->words);
+    const int64_t nt = (bs->n_words + BT - 1) / BT;
+    if (nt > 0)
+        hipLaunchKernelGGL(k_paint, dim3((unsigned)nt), dim3(BB), 0, S(ctx), runs.gs, runs.ge,
+                           runs.n, bs->words, bs->n_words);
     LIME_HIP(hipGetLastError());
     release(ctx, runs.gs);
     release(ctx, runs.ge);
@@ -191,7 +229,8 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     for (int c = 0; c < a->n_contigs; ++c) pad[c] = a->off[c + 1] - 1;
     uint32_t *d_pad;
     LIME_TRY(alloc(ctx, &d_pad, pad.size() + 1));
-    LIME_HIP(hipMemcpy(d_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
+    if (!pad.empty())
+        LIME_HIP(hipMemcpy(d_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
     oa.pad = d_pad;
     const int64_t nt = (a->n_words + BT - 1) / BT;
     uint32_t *tcnt, *toff, *total;

@@ -67,6 +67,13 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return m;
 }
 
+// bijective blockIdx -> tile map giving each XCD (blockIdx % 8) a contiguous
+// range of tiles (MI355X_MICROARCH.md: workgroups are dealt round-robin)
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t ntiles) {
+    const uint32_t q = ntiles / 8, r = ntiles % 8, x = bid % 8, i = bid / 8;
+    return x * q + (x < r ? x : r) + i;
+}
+
 // per-wave digit histogram of this wave's rows into hist[w][*]
 template <bool NZ>
 __device__ __forceinline__ void wave_hist(uint32_t (*hist)[RBINS], int w, const uint32_t *vk,
@@ -279,7 +286,13 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
 
     const int w = threadIdx.x / 64, lane = dev::lane_id();
-    const int64_t tile0 = (int64_t)blockIdx.x * RTILE;
+    // XCD-aware tile order: consecutive tiles run on one XCD, so the partial
+    // 128-B lines where a digit's run of tile t meets the same digit's run
+    // of tile t+1 are completed in one L2 instead of being written back
+    // half-filled by two XCDs (blocks are dealt round-robin over 8 XCDs;
+    // speed only -- any placement gives the same result)
+    const uint32_t tile = xcd_swizzle(blockIdx.x, ntiles);
+    const int64_t tile0 = (int64_t)tile * RTILE;
     const int64_t base = tile0 + w * WITEMS;
     // pd[k] = (position among the wave's rows of its digit) << 8 | digit;
     // packed to keep the kernel within 128 VGPRs (2 workgroups per CU)
@@ -323,7 +336,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
                 cnt[ww][d] = run;
                 run += c;
             }
-            gbase[d] = base_mat[(int64_t)d * ntiles + blockIdx.x];
+            gbase[d] = base_mat[(int64_t)d * ntiles + tile];
         }
     }
     __syncthreads();

@@ -30,8 +30,8 @@ constexpr int RB = 512;
 constexpr int RITEMS = 16;
 constexpr int RTILE = RB * RITEMS;  // 8192 items per tile
 constexpr int RBINS = 256;
-constexpr int RWAVES = RB / 64;     // 16
-constexpr int WITEMS = RTILE / RWAVES;  // 512 consecutive rows per wave
+constexpr int RWAVES = RB / 64;     // 8
+constexpr int WITEMS = RTILE / RWAVES;  // 1024 consecutive rows per wave
 
 struct SetStats {
     uint32_t err;        // bit0 contig out of range, bit1 end < start, bit2 end > contig length
@@ -148,6 +148,71 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
             vk[k] = g0;
             ve[k] = g1;
         }
+    } else if (base + WITEMS <= n) {
+        // full wave chunk: 16-B loads and stores, 4 consecutive rows per lane
+        // (the histogram below ignores order, so vk / ve may be held in any order)
+        const int4 *c4 = reinterpret_cast<const int4 *>(contig + base);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(start + base);
+        const uint4 *e4 = reinterpret_cast<const uint4 *>(end + base);
+        uint4 *g4 = reinterpret_cast<uint4 *>(gs + base);
+        uint4 *h4 = reinterpret_cast<uint4 *>(ge + base);
+        uint4 *r4 = reinterpret_cast<uint4 *>(row + base);
+#pragma unroll
+        for (int k = 0; k < RITEMS / 4; ++k) {
+            const int q = k * 64 + lane;
+            const int4 cv = c4[q];
+            const uint4 sv = s4[q], ev = e4[q];
+            const int32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
+            const uint32_t ss[4] = {sv.x, sv.y, sv.z, sv.w}, ee[4] = {ev.x, ev.y, ev.z, ev.w};
+            uint32_t a0[4], a1[4], ok[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t c = cc[j];
+                ok[j] = c >= 0 && c < n_contigs;
+                a0[j] = a1[j] = 0;
+                if (!ok[j]) {
+                    err |= 1u;
+                } else {
+                    if (ee[j] < ss[j]) err |= 2u;
+                    if (ee[j] > len[c]) err |= 4u;
+                    a0[j] = off[c] + ss[j];
+                    a1[j] = off[c] + ee[j];
+                }
+                mx = a0[j] > mx ? a0[j] : mx;
+                const uint32_t wd = a1[j] - a0[j];
+                mnw = wd < mnw ? wd : mnw;
+                mxw = wd > mxw ? wd : mxw;
+                zero |= (wd == 0);
+                vk[4 * k + j] = a0[j];
+                ve[4 * k + j] = a1[j];
+            }
+            // canonical-order check: the row before this lane's first row is
+            // the previous lane's last one (lane 0 reads it from memory)
+            uint32_t p0 = __shfl_up(a0[3], 1), p1 = __shfl_up(a1[3], 1), pok = __shfl_up(ok[3], 1);
+            const int64_t i0 = base + 4 * (int64_t)q;
+            if (lane == 0) {
+                pok = 0;
+                if (i0 > 0) {
+                    const int32_t pc = contig[i0 - 1];
+                    pok = pc >= 0 && pc < n_contigs;
+                    if (pok) {
+                        p0 = off[pc] + start[i0 - 1];
+                        p1 = off[pc] + end[i0 - 1];
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (pok && ok[j] && (p0 > a0[j] || (p0 == a0[j] && p1 > p0 && a1[j] == a0[j])))
+                    uns = 1;
+                p0 = a0[j], p1 = a1[j], pok = ok[j];
+            }
+            g4[q] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
+            h4[q] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
+            r4[q] = make_uint4((uint32_t)i0, (uint32_t)i0 + 1, (uint32_t)i0 + 2, (uint32_t)i0 + 3);
+        }
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) valid[k] = true;
     } else {
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
@@ -255,12 +320,31 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
     uint32_t vk[RITEMS], ve[RITEMS];
     bool valid[RITEMS];
+    if (base + WITEMS <= n) {
+        // a histogram ignores order: 16-B loads, 4 consecutive rows per lane
+        const uint4 *k4 = reinterpret_cast<const uint4 *>(key + base);
+        const uint4 *e4 = reinterpret_cast<const uint4 *>(ge + base);
 #pragma unroll
-    for (int k = 0; k < RITEMS; ++k) {
-        const int64_t i = base + k * 64 + lane;
-        valid[k] = i < n;
-        vk[k] = valid[k] ? key[i] : 0u;
-        ve[k] = (NZ && valid[k]) ? ge[i] : 0u;
+        for (int k = 0; k < RITEMS / 4; ++k) {
+            const uint4 v = k4[k * 64 + lane];
+            vk[4 * k] = v.x, vk[4 * k + 1] = v.y, vk[4 * k + 2] = v.z, vk[4 * k + 3] = v.w;
+            if (NZ) {
+                const uint4 u = e4[k * 64 + lane];
+                ve[4 * k] = u.x, ve[4 * k + 1] = u.y, ve[4 * k + 2] = u.z, ve[4 * k + 3] = u.w;
+            } else {
+                ve[4 * k] = ve[4 * k + 1] = ve[4 * k + 2] = ve[4 * k + 3] = 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) valid[k] = true;
+    } else {
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) {
+            const int64_t i = base + k * 64 + lane;
+            valid[k] = i < n;
+            vk[k] = valid[k] ? key[i] : 0u;
+            ve[k] = (NZ && valid[k]) ? ge[i] : 0u;
+        }
     }
     __syncthreads();
     wave_hist<NZ>(hist, w, vk, ve, valid, shift);

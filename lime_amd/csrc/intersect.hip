@@ -205,19 +205,86 @@ constexpr int FB = 512;           // fill workgroup: 8 waves
 constexpr int FW = FB / 64;
 constexpr int FOPT = OT / FB;     // owners per thread when staging a tile
 constexpr int PCAP = 2048;        // LDS partner window (16 B records)
+constexpr int PPT = PCAP / FB;    // partner rows per thread when staging
+constexpr int64_t GR = 1ll << 40;  // wave granule: default one equal chunk per wave
 
-// One workgroup writes the SBLK consecutive output records of its slice of
-// the output index space.  Per owner tile it touches it stages, in LDS,
+// 65-ary wave search on the u64 tile offsets: largest t with toff[t] <= key
+__device__ __forceinline__ int64_t wave_tile_of(const uint64_t *__restrict__ a, int64_t n,
+                                                uint64_t key) {
+    int64_t lo = 0, hi = n;  // first index with a[i] > key lies in [lo, hi]
+    const int lane = dev::lane_id();
+    while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 64) / 65;
+        const int64_t idx = lo + step * (lane + 1) - 1;
+        const bool le = idx < hi && a[idx] <= key;
+        const int c = __popcll(__ballot(le));
+        const int64_t nlo = c == 0 ? lo : lo + step * c;
+        const int64_t nhi = c == 64 ? hi : min(hi, lo + step * (c + 1) - 1);
+        lo = nlo;
+        hi = nhi;
+    }
+    const int64_t idx = lo + lane;
+    const bool le = idx < hi && a[idx] <= key;
+    return lo + __popcll(__ballot(le)) - 1;
+}
+
+// Everything a fill workgroup stages for one owner tile, held in registers
+// so that the NEXT tile's loads are in flight while the current tile's
+// records are being stored (the staging latency is hidden behind the store
+// stream instead of stalling it once per tile).
+struct TileRegs {
+    uint32_t c[FOPT], lo[FOPT], og[FOPT], oe[FOPT], orw[FOPT];
+    uint32_t pg[PPT], pe[PPT], pr[PPT];
+    uint32_t wlo, whi;
+};
+
+__device__ __forceinline__ int tile_stream(const FillArgs &fa, int64_t t) {
+    return t < fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT ? 0 : 1;
+}
+
+__device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileRegs &r) {
+    const StreamArgs &sa = fa.s[tile_stream(fa, t)];
+    const int64_t o0 = (t - sa.tile0) * OT;
+    const int nown = (int)min((int64_t)OT, sa.no - o0);
+#pragma unroll
+    for (int k = 0; k < FOPT; ++k) {
+        const int q = threadIdx.x * FOPT + k;
+        const bool v = q < nown;
+        const int64_t j = o0 + q;
+        r.c[k] = v ? fa.ocnt[sa.owner0 + j] : 0u;
+        r.lo[k] = v ? fa.olo[sa.owner0 + j] : 0u;
+        r.og[k] = v ? sa.ogs[j] : 0u;
+        r.oe[k] = v ? sa.oge[j] : 0u;
+        r.orw[k] = v ? sa.orow[j] : 0u;
+    }
+    r.wlo = fa.win[2 * t];
+    r.whi = fa.win[2 * t + 1];
+    const int wl = (int)min((int64_t)(r.whi - r.wlo), (int64_t)PCAP);
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        const int i = k * FB + threadIdx.x;
+        const bool v = i < wl;
+        r.pg[k] = v ? sa.pgs[r.wlo + i] : 0u;
+        r.pe[k] = v ? sa.pge[r.wlo + i] : 0u;
+        r.pr[k] = v ? sa.prow[r.wlo + i] : 0u;
+    }
+}
+
+// One workgroup writes the `per` consecutive output records of its slice of
+// the output index space [first, first + count).  Per owner tile it touches
+// it stages, in LDS,
 //   s_lo_off[q] = (lo_q, off_q)   partner range start, exclusive output offset
 //   s_own[q]    = (gs, ge, row, contig offset) of the owner
 //   s_par[i]    = (gs, ge, row) of partner wlo + i   (the tile's window)
-// then splits its output range into one contiguous chunk per wave; lane l of
-// a wave handles outputs base + l + 64 k, so an owner switch happens about
-// once per 82/64 iterations (C2) and is a single LDS compare, and every
-// iteration is 1 b64 + 2 b128 LDS reads and ONE 16-B store per lane, the
-// wave's 64 stores forming one contiguous 1-KiB segment.
+// then deals its output range to the waves in GR-record granules; lane l of
+// a wave handles outputs g + l + 64 k of a granule g, so an owner switch
+// happens about once per 82/64 iterations (C2) and is a single LDS compare,
+// and every iteration is 1 b64 + 2 b128 LDS reads and ONE 16-B store per
+// lane, the wave's 64 stores forming one contiguous 1-KiB segment.  The next
+// tile's staging data is prefetched into registers (TileRegs) before the
+// store loop.
 template <bool CKSUM>
-__global__ __launch_bounds__(FB) void k_fill(FillArgs fa) {
+__global__ __launch_bounds__(FB) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
     __shared__ uint2 s_lo_off[OT + 1];
     __shared__ u32x4 s_own[OT];
     __shared__ u32x4 s_par[PCAP];
@@ -225,30 +292,29 @@ __global__ __launch_bounds__(FB) void k_fill(FillArgs fa) {
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_red[2][FW];
 
-    const int64_t g0 = fa.first / SBLK;
-    const int64_t ob = max(fa.first, (g0 + blockIdx.x) * SBLK);
-    const int64_t oend = min(fa.first + fa.count, (g0 + blockIdx.x + 1) * SBLK);
+    const int64_t ob = fa.first + (int64_t)blockIdx.x * per;
+    const int64_t oend = min(fa.first + fa.count, ob + per);
     if (ob >= oend) return;
-    if (threadIdx.x == 0) s_tile = dev::upper_bound(fa.toff, 0, fa.ntiles, (uint64_t)ob) - 1;
-    __syncthreads();
     const int w = threadIdx.x / 64, lane = dev::lane_id();
+    if (w == 0) {
+        const int64_t t0 = wave_tile_of(fa.toff, fa.ntiles, (uint64_t)ob);
+        if (lane == 0) s_tile = t0;
+    }
+    __syncthreads();
     int64_t t = s_tile;
     uint64_t hsum = 0, hxor = 0;
-    while (t < fa.ntiles && (int64_t)fa.toff[t] < oend) {
-        const int st = t < fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT ? 0 : 1;
-        const StreamArgs sa = st ? fa.s[1] : fa.s[0];
+    TileRegs R;
+    tile_load(fa, t, R);
+    while (true) {
+        const int st = tile_stream(fa, t);
+        const StreamArgs &sa = fa.s[st];
         const int64_t o0 = (t - sa.tile0) * OT;
         const int nown = (int)min((int64_t)OT, sa.no - o0);
         const int64_t tbase = (int64_t)fa.toff[t];
-        // ---- owners: counts -> exclusive offsets (blocked, FOPT per thread)
-        uint32_t c[FOPT];
+        // ---- commit the staged registers to LDS
         uint32_t csum = 0;
 #pragma unroll
-        for (int k = 0; k < FOPT; ++k) {
-            const int q = threadIdx.x * FOPT + k;
-            c[k] = q < nown ? fa.ocnt[sa.owner0 + o0 + q] : 0u;
-            csum += c[k];
-        }
+        for (int k = 0; k < FOPT; ++k) csum += R.c[k];
         uint32_t ttot;
         uint32_t run = dev::block_exclusive_sum<FB>(csum, scratch, &ttot);
         const uint32_t seg_first = contig_off(fa.off, fa.n_contigs, sa.ogs[o0]);
@@ -256,46 +322,59 @@ __global__ __launch_bounds__(FB) void k_fill(FillArgs fa) {
 #pragma unroll
         for (int k = 0; k < FOPT; ++k) {
             const int q = threadIdx.x * FOPT + k;
-            uint32_t lo = 0;
             if (q < nown) {
-                const int64_t j = o0 + q;
-                lo = fa.olo[sa.owner0 + j];
-                const uint32_t og = sa.ogs[j];
-                const uint32_t sg =
-                    seg_first == seg_last ? seg_first : contig_off(fa.off, fa.n_contigs, og);
-                s_own[q] = u32x4{og, sa.oge[j], sa.orow[j], sg};
+                const uint32_t sg = seg_first == seg_last
+                                        ? seg_first
+                                        : contig_off(fa.off, fa.n_contigs, R.og[k]);
+                s_own[q] = u32x4{R.og[k], R.oe[k], R.orw[k], sg};
             }
-            s_lo_off[q] = make_uint2(lo, run);
-            run += c[k];
+            s_lo_off[q] = make_uint2(R.lo[k], run);
+            run += R.c[k];
         }
         if (threadIdx.x == 0) s_lo_off[OT] = make_uint2(0u, ttot);
-        // ---- partner window
-        const uint32_t wlo = fa.win[2 * t], whi = fa.win[2 * t + 1];
+        const uint32_t wlo = R.wlo, whi = R.whi;
         const bool par_lds = (int64_t)whi - wlo <= PCAP;
-        if (par_lds)
-            for (int i = threadIdx.x; i < (int)(whi - wlo); i += FB)
-                s_par[i] = u32x4{sa.pgs[wlo + i], sa.pge[wlo + i], sa.prow[wlo + i], 0u};
+        if (par_lds) {
+#pragma unroll
+            for (int k = 0; k < PPT; ++k) {
+                const int i = k * FB + threadIdx.x;
+                if (i < (int)(whi - wlo)) s_par[i] = u32x4{R.pg[k], R.pe[k], R.pr[k], 0u};
+            }
+        }
         __syncthreads();
-        // ---- this tile's slice of the output window, one chunk per wave
+        // ---- prefetch the next tile (its loads overlap this tile's stores)
+        const bool more = t + 1 < fa.ntiles && (int64_t)fa.toff[t + 1] < oend;
+        if (more) tile_load(fa, t + 1, R);
+        // ---- this tile's slice of the output window, in granules dealt
+        // round-robin to the waves (wave w: granules w, w + FW, ...).  The
+        // default granule is one equal chunk per wave: 2048-record granules
+        // (the fastest shape of the plain store probe, profiles/
+        // r05_bw_probe.jsonl) measured 2% slower inside the fill
+        // (profiles/r05_fill_sweep.txt)
         const int64_t lb = max(ob - tbase, (int64_t)0);
         const int64_t le = min(oend - tbase, (int64_t)ttot);
-        const int64_t per = ((le - lb + FW - 1) / FW + 63) & ~(int64_t)63;
-        const int64_t wb = lb + w * per;
-        const int64_t we = min(le, wb + per);
-        int64_t o = wb + lane;
-        if (wb < we) {
-            // owner of the wave's first output (largest q with off_q <= o)
-            int lo_q = 0, hi_q = nown;
-            const uint32_t key = (uint32_t)min(o, we - 1);
-            while (lo_q < hi_q) {
-                int mid = (lo_q + hi_q) >> 1;
-                if (s_lo_off[mid].y <= key)
-                    lo_q = mid + 1;
-                else
-                    hi_q = mid;
+        // equal shares: `rounds` granules per wave of ~GR records each, so no
+        // wave idles at the tile's closing barrier
+        const int64_t rounds = max((int64_t)1, (le - lb + FW * gran - 1) / (FW * gran));
+        const int64_t gsz = (((le - lb + FW * rounds - 1) / (FW * rounds)) + 63) & ~(int64_t)63;
+        int q = 0;
+        for (int64_t gb = lb + (int64_t)w * gsz; gb < le; gb += (int64_t)FW * gsz) {
+            const int64_t gend = min(le, gb + gsz);
+            int64_t o = gb + lane;
+            {
+                // owner of this lane's first output (largest q with off_q <= o)
+                int lo_q = q, hi_q = nown;
+                const uint32_t key = (uint32_t)min(o, gend - 1);
+                while (lo_q < hi_q) {
+                    int mid = (lo_q + hi_q) >> 1;
+                    if (s_lo_off[mid].y <= key)
+                        lo_q = mid + 1;
+                    else
+                        hi_q = mid;
+                }
+                q = lo_q - 1;
             }
-            int q = lo_q - 1;
-            for (; o < we; o += 64) {
+            for (; o < gend; o += 64) {
                 while (s_lo_off[q + 1].y <= (uint32_t)o) ++q;
                 const uint2 lof = s_lo_off[q];
                 const uint32_t p = lof.x + ((uint32_t)o - lof.y);
@@ -319,6 +398,7 @@ __global__ __launch_bounds__(FB) void k_fill(FillArgs fa) {
             }
         }
         __syncthreads();
+        if (!more) break;
         ++t;
     }
     if (CKSUM) {
@@ -460,6 +540,38 @@ FillArgs fill_args(PairsPlan *pl) {
     return fa;
 }
 
+// Output records per fill workgroup.  Default (0): one wave of resident
+// workgroups covers the window, each prefetching its next tile behind its
+// stores (1-3% faster than 131072-record workgroups,
+// profiles/r05_fill_sweep.txt); LIME_FILL_SPAN overrides it for tuning.
+int64_t fill_span(int64_t count) {
+    static const int64_t env = [] {
+        const char *e = getenv("LIME_FILL_SPAN");
+        return e ? (int64_t)atoll(e) : (int64_t)-1;
+    }();
+    int64_t per = env < 0 ? 0 : env;
+    if (per == 0) {
+        int dev = 0, cus = 256, occ = 2;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fill<false>, FB, 0);
+        const int64_t slots = (int64_t)cus * (occ > 0 ? occ : 1);
+        per = (count + slots - 1) / slots;
+    }
+    per = (per + 63) & ~(int64_t)63;
+    return per < 4096 ? 4096 : per;
+}
+
+// Wave granule of the fill (records); LIME_FILL_GRAN overrides GR for tuning.
+int64_t fill_gran() {
+    static const int64_t g = [] {
+        const char *e = getenv("LIME_FILL_GRAN");
+        const int64_t v = e ? (int64_t)atoll(e) : GR;
+        return v < 64 ? (int64_t)64 : v;
+    }();
+    return g;
+}
+
 int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_t *cksum) {
     lime_ctx *ctx = pl->ctx;
     if (count <= 0) return LIME_OK;
@@ -477,14 +589,15 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
             hipLaunchKernelGGL(k_fill_filtered<false>, dim3(grid), dim3(IB), 0, S(ctx), fa,
                                pl->threshold);
     } else {
-        const int64_t g0 = first / SBLK;
-        const int64_t g1 = (first + count + SBLK - 1) / SBLK;
-        const int64_t grid = g1 - g0;
+        const int64_t per = fill_span(count);
+        const int64_t grid = (count + per - 1) / per;
         if (grid > 0x7fffffff) return fail(LIME_ERR_OVERFLOW, "fill window too large");
         if (cksum)
-            hipLaunchKernelGGL(k_fill<true>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa);
+            hipLaunchKernelGGL(k_fill<true>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa, per,
+                               fill_gran());
         else
-            hipLaunchKernelGGL(k_fill<false>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa);
+            hipLaunchKernelGGL(k_fill<false>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa, per,
+                               fill_gran());
     }
     LIME_HIP(hipGetLastError());
     return LIME_OK;

@@ -12,13 +12,13 @@
 // contig change by itself.  Run r = [gs[first_r], M at first_{r+1}), the last
 // run ends at max(ge).
 //
-// Kernels (tile = 4096 rows):
-//   k_tile_max    per-tile max of ge                               4 B/row
-//   k_scan_max    exclusive max over tiles (one block)
-//   k_runs_count  M_i, flags, runs per tile                        8 B/row
-//   scan          exclusive sum of runs per tile
-//   k_runs_write  run starts/ends + run id of every row            8 B/row + 4 B/row + 8 B/run
-// The same scan gives the inclusive prefix max used by subtract.
+// k_merge_scan: ONE pass over the set (8 B read + 4 B run id written per
+// row, 8 B per run).  Tiles of 4096 rows are taken in ticket order; a tile
+// publishes its max(ge) and learns M at its first row by a decoupled
+// look-back over its predecessors' (flag | value) status words, flags its
+// rows, then publishes its run count and learns its first run index by a
+// second look-back.  The multi-pass kernels (k_tile_max, k_scan_max,
+// k_prefix_max) remain for subtract's inclusive prefix max.
 #include "common.hpp"
 
 namespace lime {
@@ -78,87 +78,157 @@ __device__ __forceinline__ void load_blocked(const T *__restrict__ src, int64_t 
     __syncthreads();
 }
 
-// Per tile: exclusive prefix max M of every row; returns flags as a bitmask.
-__device__ __forceinline__ uint32_t tile_flags(const uint32_t *__restrict__ gs,
-                                               const uint32_t *__restrict__ ge, int64_t base,
-                                               int64_t n, uint32_t carry, uint32_t *lds,
-                                               uint32_t *scratch, uint32_t (&M)[MITEMS],
-                                               uint32_t (&s)[MITEMS], uint32_t (&e)[MITEMS]) {
-    load_blocked(gs, base, n, 0xffffffffu, lds, s);
-    load_blocked(ge, base, n, 0u, lds, e);
+// ---------------------------------------------------------- single pass
+constexpr uint64_t ST_AGG = 1ull << 62;  // tile aggregate published
+constexpr uint64_t ST_INC = 2ull << 62;  // inclusive prefix published
+constexpr uint64_t ST_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ void st_publish(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t st_poll(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Decoupled look-back by one wave: combine (max or sum) of the values of
+// every tile before `tile`.  Lane l inspects tile base - l; a window of 64
+// predecessors is consumed once all of them have published at least an
+// aggregate, and the walk stops at the nearest inclusive prefix.  Tiles are
+// numbered in ticket order, so every predecessor is already running and
+// publishes without waiting on this tile: the spin always ends.
+template <bool MAX>
+__device__ __forceinline__ uint64_t lookback(const uint64_t *st, int64_t tile) {
+    const int lane = dev::lane_id();
+    uint64_t acc = 0;
+    for (int64_t base = tile - 1; base >= 0; base -= 64) {
+        const int64_t i = base - lane;
+        uint64_t v = ST_INC;  // before tile 0: inclusive identity
+        if (i >= 0) {
+            do {
+                v = st_poll(st + i);
+            } while ((v >> 62) == 0);
+        }
+        const uint64_t inc = __ballot((v >> 62) == 2);
+        uint64_t val = v & ST_VAL;
+        if (inc) {
+            const int first = __ffsll((unsigned long long)inc) - 1;
+            if (lane > first) val = 0;
+        }
+        const uint64_t r = MAX ? dev::wave_reduce_max(val) : dev::wave_reduce_sum(val);
+        acc = MAX ? (acc > r ? acc : r) : acc + r;
+        if (inc) break;
+    }
+    return acc;
+}
+
+struct MergeScanArgs {
+    const uint32_t *gs, *ge;
+    int64_t n;
+    uint64_t *st_max, *st_cnt;  // per-tile status words (zeroed before launch)
+    uint32_t *ticket;
+    uint32_t *run_gs, *run_ge;  // capacity n
+    uint32_t *run_of_sorted;    // may be null
+    uint64_t *total;            // runs
+};
+
+__global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
+    __shared__ uint32_t scratch[MB / 64 + 1];
+    __shared__ uint64_t s_carry;
+    __shared__ uint32_t s_tile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t n = a.n;
+    const int64_t r0 = tile * MTILE + (int64_t)threadIdx.x * MITEMS;  // blocked rows
+    uint32_t s[MITEMS], e[MITEMS];
+    if (r0 + MITEMS <= n) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(a.gs + r0);
+        const uint4 *e4 = reinterpret_cast<const uint4 *>(a.ge + r0);
+#pragma unroll
+        for (int k = 0; k < MITEMS / 4; ++k) {
+            const uint4 x = s4[k], y = e4[k];
+            s[4 * k] = x.x, s[4 * k + 1] = x.y, s[4 * k + 2] = x.z, s[4 * k + 3] = x.w;
+            e[4 * k] = y.x, e[4 * k + 1] = y.y, e[4 * k + 2] = y.z, e[4 * k + 3] = y.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < MITEMS; ++k) {
+            const bool v = r0 + k < n;
+            s[k] = v ? a.gs[r0 + k] : 0xffffffffu;
+            e[k] = v ? a.ge[r0 + k] : 0u;
+        }
+    }
     uint32_t agg = 0;
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) agg = max(agg, e[k]);
-    uint32_t tot;
-    uint32_t pre = dev::block_exclusive_max<MB>(agg, 0u, scratch, &tot);
-    uint32_t run = max(pre, carry);
+    uint32_t tmax;
+    const uint32_t pre = dev::block_exclusive_max<MB>(agg, 0u, scratch, &tmax);
+    // ---- chain 1: M at the tile's first row
+    if (threadIdx.x < 64) {
+        uint64_t ex = 0;
+        if (tile == 0) {
+            if (threadIdx.x == 0) st_publish(a.st_max, ST_INC | tmax);
+        } else {
+            if (threadIdx.x == 0) st_publish(a.st_max + tile, ST_AGG | tmax);
+            ex = lookback<true>(a.st_max, tile);
+            if (threadIdx.x == 0)
+                st_publish(a.st_max + tile, ST_INC | (ex > tmax ? ex : (uint64_t)tmax));
+        }
+        if (threadIdx.x == 0) s_carry = ex;
+    }
+    __syncthreads();
+    uint32_t M = max(pre, (uint32_t)s_carry);
+    uint32_t Mk[MITEMS];
     uint32_t flags = 0;
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) {
-        M[k] = run;
-        int64_t i = base + threadIdx.x * MITEMS + k;
-        if (i < n && run <= s[k]) flags |= 1u << k;
-        run = max(run, e[k]);
+        Mk[k] = M;
+        if (r0 + k < n && M <= s[k]) flags |= 1u << k;
+        M = max(M, e[k]);
     }
-    return flags;
-}
-
-__global__ __launch_bounds__(MB) void k_runs_count(const uint32_t *__restrict__ gs,
-                                                   const uint32_t *__restrict__ ge, int64_t n,
-                                                   const uint32_t *__restrict__ tpre,
-                                                   uint32_t *__restrict__ tcnt) {
-    __shared__ uint32_t lds[MTILE];
-    __shared__ uint32_t scratch[MB / 64 + 1];
-    const int64_t base = (int64_t)blockIdx.x * MTILE;
-    uint32_t M[MITEMS], s[MITEMS], e[MITEMS];
-    uint32_t f = tile_flags(gs, ge, base, n, tpre[blockIdx.x], lds, scratch, M, s, e);
-    uint32_t c = __popc(f);
-    c = dev::wave_reduce_sum(c);
-    __shared__ uint32_t ws[MB / 64];
-    if (dev::lane_id() == 0) ws[threadIdx.x / 64] = c;
+    uint32_t ctot;
+    const uint32_t rpre = dev::block_exclusive_sum<MB>((uint32_t)__popc(flags), scratch, &ctot);
+    // ---- chain 2: index of the tile's first run
+    if (threadIdx.x < 64) {
+        uint64_t ex = 0;
+        if (tile == 0) {
+            if (threadIdx.x == 0) st_publish(a.st_cnt, ST_INC | ctot);
+        } else {
+            if (threadIdx.x == 0) st_publish(a.st_cnt + tile, ST_AGG | ctot);
+            ex = lookback<false>(a.st_cnt, tile);
+            if (threadIdx.x == 0) st_publish(a.st_cnt + tile, ST_INC | (ex + ctot));
+        }
+        if (threadIdx.x == 0) s_carry = ex;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int i = 0; i < MB / 64; ++i) t += ws[i];
-        tcnt[blockIdx.x] = t;
-    }
-}
-
-__global__ __launch_bounds__(MB) void k_runs_write(
-    const uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge, int64_t n,
-    const uint32_t *__restrict__ tpre, const uint32_t *__restrict__ toff,
-    uint32_t *__restrict__ run_gs, uint32_t *__restrict__ run_ge,
-    uint32_t *__restrict__ run_of_sorted) {
-    __shared__ uint32_t lds[MTILE];
-    __shared__ uint32_t scratch[MB / 64 + 1];
-    const int64_t base = (int64_t)blockIdx.x * MTILE;
-    uint32_t M[MITEMS], s[MITEMS], e[MITEMS];
-    uint32_t f = tile_flags(gs, ge, base, n, tpre[blockIdx.x], lds, scratch, M, s, e);
-    uint32_t tot;
-    uint32_t r = toff[blockIdx.x] + dev::block_exclusive_sum<MB>((uint32_t)__popc(f), scratch, &tot);
+    uint32_t r = (uint32_t)s_carry + rpre;  // runs started before this thread's rows
     uint32_t rid[MITEMS];
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) {
-        int64_t i = base + threadIdx.x * MITEMS + k;
+        const int64_t i = r0 + k;
         if (i < n) {
-            if (f & (1u << k)) {
-                run_gs[r] = s[k];
-                if (r > 0) run_ge[r - 1] = M[k];
+            if (flags & (1u << k)) {
+                a.run_gs[r] = s[k];
+                if (r > 0) a.run_ge[r - 1] = Mk[k];
                 ++r;
             }
-            if (i == n - 1) run_ge[r - 1] = max(M[k], e[k]);
+            if (i == n - 1) {
+                a.run_ge[r - 1] = max(Mk[k], e[k]);
+                *a.total = r;
+            }
         }
         rid[k] = r - 1;
     }
-    if (run_of_sorted) {
-        // blocked -> striped through LDS for coalesced stores
+    if (a.run_of_sorted) {
+        if (r0 + MITEMS <= n) {
+            uint4 *o4 = reinterpret_cast<uint4 *>(a.run_of_sorted + r0);
 #pragma unroll
-        for (int k = 0; k < MITEMS; ++k) lds[threadIdx.x * MITEMS + k] = rid[k];
-        __syncthreads();
+            for (int k = 0; k < MITEMS / 4; ++k)
+                o4[k] = make_uint4(rid[4 * k], rid[4 * k + 1], rid[4 * k + 2], rid[4 * k + 3]);
+        } else {
 #pragma unroll
-        for (int k = 0; k < MITEMS; ++k) {
-            int64_t i = base + k * MB + threadIdx.x;
-            if (i < n) run_of_sorted[i] = lds[k * MB + threadIdx.x];
+            for (int k = 0; k < MITEMS; ++k)
+                if (r0 + k < n) a.run_of_sorted[r0 + k] = rid[k];
         }
     }
 }
@@ -231,29 +301,45 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
         return LIME_OK;
     }
     const int64_t nt = (n + MTILE - 1) / MTILE;
-    uint32_t *tpre, *tcnt, *toff, *total;
-    LIME_TRY(tile_prefix(ctx, set->ge, n, &tpre));
-    LIME_TRY(alloc(ctx, &tcnt, (size_t)nt));
-    LIME_TRY(alloc(ctx, &toff, (size_t)nt));
-    LIME_TRY(alloc(ctx, &total, 1));
-    hipLaunchKernelGGL(k_runs_count, dim3((unsigned)nt), dim3(MB), 0, S(ctx), set->gs, set->ge, n,
-                       (const uint32_t *)tpre, tcnt);
-    LIME_HIP(hipGetLastError());
-    LIME_TRY(scan_exclusive_u32(ctx, tcnt, toff, nt, total));
-    uint32_t nr = 0;
-    LIME_TRY(read_back(ctx, &nr, total, sizeof(nr)));
-    LIME_TRY(alloc(ctx, &res->gs, nr));
-    LIME_TRY(alloc(ctx, &res->ge, nr));
+    // status words of both chains + ticket + total in one zeroed block
+    uint64_t *st;
+    LIME_TRY(alloc(ctx, &st, (size_t)(2 * nt + 2)));
+    LIME_HIP(hipMemsetAsync(st, 0, sizeof(uint64_t) * (size_t)(2 * nt + 2), S(ctx)));
+    uint32_t *run_gs, *run_ge;
+    LIME_TRY(alloc(ctx, &run_gs, (size_t)n));
+    LIME_TRY(alloc(ctx, &run_ge, (size_t)n));
     if (want_run_ids) LIME_TRY(alloc(ctx, &res->run_of_sorted, (size_t)n));
-    hipLaunchKernelGGL(k_runs_write, dim3((unsigned)nt), dim3(MB), 0, S(ctx), set->gs, set->ge, n,
-                       (const uint32_t *)tpre, (const uint32_t *)toff, res->gs, res->ge,
-                       res->run_of_sorted);
+    MergeScanArgs a;
+    a.gs = set->gs;
+    a.ge = set->ge;
+    a.n = n;
+    a.st_max = st;
+    a.st_cnt = st + nt;
+    a.ticket = reinterpret_cast<uint32_t *>(st + 2 * nt);
+    a.total = st + 2 * nt + 1;
+    a.run_gs = run_gs;
+    a.run_ge = run_ge;
+    a.run_of_sorted = res->run_of_sorted;
+    hipLaunchKernelGGL(k_merge_scan, dim3((unsigned)nt), dim3(MB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
-    release(ctx, tpre);
-    release(ctx, tcnt);
-    release(ctx, toff);
-    release(ctx, total);
-    res->n = nr;
+    uint64_t nr = 0;
+    LIME_TRY(read_back(ctx, &nr, a.total, sizeof(nr)));
+    release(ctx, st);
+    if (nr * 2 > (uint64_t)n) {
+        // most rows start a run: keep the capacity-n arrays
+        res->gs = run_gs;
+        res->ge = run_ge;
+    } else {
+        LIME_TRY(alloc(ctx, &res->gs, (size_t)nr));
+        LIME_TRY(alloc(ctx, &res->ge, (size_t)nr));
+        LIME_HIP(hipMemcpyAsync(res->gs, run_gs, sizeof(uint32_t) * nr, hipMemcpyDeviceToDevice,
+                                S(ctx)));
+        LIME_HIP(hipMemcpyAsync(res->ge, run_ge, sizeof(uint32_t) * nr, hipMemcpyDeviceToDevice,
+                                S(ctx)));
+        release(ctx, run_gs);
+        release(ctx, run_ge);
+    }
+    res->n = (int64_t)nr;
     return LIME_OK;
 }
 

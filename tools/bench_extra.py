@@ -89,7 +89,7 @@ def main():
             ms = t1.elapsed_time(t2)
             b = 12 * n + 8 * runs  # read gs+ge, write run id per row, write runs
             return {"sort_ms": t0.elapsed_time(t1), "merge_ms": ms, "runs": runs}, \
-                {"kernel": "merge (k_tile_max, k_runs_count, k_runs_write)", "bound": "hbm",
+                {"kernel": "k_merge_scan (single pass, decoupled look-back)", "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "c4":
         ia = gen(int(1e7 * a.scale), 0xD, 50, 500)

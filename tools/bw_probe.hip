@@ -1,7 +1,7 @@
 // bw_probe.hip -- calibration of the HBM write ceiling the fill kernel is
-// judged against: streaming 16-B-per-lane stores of N records, in the same
-// block shape as k_fill (one workgroup writes SBLK consecutive records),
-// with plain vs non-temporal stores, plus a copy (read + write) reference.
+// judged against: streaming stores of N 16-B records in several shapes
+// (k_fill's block shape, persistent grid-stride, dword-per-lane, unrolled,
+// non-temporal), plus a copy (read + write) reference.
 //   ./bw_probe [records]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -36,9 +36,62 @@ __global__ __launch_bounds__(512) void k_store_wavechunk(u32x4 *out, long n, lon
     }
 }
 
+// persistent grid-stride, 16 B per lane
+template <int TB>
+__global__ __launch_bounds__(TB) void k_store_grid(u32x4 *out, long n) {
+    for (long i = (long)blockIdx.x * TB + threadIdx.x; i < n; i += (long)gridDim.x * TB) {
+        u32x4 v = {(unsigned)i, (unsigned)(i >> 7), 3u, 7u};
+        out[i] = v;
+    }
+}
+
+// 4 B per lane (256 B per wave instruction), per_block*4 dwords per block
+__global__ __launch_bounds__(256) void k_store_dword(unsigned *out, long n, long per_block) {
+    long b0 = (long)blockIdx.x * per_block;
+    long b1 = b0 + per_block < n ? b0 + per_block : n;
+    for (long i = b0 + threadIdx.x; i < b1; i += 256) out[i] = (unsigned)i;
+}
+
+// 4 independent 16-B stores in flight per iteration, wave-contiguous
+__global__ __launch_bounds__(256) void k_store_unroll4(u32x4 *out, long n, long per_block) {
+    long b0 = (long)blockIdx.x * per_block;
+    long b1 = b0 + per_block < n ? b0 + per_block : n;
+    for (long i = b0 + threadIdx.x; i < b1; i += 1024) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            long j = i + 256 * k;
+            if (j < b1) out[j] = u32x4{(unsigned)j, (unsigned)(j >> 7), 5u, 7u};
+        }
+    }
+}
+
+// 512-thread workgroup over per_block records; wave w writes granules of G
+// records at w*G, w*G + 8G, ... (G = 64: block-striped; G = per_block/8:
+// one chunk per wave)
+template <int G>
+__global__ __launch_bounds__(512) void k_store_gran(u32x4 *out, long n, long per_block) {
+    long b0 = (long)blockIdx.x * per_block;
+    long b1 = b0 + per_block < n ? b0 + per_block : n;
+    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    for (long g = b0 + (long)w * G; g < b1; g += 8L * G)
+        for (int k = 0; k < G; k += 64) {
+            long i = g + k + lane;
+            if (i < b1) out[i] = u32x4{(unsigned)i, (unsigned)(i >> 7), 9u, 7u};
+        }
+}
+
 __global__ __launch_bounds__(256) void k_copy(const u32x4 *in, u32x4 *out, long n) {
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
         out[i] = in[i];
+}
+
+__global__ __launch_bounds__(256) void k_read(const u32x4 *in, long n, unsigned *sink) {
+    unsigned acc = 0;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        u32x4 v = in[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
 }
 
 #define CK(x)                                                         \
@@ -50,60 +103,83 @@ __global__ __launch_bounds__(256) void k_copy(const u32x4 *in, u32x4 *out, long 
         }                                                             \
     } while (0)
 
+static hipEvent_t ea, eb;
+
+template <class F>
+static void timeit(const char *name, long recs, double bytes, F launch) {
+    float best = 1e30f;
+    for (int r = 0; r < 6; ++r) {
+        CK(hipEventRecord(ea));
+        launch();
+        CK(hipEventRecord(eb));
+        CK(hipEventSynchronize(eb));
+        float ms;
+        CK(hipEventElapsedTime(&ms, ea, eb));
+        if (r && ms < best) best = ms;
+    }
+    CK(hipGetLastError());
+    printf("{\"probe\": \"%s\", \"records\": %ld, \"ms\": %.3f, \"GBps\": %.1f}\n", name, recs, best,
+           bytes / best / 1e6);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     long n = argc > 1 ? atol(argv[1]) : (1L << 31);
     const long per_block = 131072;
     u32x4 *out, *in;
+    unsigned *sink;
     CK(hipMalloc(&out, n * 16));
-    hipEvent_t a, b;
-    CK(hipEventCreate(&a));
-    CK(hipEventCreate(&b));
+    CK(hipMalloc(&sink, 64));
+    CK(hipEventCreate(&ea));
+    CK(hipEventCreate(&eb));
     unsigned grid = (unsigned)((n + per_block - 1) / per_block);
-    for (int variant = 0; variant < 2; ++variant) {
-        float best = 1e30f;
-        for (int r = 0; r < 6; ++r) {
-            CK(hipEventRecord(a));
-            if (variant)
-                hipLaunchKernelGGL(k_store<true>, dim3(grid), dim3(256), 0, 0, out, n, per_block);
-            else
-                hipLaunchKernelGGL(k_store<false>, dim3(grid), dim3(256), 0, 0, out, n, per_block);
-            CK(hipEventRecord(b));
-            CK(hipEventSynchronize(b));
-            float ms;
-            CK(hipEventElapsedTime(&ms, a, b));
-            if (r && ms < best) best = ms;
+    timeit("store16_plain", n, n * 16.0, [&] {
+        hipLaunchKernelGGL(k_store<false>, dim3(grid), dim3(256), 0, 0, out, n, per_block);
+    });
+    timeit("store16_nt", n, n * 16.0, [&] {
+        hipLaunchKernelGGL(k_store<true>, dim3(grid), dim3(256), 0, 0, out, n, per_block);
+    });
+    timeit("store16_wavechunk512", n, n * 16.0, [&] {
+        hipLaunchKernelGGL(k_store_wavechunk, dim3(grid), dim3(512), 0, 0, out, n, per_block);
+    });
+    timeit("store16_unroll4", n, n * 16.0, [&] {
+        hipLaunchKernelGGL(k_store_unroll4, dim3(grid), dim3(256), 0, 0, out, n, per_block);
+    });
+    for (unsigned g : {1024u, 2048u, 4096u, 16384u})
+        for (int tb : {256, 1024}) {
+            char name[64];
+            snprintf(name, sizeof name, "store16_grid%u_tb%d", g, tb);
+            timeit(name, n, n * 16.0, [&] {
+                if (tb == 256)
+                    hipLaunchKernelGGL(k_store_grid<256>, dim3(g), dim3(256), 0, 0, out, n);
+                else
+                    hipLaunchKernelGGL(k_store_grid<1024>, dim3(g), dim3(1024), 0, 0, out, n);
+            });
         }
-        printf("{\"probe\": \"store16_%s\", \"records\": %ld, \"ms\": %.3f, \"GBps\": %.1f}\n",
-               variant ? "nt" : "plain", n, best, n * 16.0 / best / 1e6);
+    timeit("store4_dword", n * 4, n * 16.0, [&] {
+        hipLaunchKernelGGL(k_store_dword, dim3(grid), dim3(256), 0, 0, (unsigned *)out, n * 4,
+                           per_block * 4);
+    });
+    for (long pb : {131072L, 524288L}) {
+#define GRAN(G)                                                                             \
+    {                                                                                       \
+        char name[64];                                                                      \
+        snprintf(name, sizeof name, "gran%d_wg512_per%ld", G, pb);                          \
+        unsigned gg = (unsigned)((n + pb - 1) / pb);                                        \
+        timeit(name, n, n * 16.0, [&] {                                                     \
+            hipLaunchKernelGGL(k_store_gran<G>, dim3(gg), dim3(512), 0, 0, out, n, pb);     \
+        });                                                                                 \
     }
-    {
-        float best = 1e30f;
-        for (int r = 0; r < 6; ++r) {
-            CK(hipEventRecord(a));
-            hipLaunchKernelGGL(k_store_wavechunk, dim3(grid), dim3(512), 0, 0, out, n, per_block);
-            CK(hipEventRecord(b));
-            CK(hipEventSynchronize(b));
-            float ms;
-            CK(hipEventElapsedTime(&ms, a, b));
-            if (r && ms < best) best = ms;
-        }
-        printf("{\"probe\": \"store16_wavechunk512\", \"records\": %ld, \"ms\": %.3f, \"GBps\": %.1f}\n",
-               n, best, n * 16.0 / best / 1e6);
+        GRAN(64) GRAN(256) GRAN(512) GRAN(2048) GRAN(8192)
     }
     long nc = n / 2;
     CK(hipMalloc(&in, nc * 16));
     CK(hipMemset(in, 1, nc * 16));
-    float best = 1e30f;
-    for (int r = 0; r < 6; ++r) {
-        CK(hipEventRecord(a));
+    timeit("copy16", nc, nc * 32.0, [&] {
         hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, in, out, nc);
-        CK(hipEventRecord(b));
-        CK(hipEventSynchronize(b));
-        float ms;
-        CK(hipEventElapsedTime(&ms, a, b));
-        if (r && ms < best) best = ms;
-    }
-    printf("{\"probe\": \"copy16\", \"records\": %ld, \"ms\": %.3f, \"GBps\": %.1f}\n", nc, best,
-           nc * 32.0 / best / 1e6);
+    });
+    timeit("read16", n, n * 16.0, [&] {
+        hipLaunchKernelGGL(k_read, dim3(8192), dim3(256), 0, 0, out, n, sink);
+    });
     return 0;
 }

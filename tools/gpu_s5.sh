@@ -1,0 +1,6 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "intersect or scaled_c2 or stranded" > gpurun_out/s5_tests.txt 2>&1
+for g in 1024 2048 4096 1000000; do for sp in 131072 0; do
+  LIME_FILL_GRAN=$g LIME_FILL_SPAN=$sp timeout -k 10 200 python bench.py --steps 5 --no-cpu-baseline > gpurun_out/s5_bench_${g}_$sp.txt 2>&1
+done; done

@@ -45,6 +45,7 @@ struct PairsPlan {
     uint32_t *olo = nullptr, *ocnt = nullptr;  // per owner, stream 0 then stream 1
     uint64_t *toff = nullptr;                  // per tile exclusive offsets
     uint32_t *win = nullptr;                   // per tile partner window [lo, hi)
+    uint32_t *tseg = nullptr;                  // per tile contig offset (0xffffffff: mixed)
     int64_t total = 0;
 };
 
@@ -98,8 +99,52 @@ __device__ __forceinline__ int64_t wave_lower_bound(const uint32_t *__restrict__
     return lo + __popcll(__ballot(less));
 }
 
+__device__ __forceinline__ uint32_t contig_off(const uint32_t *__restrict__ off, int32_t nc,
+                                               uint32_t g) {
+    // largest c with off[c] <= g
+    int64_t c = dev::upper_bound(off, 0, (int64_t)nc, g) - 1;
+    return off[c < 0 ? 0 : c];
+}
+
+// Two independent lower_bounds by one wave, their probes interleaved so
+// both searches share the same 5-6 memory round trips.
+__device__ __forceinline__ void wave_lower_bound2(const uint32_t *__restrict__ a, int64_t n,
+                                                  int64_t key0, int64_t key1, int64_t &r0,
+                                                  int64_t &r1) {
+    int64_t lo0 = 0, hi0 = n, lo1 = 0, hi1 = n;
+    const int lane = dev::lane_id();
+    while (hi0 - lo0 > 64 || hi1 - lo1 > 64) {
+        const int64_t st0 = (hi0 - lo0 + 64) / 65, st1 = (hi1 - lo1 + 64) / 65;
+        const int64_t i0 = lo0 + st0 * (lane + 1) - 1, i1 = lo1 + st1 * (lane + 1) - 1;
+        const bool a0 = hi0 - lo0 > 64 && i0 < hi0;
+        const bool a1 = hi1 - lo1 > 64 && i1 < hi1;
+        const uint32_t v0 = a0 ? a[i0] : 0u, v1 = a1 ? a[i1] : 0u;
+        if (hi0 - lo0 > 64) {
+            const int c = __popcll(__ballot(a0 && (int64_t)v0 < key0));
+            const int64_t nlo = c == 0 ? lo0 : lo0 + st0 * c;
+            hi0 = c == 64 ? hi0 : min(hi0, lo0 + st0 * (c + 1) - 1);
+            lo0 = nlo;
+        }
+        if (hi1 - lo1 > 64) {
+            const int c = __popcll(__ballot(a1 && (int64_t)v1 < key1));
+            const int64_t nlo = c == 0 ? lo1 : lo1 + st1 * c;
+            hi1 = c == 64 ? hi1 : min(hi1, lo1 + st1 * (c + 1) - 1);
+            lo1 = nlo;
+        }
+    }
+    const int64_t j0 = lo0 + lane, j1 = lo1 + lane;
+    const bool b0 = j0 < hi0, b1 = j1 < hi1;
+    const uint32_t v0 = b0 ? a[j0] : 0u, v1 = b1 ? a[j1] : 0u;
+    r0 = lo0 + __popcll(__ballot(b0 && (int64_t)v0 < key0));
+    r1 = lo1 + __popcll(__ballot(b1 && (int64_t)v1 < key1));
+}
+
+// Per owner tile: partner window [lo, hi) and, when tseg is given, the
+// tile's contig offset (0xffffffff when its owners span several contigs).
 __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64_t ntiles,
-                                                uint32_t *__restrict__ win) {
+                                                uint32_t *__restrict__ win,
+                                                const uint32_t *__restrict__ off, int32_t nc,
+                                                uint32_t *__restrict__ tseg) {
     const int64_t t = (int64_t)blockIdx.x * (IB / 64) + threadIdx.x / 64;
     if (t >= ntiles) return;
     const int lane = dev::lane_id();
@@ -113,11 +158,16 @@ __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64
     // (subtract walks back from it even when the owner's range is empty)
     const int64_t lkey_last = (int64_t)sa.ogs[o1 - 1] + sa.lo_off;
     if (hmax < lkey_last) hmax = lkey_last;
-    const int64_t lo = wave_lower_bound(sa.pgs, sa.np, lkey);
-    const int64_t hi = wave_lower_bound(sa.pgs, sa.np, hmax);
+    int64_t lo, hi;
+    wave_lower_bound2(sa.pgs, sa.np, lkey, hmax, lo, hi);
     if (lane == 0) {
         win[2 * (sa.tile0 + t)] = (uint32_t)lo;
         win[2 * (sa.tile0 + t) + 1] = (uint32_t)hi;
+    }
+    if (tseg && lane == 1) {
+        const uint32_t a = contig_off(off, nc, sa.ogs[o0]);
+        const uint32_t b = contig_off(off, nc, sa.ogs[o1 - 1]);
+        tseg[sa.tile0 + t] = a == b ? a : 0xffffffffu;
     }
 }
 
@@ -132,6 +182,15 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
     const int64_t t = blockIdx.x;
     const int64_t o0 = t * OT;
     const int64_t o1 = min(o0 + OT, sa.no);
+    // owner loads first: they are independent of the window and overlap
+    // its two dependent round trips
+    uint32_t ogv[OPT], oev[OPT];
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+        const int64_t j = o0 + k * IB + threadIdx.x;
+        ogv[k] = j < o1 ? sa.ogs[j] : 0u;
+        oev[k] = j < o1 ? sa.oge[j] : 0u;
+    }
     const uint32_t wlo = win[2 * (sa.tile0 + t)], whi = win[2 * (sa.tile0 + t) + 1];
     const int64_t wlen = (int64_t)whi - wlo;
     const bool in_lds = wlen <= WCAP;
@@ -143,7 +202,7 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
     for (int k = 0; k < OPT; ++k) {
         const int64_t j = o0 + k * IB + threadIdx.x;
         if (j >= o1) break;
-        const uint32_t og = sa.ogs[j], oe = sa.oge[j];
+        const uint32_t og = ogv[k], oe = oev[k];
         int64_t lk, hk;
         owner_keys(og, oe, sa.lo_off, tp, lk, hk);
         // lo = lb(P, o.gs + lo_off) always (subtract's spanning walk starts
@@ -181,18 +240,13 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
     }
 }
 
-__device__ __forceinline__ uint32_t contig_off(const uint32_t *__restrict__ off, int32_t nc,
-                                               uint32_t g) {
-    // largest c with off[c] <= g
-    int64_t c = dev::upper_bound(off, 0, (int64_t)nc, g) - 1;
-    return off[c < 0 ? 0 : c];
-}
 
 struct FillArgs {
     StreamArgs s[2];
     const uint32_t *olo, *ocnt;
     const uint64_t *toff;
     const uint32_t *win;   // per tile partner window [lo, hi)
+    const uint32_t *tseg;  // per tile contig offset, 0xffffffff if mixed
     int64_t ntiles;
     const uint32_t *off;
     int32_t n_contigs;
@@ -204,8 +258,8 @@ struct FillArgs {
 constexpr int FB = 512;           // fill workgroup: 8 waves
 constexpr int FW = FB / 64;
 constexpr int FOPT = OT / FB;     // owners per thread when staging a tile
-constexpr int PCAP = 2048;        // LDS partner window (16 B records)
-constexpr int PPT = PCAP / FB;    // partner rows per thread when staging
+constexpr int PCAP = 1792;        // LDS partner window (16 B records): 3 workgroups per CU
+constexpr int PPT = (PCAP + FB - 1) / FB;  // partner rows per thread when staging
 constexpr int64_t GR = 1ll << 40;  // wave granule: default one equal chunk per wave
 
 // 65-ary wave search on the u64 tile offsets: largest t with toff[t] <= key
@@ -235,7 +289,7 @@ __device__ __forceinline__ int64_t wave_tile_of(const uint64_t *__restrict__ a, 
 struct TileRegs {
     uint32_t c[FOPT], lo[FOPT], og[FOPT], oe[FOPT], orw[FOPT];
     uint32_t pg[PPT], pe[PPT], pr[PPT];
-    uint32_t wlo, whi;
+    uint32_t wlo, whi, seg;
 };
 
 __device__ __forceinline__ int tile_stream(const FillArgs &fa, int64_t t) {
@@ -259,6 +313,7 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
     }
     r.wlo = fa.win[2 * t];
     r.whi = fa.win[2 * t + 1];
+    r.seg = fa.tseg[t];
     const int wl = (int)min((int64_t)(r.whi - r.wlo), (int64_t)PCAP);
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
@@ -267,6 +322,47 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
         r.pg[k] = v ? sa.pgs[r.wlo + i] : 0u;
         r.pe[k] = v ? sa.pge[r.wlo + i] : 0u;
         r.pr[k] = v ? sa.prow[r.wlo + i] : 0u;
+    }
+}
+
+// Emit outputs o, o + 64, ... < gend of one wave (lane-consecutive records).
+// The LDS-window form has no global loads in its loop, so the compiler
+// never makes an iteration wait (vmcnt) for the previous iteration's store:
+// each wave keeps its stores in flight.  The owner walk carries the current
+// (lo, off) pair and the next owner's pair in registers, leaving two
+// dependent LDS steps per iteration (walk, then owner + partner reads).
+template <bool LDSP, bool CKSUM>
+__device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, int st,
+                                     const uint2 *s_lo_off, const u32x4 *s_own,
+                                     const u32x4 *s_par, uint32_t wlo, int64_t tbase, int64_t o,
+                                     int64_t gend, int &q, uint64_t &hsum, uint64_t &hxor) {
+    uint2 lof = s_lo_off[q], nxt = s_lo_off[q + 1];
+    u32x4 *out = fa.out + (tbase - fa.first);
+    for (; o < gend; o += 64) {
+        const uint32_t ou = (uint32_t)o;
+        while (nxt.y <= ou) {
+            ++q;
+            lof = nxt;
+            nxt = s_lo_off[q + 1];
+        }
+        const uint32_t p = lof.x + (ou - lof.y);
+        const u32x4 ow = s_own[q];
+        u32x4 pa;
+        if (LDSP)
+            pa = s_par[p - wlo];
+        else
+            pa = u32x4{sa.pgs[p], sa.pge[p], sa.prow[p], 0u};
+        const uint32_t rs = (ow.x > pa.x ? ow.x : pa.x) - ow.w;
+        const uint32_t re = (ow.y < pa.y ? ow.y : pa.y) - ow.w;
+        const uint32_t ar = st == 0 ? ow.z : pa.z;
+        const uint32_t br = st == 0 ? pa.z : ow.z;
+        if (CKSUM) {
+            const uint64_t h = dev::pair_hash(rs, re, ar, br);
+            hsum += h;
+            hxor ^= h;
+        } else {
+            out[o] = u32x4{rs, re, ar, br};
+        }
     }
 }
 
@@ -284,7 +380,7 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
 // tile's staging data is prefetched into registers (TileRegs) before the
 // store loop.
 template <bool CKSUM>
-__global__ __launch_bounds__(FB) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
+__global__ __launch_bounds__(FB, 6) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
     __shared__ uint2 s_lo_off[OT + 1];
     __shared__ u32x4 s_own[OT];
     __shared__ u32x4 s_par[PCAP];
@@ -317,15 +413,12 @@ __global__ __launch_bounds__(FB) void k_fill(FillArgs fa, int64_t per, int64_t g
         for (int k = 0; k < FOPT; ++k) csum += R.c[k];
         uint32_t ttot;
         uint32_t run = dev::block_exclusive_sum<FB>(csum, scratch, &ttot);
-        const uint32_t seg_first = contig_off(fa.off, fa.n_contigs, sa.ogs[o0]);
-        const uint32_t seg_last = contig_off(fa.off, fa.n_contigs, sa.ogs[o0 + nown - 1]);
 #pragma unroll
         for (int k = 0; k < FOPT; ++k) {
             const int q = threadIdx.x * FOPT + k;
             if (q < nown) {
-                const uint32_t sg = seg_first == seg_last
-                                        ? seg_first
-                                        : contig_off(fa.off, fa.n_contigs, R.og[k]);
+                const uint32_t sg =
+                    R.seg != 0xffffffffu ? R.seg : contig_off(fa.off, fa.n_contigs, R.og[k]);
                 s_own[q] = u32x4{R.og[k], R.oe[k], R.orw[k], sg};
             }
             s_lo_off[q] = make_uint2(R.lo[k], run);
@@ -374,28 +467,12 @@ __global__ __launch_bounds__(FB) void k_fill(FillArgs fa, int64_t per, int64_t g
                 }
                 q = lo_q - 1;
             }
-            for (; o < gend; o += 64) {
-                while (s_lo_off[q + 1].y <= (uint32_t)o) ++q;
-                const uint2 lof = s_lo_off[q];
-                const uint32_t p = lof.x + ((uint32_t)o - lof.y);
-                const u32x4 ow = s_own[q];
-                u32x4 pa;
-                if (par_lds)
-                    pa = s_par[p - wlo];
-                else
-                    pa = u32x4{sa.pgs[p], sa.pge[p], sa.prow[p], 0u};
-                const uint32_t rs = (ow.x > pa.x ? ow.x : pa.x) - ow.w;
-                const uint32_t re = (ow.y < pa.y ? ow.y : pa.y) - ow.w;
-                const uint32_t ar = st == 0 ? ow.z : pa.z;
-                const uint32_t br = st == 0 ? pa.z : ow.z;
-                if (CKSUM) {
-                    uint64_t h = dev::pair_hash(rs, re, ar, br);
-                    hsum += h;
-                    hxor ^= h;
-                } else {
-                    fa.out[tbase + o - fa.first] = u32x4{rs, re, ar, br};
-                }
-            }
+            if (par_lds)
+                emit<true, CKSUM>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
+                                  hsum, hxor);
+            else
+                emit<false, CKSUM>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
+                                   hsum, hxor);
         }
         __syncthreads();
         if (!more) break;
@@ -530,6 +607,7 @@ FillArgs fill_args(PairsPlan *pl) {
     fa.ocnt = pl->ocnt;
     fa.toff = pl->toff;
     fa.win = pl->win;
+    fa.tseg = pl->tseg;
     fa.ntiles = pl->nt0 + pl->nt1;
     fa.off = pl->A->d_off;
     fa.n_contigs = pl->A->n_contigs;
@@ -630,6 +708,7 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
     if ((rc = alloc(ctx, &pl->olo, (size_t)(a_own + b_own))) ||
         (rc = alloc(ctx, &pl->ocnt, (size_t)(a_own + b_own))) ||
         (rc = alloc(ctx, &pl->toff, (size_t)nt)) || (rc = alloc(ctx, &pl->win, (size_t)2 * nt)) ||
+        (rc = alloc(ctx, &pl->tseg, (size_t)nt)) ||
         (rc = alloc(ctx, &tcnt, (size_t)nt)) || (rc = alloc(ctx, &total, 1))) {
         delete pl;
         return rc;
@@ -643,7 +722,8 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
                                         st == 0 ? 0 : a_own, st == 0 ? a_own : b_own);
             if (ntl == 0) continue;
             hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa,
-                               pl->tp, ntl, pl->win);
+                               pl->tp, ntl, pl->win, (const uint32_t *)O->d_off, O->n_contigs,
+                               pl->tseg);
             if (pl->filtered)
                 hipLaunchKernelGGL(k_count<true>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
                                    pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
@@ -688,7 +768,7 @@ int owner_ranges(lime_ctx *ctx, const lime_set *O, const lime_set *P, int st, in
     LIME_TRY(alloc(ctx, &tcnt, (size_t)ntl));
     StreamArgs sa = stream_args(O, P, st, threshold, 0, 0);
     hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa, tp, ntl,
-                       win);
+                       win, (const uint32_t *)nullptr, 0, (uint32_t *)nullptr);
     hipLaunchKernelGGL(k_count<false>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa, tp, threshold,
                        (const uint32_t *)win, olo, ocnt, tcnt);
     LIME_HIP(hipGetLastError());
@@ -728,6 +808,7 @@ void intersect_free(PairsPlan *pl) {
     release(ctx, pl->ocnt);
     release(ctx, pl->toff);
     release(ctx, pl->win);
+    release(ctx, pl->tseg);
     delete pl;
 }
 

@@ -131,7 +131,47 @@ struct MergeScanArgs {
     uint64_t *total;            // runs
 };
 
+// Full tile <-> blocked registers (thread t: rows 16t .. 16t+15) through
+// LDS: global traffic is lane-consecutive 16-B accesses (whole lines per
+// wave instruction); the LDS image pads 4 words after every 16 rows so the
+// blocked b128 reads (stride 80 B per lane) are conflict-free.
+constexpr int MPADW = MTILE + MTILE / 4;
+__device__ __forceinline__ int pad_word(int u4) { return 4 * u4 + 4 * (u4 >> 2); }
+
+__device__ __forceinline__ void tile_to_blocked(const uint32_t *__restrict__ src, uint32_t *lds,
+                                                uint32_t (&v)[MITEMS]) {
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+#pragma unroll
+    for (int k = 0; k < MITEMS / 4; ++k) {
+        const int u = k * MB + threadIdx.x;
+        *reinterpret_cast<uint4 *>(lds + pad_word(u)) = s4[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MITEMS / 4; ++j) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(lds + 20 * threadIdx.x + 4 * j);
+        v[4 * j] = x.x, v[4 * j + 1] = x.y, v[4 * j + 2] = x.z, v[4 * j + 3] = x.w;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void blocked_to_tile(const uint32_t (&v)[MITEMS], uint32_t *lds,
+                                                uint32_t *__restrict__ dst) {
+#pragma unroll
+    for (int j = 0; j < MITEMS / 4; ++j)
+        *reinterpret_cast<uint4 *>(lds + 20 * threadIdx.x + 4 * j) =
+            make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    __syncthreads();
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+#pragma unroll
+    for (int k = 0; k < MITEMS / 4; ++k) {
+        const int u = k * MB + threadIdx.x;
+        d4[u] = *reinterpret_cast<const uint4 *>(lds + pad_word(u));
+    }
+}
+
 __global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[MPADW];
     __shared__ uint32_t scratch[MB / 64 + 1];
     __shared__ uint64_t s_carry;
     __shared__ uint32_t s_tile;
@@ -141,15 +181,11 @@ __global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
     const int64_t n = a.n;
     const int64_t r0 = tile * MTILE + (int64_t)threadIdx.x * MITEMS;  // blocked rows
     uint32_t s[MITEMS], e[MITEMS];
-    if (r0 + MITEMS <= n) {
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(a.gs + r0);
-        const uint4 *e4 = reinterpret_cast<const uint4 *>(a.ge + r0);
-#pragma unroll
-        for (int k = 0; k < MITEMS / 4; ++k) {
-            const uint4 x = s4[k], y = e4[k];
-            s[4 * k] = x.x, s[4 * k + 1] = x.y, s[4 * k + 2] = x.z, s[4 * k + 3] = x.w;
-            e[4 * k] = y.x, e[4 * k + 1] = y.y, e[4 * k + 2] = y.z, e[4 * k + 3] = y.w;
-        }
+    const int64_t t0 = tile * MTILE;
+    const bool full = t0 + MTILE <= n;
+    if (full) {
+        tile_to_blocked(a.gs + t0, lds, s);
+        tile_to_blocked(a.ge + t0, lds, e);
     } else {
 #pragma unroll
         for (int k = 0; k < MITEMS; ++k) {
@@ -220,11 +256,8 @@ __global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
         rid[k] = r - 1;
     }
     if (a.run_of_sorted) {
-        if (r0 + MITEMS <= n) {
-            uint4 *o4 = reinterpret_cast<uint4 *>(a.run_of_sorted + r0);
-#pragma unroll
-            for (int k = 0; k < MITEMS / 4; ++k)
-                o4[k] = make_uint4(rid[4 * k], rid[4 * k + 1], rid[4 * k + 2], rid[4 * k + 3]);
+        if (full) {
+            blocked_to_tile(rid, lds, a.run_of_sorted + t0);
         } else {
 #pragma unroll
             for (int k = 0; k < MITEMS; ++k)

@@ -112,6 +112,26 @@ def test_intersect_parity(ctx, seed, t, zero, book):
     assert plan.checksum() == oracle.checksum_pairs(got) == oracle.checksum_pairs(exp)
 
 
+# Deep pile-ups: partner windows of a 1024-owner tile beyond the fill
+# kernel's LDS window (1792 rows) take the global-memory path, and windows
+# just below it fill the whole register-prefetched LDS window.
+@pytest.mark.parametrize("seed,n,contig_len,max_len", [(41, 5000, 60000, 7500),
+                                                         (42, 6000, 12000, 3000),
+                                                         (43, 3000, 5000, 4000)])
+def test_intersect_deep_windows(ctx, seed, n, contig_len, max_len):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, n, n, n_contigs=1, contig_len=contig_len, max_len=max_len,
+                       zero_frac=0.02, dup_frac=0.05)
+    sp = space_for(1, contig_len)
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    plan = ctx.intersect(a, b)
+    exp = oracle.intersect(A, B)
+    assert plan.n == len(exp["start"])
+    want = oracle.checksum_pairs(exp)
+    assert oracle.checksum_pairs(plan.fill_host()) == want
+    assert plan.checksum() == want
+
+
 @pytest.mark.parametrize("seed,zero,book", [(11, 0.0, 0.0), (12, 0.1, 0.1), (13, 0.3, 0.3)])
 def test_merge_parity(ctx, seed, zero, book):
     rng = np.random.default_rng(seed)

@@ -1,0 +1,5 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "intersect or scaled_c2 or stranded or full_size" > gpurun_out/s8_tests.txt 2>&1
+timeout -k 10 200 python tools/fill_exp.py > gpurun_out/s8_fillexp.txt 2>&1
+timeout -k 10 200 python bench.py --steps 5 --no-cpu-baseline > gpurun_out/s8_bench.txt 2>&1

@@ -50,3 +50,9 @@ clean:
 	rm -rf build oracle/build $(LIB) bin
 
 .PHONY: all clean
+
+# tuning variant: 3 fill workgroups per CU (tools/ experiments only)
+build/var3/liblime_amd.so: $(HIP_SRCS) $(SRC)/common.hpp include/lime_amd.h $(CPP_OBJS)
+	@mkdir -p build/var3
+	$(HIPCC) $(HIPFLAGS) -DLIME_FILL_WGS=3 -c $(SRC)/intersect.hip -o build/var3/intersect.o
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(filter-out $(OBJDIR)/intersect.o,$(HIP_OBJS)) build/var3/intersect.o $(CPP_OBJS)

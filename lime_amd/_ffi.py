@@ -9,6 +9,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblime_amd.so")
+# tuning experiments only (tools/): load a variant build instead
+if os.environ.get("LIME_AMD_LIB_VARIANT"):
+    LIB_PATH = os.environ["LIME_AMD_LIB_VARIANT"]
 
 LIME_OK = 0
 ERRORS = {

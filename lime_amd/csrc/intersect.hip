@@ -171,7 +171,11 @@ __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64
     }
 }
 
-template <bool FILTER>
+// Per owner: lo and either its count (OFFS = false) or its exclusive output
+// offset within the tile (OFFS = true, what the fill stages: no scan left in
+// the fill's per-tile critical path).  Thread t handles the OPT consecutive
+// owners 4t .. 4t+3 of the tile, so one block scan orders them.
+template <bool FILTER, bool OFFS>
 __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t threshold,
                                               const uint32_t *__restrict__ win,
                                               uint32_t *__restrict__ olo,
@@ -179,17 +183,26 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
                                               uint64_t *__restrict__ tcnt) {
     __shared__ uint32_t wgs[WCAP];
     __shared__ uint64_t red[IB / 64];
+    __shared__ uint32_t scratch[IB / 64 + 1];
     const int64_t t = blockIdx.x;
     const int64_t o0 = t * OT;
     const int64_t o1 = min(o0 + OT, sa.no);
     // owner loads first: they are independent of the window and overlap
     // its two dependent round trips
     uint32_t ogv[OPT], oev[OPT];
+    static_assert(OPT == 4, "owner loads are one 16-B vector per thread");
+    if (o1 - o0 == OT) {  // full tile: lane-consecutive 16-B loads (sets are 16-B aligned)
+        const uint4 g4 = reinterpret_cast<const uint4 *>(sa.ogs + o0)[threadIdx.x];
+        const uint4 e4 = reinterpret_cast<const uint4 *>(sa.oge + o0)[threadIdx.x];
+        ogv[0] = g4.x, ogv[1] = g4.y, ogv[2] = g4.z, ogv[3] = g4.w;
+        oev[0] = e4.x, oev[1] = e4.y, oev[2] = e4.z, oev[3] = e4.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < OPT; ++k) {
-        const int64_t j = o0 + k * IB + threadIdx.x;
-        ogv[k] = j < o1 ? sa.ogs[j] : 0u;
-        oev[k] = j < o1 ? sa.oge[j] : 0u;
+        for (int k = 0; k < OPT; ++k) {
+            const int64_t j = o0 + threadIdx.x * OPT + k;
+            ogv[k] = j < o1 ? sa.ogs[j] : 0u;
+            oev[k] = j < o1 ? sa.oge[j] : 0u;
+        }
     }
     const uint32_t wlo = win[2 * (sa.tile0 + t)], whi = win[2 * (sa.tile0 + t) + 1];
     const int64_t wlen = (int64_t)whi - wlo;
@@ -197,39 +210,87 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
     if (in_lds)
         for (int64_t i = threadIdx.x; i < wlen; i += IB) wgs[i] = sa.pgs[wlo + i];
     __syncthreads();
-    uint64_t sum = 0;
+    // lo = lb(P, o.gs + lo_off) always (subtract's spanning walk starts
+    // below it); hi = lb(P, o.ge - tp + 1), the range [lo, hi) being empty
+    // when hk <= lk.  In the LDS window all 2 * OPT searches of a thread run
+    // in lockstep (branchless binary lifting, fixed trip count), so their
+    // LDS reads overlap instead of forming one 2 * OPT * log2(wlen) chain.
+    int64_t lkv[OPT], hkv[OPT], lov[OPT], hiv[OPT];
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) owner_keys(ogv[k], oev[k], sa.lo_off, tp, lkv[k], hkv[k]);
+    if (in_lds) {
+        int bl[OPT], bh[OPT];
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) bl[k] = bh[k] = 0;
+        const int wl = (int)wlen;
+        for (int step = wl > 0 ? (1 << (31 - __clz(wl))) : 0; step > 0; step >>= 1) {
+#pragma unroll
+            for (int k = 0; k < OPT; ++k) {
+                if (bl[k] + step <= wl && (int64_t)wgs[bl[k] + step - 1] < lkv[k]) bl[k] += step;
+                if (bh[k] + step <= wl && (int64_t)wgs[bh[k] + step - 1] < hkv[k]) bh[k] += step;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) {
+            lov[k] = wlo + bl[k];
+            hiv[k] = hkv[k] > lkv[k] ? wlo + bh[k] : lov[k];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) {
+            lov[k] = dev::lower_bound(sa.pgs, (int64_t)wlo, (int64_t)whi, lkv[k]);
+            hiv[k] = hkv[k] > lkv[k] ? dev::lower_bound(sa.pgs, lov[k], (int64_t)whi, hkv[k])
+                                     : lov[k];
+        }
+    }
+    uint32_t cv[OPT];
+    uint32_t csum = 0;
 #pragma unroll
     for (int k = 0; k < OPT; ++k) {
-        const int64_t j = o0 + k * IB + threadIdx.x;
-        if (j >= o1) break;
-        const uint32_t og = ogv[k], oe = oev[k];
-        int64_t lk, hk;
-        owner_keys(og, oe, sa.lo_off, tp, lk, hk);
-        // lo = lb(P, o.gs + lo_off) always (subtract's spanning walk starts
-        // below it); the range [lo, hi) is empty when hk <= lk
-        int64_t lo, hi;
-        if (in_lds) {
-            lo = wlo + dev::lower_bound(wgs, 0, wlen, lk);
-            hi = hk > lk ? wlo + dev::lower_bound(wgs, lo - wlo, wlen, hk) : lo;
-        } else {
-            lo = dev::lower_bound(sa.pgs, (int64_t)wlo, (int64_t)whi, lk);
-            hi = hk > lk ? dev::lower_bound(sa.pgs, lo, (int64_t)whi, hk) : lo;
-        }
+        const int64_t j = o0 + threadIdx.x * OPT + k;
+        cv[k] = 0;
+        if (j >= o1) continue;
+        const uint32_t og = ogv[k];
+        int64_t lo = lov[k], hi = hiv[k];
         if (sa.zw_skip) {
             while (lo < whi && sa.pgs[lo] == og && sa.pge[lo] == og) ++lo;
             if (hi < lo) hi = lo;
         }
-        uint32_t c;
         if (FILTER) {
-            c = 0;
+            uint32_t c = 0;
             for (int64_t p = lo; p < hi; ++p) c += (int64_t)(sa.pge[p] - sa.pgs[p]) >= threshold;
+            cv[k] = c;
         } else {
-            c = (uint32_t)(hi - lo);
+            cv[k] = (uint32_t)(hi - lo);
         }
-        olo[sa.owner0 + j] = (uint32_t)lo;
-        ocnt[sa.owner0 + j] = c;
-        sum += c;
+        lov[k] = lo;
+        csum += cv[k];
     }
+    uint32_t run = 0;
+    if (OFFS) {
+        uint32_t tot;
+        run = dev::block_exclusive_sum<IB>(csum, scratch, &tot);
+    }
+    // blocked -> lane-consecutive through LDS (the window image is dead
+    // now), so the olo / ocnt stores are coalesced whatever owner0's alignment
+    __syncthreads();
+    uint32_t *slo = wgs, *sct = wgs + OT;
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+        slo[threadIdx.x * OPT + k] = (uint32_t)lov[k];
+        sct[threadIdx.x * OPT + k] = OFFS ? run : cv[k];
+        run += cv[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+        const int q = k * IB + threadIdx.x;
+        if (o0 + q < o1) {
+            olo[sa.owner0 + o0 + q] = slo[q];
+            ocnt[sa.owner0 + o0 + q] = sct[q];
+        }
+    }
+    uint64_t sum = csum;
     sum = dev::wave_reduce_sum(sum);
     if (dev::lane_id() == 0) red[threadIdx.x / 64] = sum;
     __syncthreads();
@@ -248,6 +309,7 @@ struct FillArgs {
     const uint32_t *win;   // per tile partner window [lo, hi)
     const uint32_t *tseg;  // per tile contig offset, 0xffffffff if mixed
     int64_t ntiles;
+    int64_t total;         // pairs of the plan
     const uint32_t *off;
     int32_t n_contigs;
     int64_t first, count;  // output window [first, first + count)
@@ -258,7 +320,11 @@ struct FillArgs {
 constexpr int FB = 512;           // fill workgroup: 8 waves
 constexpr int FW = FB / 64;
 constexpr int FOPT = OT / FB;     // owners per thread when staging a tile
-constexpr int PCAP = 1792;        // LDS partner window (16 B records): 3 workgroups per CU
+#ifndef LIME_FILL_WGS
+#define LIME_FILL_WGS 2  // fill workgroups per CU (LDS budget below)
+#endif
+// LDS partner window (16 B records): 1792 rows keep 3 workgroups per CU
+constexpr int PCAP = LIME_FILL_WGS >= 3 ? 1792 : 2048;
 constexpr int PPT = (PCAP + FB - 1) / FB;  // partner rows per thread when staging
 constexpr int64_t GR = 1ll << 40;  // wave granule: default one equal chunk per wave
 
@@ -287,9 +353,10 @@ __device__ __forceinline__ int64_t wave_tile_of(const uint64_t *__restrict__ a, 
 // records are being stored (the staging latency is hidden behind the store
 // stream instead of stalling it once per tile).
 struct TileRegs {
-    uint32_t c[FOPT], lo[FOPT], og[FOPT], oe[FOPT], orw[FOPT];
+    uint32_t off[FOPT], lo[FOPT], og[FOPT], oe[FOPT], orw[FOPT];
     uint32_t pg[PPT], pe[PPT], pr[PPT];
     uint32_t wlo, whi, seg;
+    uint64_t tnext;  // toff[t + 1] (or the plan total): the tile's end
 };
 
 __device__ __forceinline__ int tile_stream(const FillArgs &fa, int64_t t) {
@@ -305,7 +372,7 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
         const int q = threadIdx.x * FOPT + k;
         const bool v = q < nown;
         const int64_t j = o0 + q;
-        r.c[k] = v ? fa.ocnt[sa.owner0 + j] : 0u;
+        r.off[k] = v ? fa.ocnt[sa.owner0 + j] : 0u;  // tile-local offsets (k_count<_, true>)
         r.lo[k] = v ? fa.olo[sa.owner0 + j] : 0u;
         r.og[k] = v ? sa.ogs[j] : 0u;
         r.oe[k] = v ? sa.oge[j] : 0u;
@@ -314,6 +381,7 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
     r.wlo = fa.win[2 * t];
     r.whi = fa.win[2 * t + 1];
     r.seg = fa.tseg[t];
+    r.tnext = t + 1 < fa.ntiles ? fa.toff[t + 1] : (uint64_t)fa.total;
     const int wl = (int)min((int64_t)(r.whi - r.wlo), (int64_t)PCAP);
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
@@ -323,6 +391,24 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
         r.pe[k] = v ? sa.pge[r.wlo + i] : 0u;
         r.pr[k] = v ? sa.prow[r.wlo + i] : 0u;
     }
+}
+
+// Largest q in [lo, hi) with off[q].y <= key (off[lo].y <= key holds); the
+// .y are non-decreasing.  One wave, wave-uniform result.
+__device__ __forceinline__ int wave_owner_of(const uint2 *off, int lo, int hi, uint32_t key) {
+    const int lane = dev::lane_id();
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 64) / 65;
+        const int idx = lo + step * (lane + 1) - 1;
+        const bool le = idx < hi && off[idx].y <= key;
+        const int c = __popcll(__ballot(le));
+        const int nlo = c == 0 ? lo : lo + step * c;
+        hi = c == 64 ? hi : min(hi, lo + step * (c + 1) - 1);
+        lo = nlo;
+    }
+    const int idx = lo + lane;
+    const bool le = idx < hi && off[idx].y <= key;
+    return lo + __popcll(__ballot(le)) - 1;
 }
 
 // Emit outputs o, o + 64, ... < gend of one wave (lane-consecutive records).
@@ -380,7 +466,7 @@ __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, i
 // tile's staging data is prefetched into registers (TileRegs) before the
 // store loop.
 template <bool CKSUM>
-__global__ __launch_bounds__(FB, 6) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
+__global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
     __shared__ uint2 s_lo_off[OT + 1];
     __shared__ u32x4 s_own[OT];
     __shared__ u32x4 s_par[PCAP];
@@ -407,12 +493,9 @@ __global__ __launch_bounds__(FB, 6) void k_fill(FillArgs fa, int64_t per, int64_
         const int64_t o0 = (t - sa.tile0) * OT;
         const int nown = (int)min((int64_t)OT, sa.no - o0);
         const int64_t tbase = (int64_t)fa.toff[t];
-        // ---- commit the staged registers to LDS
-        uint32_t csum = 0;
-#pragma unroll
-        for (int k = 0; k < FOPT; ++k) csum += R.c[k];
-        uint32_t ttot;
-        uint32_t run = dev::block_exclusive_sum<FB>(csum, scratch, &ttot);
+        // ---- commit the staged registers to LDS (offsets come scanned
+        // from k_count: no block scan here)
+        const uint32_t ttot = (uint32_t)(R.tnext - (uint64_t)tbase);
 #pragma unroll
         for (int k = 0; k < FOPT; ++k) {
             const int q = threadIdx.x * FOPT + k;
@@ -421,8 +504,7 @@ __global__ __launch_bounds__(FB, 6) void k_fill(FillArgs fa, int64_t per, int64_
                     R.seg != 0xffffffffu ? R.seg : contig_off(fa.off, fa.n_contigs, R.og[k]);
                 s_own[q] = u32x4{R.og[k], R.oe[k], R.orw[k], sg};
             }
-            s_lo_off[q] = make_uint2(R.lo[k], run);
-            run += R.c[k];
+            s_lo_off[q] = make_uint2(R.lo[k], q < nown ? R.off[k] : ttot);
         }
         if (threadIdx.x == 0) s_lo_off[OT] = make_uint2(0u, ttot);
         const uint32_t wlo = R.wlo, whi = R.whi;
@@ -450,23 +532,15 @@ __global__ __launch_bounds__(FB, 6) void k_fill(FillArgs fa, int64_t per, int64_
         // wave idles at the tile's closing barrier
         const int64_t rounds = max((int64_t)1, (le - lb + FW * gran - 1) / (FW * gran));
         const int64_t gsz = (((le - lb + FW * rounds - 1) / (FW * rounds)) + 63) & ~(int64_t)63;
-        int q = 0;
+        int qw = 0;  // wave-uniform: owner of the wave's previous granule start
         for (int64_t gb = lb + (int64_t)w * gsz; gb < le; gb += (int64_t)FW * gsz) {
             const int64_t gend = min(le, gb + gsz);
             int64_t o = gb + lane;
-            {
-                // owner of this lane's first output (largest q with off_q <= o)
-                int lo_q = q, hi_q = nown;
-                const uint32_t key = (uint32_t)min(o, gend - 1);
-                while (lo_q < hi_q) {
-                    int mid = (lo_q + hi_q) >> 1;
-                    if (s_lo_off[mid].y <= key)
-                        lo_q = mid + 1;
-                    else
-                        hi_q = mid;
-                }
-                q = lo_q - 1;
-            }
+            // owner of the wave's first output (largest q with off_q <= gb),
+            // by a 65-ary wave search over the LDS offsets (2 steps for a
+            // 1024-owner tile); each lane then walks to its own owner
+            qw = wave_owner_of(s_lo_off, qw, nown, (uint32_t)gb);
+            int q = qw;
             if (par_lds)
                 emit<true, CKSUM>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
                                   hsum, hxor);
@@ -608,6 +682,7 @@ FillArgs fill_args(PairsPlan *pl) {
     fa.toff = pl->toff;
     fa.win = pl->win;
     fa.tseg = pl->tseg;
+    fa.total = pl->total;
     fa.ntiles = pl->nt0 + pl->nt1;
     fa.off = pl->A->d_off;
     fa.n_contigs = pl->A->n_contigs;
@@ -725,11 +800,11 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
                                pl->tp, ntl, pl->win, (const uint32_t *)O->d_off, O->n_contigs,
                                pl->tseg);
             if (pl->filtered)
-                hipLaunchKernelGGL(k_count<true>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
+                hipLaunchKernelGGL((k_count<true, false>), dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
                                    pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
                                    tcnt);
             else
-                hipLaunchKernelGGL(k_count<false>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
+                hipLaunchKernelGGL((k_count<false, true>), dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
                                    pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
                                    tcnt);
             LIME_HIP(hipGetLastError());
@@ -769,7 +844,8 @@ int owner_ranges(lime_ctx *ctx, const lime_set *O, const lime_set *P, int st, in
     StreamArgs sa = stream_args(O, P, st, threshold, 0, 0);
     hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa, tp, ntl,
                        win, (const uint32_t *)nullptr, 0, (uint32_t *)nullptr);
-    hipLaunchKernelGGL(k_count<false>, dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa, tp, threshold,
+    hipLaunchKernelGGL((k_count<false, false>), dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa, tp,
+                       threshold,
                        (const uint32_t *)win, olo, ocnt, tcnt);
     LIME_HIP(hipGetLastError());
     release(ctx, win);

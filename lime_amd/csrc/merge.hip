@@ -13,7 +13,7 @@
 // run ends at max(ge).
 //
 // k_merge_scan: ONE pass over the set (8 B read + 4 B run id written per
-// row, 8 B per run).  Tiles of 4096 rows are taken in ticket order; a tile
+// row, 8 B per run).  Tiles of 8192 rows are taken in ticket order; a tile
 // publishes its max(ge) and learns M at its first row by a decoupled
 // look-back over its predecessors' (flag | value) status words, flags its
 // rows, then publishes its run count and learns its first run index by a
@@ -104,9 +104,11 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t *st, int64_t tile) {
         const int64_t i = base - lane;
         uint64_t v = ST_INC;  // before tile 0: inclusive identity
         if (i >= 0) {
-            do {
+            v = st_poll(st + i);
+            while ((v >> 62) == 0) {
+                __builtin_amdgcn_s_sleep(1);
                 v = st_poll(st + i);
-            } while ((v >> 62) == 0);
+            }
         }
         const uint64_t inc = __ballot((v >> 62) == 2);
         uint64_t val = v & ST_VAL;
@@ -135,7 +137,9 @@ struct MergeScanArgs {
 // LDS: global traffic is lane-consecutive 16-B accesses (whole lines per
 // wave instruction); the LDS image pads 4 words after every 16 rows so the
 // blocked b128 reads (stride 80 B per lane) are conflict-free.
-constexpr int MPADW = MTILE + MTILE / 4;
+constexpr int SB = 512;              // scan workgroup
+constexpr int STILE = SB * MITEMS;   // 8192 rows per scan tile
+constexpr int MPADW = STILE + STILE / 4;
 __device__ __forceinline__ int pad_word(int u4) { return 4 * u4 + 4 * (u4 >> 2); }
 
 __device__ __forceinline__ void tile_to_blocked(const uint32_t *__restrict__ src, uint32_t *lds,
@@ -143,7 +147,7 @@ __device__ __forceinline__ void tile_to_blocked(const uint32_t *__restrict__ src
     const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
 #pragma unroll
     for (int k = 0; k < MITEMS / 4; ++k) {
-        const int u = k * MB + threadIdx.x;
+        const int u = k * SB + threadIdx.x;
         *reinterpret_cast<uint4 *>(lds + pad_word(u)) = s4[u];
     }
     __syncthreads();
@@ -165,24 +169,24 @@ __device__ __forceinline__ void blocked_to_tile(const uint32_t (&v)[MITEMS], uin
     uint4 *d4 = reinterpret_cast<uint4 *>(dst);
 #pragma unroll
     for (int k = 0; k < MITEMS / 4; ++k) {
-        const int u = k * MB + threadIdx.x;
+        const int u = k * SB + threadIdx.x;
         d4[u] = *reinterpret_cast<const uint4 *>(lds + pad_word(u));
     }
 }
 
-__global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
+__global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[MPADW];
-    __shared__ uint32_t scratch[MB / 64 + 1];
+    __shared__ uint32_t scratch[SB / 64 + 1];
     __shared__ uint64_t s_carry;
     __shared__ uint32_t s_tile;
     if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t n = a.n;
-    const int64_t r0 = tile * MTILE + (int64_t)threadIdx.x * MITEMS;  // blocked rows
+    const int64_t r0 = tile * STILE + (int64_t)threadIdx.x * MITEMS;  // blocked rows
     uint32_t s[MITEMS], e[MITEMS];
-    const int64_t t0 = tile * MTILE;
-    const bool full = t0 + MTILE <= n;
+    const int64_t t0 = tile * STILE;
+    const bool full = t0 + STILE <= n;
     if (full) {
         tile_to_blocked(a.gs + t0, lds, s);
         tile_to_blocked(a.ge + t0, lds, e);
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) agg = max(agg, e[k]);
     uint32_t tmax;
-    const uint32_t pre = dev::block_exclusive_max<MB>(agg, 0u, scratch, &tmax);
+    const uint32_t pre = dev::block_exclusive_max<SB>(agg, 0u, scratch, &tmax);
     // ---- chain 1: M at the tile's first row
     if (threadIdx.x < 64) {
         uint64_t ex = 0;
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(MB) void k_merge_scan(MergeScanArgs a) {
         M = max(M, e[k]);
     }
     uint32_t ctot;
-    const uint32_t rpre = dev::block_exclusive_sum<MB>((uint32_t)__popc(flags), scratch, &ctot);
+    const uint32_t rpre = dev::block_exclusive_sum<SB>((uint32_t)__popc(flags), scratch, &ctot);
     // ---- chain 2: index of the tile's first run
     if (threadIdx.x < 64) {
         uint64_t ex = 0;
@@ -333,7 +337,7 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
         LIME_TRY(alloc(ctx, &res->ge, 1));
         return LIME_OK;
     }
-    const int64_t nt = (n + MTILE - 1) / MTILE;
+    const int64_t nt = (n + STILE - 1) / STILE;
     // status words of both chains + ticket + total in one zeroed block
     uint64_t *st;
     LIME_TRY(alloc(ctx, &st, (size_t)(2 * nt + 2)));
@@ -353,7 +357,7 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
     a.run_gs = run_gs;
     a.run_ge = run_ge;
     a.run_of_sorted = res->run_of_sorted;
-    hipLaunchKernelGGL(k_merge_scan, dim3((unsigned)nt), dim3(MB), 0, S(ctx), a);
+    hipLaunchKernelGGL(k_merge_scan, dim3((unsigned)nt), dim3(SB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
     uint64_t nr = 0;
     LIME_TRY(read_back(ctx, &nr, a.total, sizeof(nr)));

@@ -80,6 +80,28 @@ __global__ __launch_bounds__(512) void k_store_gran(u32x4 *out, long n, long per
         }
 }
 
+// k_fill's exact store shape with constant data: persistent workgroups of
+// 512 threads, each over a contiguous range of `per` records cut into
+// "tiles" of T records; inside a tile the range is dealt to the 8 waves in
+// granules of G records (G >= T/8: one equal chunk per wave).
+__global__ __launch_bounds__(512) void k_store_fillshape(u32x4 *out, long n, long per, long T,
+                                                         long G) {
+    const long b0 = (long)blockIdx.x * per;
+    const long b1 = b0 + per < n ? b0 + per : n;
+    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    for (long t0 = b0; t0 < b1; t0 += T) {
+        const long t1 = t0 + T < b1 ? t0 + T : b1;
+        long rounds = (t1 - t0 + 8 * G - 1) / (8 * G);
+        if (rounds < 1) rounds = 1;
+        const long gsz = (((t1 - t0 + 8 * rounds - 1) / (8 * rounds)) + 63) & ~63L;
+        for (long g = t0 + w * gsz; g < t1; g += 8 * gsz) {
+            const long ge = g + gsz < t1 ? g + gsz : t1;
+            for (long i = g + lane; i < ge; i += 64) out[i] = u32x4{(unsigned)i, 1u, 2u, 3u};
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_copy(const u32x4 *in, u32x4 *out, long n) {
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
         out[i] = in[i];
@@ -172,6 +194,16 @@ int main(int argc, char **argv) {
     }
         GRAN(64) GRAN(256) GRAN(512) GRAN(2048) GRAN(8192)
     }
+    for (long G : {64L, 2048L, 1L << 40})
+        for (int wgs_per_cu : {2, 3}) {
+            const unsigned g = 256 * wgs_per_cu;
+            const long per = (n + g - 1) / g;
+            char name[96];
+            snprintf(name, sizeof name, "fillshape_T84000_G%ld_wg%d", G > n ? -1L : G, wgs_per_cu);
+            timeit(name, n, n * 16.0, [&] {
+                hipLaunchKernelGGL(k_store_fillshape, dim3(g), dim3(512), 0, 0, out, n, per, 84000L, G);
+            });
+        }
     long nc = n / 2;
     CK(hipMalloc(&in, nc * 16));
     CK(hipMemset(in, 1, nc * 16));

@@ -152,6 +152,16 @@ int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lim
 int lime_intersect_checksum(lime_pairs *plan, uint64_t *sum, uint64_t *xr);
 int lime_pairs_destroy(lime_pairs *plan);
 
+/* ------------------------------------------------------------------- window */
+/* DistributedWindow(left, right, partitionMap, threshold = distance).compute()
+ * (lime-core Window.scala:71-95, CLI cli/Window.scala:42-55): every pair
+ * (a, b) with ADAM a.isNearby(b, distance) (overlapping, or a gap of at most
+ * distance - 1 bases: ADAM's distance is gap + 1).  The records carry a's own
+ * region (Window.primitive returns the first region) and the two rows; fill
+ * and checksum them with lime_intersect_fill_* / lime_intersect_checksum. */
+int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t distance,
+                      lime_pairs **plan, int64_t *n_pairs);
+
 /* ------------------------------------------------------------ merge et al. */
 int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs);
 int lime_subtract(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,

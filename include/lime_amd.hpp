@@ -196,6 +196,92 @@ std::vector<size_t> sorted_rank(const RDD<T> &rdd) {
 
 }  // namespace detail
 
+namespace detail {
+struct PairHit {
+    size_t a, b;
+    int64_t s, e;
+};
+// Pairwise join of two keyed RDDs through the engine, one strand group at a
+// time (ReferenceRegion.overlaps / distance need equal strands), returned in
+// the reference's P = 1 emission order: left in sorted order, then cache
+// (= sorted right) order (SetTheory.scala:181-186).
+template <typename T, typename U, typename PlanFn>
+std::vector<PairHit> pair_join(const RDD<T> &left, const RDD<U> &right, Engine &eng,
+                               PlanFn make_plan) {
+    auto sp = space_of<T>({&left});
+    {  // extend with the right side's contigs
+        std::map<std::string, int64_t> ext;
+        for (size_t c = 0; c < sp->names.size(); ++c) ext[sp->names[c]] = sp->lengths[c];
+        for (auto &kv : right) {
+            auto &e = ext[kv.first.referenceName];
+            e = std::max(e, kv.first.end);
+        }
+        std::vector<std::string> n;
+        std::vector<int64_t> l;
+        for (auto &kv : ext) {
+            n.push_back(kv.first);
+            l.push_back(kv.second);
+        }
+        sp = std::make_unique<Space>(n, l);
+    }
+    auto lg = strand_groups(left);
+    auto rg = strand_groups(right);
+    std::vector<PairHit> hits;
+    for (auto &g : lg) {
+        auto it = rg.find(g.first);
+        if (it == rg.end()) continue;
+        SetHandle A, B;
+        upload(eng.ctx(), *sp, left, g.second, A);
+        upload(eng.ctx(), *sp, right, it->second, B);
+        lime_pairs *plan = nullptr;
+        int64_t n = 0;
+        check(make_plan(eng.ctx(), A.h, B.h, &plan, &n));
+        std::vector<lime_pair> p((size_t)n);
+        int rc = lime_intersect_fill_host(plan, 0, n, p.data());
+        lime_pairs_destroy(plan);
+        check(rc);
+        for (auto &x : p) hits.push_back({g.second[x.a_row], it->second[x.b_row], x.start, x.end});
+    }
+    auto lr = sorted_rank(left);
+    auto rr = sorted_rank(right);
+    std::sort(hits.begin(), hits.end(), [&](const PairHit &x, const PairHit &y) {
+        return lr[x.a] != lr[y.a] ? lr[x.a] < lr[y.a] : rr[x.b] < rr[y.b];
+    });
+    return hits;
+}
+}  // namespace detail
+
+// DistributedWindow (Window.scala:71-95): every right row nearby each left
+// row (ADAM isNearby, default distance 1000), keyed by the left region.
+template <typename T, typename U>
+class DistributedWindow {
+   public:
+    DistributedWindow(RDD<T> left, RDD<U> right, PartitionMap partitionMap = {},
+                      int64_t threshold = 1000, Engine &eng = Engine::thread_default())
+        : left_(std::move(left)), right_(std::move(right)), pm_(std::move(partitionMap)),
+          threshold_(threshold), eng_(eng) {}
+
+    std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> compute() {
+        auto hits = detail::pair_join(left_, right_, eng_, [&](lime_ctx *c, lime_set *a,
+                                                              lime_set *b, lime_pairs **pl,
+                                                              int64_t *n) {
+            return lime_window_count(c, a, b, threshold_, pl, n);
+        });
+        std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> out;
+        out.reserve(hits.size());
+        for (auto &h : hits)
+            out.push_back({left_[h.a].first, {left_[h.a].second, right_[h.b].second}});
+        return out;
+    }
+
+   private:
+    RDD<T> left_;
+    RDD<U> right_;
+    PartitionMap pm_;
+    int64_t threshold_;
+    Engine &eng_;
+};
+
 template <class T, class U>
 class DistributedIntersection {
    public:
@@ -205,46 +291,10 @@ class DistributedIntersection {
           threshold_(threshold), eng_(eng) {}
 
     std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> compute() {
-        RDD<T> &L = left_;
-        auto sp = detail::space_of<T>({&L});
-        {  // extend with the right side's contigs
-            std::map<std::string, int64_t> ext;
-            for (size_t c = 0; c < sp->names.size(); ++c) ext[sp->names[c]] = sp->lengths[c];
-            for (auto &kv : right_) {
-                auto &e = ext[kv.first.referenceName];
-                e = std::max(e, kv.first.end);
-            }
-            std::vector<std::string> n;
-            std::vector<int64_t> l;
-            for (auto &kv : ext) {
-                n.push_back(kv.first);
-                l.push_back(kv.second);
-            }
-            sp = std::make_unique<detail::Space>(n, l);
-        }
-        auto lg = detail::strand_groups(left_);
-        auto rg = detail::strand_groups(right_);
-        struct Hit { size_t a, b; int64_t s, e; };
-        std::vector<Hit> hits;
-        for (auto &g : lg) {
-            auto it = rg.find(g.first);
-            if (it == rg.end()) continue;
-            detail::SetHandle A, B;
-            detail::upload(eng_.ctx(), *sp, left_, g.second, A);
-            detail::upload(eng_.ctx(), *sp, right_, it->second, B);
-            lime_pairs *plan = nullptr;
-            int64_t n = 0;
-            check(lime_intersect_count(eng_.ctx(), A.h, B.h, threshold_, &plan, &n));
-            std::vector<lime_pair> p((size_t)n);
-            int rc = lime_intersect_fill_host(plan, 0, n, p.data());
-            lime_pairs_destroy(plan);
-            check(rc);
-            for (auto &x : p) hits.push_back({g.second[x.a_row], it->second[x.b_row], x.start, x.end});
-        }
-        auto lr = detail::sorted_rank(left_);
-        auto rr = detail::sorted_rank(right_);
-        std::sort(hits.begin(), hits.end(), [&](const Hit &x, const Hit &y) {
-            return lr[x.a] != lr[y.a] ? lr[x.a] < lr[y.a] : rr[x.b] < rr[y.b];
+        auto hits = detail::pair_join(left_, right_, eng_, [&](lime_ctx *c, lime_set *a,
+                                                              lime_set *b, lime_pairs **pl,
+                                                              int64_t *n) {
+            return lime_intersect_count(c, a, b, threshold_, pl, n);
         });
         std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> out;
         out.reserve(hits.size());

@@ -71,6 +71,7 @@ SIGNATURES = {
     "lime_set_fill_host": (C.c_int, [vp, P(i32), P(i64), P(i64), P(i64)]),
     "lime_intersect_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),
     "lime_intersect_count_owned": (C.c_int, [vp, vp, vp, i64, i64, i64, pp, P(i64)]),
+    "lime_window_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),
     "lime_intersect_fill_device": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_fill_host": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_checksum": (C.c_int, [vp, P(u64), P(u64)]),

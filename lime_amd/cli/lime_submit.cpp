@@ -8,6 +8,8 @@
 //   complement A.bed genome.txt cli/Complement.scala:154-166 (prints regions)
 //   subtract  A.bed B.bed       DistributedSubtract (API-only in the reference)
 //   sort      A.bed             cli/Sort.scala:34-38 (device radix sort)
+//   window    A.bed B.bed [-distance D]   cli/Window.scala:42-55 (keys stranded,
+//                               DistributedWindow default distance 1000)
 //
 // Everything before "--" is accepted and ignored (there is no Spark).
 // Output is one region per line, tab-separated (chrom, start, end), followed
@@ -34,6 +36,7 @@ const Cmd kCommands[] = {
     {"merge", "Merges the regions in a single input"},
     {"subtract", "Remove regions of the second input from the first"},
     {"sort", "Sorts the regions in a single input"},
+    {"window", "Compute nearby regions between two inputs"},
 };
 
 void usage() {
@@ -79,6 +82,18 @@ int run(const std::vector<std::string> &args) {
         need(2);
         auto out = DistributedIntersection<std::string, std::string>(load_bed(args[1], true),
                                                                      load_bed(args[2], true))
+                       .compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\t%s\t%s\n", o.second.first.c_str(), o.second.second.c_str());
+        }
+    } else if (cmd == "window") {
+        need(2);
+        int64_t d = 1000;
+        for (size_t i = 3; i + 1 < args.size(); ++i)
+            if (args[i] == "-distance") d = std::stoll(args[i + 1]);
+        auto out = DistributedWindow<std::string, std::string>(load_bed(args[1], true),
+                                                               load_bed(args[2], true), {}, d)
                        .compute();
         for (auto &o : out) {
             print_region(o.first);

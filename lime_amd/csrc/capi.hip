@@ -68,7 +68,9 @@ int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes) {
 // defined in the kernel translation units
 struct PairsPlan;
 int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold,
-                   int64_t a_own, int64_t b_own, PairsPlan **out);
+                   int64_t a_own, int64_t b_own, PairsPlan **out, const lime_set *A_out = nullptr,
+                   int64_t reach = -1);
+int window_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t d, PairsPlan **out);
 int intersect_fill(PairsPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
 int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr);
 void intersect_free(PairsPlan *pl);
@@ -456,6 +458,19 @@ int lime_intersect_count_owned(lime_ctx *ctx, const lime_set *a, const lime_set 
     LIME_TRY(intersect_plan(ctx, a, b, threshold, a_owned, b_owned, &pl));
     lime_pairs *p = new lime_pairs{pl, ctx};
     *plan = p;
+    if (n_pairs) *n_pairs = plan_total(pl);
+    return LIME_OK;
+}
+
+int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t distance,
+                      lime_pairs **plan, int64_t *n_pairs) {
+    if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad window arguments");
+    if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
+    if (distance < 0) return fail(LIME_ERR_ARG, "window distance must be >= 0");
+    hipSetDevice(ctx->device);
+    PairsPlan *pl = nullptr;
+    LIME_TRY(window_plan(ctx, a, b, distance, &pl));
+    *plan = new lime_pairs{pl, ctx};
     if (n_pairs) *n_pairs = plan_total(pl);
     return LIME_OK;
 }

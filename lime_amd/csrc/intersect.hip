@@ -47,6 +47,11 @@ struct PairsPlan {
     uint32_t *win = nullptr;                   // per tile partner window [lo, hi)
     uint32_t *tseg = nullptr;                  // per tile contig offset (0xffffffff: mixed)
     int64_t total = 0;
+    // window plans (DistributedWindow): A is the widened set W, A_out the
+    // caller's set whose own coordinates the pairs carry; reach = distance
+    const lime_set *A_out = nullptr;
+    lime_set *W = nullptr;  // owned: widened copy of A_out (row array borrowed)
+    int64_t reach = -1;
 };
 
 namespace {
@@ -60,11 +65,15 @@ constexpr int64_t SBLK = 131072;     // output records per fill workgroup
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct StreamArgs {
-    const uint32_t *ogs, *oge, *orow;  // owner set
-    const uint32_t *pgs, *pge, *prow;  // partner set
+    const uint32_t *ogs, *oge, *orow;  // owner set (search keys)
+    const uint32_t *pgs, *pge, *prow;  // partner set (search keys)
+    // the coordinates the output records are made of: the same arrays for
+    // intersect; the caller's unwidened rows for the window set's side
+    const uint32_t *ogs_o, *oge_o, *pgs_o, *pge_o;
     int64_t no, np;
     uint32_t lo_off;  // 0 or 1
     int zw_skip;      // skip zero-width partners at exactly o.gs
+    int64_t reach;    // window distance on the owner side (stream 0), else -1
     int64_t tile0;    // first global tile index of this stream
     int64_t owner0;   // first global owner slot of this stream (olo/ocnt)
 };
@@ -165,8 +174,8 @@ __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64
         win[2 * (sa.tile0 + t) + 1] = (uint32_t)hi;
     }
     if (tseg && lane == 1) {
-        const uint32_t a = contig_off(off, nc, sa.ogs[o0]);
-        const uint32_t b = contig_off(off, nc, sa.ogs[o1 - 1]);
+        const uint32_t a = contig_off(off, nc, sa.ogs_o[o0]);
+        const uint32_t b = contig_off(off, nc, sa.ogs_o[o1 - 1]);
         tseg[sa.tile0 + t] = a == b ? a : 0xffffffffu;
     }
 }
@@ -252,7 +261,10 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
         if (j >= o1) continue;
         const uint32_t og = ogv[k];
         int64_t lo = lov[k], hi = hiv[k];
-        if (sa.zw_skip) {
+        // a window row clipped at global 0 (contig 0, a.s < reach) is
+        // nearby a zero-width partner at 0 (distance a.s + 1 <= reach)
+        const bool keep0 = sa.reach > 0 && og == 0 && (int64_t)sa.ogs_o[j] < sa.reach;
+        if (sa.zw_skip && !keep0) {
             while (lo < whi && sa.pgs[lo] == og && sa.pge[lo] == og) ++lo;
             if (hi < lo) hi = lo;
         }
@@ -374,8 +386,8 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
         const int64_t j = o0 + q;
         r.off[k] = v ? fa.ocnt[sa.owner0 + j] : 0u;  // tile-local offsets (k_count<_, true>)
         r.lo[k] = v ? fa.olo[sa.owner0 + j] : 0u;
-        r.og[k] = v ? sa.ogs[j] : 0u;
-        r.oe[k] = v ? sa.oge[j] : 0u;
+        r.og[k] = v ? sa.ogs_o[j] : 0u;
+        r.oe[k] = v ? sa.oge_o[j] : 0u;
         r.orw[k] = v ? sa.orow[j] : 0u;
     }
     r.wlo = fa.win[2 * t];
@@ -387,8 +399,8 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
     for (int k = 0; k < PPT; ++k) {
         const int i = k * FB + threadIdx.x;
         const bool v = i < wl;
-        r.pg[k] = v ? sa.pgs[r.wlo + i] : 0u;
-        r.pe[k] = v ? sa.pge[r.wlo + i] : 0u;
+        r.pg[k] = v ? sa.pgs_o[r.wlo + i] : 0u;
+        r.pe[k] = v ? sa.pge_o[r.wlo + i] : 0u;
         r.pr[k] = v ? sa.prow[r.wlo + i] : 0u;
     }
 }
@@ -417,7 +429,7 @@ __device__ __forceinline__ int wave_owner_of(const uint2 *off, int lo, int hi, u
 // each wave keeps its stores in flight.  The owner walk carries the current
 // (lo, off) pair and the next owner's pair in registers, leaving two
 // dependent LDS steps per iteration (walk, then owner + partner reads).
-template <bool LDSP, bool CKSUM>
+template <bool LDSP, bool CKSUM, bool WIN>
 __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, int st,
                                      const uint2 *s_lo_off, const u32x4 *s_own,
                                      const u32x4 *s_par, uint32_t wlo, int64_t tbase, int64_t o,
@@ -437,9 +449,12 @@ __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, i
         if (LDSP)
             pa = s_par[p - wlo];
         else
-            pa = u32x4{sa.pgs[p], sa.pge[p], sa.prow[p], 0u};
-        const uint32_t rs = (ow.x > pa.x ? ow.x : pa.x) - ow.w;
-        const uint32_t re = (ow.y < pa.y ? ow.y : pa.y) - ow.w;
+            pa = u32x4{sa.pgs_o[p], sa.pge_o[p], sa.prow[p], 0u};
+        // intersect: the intersection; window: the left (a) row's own region
+        const uint32_t rs =
+            (WIN ? (st == 0 ? ow.x : pa.x) : (ow.x > pa.x ? ow.x : pa.x)) - ow.w;
+        const uint32_t re =
+            (WIN ? (st == 0 ? ow.y : pa.y) : (ow.y < pa.y ? ow.y : pa.y)) - ow.w;
         const uint32_t ar = st == 0 ? ow.z : pa.z;
         const uint32_t br = st == 0 ? pa.z : ow.z;
         if (CKSUM) {
@@ -465,7 +480,7 @@ __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, i
 // lane, the wave's 64 stores forming one contiguous 1-KiB segment.  The next
 // tile's staging data is prefetched into registers (TileRegs) before the
 // store loop.
-template <bool CKSUM>
+template <bool CKSUM, bool WIN>
 __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
     __shared__ uint2 s_lo_off[OT + 1];
     __shared__ u32x4 s_own[OT];
@@ -542,10 +557,10 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
             qw = wave_owner_of(s_lo_off, qw, nown, (uint32_t)gb);
             int q = qw;
             if (par_lds)
-                emit<true, CKSUM>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
+                emit<true, CKSUM, WIN>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
                                   hsum, hxor);
             else
-                emit<false, CKSUM>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
+                emit<false, CKSUM, WIN>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
                                    hsum, hxor);
         }
         __syncthreads();
@@ -655,19 +670,30 @@ __global__ __launch_bounds__(IB) void k_fill_filtered(FillArgs fa, int64_t thres
     }
 }
 
+// O_out / P_out: the sets whose coordinates the output records carry (the
+// caller's set behind a window plan's widened set), default O / P.
 StreamArgs stream_args(const lime_set *O, const lime_set *P, int st, int64_t threshold,
-                       int64_t tile0, int64_t owner0, int64_t n_own = -1) {
+                       int64_t tile0, int64_t owner0, int64_t n_own = -1,
+                       const lime_set *O_out = nullptr, const lime_set *P_out = nullptr,
+                       int64_t reach = -1) {
     StreamArgs s;
+    if (!O_out) O_out = O;
+    if (!P_out) P_out = P;
     s.ogs = O->gs;
     s.oge = O->ge;
     s.orow = O->row;
     s.pgs = P->gs;
     s.pge = P->ge;
     s.prow = P->row;
+    s.ogs_o = O_out->gs;
+    s.oge_o = O_out->ge;
+    s.pgs_o = P_out->gs;
+    s.pge_o = P_out->ge;
     s.no = n_own >= 0 ? n_own : O->n;  // owners: the first n_own rows (halo rows own nothing)
     s.np = P->n;
     s.lo_off = st == 0 ? 0u : 1u;
     s.zw_skip = (st == 0 && threshold <= 0 && P->has_zero_width) ? 1 : 0;
+    s.reach = st == 0 ? reach : -1;
     s.tile0 = tile0;
     s.owner0 = owner0;
     return s;
@@ -675,8 +701,10 @@ StreamArgs stream_args(const lime_set *O, const lime_set *P, int st, int64_t thr
 
 FillArgs fill_args(PairsPlan *pl) {
     FillArgs fa;
-    fa.s[0] = stream_args(pl->A, pl->B, 0, pl->threshold, 0, 0, pl->a_own);
-    fa.s[1] = stream_args(pl->B, pl->A, 1, pl->threshold, pl->nt0, pl->a_own, pl->b_own);
+    fa.s[0] = stream_args(pl->A, pl->B, 0, pl->threshold, 0, 0, pl->a_own, pl->A_out, nullptr,
+                          pl->reach);
+    fa.s[1] = stream_args(pl->B, pl->A, 1, pl->threshold, pl->nt0, pl->a_own, pl->b_own, nullptr,
+                          pl->A_out);
     fa.olo = pl->olo;
     fa.ocnt = pl->ocnt;
     fa.toff = pl->toff;
@@ -707,7 +735,7 @@ int64_t fill_span(int64_t count) {
         int dev = 0, cus = 256, occ = 2;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fill<false>, FB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fill<false, false>, FB, 0);
         const int64_t slots = (int64_t)cus * (occ > 0 ? occ : 1);
         per = (count + slots - 1) / slots;
     }
@@ -745,15 +773,44 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
         const int64_t per = fill_span(count);
         const int64_t grid = (count + per - 1) / per;
         if (grid > 0x7fffffff) return fail(LIME_ERR_OVERFLOW, "fill window too large");
-        if (cksum)
-            hipLaunchKernelGGL(k_fill<true>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa, per,
-                               fill_gran());
+        const dim3 g((unsigned)grid);
+        const bool win = pl->reach >= 0;
+        if (cksum && win)
+            hipLaunchKernelGGL((k_fill<true, true>), g, dim3(FB), 0, S(ctx), fa, per, fill_gran());
+        else if (cksum)
+            hipLaunchKernelGGL((k_fill<true, false>), g, dim3(FB), 0, S(ctx), fa, per, fill_gran());
+        else if (win)
+            hipLaunchKernelGGL((k_fill<false, true>), g, dim3(FB), 0, S(ctx), fa, per, fill_gran());
         else
-            hipLaunchKernelGGL(k_fill<false>, dim3((unsigned)grid), dim3(FB), 0, S(ctx), fa, per,
+            hipLaunchKernelGGL((k_fill<false, false>), g, dim3(FB), 0, S(ctx), fa, per,
                                fill_gran());
     }
     LIME_HIP(hipGetLastError());
     return LIME_OK;
+}
+
+// DistributedWindow's widened set (Window.scala:34-39 condition isNearby):
+// with ADAM's distance (0 if overlapping, gap + 1 otherwise, SURVEY.md
+// Appendix A), a and b are within d >= 1 iff b strictly overlaps
+// W(a) = [a.s - d, a.e + d), so a window is the intersection join of W(A)
+// with B.  W is clipped to the contig's pad positions (off[c] - 1 and
+// off[c + 1]), so no row of a neighbouring contig can fall inside it; the
+// map is monotone in a.s, so W keeps A's sorted order.
+__global__ __launch_bounds__(256) void k_widen(const uint32_t *__restrict__ gs,
+                                               const uint32_t *__restrict__ ge, int64_t n,
+                                               int64_t d, const uint32_t *__restrict__ off,
+                                               int32_t nc, uint32_t *__restrict__ ws,
+                                               uint32_t *__restrict__ we) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = gs[i];
+    int64_t c = dev::upper_bound(off, 0, (int64_t)nc, g) - 1;
+    if (c < 0) c = 0;
+    const int64_t lo = c == 0 ? 0 : (int64_t)off[c] - 1;
+    const int64_t hi = (int64_t)off[c + 1];
+    const int64_t s = (int64_t)g - d, e = (int64_t)ge[i] + d;
+    ws[i] = (uint32_t)(s > lo ? s : lo);
+    we[i] = (uint32_t)(e < hi ? e : hi);
 }
 
 }  // namespace
@@ -761,14 +818,18 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
 // Owners are the first a_own rows of A (stream 0) and b_own rows of B
 // (stream 1); the remaining rows are a halo (partners only), used when a
 // coordinate shard carries its right neighbours' boundary rows.
+// A_out / reach: window plans (see window_plan); nullptr / -1 for intersect.
 int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold,
-                   int64_t a_own, int64_t b_own, PairsPlan **out) {
+                   int64_t a_own, int64_t b_own, PairsPlan **out, const lime_set *A_out,
+                   int64_t reach) {
     if (a_own < 0 || a_own > A->n) a_own = A->n;
     if (b_own < 0 || b_own > B->n) b_own = B->n;
     PairsPlan *pl = new PairsPlan();
     pl->ctx = ctx;
     pl->A = A;
     pl->B = B;
+    pl->A_out = A_out;
+    pl->reach = reach;
     pl->a_own = a_own;
     pl->b_own = b_own;
     pl->threshold = threshold;
@@ -794,7 +855,9 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
             const lime_set *P = st == 0 ? B : A;
             const int64_t ntl = st == 0 ? pl->nt0 : pl->nt1;
             StreamArgs sa = stream_args(O, P, st, threshold, st == 0 ? 0 : pl->nt0,
-                                        st == 0 ? 0 : a_own, st == 0 ? a_own : b_own);
+                                        st == 0 ? 0 : a_own, st == 0 ? a_own : b_own,
+                                        st == 0 ? A_out : nullptr, st == 0 ? nullptr : A_out,
+                                        reach);
             if (ntl == 0) continue;
             hipLaunchKernelGGL(k_windows, dim3(blocks_for(ntl, IB / 64)), dim3(IB), 0, S(ctx), sa,
                                pl->tp, ntl, pl->win, (const uint32_t *)O->d_off, O->n_contigs,
@@ -878,8 +941,56 @@ int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr) {
 
 int64_t plan_total(const PairsPlan *pl) { return pl->total; }
 
+// Pairs (a, b) with ADAM a.isNearby(b, d) (DistributedWindow,
+// Window.scala:71-95); the records carry a's own region (primitive returns
+// the first region, :17-22).
+int window_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t d,
+                PairsPlan **out) {
+    if (d < 1) return intersect_plan(ctx, A, B, 0, -1, -1, out, A, 0);
+    lime_set *W = new lime_set();
+    W->ctx = ctx;
+    W->n = A->n;
+    W->row = A->row;  // borrowed: W's row i is A's row i
+    W->d_off = A->d_off;
+    W->n_contigs = A->n_contigs;
+    W->off = A->off;
+    W->len = A->len;
+    W->min_width = A->min_width;
+    W->max_width = A->max_width;
+    W->has_zero_width = false;  // every W row is >= 2d wide or clipped to > 0
+    int rc = LIME_OK;
+    if ((rc = alloc(ctx, &W->gs, (size_t)std::max<int64_t>(A->n, 1))) ||
+        (rc = alloc(ctx, &W->ge, (size_t)std::max<int64_t>(A->n, 1)))) {
+        release(ctx, W->gs);
+        delete W;
+        return rc;
+    }
+    if (A->n > 0) {
+        hipLaunchKernelGGL(k_widen, dim3(blocks_for(A->n, 256)), dim3(256), 0, S(ctx), A->gs,
+                           A->ge, A->n, d, (const uint32_t *)A->d_off, A->n_contigs, W->gs,
+                           W->ge);
+        LIME_HIP(hipGetLastError());
+    }
+    PairsPlan *pl = nullptr;
+    rc = intersect_plan(ctx, W, B, 0, -1, -1, &pl, A, d);
+    if (rc != LIME_OK) {
+        release(ctx, W->gs);
+        release(ctx, W->ge);
+        delete W;
+        return rc;
+    }
+    pl->W = W;
+    *out = pl;
+    return LIME_OK;
+}
+
 void intersect_free(PairsPlan *pl) {
     lime_ctx *ctx = pl->ctx;
+    if (pl->W) {
+        release(ctx, pl->W->gs);
+        release(ctx, pl->W->ge);
+        delete pl->W;
+    }
     release(ctx, pl->olo);
     release(ctx, pl->ocnt);
     release(ctx, pl->toff);

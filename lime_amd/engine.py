@@ -294,6 +294,14 @@ class Context:
                                                 C.byref(n)))
         return Pairs(self, h, n.value, keep=(a, b))
 
+    def window(self, a, b, distance=1000):
+        """DistributedWindow: pairs (a, b) with a.isNearby(b, distance); the
+        pair records carry a's own region."""
+        h, n = vp(), i64()
+        check(_lib().lime_window_count(self._h, a._h, b._h, int(distance), C.byref(h),
+                                       C.byref(n)))
+        return Pairs(self, h, n.value, keep=(a, b))
+
     def merge(self, a):
         h, n = vp(), i64()
         check(_lib().lime_merge(self._h, a._h, C.byref(h), C.byref(n)))

@@ -148,6 +148,39 @@ class DistributedIntersection(_Op):
                 for a, b, s, e in out]
 
 
+class DistributedWindow(_Op):
+    """Window.scala:71-95: (leftRegion, (T, U)) for every right row nearby
+    (ADAM isNearby, default distance 1000) each left row."""
+
+    def __init__(self, leftRdd, rightRdd, partitionMap=None, threshold=1000, ctx=None):
+        super().__init__(ctx)
+        self.left, self.right = list(leftRdd), list(rightRdd)
+        self.partitionMap, self.threshold = partitionMap, int(threshold)
+
+    def compute(self):
+        lr, lv = _rows(self.left)
+        rr, rv = _rows(self.right)
+        space = _space_for(lr, rr)
+        lg, rg = _strand_groups(lr), _strand_groups(rr)
+        out = []
+        for strand, lrows in lg.items():
+            rrows = rg.get(strand)
+            if not rrows:
+                continue
+            A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
+            B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
+            plan = self.ctx.window(A, B, self.threshold)
+            for p in plan.fill_host():
+                out.append((lrows[p["a_row"]], rrows[p["b_row"]]))
+            plan.close()
+            A.close()
+            B.close()
+        # P = 1 emission order: left in sorted order, then cache order
+        lrank, rrank = _sorted_rank(lr), _sorted_rank(rr)
+        out.sort(key=lambda t: (lrank[t[0]], rrank[t[1]]))
+        return [(lr[a], (lv[a], rv[b])) for a, b in out]
+
+
 class DistributedSubtract(_Op):
     def __init__(self, leftRdd, rightRdd, partitionMap=None, threshold=0, ctx=None,
                  mode=_ffi.SUBTRACT_LIME):

@@ -23,6 +23,8 @@
  *     set-difference definition of SURVEY.md Appendix A.3.
  *   - merge: SetTheory.scala:208-225 (localCompute fold; condition/primitive
  *     called without threshold -> 0, quirk Q6), Merge.scala:8-31.
+ *   - window: Window.scala:51-95 (cache predicates and processHits) over the
+ *     same sweep, with ADAM's isNearby / distance (gap + 1) restated.
  *   - complement: Complement.scala:11-128 as pinned by ComplementSuite.scala
  *     (canonical P=1-independent form): gaps of
  *     merge(A) per genome contig in String order, zero-width gaps dropped,
@@ -186,6 +188,56 @@ int64_t lo_intersect(int64_t nl, const int32_t *lc, const int64_t *ls, const int
                 int64_t e = cur->end < r->end ? cur->end : r->end;
                 lo_emit(&out, cur->contig, s, e, cur->row, r->row);
             }
+        }
+    }
+    free(cache.v);
+    free(L);
+    free(R);
+    return out.count;
+}
+
+/* ---------------------------------------------------------------- window */
+
+/* ADAM ReferenceRegion.distance (3rd-party, restated):
+ * None across contigs (or strands, as overlaps), 0 if overlapping, else the
+ * gap + 1 ("abutting regions are at distance 1").  isNearby(o, d) =
+ * distance(o).exists(_ <= d).  The +1 and the strand test are not pinned by
+ * WindowSuite (its pairs are all within a few bases or overlapping). */
+static int lo_nearby(const lo_region *a, const lo_region *o, int64_t d) {
+    if (a->contig != o->contig || a->strand != o->strand) return 0;
+    if (lo_overlaps(a, o)) return 0 <= d;
+    int64_t dist = o->start >= a->end ? o->start - a->end + 1 : a->start - o->end + 1;
+    return dist <= d;
+}
+
+/* Window.scala:71-95 over the SetTheory.scala:131-187 sweep, with Window's
+ * own cache predicates (:51-68): prune <=> cached < to && !to.isNearby(cached,
+ * threshold); advance <=> cand <= until || until.isNearby(cand, threshold).
+ * processHits (:84-95) emits (L, (L.value, R.value)) for every cached R with
+ * L.isNearby(R, threshold), in cache order. */
+int64_t lo_window(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
+                  const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
+                  const int64_t *re, const int8_t *rstr, int64_t d, int64_t cap, int32_t *oc,
+                  int64_t *os, int64_t *oe, int64_t *olrow, int64_t *orrow) {
+    lo_region *L = lo_load(nl, lc, ls, le, lstr);
+    lo_region *R = lo_load(nr, rc, rs, re, rstr);
+    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+    lo_cache cache = {0};
+    int64_t rpos = 0;
+    for (int64_t i = 0; i < nl; ++i) {
+        const lo_region *cur = &L[i];
+        while (rpos < nr && (lo_cmp(&R[rpos], cur) <= 0 || lo_nearby(cur, &R[rpos], d)))
+            cache_push(&cache, &R[rpos++]);
+        int64_t index = -1; /* pruneCache, Q8: all prunable -> trim nothing */
+        for (int64_t k = cache.head; k < cache.tail; ++k)
+            if (!(lo_cmp(cache.v[k], cur) < 0 && !lo_nearby(cur, cache.v[k], d))) {
+                index = k - cache.head;
+                break;
+            }
+        if (index > 0) cache.head += index;
+        for (int64_t k = cache.head; k < cache.tail; ++k) {
+            const lo_region *r = cache.v[k];
+            if (lo_nearby(cur, r, d)) lo_emit(&out, cur->contig, cur->start, cur->end, cur->row, r->row);
         }
     }
     free(cache.v);

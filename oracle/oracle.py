@@ -41,6 +41,8 @@ def lib():
         L.lo_subtract.restype = i64
         L.lo_subtract.argtypes = pair_args + [C.c_int, i64, P(i32), P(i64), P(i64), P(i64),
                                               P(i64)]
+        L.lo_window.restype = i64
+        L.lo_window.argtypes = pair_args + [i64, P(i32), P(i64), P(i64), P(i64), P(i64)]
         L.lo_merge.restype = i64
         L.lo_merge.argtypes = [i64, P(i32), P(i64), P(i64), P(i8), i64, P(i32), P(i64), P(i64),
                                P(i8), P(i64)]
@@ -86,6 +88,21 @@ def intersect(a, b, threshold=0):
     n = L.lo_intersect(*args, 0, None, None, None, None, None)
     o = _out(n)
     L.lo_intersect(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))])
+    return _result(o)
+
+
+def window(a, b, distance=1000):
+    """Window.scala sweep restated (lo_window): pairs (a, b) with
+    a.isNearby(b, distance); start / end are a's own region.  Reference
+    emission order (left sorted order, then cache order)."""
+    L = lib()
+    na, ac, as_, ae, ast = _in(*a)
+    nb, bc, bs, be, bst = _in(*b)
+    args = [na, _p(ac, i32), _p(as_, i64), _p(ae, i64), _p(ast, i8), nb, _p(bc, i32),
+            _p(bs, i64), _p(be, i64), _p(bst, i8), int(distance)]
+    n = L.lo_window(*args, 0, None, None, None, None, None)
+    o = _out(n)
+    L.lo_window(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))])
     return _result(o)
 
 

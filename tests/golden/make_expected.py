@@ -29,6 +29,8 @@ def main():
         "subtract": regions("SubtractSuite.scala"),
         "complement": regions("ComplementSuite.scala"),
         "merge_count": 1,
+        # WindowSuite.scala:22-31: (left, right) region pairs, bedtools window
+        "window": [r for r in zip(*[iter(regions("WindowSuite.scala"))] * 2)],
         # full truth for intersect_with_overlap_00 x _01 (left sorted order,
         # then right order), derived by hand from the fixture rows
         "intersection_full": [

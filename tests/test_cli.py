@@ -22,7 +22,7 @@ def g(name):
 def test_usage_and_version():
     r = run()
     assert r.returncode == 0 and "Choose one of the following commands" in r.stdout
-    for cmd in ("complement", "intersect", "merge", "subtract", "sort"):
+    for cmd in ("complement", "intersect", "merge", "subtract", "sort", "window"):
         assert cmd in r.stdout
     r = run("-version")
     assert r.returncode == 0 and r.stdout.startswith("Version 0")
@@ -63,3 +63,18 @@ def test_cli_intersect_subtract_merge_complement_sort():
     assert len(out) == 28691
     key = [(c.encode("utf-16-be"), int(s), int(e)) for c, s, e, _ in out]
     assert key == sorted(key)
+
+
+@pytest.mark.gpu
+def test_cli_window():
+    # WindowSuite.scala:8-34 through the CLI (cli/Window.scala, distance 1000)
+    out = lines(run("window", g("intersect_with_overlap_00.bed"), g("window_with_overlap_01.bed")))
+    assert [[[c, int(s), int(e)]] for c, s, e, *_ in out] == \
+        [[p[0]] for p in expected()["window"]]
+    # -distance 9 keeps the 9-base gap (distance 10 > 9 drops it: gap + 1)
+    out = lines(run("window", g("intersect_with_overlap_00.bed"), g("window_with_overlap_01.bed"),
+                    "-distance", "10"))
+    assert ["chr1", "135453", "139441", "CpG:_99", "CpG:_116"] in out
+    out = lines(run("window", g("intersect_with_overlap_00.bed"), g("window_with_overlap_01.bed"),
+                    "-distance", "9"))
+    assert ["chr1", "135453", "139441", "CpG:_99", "CpG:_116"] not in out

@@ -8,8 +8,8 @@ import pytest
 
 from lime_amd import LimeError, Space, SUBTRACT_LIME, SUBTRACT_SET, synth
 from lime_amd.set_theory import (DistributedComplement, DistributedIntersection,
-                                 DistributedMerge, DistributedSubtract, NoSuchElementException,
-                                 ReferenceRegion)
+                                 DistributedMerge, DistributedSubtract, DistributedWindow,
+                                 NoSuchElementException, ReferenceRegion)
 from oracle import oracle
 from tests.util import (GOLDEN, as_sorted_tuples, expected, random_sets, read_bed_py,
                         read_genome_py)
@@ -59,6 +59,17 @@ def test_complement_suite(ctx):
     bounds = {n: ReferenceRegion(n, 0, l) for n, l in zip(names, lens)}
     out = DistributedComplement(keyed("cpg_20merge.bed"), None, bounds, ctx=ctx).compute()
     assert [r for r, _ in out] == rr(expected()["complement"])
+
+
+def test_window_suite(ctx):
+    # WindowSuite.scala:8-34 (default distance 1000): all 10 bedtools pairs
+    out = DistributedWindow(keyed("intersect_with_overlap_00.bed"),
+                            keyed("window_with_overlap_01.bed"), None, ctx=ctx).compute()
+    got = [[[r.referenceName, r.start, r.end]] for r, _ in out]
+    assert [g[0] for g in got] == [p[0] for p in expected()["window"]]
+    right = {n: (c, a, b) for c, a, b, n in zip(*read_bed_py(
+        os.path.join(GOLDEN, "window_with_overlap_01.bed")))}
+    assert [list(right[v[1]]) for _, v in out] == [p[1] for p in expected()["window"]]
 
 
 def test_complement_missing_contig_raises(ctx):
@@ -130,6 +141,30 @@ def test_intersect_deep_windows(ctx, seed, n, contig_len, max_len):
     want = oracle.checksum_pairs(exp)
     assert oracle.checksum_pairs(plan.fill_host()) == want
     assert plan.checksum() == want
+
+
+@pytest.mark.parametrize("seed,d", [(61, 0), (62, 1), (63, 7), (64, 150), (65, 1000),
+                                    (66, 40000)])
+def test_window_parity(ctx, seed, d):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 2500, 2000, n_contigs=3, contig_len=30000, max_len=400,
+                       zero_frac=0.1, dup_frac=0.05, book_frac=0.1)
+    # contig-edge rows: zero-width and short rows at both ends of every contig
+    for X in (A, B):
+        k = len(X[1])
+        for i, (c, s0, l) in enumerate([(0, 0, 0), (0, 0, 3), (1, 0, 0), (1, 30000, 0),
+                                        (2, 29990, 10), (0, 30000, 0), (2, 0, 0)]):
+            X[0][k - 1 - i], X[1][k - 1 - i], X[2][k - 1 - i] = c, s0, s0 + l
+    sp = space_for(3, 30000)
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    plan = ctx.window(a, b, d)
+    exp = oracle.window(A, B, d)
+    assert plan.n == len(exp["start"])
+    p = plan.fill_host()
+    got = {"contig": A[0][p["a_row"]], "start": p["start"], "end": p["end"],
+           "a_row": p["a_row"], "b_row": p["b_row"]}
+    assert as_sorted_tuples(got) == as_sorted_tuples(exp)
+    assert plan.checksum() == oracle.checksum_pairs(exp)
 
 
 @pytest.mark.parametrize("seed,zero,book", [(11, 0.0, 0.0), (12, 0.1, 0.1), (13, 0.3, 0.3)])

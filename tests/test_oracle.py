@@ -55,6 +55,53 @@ def test_subtract_suite(io):
     assert regions(oracle.subtract(A, B, mode=oracle.SUB_SET), names) == expected()["subtract"]
 
 
+def test_window_suite():
+    # WindowSuite.scala:8-34: left intersect_with_overlap_00, right
+    # window_with_overlap_01, default distance 1000; all 10 bedtools pairs
+    a, _, _, _ = read_bed_py(os.path.join(GOLDEN, "intersect_with_overlap_00.bed"))
+    b, _, _, _ = read_bed_py(os.path.join(GOLDEN, "window_with_overlap_01.bed"))
+    rank = ranked(a + b)
+    names = sorted(rank, key=rank.get)
+    A = load("intersect_with_overlap_00.bed", rank)
+    B = load("window_with_overlap_01.bed", rank)
+    got = oracle.window(A, B, 1000)
+    pairs = [[[names[c], int(s), int(e)],
+              [names[B[0][r]], int(B[1][r]), int(B[2][r])]]
+             for c, s, e, r in zip(got["contig"], got["start"], got["end"], got["b_row"])]
+    assert pairs == expected()["window"]
+
+
+def nearby_brute(a, b, d):
+    """ADAM isNearby restated independently: same contig, overlap (strict,
+    Appendix A) or gap + 1 <= d."""
+    (ac, as_, ae), (bc, bs, be) = a, b
+    out = []
+    for i in range(len(as_)):
+        for j in range(len(bs)):
+            if ac[i] != bc[j]:
+                continue
+            if ae[i] > bs[j] and as_[i] < be[j]:
+                dist = 0
+            elif bs[j] >= ae[i]:
+                dist = bs[j] - ae[i] + 1
+            else:
+                dist = as_[i] - be[j] + 1
+            if dist <= d:
+                out.append((int(i), int(j)))
+    return sorted(out)
+
+
+@pytest.mark.parametrize("seed,d", [(51, 1), (52, 7), (53, 150), (54, 1000)])
+def test_window_vs_brute(seed, d):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 300, 250, n_contigs=3, contig_len=6000, max_len=200,
+                       zero_frac=0.1, dup_frac=0.05, book_frac=0.1)
+    got = oracle.window(A, B, d)
+    assert sorted(zip(got["a_row"].tolist(), got["b_row"].tolist())) == nearby_brute(A, B, d)
+    # records carry the left row's own region
+    assert (got["start"] == A[1][got["a_row"]]).all() and (got["end"] == A[2][got["a_row"]]).all()
+
+
 def test_merge_suite():
     chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, "cpg_20merge.bed"))
     rank = ranked(chrom)

@@ -1,0 +1,3 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s17_tests.txt 2>&1

@@ -434,6 +434,75 @@ class DistributedMerge {
     Engine &eng_;
 };
 
+// Cluster.scala:8-121: Merge's fold, keyed by each cluster's FIRST member
+// region (postProcess :33-35).  The fold passes no threshold (quirk Q6), so
+// every variant is the strict-overlap fold: strand-blind (covers) for the
+// unstranded variants, per strand (overlaps) for the stranded ones.
+template <class T, bool STRANDED>
+class ClusterOp {
+   public:
+    ClusterOp(RDD<T> rdd, PartitionMap partitionMap = {}, int64_t threshold = 0,
+              Engine &eng = Engine::thread_default())
+        : rdd_(std::move(rdd)), pm_(std::move(partitionMap)), threshold_(threshold), eng_(eng) {}
+
+    std::vector<std::pair<ReferenceRegion, std::vector<T>>> compute() {
+        auto sp = detail::space_of<T>({&rdd_});
+        auto rank = detail::sorted_rank(rdd_);
+        std::map<int, std::vector<size_t>> groups;
+        if (STRANDED) {
+            for (auto &g : detail::strand_groups(rdd_)) groups[(int)g.first] = g.second;
+        } else {
+            auto &all = groups[0];
+            for (size_t i = 0; i < rdd_.size(); ++i) all.push_back(i);
+        }
+        std::vector<std::vector<size_t>> clusters;  // member rows in fold order
+        for (auto &g : groups) {
+            if (g.second.empty()) continue;
+            detail::SetHandle A;
+            detail::upload(eng_.ctx(), *sp, rdd_, g.second, A);
+            lime_result *res = nullptr;
+            int64_t cnt = 0;
+            check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
+            std::vector<int64_t> rid(g.second.size());
+            int rc = lime_result_run_of_row(res, rid.data());
+            lime_result_destroy(res);
+            check(rc);
+            std::vector<size_t> members(g.second.size());
+            std::iota(members.begin(), members.end(), 0);
+            std::sort(members.begin(), members.end(),
+                      [&](size_t x, size_t y) { return rank[g.second[x]] < rank[g.second[y]]; });
+            size_t base = clusters.size();
+            clusters.resize(base + (size_t)cnt);
+            for (size_t m : members) clusters[base + (size_t)rid[m]].push_back(g.second[m]);
+        }
+        std::sort(clusters.begin(), clusters.end(),
+                  [&](const std::vector<size_t> &x, const std::vector<size_t> &y) {
+                      return rank[x[0]] < rank[y[0]];
+                  });
+        std::vector<std::pair<ReferenceRegion, std::vector<T>>> out;
+        for (auto &c : clusters) {
+            std::vector<T> v;
+            for (size_t i : c) v.push_back(rdd_[i].second);
+            out.push_back({rdd_[c[0]].first, std::move(v)});
+        }
+        return out;
+    }
+
+   private:
+    RDD<T> rdd_;
+    PartitionMap pm_;
+    int64_t threshold_;
+    Engine &eng_;
+};
+template <class T>
+using UnstrandedCluster = ClusterOp<T, false>;
+template <class T>
+using UnstrandedClusterWithMinimumOverlap = ClusterOp<T, false>;
+template <class T>
+using StrandedCluster = ClusterOp<T, true>;
+template <class T>
+using StrandedClusterWithMinimumOverlap = ClusterOp<T, true>;
+
 template <class T>
 class DistributedComplement {
    public:

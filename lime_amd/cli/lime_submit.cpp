@@ -8,6 +8,9 @@
 //   complement A.bed genome.txt cli/Complement.scala:154-166 (prints regions)
 //   subtract  A.bed B.bed       DistributedSubtract (API-only in the reference)
 //   sort      A.bed             cli/Sort.scala:34-38 (device radix sort)
+//   cluster   A.bed             cli/Cluster.scala:36-44 (UnstrandedCluster; the
+//                               reference defines it but LimeMain does not
+//                               register it)
 //   window    A.bed B.bed [-distance D]   cli/Window.scala:42-55 (keys stranded,
 //                               DistributedWindow default distance 1000)
 //
@@ -37,6 +40,7 @@ const Cmd kCommands[] = {
     {"subtract", "Remove regions of the second input from the first"},
     {"sort", "Sorts the regions in a single input"},
     {"window", "Compute nearby regions between two inputs"},
+    {"cluster", "Cluster (but don't merge) overlapping/nearby intervals"},
 };
 
 void usage() {
@@ -86,6 +90,15 @@ int run(const std::vector<std::string> &args) {
         for (auto &o : out) {
             print_region(o.first);
             printf("\t%s\t%s\n", o.second.first.c_str(), o.second.second.c_str());
+        }
+    } else if (cmd == "cluster") {
+        need(1);
+        auto out = UnstrandedCluster<std::string>(load_bed(args[1], true)).compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\t%zu", o.second.size());
+            for (auto &v : o.second) printf("\t%s", v.c_str());
+            printf("\n");
         }
     } else if (cmd == "window") {
         need(2);

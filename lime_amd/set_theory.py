@@ -12,6 +12,11 @@ lime-core/src/main/scala/org/bdgenomics/lime/set_theory/:
     DistributedComplement(rddToCompute, partitionMap, referenceNameBounds,
                           threshold=0).compute()
         -> [(ReferenceRegion, [])]                 Complement.scala:131-134
+    DistributedWindow(leftRdd, rightRdd, partitionMap, threshold=1000).compute()
+        -> [(ReferenceRegion, (T, U))]             Window.scala:71-95
+    UnstrandedCluster / StrandedCluster / ...WithMinimumOverlap(rddToCompute,
+                          partitionMap, threshold=0).compute()
+        -> [(ReferenceRegion, [T])]                Cluster.scala:38-121
 
 An "RDD" here is any iterable of (ReferenceRegion, value) pairs held on the
 host.  `partitionMap` is accepted for signature parity and ignored: the
@@ -260,3 +265,54 @@ class DistributedComplement(_Op):
         h = self.ctx.complement(space, A).to_host()
         return [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
                                  int(h["end"][k])), []) for k in range(len(h["start"]))]
+
+
+class _Cluster(_Op):
+    """Cluster.scala:8-36: the SetTheory.scala:208-225 fold of Merge, keyed by
+    the cluster's FIRST member region (postProcess :33-35) instead of the
+    hull.  localCompute passes no threshold to `condition` (quirk Q6), so at
+    P = 1 every variant is the strict-overlap fold: covers (strand-blind) for
+    the Unstranded variants, overlaps (equal strands) for the Stranded ones."""
+    STRANDED = False
+
+    def __init__(self, rddToCompute, partitionMap=None, threshold=0, ctx=None):
+        super().__init__(ctx)
+        self.rdd = list(rddToCompute)
+        self.partitionMap, self.threshold = partitionMap, int(threshold)
+
+    def compute(self):
+        regs, vals = _rows(self.rdd)
+        space = _space_for(regs)
+        groups = _strand_groups(regs) if self.STRANDED else {None: list(range(len(regs)))}
+        rank = _sorted_rank(regs)
+        out = []
+        for rows in groups.values():
+            A = self.ctx.set_from_host(space, *_arrays(space, regs, rows))
+            res = self.ctx.merge(A)
+            rid = res.run_of_row(len(rows))
+            members = [[] for _ in range(res.n)]
+            for local in sorted(range(len(rows)), key=lambda i: rank[rows[i]]):
+                members[rid[local]].append(rows[local])
+            res.close()
+            A.close()
+            out += [m for m in members if m]
+        out.sort(key=lambda m: rank[m[0]])  # fold order: by the first member
+        return [(regs[m[0]], [vals[i] for i in m]) for m in out]
+
+
+class UnstrandedCluster(_Cluster):
+    """Cluster.scala:38-57 (condition: covers, strand-blind)."""
+
+
+class UnstrandedClusterWithMinimumOverlap(_Cluster):
+    """Cluster.scala:80-100 (coversBy >= threshold; Q6: threshold 0 in the fold)."""
+
+
+class StrandedCluster(_Cluster):
+    """Cluster.scala:59-78 (condition: overlaps, equal strands)."""
+    STRANDED = True
+
+
+class StrandedClusterWithMinimumOverlap(_Cluster):
+    """Cluster.scala:102-121 (overlapsBy >= threshold; Q6: threshold 0 in the fold)."""
+    STRANDED = True

@@ -22,7 +22,7 @@ def g(name):
 def test_usage_and_version():
     r = run()
     assert r.returncode == 0 and "Choose one of the following commands" in r.stdout
-    for cmd in ("complement", "intersect", "merge", "subtract", "sort", "window"):
+    for cmd in ("complement", "intersect", "merge", "subtract", "sort", "window", "cluster"):
         assert cmd in r.stdout
     r = run("-version")
     assert r.returncode == 0 and r.stdout.startswith("Version 0")
@@ -78,3 +78,11 @@ def test_cli_window():
     out = lines(run("window", g("intersect_with_overlap_00.bed"), g("window_with_overlap_01.bed"),
                     "-distance", "9"))
     assert ["chr1", "135453", "139441", "CpG:_99", "CpG:_116"] not in out
+
+
+@pytest.mark.gpu
+def test_cli_cluster():
+    # cli/Cluster.scala + ClusterSuite: one cluster keyed by the first member
+    out = lines(run("cluster", g("cpg_20merge.bed")))
+    assert len(out) == 1 and out[0][3] == "20"
+    assert out[0][:3] == ["chr1", "28735", "29810"]

@@ -9,7 +9,8 @@ import pytest
 from lime_amd import LimeError, Space, SUBTRACT_LIME, SUBTRACT_SET, synth
 from lime_amd.set_theory import (DistributedComplement, DistributedIntersection,
                                  DistributedMerge, DistributedSubtract, DistributedWindow,
-                                 NoSuchElementException, ReferenceRegion)
+                                 NoSuchElementException, ReferenceRegion, StrandedCluster,
+                                 UnstrandedCluster, UnstrandedClusterWithMinimumOverlap)
 from oracle import oracle
 from tests.util import (GOLDEN, as_sorted_tuples, expected, random_sets, read_bed_py,
                         read_genome_py)
@@ -70,6 +71,60 @@ def test_window_suite(ctx):
     right = {n: (c, a, b) for c, a, b, n in zip(*read_bed_py(
         os.path.join(GOLDEN, "window_with_overlap_01.bed")))}
     assert [list(right[v[1]]) for _, v in out] == [p[1] for p in expected()["window"]]
+
+
+def test_cluster_suite(ctx):
+    # ClusterSuite.scala:8-16: cpg_20merge.bed clusters into one
+    rows = keyed("cpg_20merge.bed")
+    out = UnstrandedCluster(rows, None, ctx=ctx).compute()
+    assert len(out) == 1
+    first = min(rows, key=lambda kv: (kv[0].start, kv[0].end))
+    assert out[0][0] == first[0]  # keyed by the first member, not the hull
+    assert len(out[0][1]) == 20
+
+
+def _fold_clusters(regs, stranded):
+    """Merge.scala / Cluster.scala fold restated on the sorted rows: a new
+    cluster whenever the row does not strictly overlap the running hull (or,
+    stranded, has another strand); returns member index lists in fold order."""
+    order = sorted(range(len(regs)), key=lambda i: (regs[i].referenceName, regs[i].start,
+                                                    regs[i].end, regs[i].strand, i))
+    groups = {}
+    for i in order:
+        groups.setdefault(regs[i].strand if stranded else None, []).append(i)
+    out = []
+    for rows in groups.values():
+        cur, hull = [], None
+        for i in rows:
+            r = regs[i]
+            if cur and r.referenceName == hull[0] and r.start < hull[2] and r.end > hull[1]:
+                cur.append(i)
+                hull = (hull[0], min(hull[1], r.start), max(hull[2], r.end))
+            else:
+                if cur:
+                    out.append(cur)
+                cur, hull = [i], (r.referenceName, r.start, r.end)
+        if cur:
+            out.append(cur)
+    pos = {i: k for k, i in enumerate(order)}
+    out.sort(key=lambda m: pos[m[0]])
+    return out
+
+
+@pytest.mark.parametrize("seed", [71, 72])
+def test_cluster_parity(ctx, seed):
+    rng = np.random.default_rng(seed)
+    (c, s0, e0), _ = random_sets(rng, 3000, 1, n_contigs=3, contig_len=40000, max_len=300,
+                                 zero_frac=0.05, dup_frac=0.05, book_frac=0.1)
+    strands = rng.choice(["FORWARD", "REVERSE"], len(c))
+    regs = [ReferenceRegion(NAMES[ci], int(a), int(b), st) for ci, a, b, st in
+            zip(c, s0, e0, strands)]
+    rows = [(r, i) for i, r in enumerate(regs)]
+    for op, stranded in ((UnstrandedCluster, False), (UnstrandedClusterWithMinimumOverlap, False),
+                         (StrandedCluster, True)):
+        got = op(rows, None, ctx=ctx).compute()
+        exp = _fold_clusters(regs, stranded)
+        assert [(k, v) for k, v in got] == [(regs[m[0]], m) for m in exp]
 
 
 def test_complement_missing_contig_raises(ctx):

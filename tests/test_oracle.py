@@ -102,6 +102,15 @@ def test_window_vs_brute(seed, d):
     assert (got["start"] == A[1][got["a_row"]]).all() and (got["end"] == A[2][got["a_row"]]).all()
 
 
+def test_cluster_suite():
+    # ClusterSuite.scala:8-16: UnstrandedCluster of cpg_20merge.bed is one
+    # cluster (the Merge fold, strand-blind, keyed by the first member)
+    chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, "cpg_20merge.bed"))
+    rank = ranked(chrom)
+    res = oracle.merge((np.array([rank[c] for c in chrom], np.int32), s, e))
+    assert len(res["start"]) == 1 and (res["run_of_row"] == 0).all()
+
+
 def test_merge_suite():
     chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, "cpg_20merge.bed"))
     rank = ranked(chrom)

@@ -65,6 +65,7 @@ typedef struct lime_set lime_set;       /* sorted, device-resident interval set 
 typedef struct lime_pairs lime_pairs;   /* intersect plan: pair count + fill state  */
 typedef struct lime_result lime_result; /* merge / subtract / complement output     */
 typedef struct lime_bed lime_bed;       /* parsed BED file (host memory)            */
+typedef struct lime_dbed lime_dbed;     /* parsed BED text (device memory)          */
 typedef struct lime_bitset lime_bitset; /* bit-per-base set over a space            */
 
 /* One intersect output record: the intersection region in contig-local
@@ -220,6 +221,26 @@ const int8_t *lime_bed_strands(const lime_bed *bed);
 const char *lime_bed_name(const lime_bed *bed, int64_t row); /* 4th column or "" */
 void lime_bed_free(lime_bed *bed);
 /* genome file: "name<TAB>length" per line (cli/Complement.scala:43-44) */
+
+/* BED text parsed ON THE DEVICE (ADAM sc.loadBed replacement, cli/
+ * Intersection.scala:42-45): `text` holds nbytes of BED in host memory; the
+ * records stay in HBM as contig id (order of first appearance, names via
+ * lime_dbed_contig_name), u32 start / end, strand code, and the byte offset +
+ * length of the 4th column in `text`.  Same record rules and error codes as
+ * lime_bed_read; coordinates outside [0, 2^32) are LIME_ERR_RANGE. */
+int lime_bed_parse_device(lime_ctx *ctx, const char *text, int64_t nbytes, lime_dbed **out);
+int64_t lime_dbed_rows(const lime_dbed *bed);
+int32_t lime_dbed_contigs(const lime_dbed *bed);
+const char *lime_dbed_contig_name(const lime_dbed *bed, int32_t i);
+int lime_dbed_device_arrays(const lime_dbed *bed, const int32_t **contig, const uint32_t **start,
+                            const uint32_t **end, const int8_t **strand);
+int lime_dbed_fill_host(const lime_dbed *bed, int32_t *contig, int64_t *start, int64_t *end,
+                        int8_t *strand, int64_t *name_off, int32_t *name_len);
+/* Rewrite the device contig ids in place: id i -> new_id_of_contig[i] (n =
+ * lime_dbed_contigs), e.g. to a lime_space's String-order ids before
+ * lime_set_create_device.  Once per handle. */
+int lime_dbed_remap_contigs(lime_dbed *bed, const int32_t *new_id_of_contig, int32_t n);
+void lime_dbed_free(lime_dbed *bed);
 int lime_genome_read(const char *path, int32_t *n_out, char ***names_out, int64_t **lengths_out);
 void lime_genome_free(int32_t n, char **names, int64_t *lengths);
 uint64_t lime_pair_hash(uint32_t start, uint32_t end, uint32_t a_row, uint32_t b_row);

@@ -102,6 +102,14 @@ SIGNATURES = {
     "lime_bed_strands": (P(C.c_int8), [vp]),
     "lime_bed_name": (C.c_char_p, [vp, i64]),
     "lime_bed_free": (None, [vp]),
+    "lime_bed_parse_device": (C.c_int, [vp, C.c_char_p, i64, pp]),
+    "lime_dbed_rows": (i64, [vp]),
+    "lime_dbed_contigs": (i32, [vp]),
+    "lime_dbed_contig_name": (C.c_char_p, [vp, i32]),
+    "lime_dbed_device_arrays": (C.c_int, [vp, pp, pp, pp, pp]),
+    "lime_dbed_fill_host": (C.c_int, [vp, P(i32), P(i64), P(i64), P(C.c_int8), P(i64), P(i32)]),
+    "lime_dbed_remap_contigs": (C.c_int, [vp, P(i32), i32]),
+    "lime_dbed_free": (None, [vp]),
     "lime_genome_read": (C.c_int, [C.c_char_p, P(i32), P(P(C.c_char_p)), P(P(i64))]),
     "lime_genome_free": (None, [i32, P(C.c_char_p), P(i64)]),
     "lime_pair_hash": (u64, [u32, u32, u32, u32]),

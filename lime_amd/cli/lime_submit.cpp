@@ -55,21 +55,37 @@ Strand strand_of(int8_t s) {
                                                                         : Strand::Independent;
 }
 
+// BED -> keyed RDD: the text is parsed on the device (lime_bed_parse_device,
+// the sc.loadBed replacement); records and names come back to the host
+// because the operator mirror keys host-side payloads.
 RDD<std::string> load_bed(const std::string &path, bool stranded) {
-    lime_bed *b = nullptr;
-    check(lime_bed_read(path.c_str(), &b));
-    int64_t n = lime_bed_rows(b);
-    const int32_t *c = lime_bed_contig_ids(b);
-    const int64_t *s = lime_bed_starts(b);
-    const int64_t *e = lime_bed_ends(b);
-    const int8_t *st = lime_bed_strands(b);
+    std::string text;
+    {
+        FILE *f = fopen(path.c_str(), "rb");
+        if (!f) throw Error(LIME_ERR_IO, "cannot read " + path);
+        char buf[1 << 16];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, k);
+        fclose(f);
+    }
+    lime_dbed *b = nullptr;
+    check(lime_bed_parse_device(Engine::thread_default().ctx(), text.data(),
+                                (int64_t)text.size(), &b));
+    const int64_t n = lime_dbed_rows(b);
+    std::vector<int32_t> c((size_t)n), nl((size_t)n);
+    std::vector<int64_t> s((size_t)n), e((size_t)n), no((size_t)n);
+    std::vector<int8_t> st((size_t)n);
+    int rc = lime_dbed_fill_host(b, c.data(), s.data(), e.data(), st.data(), no.data(), nl.data());
+    std::vector<std::string> names;
+    for (int32_t i = 0; i < lime_dbed_contigs(b); ++i) names.push_back(lime_dbed_contig_name(b, i));
+    lime_dbed_free(b);
+    check(rc);
     RDD<std::string> rdd;
     rdd.reserve((size_t)n);
     for (int64_t i = 0; i < n; ++i)
-        rdd.push_back({ReferenceRegion(lime_bed_contig_name(b, c[i]), s[i], e[i],
+        rdd.push_back({ReferenceRegion(names[c[i]], s[i], e[i],
                                        stranded ? strand_of(st[i]) : Strand::Independent),
-                       lime_bed_name(b, i)});
-    lime_bed_free(b);
+                       text.substr((size_t)no[i], (size_t)nl[i])});
     return rdd;
 }
 

@@ -302,6 +302,13 @@ class Context:
                                        C.byref(n)))
         return Pairs(self, h, n.value, keep=(a, b))
 
+    def parse_bed(self, text):
+        """Parse BED text (bytes) on the device -> DeviceBed (arrays in HBM)."""
+        h = vp()
+        text = bytes(text)
+        check(_lib().lime_bed_parse_device(self._h, text, len(text), C.byref(h)))
+        return DeviceBed(self, h, text)
+
     def merge(self, a):
         h, n = vp(), i64()
         check(_lib().lime_merge(self._h, a._h, C.byref(h), C.byref(n)))
@@ -349,6 +356,61 @@ class Context:
     def close(self):
         if getattr(self, "_h", None):
             _lib().lime_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBed:
+    """lime_dbed: BED records parsed on the device (ADAM loadBed replacement)."""
+
+    def __init__(self, ctx, handle, text):
+        self.ctx, self._h, self.text = ctx, handle, text
+
+    @property
+    def n(self):
+        return int(_lib().lime_dbed_rows(self._h))
+
+    @property
+    def names(self):
+        lib = _lib()
+        return [lib.lime_dbed_contig_name(self._h, i).decode()
+                for i in range(lib.lime_dbed_contigs(self._h))]
+
+    def device_arrays(self):
+        c, s, e, st = vp(), vp(), vp(), vp()
+        check(_lib().lime_dbed_device_arrays(self._h, C.byref(c), C.byref(s), C.byref(e),
+                                             C.byref(st)))
+        return c.value, s.value, e.value, st.value
+
+    def to_host(self):
+        n = self.n
+        out = {"contig": np.zeros(n, np.int32), "start": np.zeros(n, np.int64),
+               "end": np.zeros(n, np.int64), "strand": np.zeros(n, np.int8),
+               "name_off": np.zeros(n, np.int64), "name_len": np.zeros(n, np.int32)}
+        check(_lib().lime_dbed_fill_host(self._h, _ptr(out["contig"], i32),
+                                         _ptr(out["start"], i64), _ptr(out["end"], i64),
+                                         _ptr(out["strand"], C.c_int8),
+                                         _ptr(out["name_off"], i64), _ptr(out["name_len"], i32)))
+        out["name"] = [self.text[o:o + k].decode() for o, k in zip(out["name_off"].tolist(),
+                                                                   out["name_len"].tolist())]
+        return out
+
+    def to_set(self, space):
+        """Remap contig ids to `space` on the device and build the sorted set
+        from the device arrays (no host round trip of the records)."""
+        ids = np.array([space.index[nm] for nm in self.names], dtype=np.int32)
+        check(_lib().lime_dbed_remap_contigs(self._h, _ptr(ids, i32), len(ids)))
+        c, s, e, _ = self.device_arrays()
+        return self.ctx.set_from_device(space, self.n, c, s, e)
+
+    def close(self):
+        if self._h:
+            _lib().lime_dbed_free(self._h)
             self._h = None
 
     def __del__(self):

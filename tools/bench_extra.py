@@ -11,6 +11,9 @@
   C5  8-way intersection over 1e9 rows (8 x 1.25e8, len U[10,40], seeds
       0x50..0x57): sort each set -> bitsets -> 8-way AND runs.  On one GPU
       (the whole genome); unit: intervals/s
+  bed BED text parse on the device (lime_bed_parse_device, 8(f) row 1):
+      1e7 BED6 lines over hg38 (host text, H2D inside the call); unit:
+      lines/s, with the host reader (lime_bed_read, 1 thread) beside it
 
 Inputs are generated on the device (counter-based RNG) outside the timed
 region; every step starts from unsorted rows in HBM.
@@ -29,7 +32,7 @@ HBM = 8000.0
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c4", "c5"], required=True)
+    p.add_argument("--workload", choices=["c3", "c4", "c5", "bed"], required=True)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scale", type=float, default=1.0, help="row-count scale (testing)")
@@ -67,6 +70,9 @@ def main():
         n, c, s, e = x
         return ctx.set_from_device(space, n, c.data_ptr(), s.data_ptr(), e.data_ptr())
 
+    if a.workload == "bed":
+        bed_bench(a, ctx, space)
+        return
     if a.workload == "c3":
         inp = gen(int(5e8 * a.scale), 0xC, 150, 600, pile=(2_000_000, 150))
         n = inp[0]
@@ -166,6 +172,58 @@ def main():
                       "ms_per_step": dt * 1e3, "steps": a.steps, "breakdown_ms": br,
                       "roofline": rf}), flush=True)
     ctx.close()
+
+
+def bed_bench(a, ctx, space):
+    import tempfile
+
+    import numpy as np
+    import torch
+    from lime_amd.engine import read_bed
+    n = int(1e7 * a.scale)
+    rng = np.random.default_rng(9)
+    names = np.array(space.names)
+    c = rng.integers(0, len(names), n)
+    s = rng.integers(0, 150_000_000, n)
+    e = s + rng.integers(50, 5000, n)
+    st = rng.choice(np.array(["+", "-", "."]), n)
+    lines = np.char.add(np.char.add(np.char.add(names[c], "\t"), s.astype(str)), "\t")
+    lines = np.char.add(np.char.add(lines, e.astype(str)), "\tr\t0\t")
+    lines = np.char.add(lines, st)
+    text = ("\n".join(lines.tolist()) + "\n").encode()
+    del lines
+    ts = []
+    for r in range(a.warmup + a.steps):
+        t = time.perf_counter()
+        d = ctx.parse_bed(text)
+        ctx.synchronize()
+        ts.append(time.perf_counter() - t)
+        assert d.n == n
+        d.close()
+    dt = sorted(ts[a.warmup:])[len(ts[a.warmup:]) // 2]
+    buf = torch.frombuffer(bytearray(text), dtype=torch.uint8)
+    t = time.perf_counter()
+    g = buf.to("cuda:0")
+    torch.cuda.synchronize()
+    h2d = time.perf_counter() - t
+    del g
+    with tempfile.NamedTemporaryFile(suffix=".bed", dir="/dev/shm" if os.path.isdir("/dev/shm")
+                                     else None) as f:
+        f.write(text)
+        f.flush()
+        t = time.perf_counter()
+        host = read_bed(f.name)
+        th = time.perf_counter() - t
+    assert len(host["start"]) == n
+    print(json.dumps({"workload": "bed", "config": f"device BED parse of {n} BED6 lines "
+                      f"({len(text) / 1e9:.2f} GB text, host memory, H2D inside the call)",
+                      "value": n / dt, "unit": "lines/s", "ms_per_step": dt * 1e3,
+                      "steps": a.steps, "text_GBps_end_to_end": len(text) / dt / 1e9,
+                      "breakdown_ms": {"h2d_pageable_ms": h2d * 1e3,
+                                       "device_ms_excl_h2d": (dt - h2d) * 1e3},
+                      "host_reader": {"value": n / th, "unit": "lines/s", "cores": 1,
+                                      "kind": "lime_bed_read (bed.cpp), incl. file read"}}),
+          flush=True)
 
 
 if __name__ == "__main__":

@@ -104,6 +104,14 @@ int64_t lime_space_offset(const lime_space *space, int32_t contig);
  * Rows keep their input index (0..n-1) as the payload handle. */
 int lime_set_create_host(lime_ctx *ctx, const lime_space *space, int64_t n, const int32_t *contig,
                          const int64_t *start, const int64_t *end, lime_set **out);
+/* Stranded set (the CLI keys ReferenceRegion.stranded): strand codes per row
+ * (0 independent, 1 forward, 2 reverse, 3 unknown).  Sorted in the full
+ * RegionOrdering (start, end, strand); lime_merge on it follows the
+ * reference fold exactly: a run breaks where the strand changes
+ * (Merge.condition = overlaps, which requires equal strands). */
+int lime_set_create_host_stranded(lime_ctx *ctx, const lime_space *space, int64_t n,
+                                  const int32_t *contig, const int64_t *start,
+                                  const int64_t *end, const int8_t *strand, lime_set **out);
 /* Device arrays (u32 contig-local coordinates) already resident in HBM:
  * validated and sorted on the context's stream, inputs are not modified. */
 int lime_set_create_device(lime_ctx *ctx, const lime_space *space, int64_t n,

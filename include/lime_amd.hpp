@@ -36,6 +36,12 @@
 namespace lime {
 
 enum class Strand : int8_t { Independent = 0, Forward = 1, Reverse = 2, Unknown = 3 };
+// RegionOrdering compares bdg-formats' Strand enum ordinals (FORWARD,
+// REVERSE, INDEPENDENT, UNKNOWN)
+inline int strand_ord(Strand s) {
+    static const int ord[4] = {2, 0, 1, 3};
+    return ord[(int)s & 3];
+}
 
 struct ReferenceRegion {
     std::string referenceName;
@@ -133,9 +139,10 @@ struct SetHandle {
 
 template <class T>
 void upload(lime_ctx *ctx, const Space &sp, const RDD<T> &rdd, const std::vector<size_t> &rows,
-            SetHandle &out) {
+            SetHandle &out, bool stranded = false) {
     std::vector<int32_t> c(rows.size());
     std::vector<int64_t> s(rows.size()), e(rows.size());
+    std::vector<int8_t> st(rows.size());
     for (size_t k = 0; k < rows.size(); ++k) {
         const auto &r = rdd[rows[k]].first;
         auto it = sp.index.find(r.referenceName);
@@ -143,9 +150,22 @@ void upload(lime_ctx *ctx, const Space &sp, const RDD<T> &rdd, const std::vector
         c[k] = it->second;
         s[k] = r.start;
         e[k] = r.end;
+        st[k] = (int8_t)r.strand;
     }
-    check(lime_set_create_host(ctx, sp.h, (int64_t)rows.size(), c.data(), s.data(), e.data(),
-                               &out.h));
+    if (stranded)
+        check(lime_set_create_host_stranded(ctx, sp.h, (int64_t)rows.size(), c.data(), s.data(),
+                                            e.data(), st.data(), &out.h));
+    else
+        check(lime_set_create_host(ctx, sp.h, (int64_t)rows.size(), c.data(), s.data(),
+                                   e.data(), &out.h));
+}
+
+// more than one distinct strand among the rows
+template <class T>
+bool mixed_strands(const RDD<T> &rdd) {
+    for (size_t i = 1; i < rdd.size(); ++i)
+        if (rdd[i].first.strand != rdd[0].first.strand) return true;
+    return false;
 }
 
 template <class T>
@@ -187,7 +207,7 @@ std::vector<size_t> sorted_rank(const RDD<T> &rdd) {
         if (key[a] != key[b]) return key[a] < key[b];
         if (x.start != y.start) return x.start < y.start;
         if (x.end != y.end) return x.end < y.end;
-        return (int)x.strand < (int)y.strand;
+        return strand_ord(x.strand) < strand_ord(y.strand);
     });
     std::vector<size_t> rank(rdd.size());
     for (size_t k = 0; k < idx.size(); ++k) rank[idx[k]] = k;
@@ -386,45 +406,37 @@ class DistributedMerge {
                      Engine &eng = Engine::thread_default())
         : rdd_(std::move(rdd)), pm_(std::move(partitionMap)), threshold_(threshold), eng_(eng) {}
 
+    // the SetTheory.scala:208-225 fold; mixed strands run as ONE stranded set
+    // (RegionOrdering order, a run break at every strand change)
     std::vector<std::pair<ReferenceRegion, std::vector<T>>> compute() {
         auto sp = detail::space_of<T>({&rdd_});
         auto rank = detail::sorted_rank(rdd_);
+        std::vector<size_t> all(rdd_.size());
+        std::iota(all.begin(), all.end(), 0);
+        detail::SetHandle A;
+        detail::upload(eng_.ctx(), *sp, rdd_, all, A, detail::mixed_strands(rdd_));
+        lime_result *res = nullptr;
+        int64_t cnt = 0;
+        check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
+        std::vector<int32_t> c((size_t)cnt);
+        std::vector<int64_t> s((size_t)cnt), e((size_t)cnt), rid(all.size());
+        int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), nullptr, nullptr);
+        if (rc == LIME_OK) rc = lime_result_run_of_row(res, rid.data());
+        lime_result_destroy(res);
+        check(rc);
+        std::vector<std::vector<size_t>> members((size_t)cnt);
+        std::vector<size_t> order(all);
+        std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return rank[x] < rank[y]; });
+        for (size_t m : order) members[(size_t)rid[m]].push_back(m);
         std::vector<std::pair<ReferenceRegion, std::vector<T>>> out;
-        std::vector<std::pair<size_t, size_t>> order;  // (first member rank, out index)
-        for (auto &g : detail::strand_groups(rdd_)) {
-            detail::SetHandle A;
-            detail::upload(eng_.ctx(), *sp, rdd_, g.second, A);
-            lime_result *res = nullptr;
-            int64_t cnt = 0;
-            check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
-            std::vector<int32_t> c((size_t)cnt);
-            std::vector<int64_t> s((size_t)cnt), e((size_t)cnt), rid(g.second.size());
-            int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), nullptr, nullptr);
-            if (rc == LIME_OK) rc = lime_result_run_of_row(res, rid.data());
-            lime_result_destroy(res);
-            check(rc);
-            size_t base = out.size();
-            for (int64_t k = 0; k < cnt; ++k)
-                out.push_back({ReferenceRegion(sp->names[c[k]], s[k], e[k], g.first), {}});
-            std::vector<size_t> members(g.second.size());
-            std::iota(members.begin(), members.end(), 0);
-            std::sort(members.begin(), members.end(),
-                      [&](size_t x, size_t y) { return rank[g.second[x]] < rank[g.second[y]]; });
-            for (size_t m : members) out[base + rid[m]].second.push_back(rdd_[g.second[m]].second);
+        for (int64_t k = 0; k < cnt; ++k) {
+            const Strand st = members[k].empty() ? Strand::Independent
+                                                 : rdd_[members[k][0]].first.strand;
+            std::vector<T> v;
+            for (size_t m : members[k]) v.push_back(rdd_[m].second);
+            out.push_back({ReferenceRegion(sp->names[c[k]], s[k], e[k], st), std::move(v)});
         }
-        std::vector<size_t> idx(out.size());
-        std::iota(idx.begin(), idx.end(), 0);
-        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
-            const auto &a = out[x].first, &b = out[y].first;
-            auto ka = detail::u16(a.referenceName), kb = detail::u16(b.referenceName);
-            if (ka != kb) return ka < kb;
-            if (a.start != b.start) return a.start < b.start;
-            if (a.end != b.end) return a.end < b.end;
-            return (int)a.strand < (int)b.strand;
-        });
-        std::vector<std::pair<ReferenceRegion, std::vector<T>>> sorted;
-        for (size_t i : idx) sorted.push_back(std::move(out[i]));
-        return sorted;
+        return out;
     }
 
    private:
@@ -437,7 +449,8 @@ class DistributedMerge {
 // Cluster.scala:8-121: Merge's fold, keyed by each cluster's FIRST member
 // region (postProcess :33-35).  The fold passes no threshold (quirk Q6), so
 // every variant is the strict-overlap fold: strand-blind (covers) for the
-// unstranded variants, per strand (overlaps) for the stranded ones.
+// unstranded variants; overlaps (a run break at every strand change, one
+// stranded set) for the stranded ones.
 template <class T, bool STRANDED>
 class ClusterOp {
    public:
@@ -448,32 +461,24 @@ class ClusterOp {
     std::vector<std::pair<ReferenceRegion, std::vector<T>>> compute() {
         auto sp = detail::space_of<T>({&rdd_});
         auto rank = detail::sorted_rank(rdd_);
-        std::map<int, std::vector<size_t>> groups;
-        if (STRANDED) {
-            for (auto &g : detail::strand_groups(rdd_)) groups[(int)g.first] = g.second;
-        } else {
-            auto &all = groups[0];
-            for (size_t i = 0; i < rdd_.size(); ++i) all.push_back(i);
-        }
+        std::vector<size_t> all(rdd_.size());
+        std::iota(all.begin(), all.end(), 0);
         std::vector<std::vector<size_t>> clusters;  // member rows in fold order
-        for (auto &g : groups) {
-            if (g.second.empty()) continue;
+        if (!all.empty()) {
             detail::SetHandle A;
-            detail::upload(eng_.ctx(), *sp, rdd_, g.second, A);
+            detail::upload(eng_.ctx(), *sp, rdd_, all, A, STRANDED && detail::mixed_strands(rdd_));
             lime_result *res = nullptr;
             int64_t cnt = 0;
             check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
-            std::vector<int64_t> rid(g.second.size());
+            std::vector<int64_t> rid(all.size());
             int rc = lime_result_run_of_row(res, rid.data());
             lime_result_destroy(res);
             check(rc);
-            std::vector<size_t> members(g.second.size());
-            std::iota(members.begin(), members.end(), 0);
-            std::sort(members.begin(), members.end(),
-                      [&](size_t x, size_t y) { return rank[g.second[x]] < rank[g.second[y]]; });
-            size_t base = clusters.size();
-            clusters.resize(base + (size_t)cnt);
-            for (size_t m : members) clusters[base + (size_t)rid[m]].push_back(g.second[m]);
+            std::vector<size_t> order(all);
+            std::sort(order.begin(), order.end(),
+                      [&](size_t x, size_t y) { return rank[x] < rank[y]; });
+            clusters.resize((size_t)cnt);
+            for (size_t m : order) clusters[(size_t)rid[m]].push_back(m);
         }
         std::sort(clusters.begin(), clusters.end(),
                   [&](const std::vector<size_t> &x, const std::vector<size_t> &y) {

@@ -60,6 +60,8 @@ SIGNATURES = {
     "lime_space_span": (i64, [vp]),
     "lime_space_offset": (i64, [vp, i32]),
     "lime_set_create_host": (C.c_int, [vp, vp, i64, P(i32), P(i64), P(i64), pp]),
+    "lime_set_create_host_stranded": (C.c_int, [vp, vp, i64, P(i32), P(i64), P(i64),
+                                                P(C.c_int8), pp]),
     "lime_set_create_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_set_create_global": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_set_destroy": (C.c_int, [vp]),

@@ -134,16 +134,21 @@ static lime_set *new_set(lime_ctx *ctx, const lime_space *sp, int64_t n) {
     return s;
 }
 
+// d_strand (optional, device, input order, taken over by the set): a
+// stranded set, sorted by (gs, ge, strand)
 static int create_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
                               const int32_t *d_contig, const uint32_t *d_start,
-                              const uint32_t *d_end, lime_set **out) {
+                              const uint32_t *d_end, lime_set **out,
+                              int8_t *d_strand = nullptr) {
     lime_set *s = new_set(ctx, sp, n);
+    s->strand_in = d_strand;
     uint32_t *d_len = nullptr;
     int rc = upload_space(ctx, sp, &s->d_off, &d_len);
     if (rc == LIME_OK) rc = sort_set(ctx, s, d_contig, d_start, d_end, d_len);
     release(ctx, d_len);
     if (rc != LIME_OK) {
         release(ctx, s->d_off);
+        release(ctx, s->strand_in);
         delete s;
         return rc;
     }
@@ -285,8 +290,25 @@ int64_t lime_space_offset(const lime_space *sp, int32_t c) {
 }
 
 // -------------------------------------------------------------------- sets
+static int create_host(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *contig,
+                       const int64_t *start, const int64_t *end, const int8_t *strand,
+                       lime_set **out);
+
 int lime_set_create_host(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *contig,
                          const int64_t *start, const int64_t *end, lime_set **out) {
+    return create_host(ctx, sp, n, contig, start, end, nullptr, out);
+}
+
+int lime_set_create_host_stranded(lime_ctx *ctx, const lime_space *sp, int64_t n,
+                                  const int32_t *contig, const int64_t *start,
+                                  const int64_t *end, const int8_t *strand, lime_set **out) {
+    if (n > 0 && !strand) return fail(LIME_ERR_ARG, "bad set arguments");
+    return create_host(ctx, sp, n, contig, start, end, strand, out);
+}
+
+static int create_host(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *contig,
+                       const int64_t *start, const int64_t *end, const int8_t *strand,
+                       lime_set **out) {
     if (!ctx || !sp || !out || n < 0 || (n > 0 && (!contig || !start || !end)))
         return fail(LIME_ERR_ARG, "bad set arguments");
     if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
@@ -313,7 +335,15 @@ int lime_set_create_host(lime_ctx *ctx, const lime_space *sp, int64_t n, const i
         LIME_HIP(hipMemcpyAsync(de, e32.data(), 4 * (size_t)n, hipMemcpyHostToDevice, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));
     }
-    int rc = create_from_device(ctx, sp, n, dc, ds, de, out);
+    int8_t *dst = nullptr;
+    if (strand) {
+        LIME_TRY(alloc(ctx, &dst, (size_t)std::max<int64_t>(n, 1)));
+        if (n > 0) {
+            LIME_HIP(hipMemcpyAsync(dst, strand, (size_t)n, hipMemcpyHostToDevice, S(ctx)));
+            LIME_HIP(hipStreamSynchronize(S(ctx)));
+        }
+    }
+    int rc = create_from_device(ctx, sp, n, dc, ds, de, out, dst);
     release(ctx, dc);
     release(ctx, ds);
     release(ctx, de);
@@ -337,6 +367,7 @@ int lime_set_destroy(lime_set *s) {
     release(ctx, s->row);
     release(ctx, s->d_off);
     release(ctx, s->pmax);
+    release(ctx, s->strand_in);
     delete s;
     return LIME_OK;
 }

@@ -81,6 +81,10 @@ struct lime_set {
     bool has_zero_width = false;
     // lazily built: inclusive prefix max of ge (for subtract)
     mutable uint32_t *pmax = nullptr;
+    // stranded sets (lime_set_create_host_stranded): strand code per INPUT
+    // row; the set is sorted by (gs, ge, strand) and merge breaks runs at
+    // strand changes (the reference fold's overlaps test)
+    int8_t *strand_in = nullptr;
 };
 
 struct lime_result {

@@ -131,6 +131,8 @@ struct MergeScanArgs {
     uint32_t *run_gs, *run_ge;  // capacity n
     uint32_t *run_of_sorted;    // may be null
     uint64_t *total;            // runs
+    const int8_t *strand;       // stranded sets: strand per input row
+    const uint32_t *row;        // sorted row ids (strand lookups)
 };
 
 // Full tile <-> blocked registers (thread t: rows 16t .. 16t+15) through
@@ -174,9 +176,54 @@ __device__ __forceinline__ void blocked_to_tile(const uint32_t (&v)[MITEMS], uin
     }
 }
 
+// Segmented max (stranded merge): a segment starts at every strand change;
+// (b, v) = (segment start seen, max since the last start).
+struct SegMax {
+    uint32_t b, v;
+};
+__device__ __forceinline__ SegMax seg_combine(SegMax x, SegMax y) {  // x before y
+    return SegMax{x.b | y.b, y.b ? y.v : (x.v > y.v ? x.v : y.v)};
+}
+// block-wide exclusive segmented-max scan (identity {0, 0}); *total = all
+template <int BLOCK>
+__device__ SegMax block_exclusive_segmax(SegMax x, SegMax *scratch, SegMax *total) {
+    constexpr int NW = BLOCK / 64;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    SegMax inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        SegMax o{(uint32_t)__shfl_up((int)inc.b, d, 64), (uint32_t)__shfl_up((int)inc.v, d, 64)};
+        if (lane >= d) inc = seg_combine(o, inc);
+    }
+    SegMax exc{(uint32_t)__shfl_up((int)inc.b, 1, 64), (uint32_t)__shfl_up((int)inc.v, 1, 64)};
+    if (lane == 0) exc = SegMax{0u, 0u};
+    if (lane == 63) scratch[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SegMax run{0u, 0u};
+        for (int i = 0; i < NW; ++i) {
+            const SegMax t = scratch[i];
+            scratch[i] = run;
+            run = seg_combine(run, t);
+        }
+        scratch[NW] = run;
+    }
+    __syncthreads();
+    const SegMax res = seg_combine(scratch[w], exc);
+    *total = scratch[NW];
+    __syncthreads();
+    return res;
+}
+
+// STR: stranded set -- a run also breaks where the strand changes (the
+// reference fold's Merge.condition is overlaps, which needs equal strands);
+// the max-end carry restarts there, so a tile holding a strand change
+// publishes its inclusive carry without looking back.
+template <bool STR>
 __global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[MPADW];
     __shared__ uint32_t scratch[SB / 64 + 1];
+    __shared__ SegMax sscratch[SB / 64 + 1];
     __shared__ uint64_t s_carry;
     __shared__ uint32_t s_tile;
     if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
@@ -198,33 +245,59 @@ __global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
             e[k] = v ? a.ge[r0 + k] : 0u;
         }
     }
-    uint32_t agg = 0;
+    uint32_t brk = 0;  // bit k: row r0 + k starts a strand segment
+    if (STR) {
+        int prev = r0 > 0 && r0 - 1 < n ? a.strand[a.row[r0 - 1]] : -1;
 #pragma unroll
-    for (int k = 0; k < MITEMS; ++k) agg = max(agg, e[k]);
-    uint32_t tmax;
-    const uint32_t pre = dev::block_exclusive_max<SB>(agg, 0u, scratch, &tmax);
-    // ---- chain 1: M at the tile's first row
+        for (int k = 0; k < MITEMS; ++k) {
+            if (r0 + k < n) {
+                const int c = a.strand[a.row[r0 + k]];
+                if (c != prev) brk |= 1u << k;
+                prev = c;
+            }
+        }
+    }
+    // thread aggregate and the tile's exclusive carry
+    SegMax agg{0u, 0u};
+#pragma unroll
+    for (int k = 0; k < MITEMS; ++k) {
+        if (brk & (1u << k)) agg = SegMax{1u, 0u};
+        agg.v = max(agg.v, e[k]);
+    }
+    SegMax tot;
+    SegMax pre;
+    if (STR) {
+        pre = block_exclusive_segmax<SB>(agg, sscratch, &tot);
+    } else {
+        uint32_t tmax;
+        pre = SegMax{0u, dev::block_exclusive_max<SB>(agg.v, 0u, scratch, &tmax)};
+        tot = SegMax{0u, tmax};
+    }
+    // ---- chain 1: max end (since the last strand change) before the tile
     if (threadIdx.x < 64) {
         uint64_t ex = 0;
-        if (tile == 0) {
-            if (threadIdx.x == 0) st_publish(a.st_max, ST_INC | tmax);
+        if (tile == 0 || tot.b) {  // nothing before matters past a segment start
+            if (threadIdx.x == 0) st_publish(a.st_max + tile, ST_INC | tot.v);
+            if (!tot.b || tile == 0) ex = 0;
+            if (tile > 0 && tot.b) ex = lookback<true>(a.st_max, tile);
         } else {
-            if (threadIdx.x == 0) st_publish(a.st_max + tile, ST_AGG | tmax);
+            if (threadIdx.x == 0) st_publish(a.st_max + tile, ST_AGG | tot.v);
             ex = lookback<true>(a.st_max, tile);
             if (threadIdx.x == 0)
-                st_publish(a.st_max + tile, ST_INC | (ex > tmax ? ex : (uint64_t)tmax));
+                st_publish(a.st_max + tile, ST_INC | (ex > tot.v ? ex : (uint64_t)tot.v));
         }
         if (threadIdx.x == 0) s_carry = ex;
     }
     __syncthreads();
-    uint32_t M = max(pre, (uint32_t)s_carry);
+    uint32_t M = pre.b ? pre.v : max(pre.v, (uint32_t)s_carry);
     uint32_t Mk[MITEMS];
     uint32_t flags = 0;
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) {
-        Mk[k] = M;
-        if (r0 + k < n && M <= s[k]) flags |= 1u << k;
-        M = max(M, e[k]);
+        Mk[k] = M;  // the run so far; its end if row k starts a new run
+        const bool b = (brk >> k) & 1u;
+        if (r0 + k < n && (b || M <= s[k])) flags |= 1u << k;
+        M = b ? e[k] : max(M, e[k]);
     }
     uint32_t ctot;
     const uint32_t rpre = dev::block_exclusive_sum<SB>((uint32_t)__popc(flags), scratch, &ctot);
@@ -253,7 +326,7 @@ __global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
                 ++r;
             }
             if (i == n - 1) {
-                a.run_ge[r - 1] = max(Mk[k], e[k]);
+                a.run_ge[r - 1] = ((brk >> k) & 1u) ? e[k] : max(Mk[k], e[k]);
                 *a.total = r;
             }
         }
@@ -357,7 +430,12 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
     a.run_gs = run_gs;
     a.run_ge = run_ge;
     a.run_of_sorted = res->run_of_sorted;
-    hipLaunchKernelGGL(k_merge_scan, dim3((unsigned)nt), dim3(SB), 0, S(ctx), a);
+    a.strand = set->strand_in;
+    a.row = set->row;
+    if (set->strand_in)
+        hipLaunchKernelGGL(k_merge_scan<true>, dim3((unsigned)nt), dim3(SB), 0, S(ctx), a);
+    else
+        hipLaunchKernelGGL(k_merge_scan<false>, dim3((unsigned)nt), dim3(SB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
     uint64_t nr = 0;
     LIME_TRY(read_back(ctx, &nr, a.total, sizeof(nr)));

@@ -43,18 +43,37 @@ struct SetStats {
     uint32_t pad[2];
 };
 
-// digit of an item: 8-bit digit of gs, or the zero-width bit (0 = zero width)
-template <bool NZ>
-__device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, int shift) {
-    if (NZ) return e > k ? 1u : 0u;
+// Pass kinds: an 8-bit digit of gs (M_GS); the zero-width bit (M_NZ, 0 =
+// zero width); an 8-bit digit of ge (M_GE); the strand code of the row
+// (M_ST).  Stranded sets sort by (gs, ge, strand) -- RegionOrdering -- with
+// passes ST, GE x4, GS x4; plain sets by (gs, zero-width first) with NZ?, GS.
+enum { M_GS = 0, M_NZ = 1, M_GE = 2, M_ST = 3 };
+
+template <int M>
+__device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, uint32_t r, int shift,
+                                             const int8_t *st) {
+    if (M == M_NZ) return e > k ? 1u : 0u;
+    if (M == M_GE) return (e >> shift) & (RBINS - 1);
+    // strand codes 0 independent, 1 forward, 2 reverse, 3 unknown sort by
+    // bdg-formats' enum ordinal: FORWARD, REVERSE, INDEPENDENT, UNKNOWN
+    if (M == M_ST) return (0xd2u >> (2 * ((uint32_t)(uint8_t)st[r] & 3u))) & 3u;
     return (k >> shift) & (RBINS - 1);
 }
 
 // lanes of the wave holding the same digit (among `valid` lanes)
-template <bool NZ>
+template <int M>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     uint64_t m = __ballot(valid);
-    if (NZ) {
+    if (M == M_ST) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            uint32_t bit = (d >> b) & 1u;
+            uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        return m;
+    }
+    if (M == M_NZ) {
         uint64_t b = __ballot(d & 1u);
         return m & ((d & 1u) ? b : ~b);
     }
@@ -75,13 +94,14 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t ntiles) {
 }
 
 // per-wave digit histogram of this wave's rows into hist[w][*]
-template <bool NZ>
+template <int M>
 __device__ __forceinline__ void wave_hist(uint32_t (*hist)[RBINS], int w, const uint32_t *vk,
-                                          const uint32_t *ve, const bool *valid, int shift) {
+                                          const uint32_t *ve, const uint32_t *vr,
+                                          const bool *valid, int shift, const int8_t *st) {
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
-        uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
-        uint64_t m = match_digit<NZ>(d, valid[k]);
+        uint32_t d = digit_of<M>(vk[k], ve[k], vr[k], shift, st);
+        uint64_t m = match_digit<M>(d, valid[k]);
         if (valid[k] && (m & dev::lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
     }
 }
@@ -251,7 +271,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     }
     }
     __syncthreads();
-    wave_hist<false>(hist, w, vk, ve, valid, 0);
+    wave_hist<M_GS>(hist, w, vk, ve, vk, valid, 0, nullptr);
     err = dev::wave_reduce_or(err);
     mx = dev::wave_reduce_max(mx);
     mnw = dev::wave_reduce_min(mnw);
@@ -310,29 +330,39 @@ __global__ __launch_bounds__(256) void k_stats(const SetStats *__restrict__ part
     }
 }
 
-template <bool NZ>
+template <int M>
 __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
-                                             const uint32_t *__restrict__ ge, int64_t n, int shift,
+                                             const uint32_t *__restrict__ ge,
+                                             const uint32_t *__restrict__ row, int64_t n, int shift,
+                                             const int8_t *__restrict__ st,
                                              uint32_t *__restrict__ counts, uint32_t ntiles) {
     __shared__ uint32_t hist[RWAVES][RBINS];
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
-    uint32_t vk[RITEMS], ve[RITEMS];
+    constexpr bool NEED_E = M == M_NZ || M == M_GE;
+    uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS];
     bool valid[RITEMS];
     if (base + WITEMS <= n) {
         // a histogram ignores order: 16-B loads, 4 consecutive rows per lane
         const uint4 *k4 = reinterpret_cast<const uint4 *>(key + base);
         const uint4 *e4 = reinterpret_cast<const uint4 *>(ge + base);
+        const uint4 *r4 = reinterpret_cast<const uint4 *>(row + base);
 #pragma unroll
         for (int k = 0; k < RITEMS / 4; ++k) {
             const uint4 v = k4[k * 64 + lane];
             vk[4 * k] = v.x, vk[4 * k + 1] = v.y, vk[4 * k + 2] = v.z, vk[4 * k + 3] = v.w;
-            if (NZ) {
+            if (NEED_E) {
                 const uint4 u = e4[k * 64 + lane];
                 ve[4 * k] = u.x, ve[4 * k + 1] = u.y, ve[4 * k + 2] = u.z, ve[4 * k + 3] = u.w;
             } else {
                 ve[4 * k] = ve[4 * k + 1] = ve[4 * k + 2] = ve[4 * k + 3] = 0u;
+            }
+            if (M == M_ST) {
+                const uint4 u = r4[k * 64 + lane];
+                vr[4 * k] = u.x, vr[4 * k + 1] = u.y, vr[4 * k + 2] = u.z, vr[4 * k + 3] = u.w;
+            } else {
+                vr[4 * k] = vr[4 * k + 1] = vr[4 * k + 2] = vr[4 * k + 3] = 0u;
             }
         }
 #pragma unroll
@@ -343,21 +373,23 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
             const int64_t i = base + k * 64 + lane;
             valid[k] = i < n;
             vk[k] = valid[k] ? key[i] : 0u;
-            ve[k] = (NZ && valid[k]) ? ge[i] : 0u;
+            ve[k] = (NEED_E && valid[k]) ? ge[i] : 0u;
+            vr[k] = (M == M_ST && valid[k]) ? row[i] : 0u;
         }
     }
     __syncthreads();
-    wave_hist<NZ>(hist, w, vk, ve, valid, shift);
+    wave_hist<M>(hist, w, vk, ve, vr, valid, shift, st);
     __syncthreads();
     flush_hist(hist, counts, ntiles);
 }
 
-template <bool NZ>
+template <int M>
 // 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
 __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
                                                 const uint32_t *__restrict__ ge_in,
                                                 const uint32_t *__restrict__ row_in, int64_t n,
-                                                int shift, const uint32_t *__restrict__ base_mat,
+                                                int shift, const int8_t *__restrict__ st,
+                                                const uint32_t *__restrict__ base_mat,
                                                 uint32_t ntiles, uint32_t *__restrict__ key_out,
                                                 uint32_t *__restrict__ ge_out,
                                                 uint32_t *__restrict__ row_out) {
@@ -365,7 +397,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     __shared__ uint32_t dstart[RBINS];
     __shared__ uint32_t gbase[RBINS];
     __shared__ uint32_t scratch[RWAVES + 1];
-    __shared__ uint32_t sk[RTILE], se[RTILE], sr[NZ ? RTILE : 1];
+    constexpr bool ALL3 = M != M_GS;  // digit not recomputable from the key alone
+    __shared__ uint32_t sk[RTILE], se[RTILE], sr[ALL3 ? RTILE : 1];
 
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
 
@@ -396,8 +429,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
         const bool valid = k * 64 + lane < lim;
-        const uint32_t d = digit_of<NZ>(vk[k], ve[k], shift);
-        const uint64_t m = match_digit<NZ>(d, valid);
+        const uint32_t d = valid ? digit_of<M>(vk[k], ve[k], vr[k], shift, st) : 0u;
+        const uint64_t m = match_digit<M>(d, valid);
         const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
         const uint32_t old = valid ? cnt[w][d] : 0u;
         pd[k] = ((old + rank) << 8) | d;
@@ -430,7 +463,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
         lp[k] = k * 64 + lane < lim ? cnt[w][pd[k] & 0xffu] + (pd[k] >> 8) : 0xffffffffu;
-    if (NZ) {  // digit needs (key, end): stage all three arrays at once
+    if (ALL3) {  // digit needs (key, end, row): stage all three arrays at once
 #pragma unroll
         for (int k = 0; k < RITEMS; ++k)
             if (lp[k] != 0xffffffffu) {
@@ -441,8 +474,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         __syncthreads();
         for (int j = threadIdx.x; j < count; j += RB) {
             const uint32_t k = sk[j], e = se[j];
-            const uint32_t g = gbase[digit_of<NZ>(k, e, shift)] + (uint32_t)j -
-                               dstart[digit_of<NZ>(k, e, shift)];
+            const uint32_t d = digit_of<M>(k, e, sr[j], shift, st);
+            const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
             key_out[g] = k;
             ge_out[g] = e;
             row_out[g] = sr[j];
@@ -457,7 +490,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
         const uint32_t k = sk[j];
-        const uint32_t d = digit_of<NZ>(k, 0u, shift);
+        const uint32_t d = digit_of<M>(k, 0u, 0u, shift, st);
         key_out[gbase[d] + (uint32_t)j - dstart[d]] = k;
     }
 #pragma unroll
@@ -465,7 +498,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         if (lp[k] != 0xffffffffu) se[lp[k]] = ve[k];
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t d = digit_of<NZ>(sk[j], 0u, shift);
+        const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
         ge_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
     }
     __syncthreads();
@@ -474,30 +507,42 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         if (lp[k] != 0xffffffffu) se[lp[k]] = vr[k];
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t d = digit_of<NZ>(sk[j], 0u, shift);
+        const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
         row_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
     }
 }
 
-int radix_pass(lime_ctx *ctx, bool nz, int shift, bool have_hist, int64_t n, const uint32_t *k0,
-               const uint32_t *e0, const uint32_t *r0, uint32_t *k1, uint32_t *e1, uint32_t *r1,
-               uint32_t *mat, uint32_t ntiles) {
-    if (!have_hist) {
-        if (nz)
-            hipLaunchKernelGGL(k_hist<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift,
-                               mat, ntiles);
-        else
-            hipLaunchKernelGGL(k_hist<false>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, n, shift,
-                               mat, ntiles);
-        LIME_HIP(hipGetLastError());
+template <int M>
+void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint32_t *k0,
+                 const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
+                 uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int &rc) {
+    if (!have_hist)
+        hipLaunchKernelGGL(k_hist<M>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n, shift, st,
+                           mat, ntiles);
+    if ((rc = scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr)) != LIME_OK)
+        return;
+    hipLaunchKernelGGL(k_scatter<M>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n, shift, st,
+                       (const uint32_t *)mat, ntiles, k1, e1, r1);
+}
+
+int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, const uint32_t *k0,
+               const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
+               uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles) {
+    int rc = LIME_OK;
+    switch (mode) {
+        case M_NZ:
+            launch_pass<M_NZ>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            break;
+        case M_GE:
+            launch_pass<M_GE>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            break;
+        case M_ST:
+            launch_pass<M_ST>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            break;
+        default:
+            launch_pass<M_GS>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
     }
-    LIME_TRY(scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr));
-    if (nz)
-        hipLaunchKernelGGL(k_scatter<true>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n,
-                           shift, (const uint32_t *)mat, ntiles, k1, e1, r1);
-    else
-        hipLaunchKernelGGL(k_scatter<false>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n,
-                           shift, (const uint32_t *)mat, ntiles, k1, e1, r1);
+    if (rc != LIME_OK) return rc;
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
@@ -560,20 +605,30 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     set->max_width = h.max_width;
     set->has_zero_width = h.has_zero != 0;
 
-    if (n > 1 && h.unsorted) {
+    const bool stranded = set->strand_in != nullptr;
+    if (n > 1 && (h.unsorted || stranded)) {
         uint32_t *k1, *e1, *r1;
         LIME_TRY(alloc(ctx, &k1, (size_t)n));
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
         LIME_TRY(alloc(ctx, &r1, (size_t)n));
         const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
-        std::vector<std::pair<bool, int>> passes;
-        if (set->has_zero_width) passes.push_back({true, 0});
-        for (int sh = 0; sh < bits; sh += 8) passes.push_back({false, sh});
-        // k_prep already histogrammed digit 0 of the prep layout
-        bool have = !set->has_zero_width;
+        std::vector<std::pair<int, int>> passes;  // (mode, shift), least significant first
+        if (stranded) {
+            // RegionOrdering (start, end, strand): strand, then ge, then gs.
+            // The strand pass runs first, while row i is still input row i.
+            const uint32_t span = set->off.empty() ? 0xffffffffu : set->off.back();
+            const int ebits = span ? 32 - __builtin_clz(span) : 1;
+            passes.push_back({M_ST, 0});
+            for (int sh = 0; sh < ebits; sh += 8) passes.push_back({M_GE, sh});
+        } else if (set->has_zero_width) {
+            passes.push_back({M_NZ, 0});
+        }
+        for (int sh = 0; sh < bits; sh += 8) passes.push_back({M_GS, sh});
+        // k_prep already histogrammed digit 0 of gs in the prep layout
+        bool have = passes.front().first == M_GS;
         for (auto &p : passes) {
-            LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, k1, e1, r1, mat,
-                                ntiles));
+            LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
+                                e1, r1, mat, ntiles));
             have = false;
             std::swap(k0, k1);
             std::swap(e0, e1);

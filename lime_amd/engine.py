@@ -273,6 +273,20 @@ class Context:
                                           _ptr(start, i64), _ptr(end, i64), C.byref(h)))
         return IntervalSet(self, h, space)
 
+    def set_from_host_stranded(self, space, contig, start, end, strand):
+        """Stranded set: sorted by (start, end, strand); merge breaks runs at
+        strand changes (the reference fold)."""
+        contig = np.ascontiguousarray(contig, dtype=np.int32)
+        start = np.ascontiguousarray(start, dtype=np.int64)
+        end = np.ascontiguousarray(end, dtype=np.int64)
+        strand = np.ascontiguousarray(strand, dtype=np.int8)
+        h = vp()
+        check(_lib().lime_set_create_host_stranded(self._h, space.handle, len(contig),
+                                                   _ptr(contig, i32), _ptr(start, i64),
+                                                   _ptr(end, i64), _ptr(strand, C.c_int8),
+                                                   C.byref(h)))
+        return IntervalSet(self, h, space)
+
     def set_from_device(self, space, n, d_contig, d_start, d_end):
         h = vp()
         check(_lib().lime_set_create_device(self._h, space.handle, int(n), d_contig, d_start,

@@ -22,9 +22,12 @@ An "RDD" here is any iterable of (ReferenceRegion, value) pairs held on the
 host.  `partitionMap` is accepted for signature parity and ignored: the
 engine is partition-free and its output equals the reference's single-
 partition (P = 1) execution, in the same emission order (SURVEY.md
-Appendix A).  Strand: rows are grouped by strand and each group runs through
-the engine separately, which is exactly ReferenceRegion.overlaps' strand
-equality; complement ignores strand (its gap regions carry none).
+Appendix A).  Strand: for the pairwise operators rows are grouped by strand
+and each group runs through the engine separately, which is exactly
+ReferenceRegion.overlaps' strand equality; merge and the stranded clusters
+run mixed strands as one stranded set (a run breaks at every strand change
+of the (start, end, strand) order, as the reference fold does); complement
+ignores strand (its gap regions carry none).
 """
 from collections import namedtuple
 
@@ -33,7 +36,9 @@ import numpy as np
 from . import _ffi
 from .engine import Context, Space
 
-STRANDS = ("INDEPENDENT", "FORWARD", "REVERSE", "UNKNOWN")
+STRANDS = ("INDEPENDENT", "FORWARD", "REVERSE", "UNKNOWN")  # engine codes 0..3
+# RegionOrdering compares bdg-formats' Strand enum ordinals
+_STRAND_ORD = {"FORWARD": 0, "REVERSE": 1, "INDEPENDENT": 2, "UNKNOWN": 3}
 _STRAND_CODE = {s: i for i, s in enumerate(STRANDS)}
 
 
@@ -103,7 +108,7 @@ def _sorted_rank(regions):
     """Rank of every row in RegionOrdering (name, start, end, strand), stable."""
     keys = sorted(range(len(regions)), key=lambda i: (
         _java_key(regions[i].referenceName), regions[i].start, regions[i].end,
-        _STRAND_CODE.get(regions[i].strand, 0), i))
+        _STRAND_ORD.get(regions[i].strand, 4), i))
     rank = np.empty(len(regions), dtype=np.int64)
     rank[keys] = np.arange(len(regions))
     return rank
@@ -221,24 +226,31 @@ class DistributedMerge(_Op):
         self.partitionMap, self.threshold = partitionMap, int(threshold)
 
     def _runs(self):
+        """The SetTheory.scala:208-225 fold.  Mixed strands run as ONE
+        stranded set: RegionOrdering (start, end, strand) and a run break at
+        every strand change, exactly the fold's overlaps test."""
         regs, vals = _rows(self.rdd)
         space = _space_for(regs)
-        runs = []
-        for strand, rows in _strand_groups(regs).items():
-            A = self.ctx.set_from_host(space, *_arrays(space, regs, rows))
-            res = self.ctx.merge(A)
-            h = res.to_host()
-            rid = res.run_of_row(len(rows))
-            members = [[] for _ in range(len(h["start"]))]
-            # Iterable[T] in fold order = sorted order of the member rows
-            rank = _sorted_rank([regs[r] for r in rows])
-            for local in np.argsort(rank, kind="stable"):
-                members[rid[local]].append(vals[rows[local]])
-            for k in range(len(h["start"])):
-                runs.append((ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
-                                             int(h["end"][k]), strand), members[k]))
-        runs.sort(key=lambda t: (_java_key(t[0].referenceName), t[0].start, t[0].end,
-                                 _STRAND_CODE.get(t[0].strand, 0)))
+        rows = list(range(len(regs)))
+        rank = _sorted_rank(regs)
+        c, s, e = _arrays(space, regs, rows)
+        if len({r.strand for r in regs}) > 1:
+            st = np.array([_STRAND_CODE.get(r.strand, 0) for r in regs], dtype=np.int8)
+            A = self.ctx.set_from_host_stranded(space, c, s, e, st)
+        else:
+            A = self.ctx.set_from_host(space, c, s, e)
+        res = self.ctx.merge(A)
+        h = res.to_host()
+        rid = res.run_of_row(len(rows))
+        members = [[] for _ in range(len(h["start"]))]
+        for i in np.argsort(rank, kind="stable"):
+            members[rid[i]].append(i)
+        runs = [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
+                                 int(h["end"][k]), regs[members[k][0]].strand if members[k]
+                                 else "INDEPENDENT"), [vals[i] for i in members[k]])
+                for k in range(len(h["start"]))]
+        res.close()
+        A.close()
         return runs
 
     def compute(self):
@@ -283,21 +295,22 @@ class _Cluster(_Op):
     def compute(self):
         regs, vals = _rows(self.rdd)
         space = _space_for(regs)
-        groups = _strand_groups(regs) if self.STRANDED else {None: list(range(len(regs)))}
         rank = _sorted_rank(regs)
-        out = []
-        for rows in groups.values():
-            A = self.ctx.set_from_host(space, *_arrays(space, regs, rows))
-            res = self.ctx.merge(A)
-            rid = res.run_of_row(len(rows))
-            members = [[] for _ in range(res.n)]
-            for local in sorted(range(len(rows)), key=lambda i: rank[rows[i]]):
-                members[rid[local]].append(rows[local])
-            res.close()
-            A.close()
-            out += [m for m in members if m]
-        out.sort(key=lambda m: rank[m[0]])  # fold order: by the first member
-        return [(regs[m[0]], [vals[i] for i in m]) for m in out]
+        c, s, e = _arrays(space, regs, list(range(len(regs))))
+        if self.STRANDED and len({r.strand for r in regs}) > 1:
+            st = np.array([_STRAND_CODE.get(r.strand, 0) for r in regs], dtype=np.int8)
+            A = self.ctx.set_from_host_stranded(space, c, s, e, st)
+        else:
+            A = self.ctx.set_from_host(space, c, s, e)
+        res = self.ctx.merge(A)
+        rid = res.run_of_row(len(regs))
+        members = [[] for _ in range(res.n)]
+        for i in np.argsort(rank, kind="stable"):
+            members[rid[i]].append(int(i))
+        res.close()
+        A.close()
+        # fold order = run order = order of each cluster's first member
+        return [(regs[m[0]], [vals[i] for i in m]) for m in members if m]
 
 
 class UnstrandedCluster(_Cluster):

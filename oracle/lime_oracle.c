@@ -51,13 +51,22 @@ typedef struct {
 
 /* ------------------------------------------------------------------ order */
 
+/* Strand codes are 0 independent, 1 forward, 2 reverse, 3 unknown; the
+ * ordering compares bdg-formats' Strand enum ordinals (FORWARD, REVERSE,
+ * INDEPENDENT, UNKNOWN -- 3rd-party schema, restated). */
+static int lo_strand_ord(int8_t c) {
+    static const int ord[4] = {2, 0, 1, 3};
+    return (c >= 0 && c < 4) ? ord[(int)c] : 4;
+}
+
 /* RegionOrdering: (referenceName, start, end, strand); ties by input row so
  * that equal regions keep input order (Spark's sort is stable per partition). */
 static int lo_cmp(const lo_region *a, const lo_region *b) {
     if (a->contig != b->contig) return a->contig < b->contig ? -1 : 1;
     if (a->start != b->start) return a->start < b->start ? -1 : 1;
     if (a->end != b->end) return a->end < b->end ? -1 : 1;
-    if (a->strand != b->strand) return a->strand < b->strand ? -1 : 1;
+    if (a->strand != b->strand)
+        return lo_strand_ord(a->strand) < lo_strand_ord(b->strand) ? -1 : 1;
     return 0;
 }
 static int lo_qsort_cmp(const void *x, const void *y) {

@@ -83,32 +83,63 @@ def test_cluster_suite(ctx):
     assert len(out[0][1]) == 20
 
 
+_ORD = {"FORWARD": 0, "REVERSE": 1, "INDEPENDENT": 2, "UNKNOWN": 3}
+
+
 def _fold_clusters(regs, stranded):
-    """Merge.scala / Cluster.scala fold restated on the sorted rows: a new
-    cluster whenever the row does not strictly overlap the running hull (or,
-    stranded, has another strand); returns member index lists in fold order."""
+    """Merge.scala / Cluster.scala fold restated on the rows in RegionOrdering
+    (name, start, end, strand enum ordinal): a new cluster whenever the row
+    does not strictly overlap the running hull or, stranded, has another
+    strand; returns member index lists in fold order."""
     order = sorted(range(len(regs)), key=lambda i: (regs[i].referenceName, regs[i].start,
-                                                    regs[i].end, regs[i].strand, i))
-    groups = {}
+                                                    regs[i].end, _ORD[regs[i].strand], i))
+    out, cur, hull = [], [], None
     for i in order:
-        groups.setdefault(regs[i].strand if stranded else None, []).append(i)
-    out = []
-    for rows in groups.values():
-        cur, hull = [], None
-        for i in rows:
-            r = regs[i]
-            if cur and r.referenceName == hull[0] and r.start < hull[2] and r.end > hull[1]:
-                cur.append(i)
-                hull = (hull[0], min(hull[1], r.start), max(hull[2], r.end))
-            else:
-                if cur:
-                    out.append(cur)
-                cur, hull = [i], (r.referenceName, r.start, r.end)
-        if cur:
-            out.append(cur)
-    pos = {i: k for k, i in enumerate(order)}
-    out.sort(key=lambda m: pos[m[0]])
+        r = regs[i]
+        if (cur and r.referenceName == hull[0] and r.start < hull[2] and r.end > hull[1]
+                and (not stranded or r.strand == hull[3])):
+            cur.append(i)
+            hull = (hull[0], min(hull[1], r.start), max(hull[2], r.end), hull[3])
+        else:
+            if cur:
+                out.append(cur)
+            cur, hull = [i], (r.referenceName, r.start, r.end, r.strand)
+    if cur:
+        out.append(cur)
     return out
+
+
+@pytest.mark.parametrize("seed", [81, 82, 83])
+def test_stranded_merge_parity(ctx, seed):
+    # the reference fold with mixed strands (the CLI keys stranded regions):
+    # RegionOrdering (start, end, strand) and a run break at every strand
+    # change; engine stranded set == C oracle == restated fold
+    rng = np.random.default_rng(seed)
+    (c, s0, e0), _ = random_sets(rng, 4000, 1, n_contigs=3, contig_len=20000, max_len=400,
+                                 zero_frac=0.05, dup_frac=0.1, book_frac=0.05)
+    codes = rng.integers(0, 4, len(c)).astype(np.int8)
+    # ties: copies of rows with another strand
+    k = rng.random(len(c)) < 0.1
+    src = rng.integers(0, len(c), len(c))
+    c[k], s0[k], e0[k] = c[src[k]], s0[src[k]], e0[src[k]]
+    sp = space_for(3, 20000)
+    A = ctx.set_from_host_stranded(sp, c, s0, e0, codes)
+    res = ctx.merge(A)
+    got = res.to_host()
+    rid = res.run_of_row(len(c))
+    exp = oracle.merge((c, s0, e0, codes))
+    assert got["start"].tolist() == exp["start"].tolist()
+    assert got["end"].tolist() == exp["end"].tolist()
+    assert got["contig"].tolist() == exp["contig"].tolist()
+    assert rid.tolist() == exp["run_of_row"].tolist()
+    # the operator mirror on ReferenceRegions, against the restated fold
+    names = ["INDEPENDENT", "FORWARD", "REVERSE", "UNKNOWN"]
+    regs = [ReferenceRegion(NAMES[ci], int(a), int(b), names[st]) for ci, a, b, st in
+            zip(c, s0, e0, codes)]
+    out = DistributedMerge([(r, i) for i, r in enumerate(regs)], None, ctx=ctx).compute()
+    fold = _fold_clusters(regs, True)
+    assert [v for _, v in out] == fold
+    assert [k.strand for k, _ in out] == [regs[m[0]].strand for m in fold]
 
 
 @pytest.mark.parametrize("seed", [71, 72])

@@ -111,6 +111,33 @@ def test_cluster_suite():
     assert len(res["start"]) == 1 and (res["run_of_row"] == 0).all()
 
 
+@pytest.mark.parametrize("seed", [91, 92])
+def test_stranded_merge_fold(seed):
+    # lo_merge with strands = the SetTheory.scala:208-225 fold restated here
+    # independently: RegionOrdering (name, start, end, bdg-formats Strand
+    # ordinal FORWARD < REVERSE < INDEPENDENT < UNKNOWN), new run when the row
+    # does not strictly overlap the head hull or has another strand
+    rng = np.random.default_rng(seed)
+    (c, s, e), _ = random_sets(rng, 1500, 1, n_contigs=2, contig_len=8000, max_len=300,
+                               zero_frac=0.05, dup_frac=0.1, book_frac=0.05)
+    st = rng.integers(0, 4, len(c)).astype(np.int8)
+    ordv = {0: 2, 1: 0, 2: 1, 3: 3}
+    order = sorted(range(len(c)), key=lambda i: (c[i], s[i], e[i], ordv[int(st[i])], i))
+    runs, rid, hull = [], np.zeros(len(c), np.int64), None
+    for i in order:
+        if hull and c[i] == hull[0] and s[i] < hull[2] and e[i] > hull[1] and st[i] == hull[3]:
+            hull = (hull[0], min(hull[1], s[i]), max(hull[2], e[i]), hull[3])
+            runs[-1] = hull
+        else:
+            hull = (c[i], s[i], e[i], st[i])
+            runs.append(hull)
+        rid[i] = len(runs) - 1
+    got = oracle.merge((c, s, e, st))
+    assert list(zip(got["contig"].tolist(), got["start"].tolist(), got["end"].tolist())) == \
+        [(int(a), int(b), int(x)) for a, b, x, _ in runs]
+    assert got["run_of_row"].tolist() == rid.tolist()
+
+
 def test_merge_suite():
     chrom, s, e, _ = read_bed_py(os.path.join(GOLDEN, "cpg_20merge.bed"))
     rank = ranked(chrom)

@@ -21,7 +21,11 @@ LIB      = lime_amd/liblime_amd.so
 ORACLE   = oracle/build/liblime_oracle.so
 CLI      = bin/lime-submit
 
-all: $(LIB) $(ORACLE) $(CLI) bin/bw_probe
+all: $(LIB) $(ORACLE) $(CLI) bin/bw_probe bin/alloc_probe
+
+bin/alloc_probe: tools/alloc_probe.hip
+	@mkdir -p bin
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -Wno-unused-result -o $@ $<
 
 bin/bw_probe: tools/bw_probe.hip
 	@mkdir -p bin

@@ -173,10 +173,22 @@ __global__ __launch_bounds__(IB) void k_windows(StreamArgs sa, int64_t tp, int64
         win[2 * (sa.tile0 + t)] = (uint32_t)lo;
         win[2 * (sa.tile0 + t) + 1] = (uint32_t)hi;
     }
-    if (tseg && lane == 1) {
-        const uint32_t a = contig_off(off, nc, sa.ogs_o[o0]);
-        const uint32_t b = contig_off(off, nc, sa.ogs_o[o1 - 1]);
-        tseg[sa.tile0 + t] = a == b ? a : 0xffffffffu;
+    if (tseg) {
+        // contig offsets of the tile's first and last owner: one ballot over
+        // off[] for up to 64 contigs, a binary search otherwise
+        const uint32_t g0 = sa.ogs_o[o0], g1 = sa.ogs_o[o1 - 1];
+        uint32_t a, b;
+        if (nc <= 64) {
+            const uint32_t v = lane < nc ? off[lane] : 0xffffffffu;
+            const int c0 = __popcll(__ballot(lane < nc && v <= g0)) - 1;
+            const int c1 = __popcll(__ballot(lane < nc && v <= g1)) - 1;
+            a = off[c0 < 0 ? 0 : c0];
+            b = off[c1 < 0 ? 0 : c1];
+        } else {
+            a = contig_off(off, nc, g0);
+            b = contig_off(off, nc, g1);
+        }
+        if (lane == 0) tseg[sa.tile0 + t] = a == b ? a : 0xffffffffu;
     }
 }
 

@@ -29,12 +29,10 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("k_fill<false>", "k_scatter<false>", "k_prep", "k_count<false>", "k_hist<false>",
-              "k_runs_write", "k_runs_count", "k_windows", "k_tile_max"):
-        base = k.split("<")[0]
-        if base in name and (("<" not in k) or ("<false>" in name)):
-            return k
-    return name[:60]
+    """kernel name -> short label, template arguments kept"""
+    import re
+    m = re.search(r"(k_\w+(?:<[^>(]*>)?)\(", name)
+    return m.group(1) if m else name[:60]
 
 
 def main():
@@ -49,7 +47,7 @@ def main():
         rows[short(name)] = {"dispatches": max(len(f), len(w)),
                              "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                              "hbm_bytes_per_launch": (fb or 0) + (wb or 0)}
-    fill = rows.get("k_fill<false>", {})
+    fill = rows.get("k_fill<false, false>", rows.get("k_fill<false>", {}))
     res = {"note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs; FETCH x2 "
                    "(gfx950 half-count on wide streaming reads), KiB -> bytes",
            "hbm_bytes_per_launch": fill.get("hbm_bytes_per_launch"),

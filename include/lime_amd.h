@@ -190,6 +190,16 @@ int lime_result_device_arrays(const lime_result *res, const uint32_t **gstart,
 int lime_result_copy_range(const lime_result *res, int64_t first, int64_t count, uint32_t *gstart,
                            uint32_t *gend);
 int lime_result_destroy(lime_result *res);
+/* BED writer on the device (the output side of loadBed, SURVEY.md 8(f) row
+ * 1): the rows of a sorted set (in sorted order) or of a result, as
+ * "chrom<TAB>start<TAB>end\n" lines in contig-local coordinates, into a
+ * caller-owned HOST buffer.  names[c] = name of contig c of the object's
+ * space (String order).  Two-call protocol: with cap < *len (e.g. out =
+ * NULL, cap = 0) only the byte count *len is returned. */
+int lime_set_format_bed(const lime_set *set, const char *const *names, char *out, int64_t cap,
+                        int64_t *len);
+int lime_result_format_bed(const lime_result *res, const char *const *names, char *out,
+                           int64_t cap, int64_t *len);
 
 /* ----------------------------------------------------- bit-per-base path */
 int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out);

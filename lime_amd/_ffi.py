@@ -112,6 +112,8 @@ SIGNATURES = {
     "lime_dbed_fill_host": (C.c_int, [vp, P(i32), P(i64), P(i64), P(C.c_int8), P(i64), P(i32)]),
     "lime_dbed_remap_contigs": (C.c_int, [vp, P(i32), i32]),
     "lime_dbed_free": (None, [vp]),
+    "lime_set_format_bed": (C.c_int, [vp, P(C.c_char_p), C.c_char_p, i64, P(i64)]),
+    "lime_result_format_bed": (C.c_int, [vp, P(C.c_char_p), C.c_char_p, i64, P(i64)]),
     "lime_genome_read": (C.c_int, [C.c_char_p, P(i32), P(P(C.c_char_p)), P(P(i64))]),
     "lime_genome_free": (None, [i32, P(C.c_char_p), P(i64)]),
     "lime_pair_hash": (u64, [u32, u32, u32, u32]),

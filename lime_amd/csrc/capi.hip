@@ -71,6 +71,10 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
                    int64_t a_own, int64_t b_own, PairsPlan **out, const lime_set *A_out = nullptr,
                    int64_t reach = -1);
 int window_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t d, PairsPlan **out);
+int format_bed(lime_ctx *ctx, const std::vector<uint32_t> &off,
+               const std::vector<std::string> &names, int64_t n, const uint32_t *gs,
+               const uint32_t *ge, const uint32_t *extra, char *out, int64_t cap,
+               int64_t *total_len);
 int intersect_fill(PairsPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
 int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr);
 void intersect_free(PairsPlan *pl);
@@ -636,6 +640,33 @@ int lime_result_run_of_row(const lime_result *r, int64_t *run_of_row) {
     LIME_TRY(d2h(ctx, row, (const uint32_t *)r->src->row, r->src->n));
     for (int64_t i = 0; i < r->src->n; ++i) run_of_row[row[i]] = rid[i];
     return LIME_OK;
+}
+
+static int names_of(const char *const *names, int32_t n, std::vector<std::string> &v) {
+    if (n > 0 && !names) return fail(LIME_ERR_ARG, "contig names are null");
+    for (int32_t i = 0; i < n; ++i) {
+        if (!names[i]) return fail(LIME_ERR_ARG, "contig name is null");
+        v.emplace_back(names[i]);
+    }
+    return LIME_OK;
+}
+
+int lime_set_format_bed(const lime_set *s, const char *const *names, char *out, int64_t cap,
+                        int64_t *len) {
+    if (!s || !len) return fail(LIME_ERR_ARG, "bad format arguments");
+    std::vector<std::string> nm;
+    LIME_TRY(names_of(names, s->n_contigs, nm));
+    hipSetDevice(s->ctx->device);
+    return format_bed(s->ctx, s->off, nm, s->n, s->gs, s->ge, nullptr, out, cap, len);
+}
+
+int lime_result_format_bed(const lime_result *r, const char *const *names, char *out,
+                           int64_t cap, int64_t *len) {
+    if (!r || !len) return fail(LIME_ERR_ARG, "bad format arguments");
+    std::vector<std::string> nm;
+    LIME_TRY(names_of(names, r->n_contigs, nm));
+    hipSetDevice(r->ctx->device);
+    return format_bed(r->ctx, r->off, nm, r->n, r->gs, r->ge, nullptr, out, cap, len);
 }
 
 int lime_result_device_arrays(const lime_result *r, const uint32_t **gs, const uint32_t **ge) {

@@ -35,6 +35,16 @@ def java_string_order(names):
     return out[:n]
 
 
+def _format_bed(fn, handle, space):
+    """two-call device BED writer -> bytes"""
+    names = (C.c_char_p * max(len(space.names), 1))(*[n.encode() for n in space.names])
+    n = i64()
+    check(fn(handle, names, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(max(n.value, 1))
+    check(fn(handle, names, buf, n.value, C.byref(n)))
+    return buf.raw[:n.value]
+
+
 class Space:
     """Contigs in Java String order with their lengths (the coordinate space)."""
 
@@ -104,6 +114,10 @@ class IntervalSet:
         check(_lib().lime_set_device_arrays(self._h, C.byref(gs), C.byref(ge), C.byref(row)))
         return gs.value, ge.value, row.value
 
+    def to_bed(self):
+        """the sorted rows as BED3 text, formatted on the device"""
+        return _format_bed(_lib().lime_set_format_bed, self._h, self.space)
+
     def lower_bound(self, gkey):
         """first sorted row with global start >= gkey"""
         r = _lib().lime_set_lower_bound(self._h, int(gkey))
@@ -154,6 +168,10 @@ class Result:
                                            _ptr(out["start"], i64), _ptr(out["end"], i64),
                                            _ptr(out["a_row"], i64), _ptr(out["b_row"], i64)))
         return out
+
+    def to_bed(self):
+        """the result's regions as BED3 text, formatted on the device"""
+        return _format_bed(_lib().lime_result_format_bed, self._h, self.space)
 
     def run_of_row(self, n_rows):
         out = np.zeros(n_rows, dtype=np.int64)

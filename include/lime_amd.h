@@ -202,6 +202,13 @@ int lime_result_format_bed(const lime_result *res, const char *const *names, cha
                            int64_t cap, int64_t *len);
 
 /* ----------------------------------------------------- bit-per-base path */
+/* The bit-per-base set straight from UNSORTED device rows (u32 contig-local
+ * coordinates, as lime_set_create_device): rows are only grouped by
+ * 65536-base bin (two radix passes) and painted tile by tile -- no full sort
+ * and no merge.  Same bits as lime_bitset_from_set on the sorted set. */
+int lime_bitset_from_device(lime_ctx *ctx, const lime_space *space, int64_t n,
+                            const int32_t *d_contig, const uint32_t *d_start,
+                            const uint32_t *d_end, lime_bitset **out);
 int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out);
 /* op: 0 = a, 1 = not a (within contigs), 2 = a and b, 3 = a and not b */
 int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bitset *b,

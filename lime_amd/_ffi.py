@@ -87,6 +87,7 @@ SIGNATURES = {
     "lime_result_device_arrays": (C.c_int, [vp, pp, pp]),
     "lime_result_destroy": (C.c_int, [vp]),
     "lime_bitset_from_set": (C.c_int, [vp, vp, pp]),
+    "lime_bitset_from_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_bitset_runs": (C.c_int, [vp, C.c_int, vp, vp, pp, P(i64)]),
     "lime_bitset_and_runs": (C.c_int, [vp, C.c_int, P(vp), pp, P(i64)]),
     "lime_bitset_popcount": (i64, [vp, vp]),

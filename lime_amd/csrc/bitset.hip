@@ -57,6 +57,81 @@ __global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
     for (int i = threadIdx.x; i < cnt; i += BB) words[w0 + i] = img[i];
 }
 
+// Binned rows -> bits: rows grouped by gs >> 16 (two radix passes instead of
+// a full sort + merge).  A tile (4096 words = 2^18 bases = 4 bins) paints
+// the rows that START in it into its LDS image (clipped at the tile end) and
+// stores it once; the remainders of rows reaching past the tile are queued
+// and OR-ed into global words by k_paint_cross after every tile is stored.
+constexpr int BINSH = 16;
+__device__ __forceinline__ int64_t lb_bin(const uint32_t *gs, int64_t n, uint32_t bin) {
+    int64_t lo = 0, hi = n;  // first row with (gs >> BINSH) >= bin
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((gs[mid] >> BINSH) < bin)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void paint_lds(unsigned long long *img, uint64_t s, uint64_t e) {
+    const uint64_t a = s >> 6, b = (e - 1) >> 6;
+    for (uint64_t w = a; w <= b; ++w) {
+        const uint64_t lo = w == a ? (s & 63) : 0;
+        const uint64_t hi = w == b ? ((e - 1) & 63) : 63;
+        const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
+        atomicOr(&img[w], (unsigned long long)m);
+    }
+}
+
+__global__ __launch_bounds__(BB) void k_paint_rows(const uint32_t *__restrict__ gs,
+                                                   const uint32_t *__restrict__ ge, int64_t n,
+                                                   uint64_t *__restrict__ words, int64_t n_words,
+                                                   uint64_t *__restrict__ cross,
+                                                   unsigned int *__restrict__ ncross) {
+    static_assert((int64_t)BT * 64 == (1ll << (BINSH + 2)), "tile = 4 bins");
+    __shared__ unsigned long long img[BT];
+    __shared__ int64_t s_r[2];
+    const int64_t w0 = (int64_t)blockIdx.x * BT;
+    const uint64_t blo = (uint64_t)w0 * 64, bhi = blo + (uint64_t)BT * 64;
+    for (int i = threadIdx.x; i < BT; i += BB) img[i] = 0ull;
+    if (threadIdx.x == 0) s_r[0] = lb_bin(gs, n, (uint32_t)(blo >> BINSH));
+    if (threadIdx.x == 64) s_r[1] = bhi >> BINSH > 0xffffffffull ? n : lb_bin(gs, n, (uint32_t)(bhi >> BINSH));
+    __syncthreads();
+    for (int64_t r = s_r[0] + threadIdx.x; r < s_r[1]; r += BB) {
+        const uint64_t g0 = gs[r], g1 = ge[r];
+        if (g1 <= g0) continue;
+        paint_lds(img, g0 - blo, min(g1, bhi) - blo);
+        if (g1 > bhi) cross[atomicAdd(ncross, 1u)] = (bhi << 32) | g1;  // remainder [bhi, g1)
+    }
+    __syncthreads();
+    const int cnt = (int)min((int64_t)BT, n_words - w0);
+    for (int i = threadIdx.x; i < cnt; i += BB) words[w0 + i] = img[i];
+}
+
+// bits [s, e) of global words (after every tile is stored)
+__device__ __forceinline__ void paint_global(uint64_t *words, uint64_t s, uint64_t e) {
+    const uint64_t a = s >> 6, b = (e - 1) >> 6;
+    for (uint64_t w = a; w <= b; ++w) {
+        const uint64_t lo = w == a ? (s & 63) : 0;
+        const uint64_t hi = w == b ? ((e - 1) & 63) : 63;
+        const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
+        if (m == ~0ull)
+            words[w] = m;  // full word: idempotent plain store
+        else
+            atomicOr((unsigned long long *)&words[w], (unsigned long long)m);
+    }
+}
+
+__global__ __launch_bounds__(BB) void k_paint_cross(const uint64_t *__restrict__ cross,
+                                                    const unsigned int *__restrict__ ncross,
+                                                    uint64_t *__restrict__ words) {
+    const int64_t nx = *ncross;
+    for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < nx; i += (int64_t)gridDim.x * BB)
+        paint_global(words, cross[i] >> 32, cross[i] & 0xffffffffull);
+}
+
 struct OpArgs {
     const uint64_t *w[MAXK];
     int k;
@@ -211,6 +286,31 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     LIME_HIP(hipGetLastError());
     release(ctx, runs.gs);
     release(ctx, runs.ge);
+    return LIME_OK;
+}
+
+// bits of a BINNED set (min_shift == 16): no merge, no full sort
+int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
+    const int64_t span = (int64_t)a->off[a->n_contigs];
+    bs->span = span;
+    bs->n_words = (span + 63) / 64;
+    LIME_TRY(alloc(ctx, &bs->words, (size_t)bs->n_words));
+    const int64_t nt = (bs->n_words + BT - 1) / BT;
+    uint64_t *cross;
+    unsigned int *ncross;
+    LIME_TRY(alloc(ctx, &cross, (size_t)std::max<int64_t>(a->n, 1)));
+    LIME_TRY(alloc(ctx, &ncross, 1));
+    LIME_HIP(hipMemsetAsync(ncross, 0, sizeof(unsigned int), S(ctx)));
+    if (nt > 0)
+        hipLaunchKernelGGL(k_paint_rows, dim3((unsigned)nt), dim3(BB), 0, S(ctx), a->gs, a->ge,
+                           a->n, bs->words, bs->n_words, cross, ncross);
+    if (a->n > 0)
+        hipLaunchKernelGGL(k_paint_cross, dim3(std::min<unsigned>(blocks_for(a->n, BB), 2048u)),
+                           dim3(BB), 0, S(ctx),
+                           (const uint64_t *)cross, (const unsigned int *)ncross, bs->words);
+    LIME_HIP(hipGetLastError());
+    release(ctx, cross);
+    release(ctx, ncross);
     return LIME_OK;
 }
 

@@ -85,6 +85,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
 int complement_run(lime_ctx *ctx, const lime_result *runs, const uint32_t *d_off,
                    const uint32_t *d_len, int32_t nc, lime_result *res);
 int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
+int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
 int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t n, uint64_t seed, uint32_t lo,
@@ -143,9 +144,10 @@ static lime_set *new_set(lime_ctx *ctx, const lime_space *sp, int64_t n) {
 static int create_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
                               const int32_t *d_contig, const uint32_t *d_start,
                               const uint32_t *d_end, lime_set **out,
-                              int8_t *d_strand = nullptr) {
+                              int8_t *d_strand = nullptr, int min_shift = 0) {
     lime_set *s = new_set(ctx, sp, n);
     s->strand_in = d_strand;
+    s->min_shift = min_shift;
     uint32_t *d_len = nullptr;
     int rc = upload_space(ctx, sp, &s->d_off, &d_len);
     if (rc == LIME_OK) rc = sort_set(ctx, s, d_contig, d_start, d_end, d_len);
@@ -698,6 +700,31 @@ int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out) {
     bs->off = a->off;
     bs->len = a->len;
     int rc = bitset_build(ctx, a, bs);
+    if (rc != LIME_OK) {
+        delete bs;
+        return rc;
+    }
+    *out = bs;
+    return LIME_OK;
+}
+
+int lime_bitset_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
+                            const int32_t *d_contig, const uint32_t *d_start,
+                            const uint32_t *d_end, lime_bitset **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_contig || !d_start || !d_end)))
+        return fail(LIME_ERR_ARG, "bad bitset arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    // rows grouped by 65536-base bin (two radix passes), then painted
+    lime_set *tmp = nullptr;
+    LIME_TRY(create_from_device(ctx, sp, n, d_contig, d_start, d_end, &tmp, nullptr, 16));
+    lime_bitset *bs = new lime_bitset();
+    bs->ctx = ctx;
+    bs->n_contigs = tmp->n_contigs;
+    bs->off = tmp->off;
+    bs->len = tmp->len;
+    int rc = bitset_build_binned(ctx, tmp, bs);
+    lime_set_destroy(tmp);
     if (rc != LIME_OK) {
         delete bs;
         return rc;

@@ -85,6 +85,9 @@ struct lime_set {
     // row; the set is sorted by (gs, ge, strand) and merge breaks runs at
     // strand changes (the reference fold's overlaps test)
     int8_t *strand_in = nullptr;
+    // binned sets (bitset painting from unsorted rows): only the gs digits
+    // at shifts >= min_shift are sorted, i.e. rows grouped by gs >> min_shift
+    int min_shift = 0;
 };
 
 struct lime_result {

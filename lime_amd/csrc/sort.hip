@@ -606,7 +606,9 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     set->has_zero_width = h.has_zero != 0;
 
     const bool stranded = set->strand_in != nullptr;
-    if (n > 1 && (h.unsorted || stranded)) {
+    // (a binned set whose keys all share one bin needs no pass)
+    if (n > 1 && (h.unsorted || stranded) &&
+        !(set->min_shift > 0 && (h.max_gs >> set->min_shift) == 0)) {
         uint32_t *k1, *e1, *r1;
         LIME_TRY(alloc(ctx, &k1, (size_t)n));
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
@@ -620,12 +622,13 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             const int ebits = span ? 32 - __builtin_clz(span) : 1;
             passes.push_back({M_ST, 0});
             for (int sh = 0; sh < ebits; sh += 8) passes.push_back({M_GE, sh});
-        } else if (set->has_zero_width) {
+        } else if (set->has_zero_width && set->min_shift == 0) {
             passes.push_back({M_NZ, 0});
         }
-        for (int sh = 0; sh < bits; sh += 8) passes.push_back({M_GS, sh});
+        for (int sh = 0; sh < bits; sh += 8)
+            if (sh >= set->min_shift) passes.push_back({M_GS, sh});
         // k_prep already histogrammed digit 0 of gs in the prep layout
-        bool have = passes.front().first == M_GS;
+        bool have = passes.front().first == M_GS && passes.front().second == 0;
         for (auto &p : passes) {
             LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
                                 e1, r1, mat, ntiles));

@@ -362,6 +362,13 @@ class Context:
         check(_lib().lime_bitset_from_set(self._h, a._h, C.byref(h)))
         return Bitset(self, h, a.space)
 
+    def bitset_from_device(self, space, n, d_contig, d_start, d_end):
+        """bit-per-base set straight from UNSORTED device rows (binned paint)"""
+        h = vp()
+        check(_lib().lime_bitset_from_device(self._h, space.handle, int(n), vp(d_contig),
+                                             vp(d_start), vp(d_end), C.byref(h)))
+        return Bitset(self, h, space)
+
     def bitset_runs(self, op, a, b=None):
         h, n = vp(), i64()
         check(_lib().lime_bitset_runs(self._h, int(op), a._h, b._h if b is not None else None,

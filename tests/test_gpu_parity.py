@@ -416,6 +416,28 @@ def test_full_size_c2_count_property(ctx):
     assert 1.5e10 < plan.n < 1.75e10  # E[pairs] ~ 1.63e10
 
 
+@pytest.mark.parametrize("seed,max_len", [(52, 300), (53, 700000)])
+def test_bitset_from_unsorted_rows(ctx, seed, max_len):
+    # binned paint from unsorted device rows == paint from the sorted set's
+    # merged runs: same coverage, same runs of every op (rows up to 0.7 Mb
+    # cross several 2^18-base tiles; zero-width rows paint nothing)
+    import torch
+    rng = np.random.default_rng(seed)
+    A, _ = random_sets(rng, 30000, 1, n_contigs=3, contig_len=2_000_000, max_len=max_len,
+                       zero_frac=0.05, dup_frac=0.02)
+    sp = space_for(3, 2_000_000)
+    dev = torch.device("cuda", 0)
+    t = [torch.from_numpy(np.ascontiguousarray(x).astype(np.int32)).to(dev) for x in A]
+    torch.cuda.synchronize()
+    bu = ctx.bitset_from_device(sp, len(A[0]), *(x.data_ptr() for x in t))
+    bs = ctx.bitset(ctx.set_from_host(sp, *A))
+    assert bu.popcount() == bs.popcount()
+    for op in (0, 1):
+        assert ctx.bitset_runs(op, bu).to_host()["start"].tolist() == \
+            ctx.bitset_runs(op, bs).to_host()["start"].tolist()
+    assert ctx.bitset_runs(3, bu, bs).n == 0 and ctx.bitset_runs(3, bs, bu).n == 0
+
+
 def test_bitset_paths(ctx):
     rng = np.random.default_rng(51)
     A, B = random_sets(rng, 20000, 20000, n_contigs=3, contig_len=200000, max_len=300)

@@ -117,6 +117,12 @@ int lime_set_create_host_stranded(lime_ctx *ctx, const lime_space *space, int64_
 int lime_set_create_device(lime_ctx *ctx, const lime_space *space, int64_t n,
                            const int32_t *d_contig, const uint32_t *d_start,
                            const uint32_t *d_end, lime_set **out);
+/* Same with strand codes in HBM (NULL = every row independent): sorted in the
+ * full RegionOrdering (start, end, strand), as lime_set_create_host_stranded. */
+int lime_set_create_device_stranded(lime_ctx *ctx, const lime_space *space, int64_t n,
+                                    const int32_t *d_contig, const uint32_t *d_start,
+                                    const uint32_t *d_end, const int8_t *d_strand,
+                                    lime_set **out);
 /* Device arrays already in the space's GLOBAL coordinates (gstart, gend) with
  * caller-chosen row ids -- e.g. a coordinate shard's own sorted rows followed
  * by its halo.  Validated (gend >= gstart, inside the span) and sorted only if
@@ -170,6 +176,20 @@ int lime_pairs_destroy(lime_pairs *plan);
  * and checksum them with lime_intersect_fill_* / lime_intersect_checksum. */
 int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t distance,
                       lime_pairs **plan, int64_t *n_pairs);
+
+/* ------------------------------------------------------------------ closest */
+#define LIME_CLOSEST 0 /* SingleClosest (lime-core Closest.scala:34-214), the CLI's op */
+
+/* SingleClosest(left = a, right = b, partitionMap).compute() (Closest.scala
+ * :34-214, CLI cli/Closest.scala:45-58) as the reference's sweep computes it on
+ * one partition, mutable currentClosest included: for each left row the right
+ * rows of its cache at the same unstrandedDistance as the current closest,
+ * in cache order.  Both sets must be in full RegionOrdering (built with
+ * lime_set_create_host_stranded; strand codes 0 when unstranded).  The records
+ * carry a's own region (primitive returns the first region) and the two rows;
+ * fill and checksum them with lime_intersect_fill_* / lime_intersect_checksum. */
+int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int mode,
+                       lime_pairs **plan, int64_t *n_pairs);
 
 /* ------------------------------------------------------------ merge et al. */
 int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs);

@@ -217,6 +217,25 @@ std::vector<size_t> sorted_rank(const RDD<T> &rdd) {
 }  // namespace detail
 
 namespace detail {
+// the contigs of both sides, each as long as its furthest end
+template <class T, class U>
+std::unique_ptr<Space> join_space(const RDD<T> &left, const RDD<U> &right) {
+    auto sp = space_of<T>({&left});
+    std::map<std::string, int64_t> ext;
+    for (size_t c = 0; c < sp->names.size(); ++c) ext[sp->names[c]] = sp->lengths[c];
+    for (auto &kv : right) {
+        auto &e = ext[kv.first.referenceName];
+        e = std::max(e, kv.first.end);
+    }
+    std::vector<std::string> n;
+    std::vector<int64_t> l;
+    for (auto &kv : ext) {
+        n.push_back(kv.first);
+        l.push_back(kv.second);
+    }
+    return std::make_unique<Space>(n, l);
+}
+
 struct PairHit {
     size_t a, b;
     int64_t s, e;
@@ -228,22 +247,7 @@ struct PairHit {
 template <typename T, typename U, typename PlanFn>
 std::vector<PairHit> pair_join(const RDD<T> &left, const RDD<U> &right, Engine &eng,
                                PlanFn make_plan) {
-    auto sp = space_of<T>({&left});
-    {  // extend with the right side's contigs
-        std::map<std::string, int64_t> ext;
-        for (size_t c = 0; c < sp->names.size(); ++c) ext[sp->names[c]] = sp->lengths[c];
-        for (auto &kv : right) {
-            auto &e = ext[kv.first.referenceName];
-            e = std::max(e, kv.first.end);
-        }
-        std::vector<std::string> n;
-        std::vector<int64_t> l;
-        for (auto &kv : ext) {
-            n.push_back(kv.first);
-            l.push_back(kv.second);
-        }
-        sp = std::make_unique<Space>(n, l);
-    }
+    auto sp = join_space(left, right);
     auto lg = strand_groups(left);
     auto rg = strand_groups(right);
     std::vector<PairHit> hits;
@@ -299,6 +303,48 @@ class DistributedWindow {
     RDD<U> right_;
     PartitionMap pm_;
     int64_t threshold_;
+    Engine &eng_;
+};
+
+// SingleClosest (Closest.scala:34-214, the CLI's closest): for each left row
+// in RegionOrdering, the cached right rows at the same unstrandedDistance as
+// the sweep's currentClosest, keyed by the left region; the reference's sweep
+// on one partition (lime_closest_count).  Rows of every strand go into one
+// stranded set per side (the order includes strand, the distance ignores it).
+template <typename T, typename U>
+class SingleClosest {
+   public:
+    SingleClosest(RDD<T> left, RDD<U> right, PartitionMap partitionMap = {},
+                  Engine &eng = Engine::thread_default())
+        : left_(std::move(left)), right_(std::move(right)), pm_(std::move(partitionMap)),
+          eng_(eng) {}
+
+    std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> compute() {
+        auto sp = detail::join_space(left_, right_);
+        std::vector<size_t> la(left_.size()), ra(right_.size());
+        for (size_t i = 0; i < la.size(); ++i) la[i] = i;
+        for (size_t i = 0; i < ra.size(); ++i) ra[i] = i;
+        detail::SetHandle A, B;
+        detail::upload(eng_.ctx(), *sp, left_, la, A, true);
+        detail::upload(eng_.ctx(), *sp, right_, ra, B, true);
+        lime_pairs *plan = nullptr;
+        int64_t n = 0;
+        check(lime_closest_count(eng_.ctx(), A.h, B.h, LIME_CLOSEST, &plan, &n));
+        std::vector<lime_pair> p((size_t)n);
+        int rc = lime_intersect_fill_host(plan, 0, n, p.data());
+        lime_pairs_destroy(plan);
+        check(rc);
+        std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> out;
+        out.reserve(p.size());
+        for (auto &x : p)
+            out.push_back({left_[x.a_row].first, {left_[x.a_row].second, right_[x.b_row].second}});
+        return out;
+    }
+
+   private:
+    RDD<T> left_;
+    RDD<U> right_;
+    PartitionMap pm_;
     Engine &eng_;
 };
 

@@ -63,6 +63,7 @@ SIGNATURES = {
     "lime_set_create_host_stranded": (C.c_int, [vp, vp, i64, P(i32), P(i64), P(i64),
                                                 P(C.c_int8), pp]),
     "lime_set_create_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
+    "lime_set_create_device_stranded": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, pp]),
     "lime_set_create_global": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_set_destroy": (C.c_int, [vp]),
     "lime_set_size": (i64, [vp]),
@@ -74,6 +75,7 @@ SIGNATURES = {
     "lime_intersect_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),
     "lime_intersect_count_owned": (C.c_int, [vp, vp, vp, i64, i64, i64, pp, P(i64)]),
     "lime_window_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),
+    "lime_closest_count": (C.c_int, [vp, vp, vp, C.c_int, pp, P(i64)]),
     "lime_intersect_fill_device": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_fill_host": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_checksum": (C.c_int, [vp, P(u64), P(u64)]),

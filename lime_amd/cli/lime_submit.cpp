@@ -13,6 +13,8 @@
 //                               register it)
 //   window    A.bed B.bed [-distance D]   cli/Window.scala:42-55 (keys stranded,
 //                               DistributedWindow default distance 1000)
+//   closest   A.bed B.bed       cli/Closest.scala:45-58 (keys stranded,
+//                               SingleClosest)
 //
 // Everything before "--" is accepted and ignored (there is no Spark).
 // Output is one region per line, tab-separated (chrom, start, end), followed
@@ -41,6 +43,7 @@ const Cmd kCommands[] = {
     {"sort", "Sorts the regions in a single input"},
     {"window", "Compute nearby regions between two inputs"},
     {"cluster", "Cluster (but don't merge) overlapping/nearby intervals"},
+    {"closest", "Find the closest region in the second input for each region of the first"},
 };
 
 void usage() {
@@ -123,6 +126,15 @@ int run(const std::vector<std::string> &args) {
             if (args[i] == "-distance") d = std::stoll(args[i + 1]);
         auto out = DistributedWindow<std::string, std::string>(load_bed(args[1], true),
                                                                load_bed(args[2], true), {}, d)
+                       .compute();
+        for (auto &o : out) {
+            print_region(o.first);
+            printf("\t%s\t%s\n", o.second.first.c_str(), o.second.second.c_str());
+        }
+    } else if (cmd == "closest") {
+        need(2);
+        auto out = SingleClosest<std::string, std::string>(load_bed(args[1], true),
+                                                           load_bed(args[2], true))
                        .compute();
         for (auto &o : out) {
             print_region(o.first);

@@ -59,6 +59,11 @@ void Pool::release_all() {
 }
 
 int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes) {
+    if (bytes > 4096) {  // larger than the pinned scratch: pageable copy
+        LIME_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, S(c)));
+        LIME_HIP(hipStreamSynchronize(S(c)));
+        return LIME_OK;
+    }
     LIME_HIP(hipMemcpyAsync(c->pinned, dev, bytes, hipMemcpyDeviceToHost, S(c)));
     LIME_HIP(hipStreamSynchronize(S(c)));
     memcpy(host, c->pinned, bytes);
@@ -75,6 +80,12 @@ int format_bed(lime_ctx *ctx, const std::vector<uint32_t> &off,
                const std::vector<std::string> &names, int64_t n, const uint32_t *gs,
                const uint32_t *ge, const uint32_t *extra, char *out, int64_t cap,
                int64_t *total_len);
+struct ClosestPlan;
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan **out);
+int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
+int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr);
+void closest_free(ClosestPlan *pl);
+int64_t closest_total(const ClosestPlan *pl);
 int intersect_fill(PairsPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
 int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr);
 void intersect_free(PairsPlan *pl);
@@ -144,9 +155,11 @@ static lime_set *new_set(lime_ctx *ctx, const lime_space *sp, int64_t n) {
 static int create_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
                               const int32_t *d_contig, const uint32_t *d_start,
                               const uint32_t *d_end, lime_set **out,
-                              int8_t *d_strand = nullptr, int min_shift = 0) {
+                              int8_t *d_strand = nullptr, int min_shift = 0,
+                              bool strand_uniform = false) {
     lime_set *s = new_set(ctx, sp, n);
     s->strand_in = d_strand;
+    s->strand_uniform = strand_uniform;
     s->min_shift = min_shift;
     uint32_t *d_len = nullptr;
     int rc = upload_space(ctx, sp, &s->d_off, &d_len);
@@ -349,7 +362,9 @@ static int create_host(lime_ctx *ctx, const lime_space *sp, int64_t n, const int
             LIME_HIP(hipStreamSynchronize(S(ctx)));
         }
     }
-    int rc = create_from_device(ctx, sp, n, dc, ds, de, out, dst);
+    bool uniform = true;
+    for (int64_t i = 1; strand && i < n && uniform; ++i) uniform = strand[i] == strand[0];
+    int rc = create_from_device(ctx, sp, n, dc, ds, de, out, dst, 0, strand && uniform);
     release(ctx, dc);
     release(ctx, ds);
     release(ctx, de);
@@ -363,6 +378,25 @@ int lime_set_create_device(lime_ctx *ctx, const lime_space *sp, int64_t n, const
     if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
     hipSetDevice(ctx->device);
     return create_from_device(ctx, sp, n, d_contig, d_start, d_end, out);
+}
+
+int lime_set_create_device_stranded(lime_ctx *ctx, const lime_space *sp, int64_t n,
+                                    const int32_t *d_contig, const uint32_t *d_start,
+                                    const uint32_t *d_end, const int8_t *d_strand,
+                                    lime_set **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_contig || !d_start || !d_end)))
+        return fail(LIME_ERR_ARG, "bad set arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    int8_t *dst;  // the set keeps its own copy of the codes
+    LIME_TRY(alloc(ctx, &dst, (size_t)std::max<int64_t>(n, 1)));
+    if (n > 0) {
+        if (d_strand)
+            LIME_HIP(hipMemcpyAsync(dst, d_strand, (size_t)n, hipMemcpyDeviceToDevice, S(ctx)));
+        else
+            LIME_HIP(hipMemsetAsync(dst, 0, (size_t)n, S(ctx)));
+    }
+    return create_from_device(ctx, sp, n, d_contig, d_start, d_end, out, dst, 0, !d_strand);
 }
 
 int lime_set_destroy(lime_set *s) {
@@ -477,7 +511,13 @@ static bool same_space(const lime_set *a, const lime_set *b) {
 struct lime_pairs {
     PairsPlan *plan;
     lime_ctx *ctx;
+    ClosestPlan *closest = nullptr;  // set instead of plan for lime_closest_count
 };
+
+static int pairs_fill(lime_pairs *p, int64_t first, int64_t count, lime_pair *d_out) {
+    return p->closest ? closest_fill(p->closest, first, count, d_out)
+                      : intersect_fill(p->plan, first, count, d_out);
+}
 
 int lime_intersect_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,
                          lime_pairs **plan, int64_t *n_pairs) {
@@ -512,10 +552,29 @@ int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64
     return LIME_OK;
 }
 
+int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int mode,
+                       lime_pairs **plan, int64_t *n_pairs) {
+    if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad closest arguments");
+    if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
+    if (mode != LIME_CLOSEST)
+        return fail(LIME_ERR_ARG, "closest mode must be LIME_CLOSEST (SingleClosest)");
+    if (!a->strand_in || !b->strand_in || a->min_shift || b->min_shift)
+        return fail(LIME_ERR_ARG,
+                    "closest needs sets in full RegionOrdering (lime_set_create_host_stranded)");
+    hipSetDevice(ctx->device);
+    ClosestPlan *cl = nullptr;
+    LIME_TRY(closest_plan(ctx, a, b, &cl));
+    lime_pairs *p = new lime_pairs{nullptr, ctx};
+    p->closest = cl;
+    *plan = p;
+    if (n_pairs) *n_pairs = closest_total(cl);
+    return LIME_OK;
+}
+
 int lime_intersect_fill_device(lime_pairs *plan, int64_t first, int64_t count, lime_pair *d_out) {
     if (!plan || (count > 0 && !d_out)) return fail(LIME_ERR_ARG, "bad fill arguments");
     hipSetDevice(plan->ctx->device);
-    return intersect_fill(plan->plan, first, count, d_out);
+    return pairs_fill(plan, first, count, d_out);
 }
 
 int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lime_pair *out) {
@@ -527,7 +586,7 @@ int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lim
     LIME_TRY(alloc(ctx, &stage, (size_t)std::min(chunk, std::max(count, (int64_t)1))));
     for (int64_t f = 0; f < count; f += chunk) {
         const int64_t c = std::min(chunk, count - f);
-        LIME_TRY(intersect_fill(plan->plan, first + f, c, stage));
+        LIME_TRY(pairs_fill(plan, first + f, c, stage));
         LIME_HIP(hipMemcpyAsync(out + f, stage, sizeof(lime_pair) * (size_t)c,
                                 hipMemcpyDeviceToHost, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));
@@ -539,12 +598,16 @@ int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lim
 int lime_intersect_checksum(lime_pairs *plan, uint64_t *sum, uint64_t *xr) {
     if (!plan || !sum || !xr) return fail(LIME_ERR_ARG, "bad checksum arguments");
     hipSetDevice(plan->ctx->device);
+    if (plan->closest) return closest_checksum(plan->closest, sum, xr);
     return intersect_checksum(plan->plan, sum, xr);
 }
 
 int lime_pairs_destroy(lime_pairs *plan) {
     if (!plan) return LIME_OK;
-    intersect_free(plan->plan);
+    if (plan->closest)
+        closest_free(plan->closest);
+    else
+        intersect_free(plan->plan);
     delete plan;
     return LIME_OK;
 }

@@ -1,0 +1,593 @@
+// closest.hip -- SingleClosest (lime-core Closest.scala:34-214, the CLI's
+// `closest`, cli/Closest.scala:45-58) on the device, exactly as the
+// reference's sweep computes it on one partition: left rows in RegionOrdering,
+// a right pointer j advanced while advanceCacheCondition holds (each success
+// sets the mutable currentClosest C to the candidate, so C = R[j-1]), a cache
+// R[p, j) trimmed at its head by pruneCacheCondition (with SetTheory.scala
+// :131-141's "index <= 0 -> trim nothing"), and processHits emitting every
+// cached R at the same unstrandedDistance from L as C.
+//
+// The sweep is sequential; its state (j, p) is recovered here in parallel.
+//
+// Right pointer.  Within contig c (rights [r0, r1)), for left L the advance
+// stops at position k in (r0, r1) iff dist(L, R[k]) > dist(L, R[k-1]).  With
+// A(L) = first right starting at or after L.end, a stop below A(L) is a "jag"
+// (R[k-1].end > R[k].end) whose R[k] lies wholly before L -- and stays before
+// every later left, so once the pointer halts at one it never moves again on
+// this contig.  Without such a halt the pointer after left i is
+//     U_i = max_{i' <= i} N_{i'},
+// N = the left's own stop at or after A (A itself when dist grows there, else
+// the next distinct start).  So: N per left, one prefix max, then per left
+// "is there an active jag in [U_{i-1}, A_i)?"; the first such left fixes the
+// contig's stuck position.  The pointer crosses into the next left contig only
+// if it reached r1 and no rights lie on contigs in between; otherwise the
+// sweep is stuck on another contig for good and emits nothing more
+// (contig liveness, a host pass over <= n_contigs entries).
+//
+// Cache head.  p_i = first k in [p_{i-1}, j_i) with dist(L_i, R[k]) <= D_i
+// (D_i = dist(L_i, C)), else p_{i-1}.  The map x -> F_i(x) is monotone, so
+// starting from the prefix max of F_i(r0) (a lower bound) and applying
+// p_i <- F_i(p_{i-1}) for all lefts at once converges upwards to the exact
+// chain; on the inputs tried it is exact after the first round, which the
+// next round confirms.  F_i(r0) is one binary search of the right set's
+// prefix max of ends; F_i(x) scans the ends with a two-level block-max skip.
+//
+// Output per left: every k in [p_i, j_i) with dist(L_i, R[k]) == D_i, in
+// index order (= cache order), as (L, (L.row, R.row)) records.
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace lime {
+
+struct ClosestPlan {
+    lime_ctx *ctx = nullptr;
+    const lime_set *A = nullptr, *B = nullptr;
+    int64_t nl = 0;
+    uint32_t *jp = nullptr;    // per left: right pointer j after the left
+    uint32_t *pp = nullptr;    // per left: cache head p after the left
+    uint32_t *dd = nullptr;    // per left: D (0xffffffff: no output)
+    uint64_t *off = nullptr;   // per left: exclusive output offsets
+    uint32_t *rb = nullptr;    // n_contigs + 1 right contig bounds
+    int64_t total = 0;
+    int rounds = 0;            // cache-head rounds until the fixed point
+};
+
+namespace {
+
+constexpr int CB = 256;
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int OCAP = 4096;  // contig offsets staged in LDS
+
+__device__ __forceinline__ int contig_of(const uint32_t *off, int32_t nc, uint32_t g) {
+    int lo = 0, hi = nc;  // largest c with off[c] <= g
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= g)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// ADAM unstrandedDistance for rows of one contig: 0 if covering, else gap + 1
+__device__ __forceinline__ uint32_t udist(uint32_t ls, uint32_t le, uint32_t rs, uint32_t re) {
+    if (le > rs && ls < re) return 0u;
+    return rs >= le ? rs - le + 1u : ls - re + 1u;
+}
+
+struct Rights {
+    const uint32_t *gs, *ge, *row, *pmax;
+    const uint32_t *jag;            // per right: end if a jag, else NONE
+    const uint32_t *jmin1, *jmin2;  // block minima of jag (64, 4096 rows)
+    const uint32_t *gmax1, *gmax2;  // block maxima of ge
+    int64_t n;
+};
+
+struct Lefts {
+    const uint32_t *gs, *ge, *row;
+    int64_t n;
+    const uint32_t *off;  // space offsets
+    int32_t nc;
+    const uint32_t *rb;   // right contig bounds
+};
+
+// first k in [lo, hi) with v[k] <= t (MIN) / v[k] >= t (!MIN), hi if none;
+// whole 64- and 4096-row blocks are skipped by their minimum / maximum
+template <bool MIN>
+__device__ __forceinline__ int64_t first_hit(const uint32_t *v, const uint32_t *l1,
+                                             const uint32_t *l2, int64_t lo, int64_t hi,
+                                             uint64_t t) {
+    auto hit = [&](uint32_t x) { return MIN ? (uint64_t)x <= t : (uint64_t)x >= t; };
+    int64_t k = lo;
+    while (k < hi && (k & 63)) {
+        if (hit(v[k])) return k;
+        ++k;
+    }
+    while (k < hi) {
+        if (!(k & 4095) && !hit(l2[k >> 12])) {
+            k += 4096;
+            continue;
+        }
+        if (!hit(l1[k >> 6])) {
+            k += 64;
+            continue;
+        }
+        const int64_t e = min(k + 64, hi);
+        for (; k < e; ++k)
+            if (hit(v[k])) return k;
+    }
+    return hi;
+}
+
+__global__ __launch_bounds__(CB) void k_bounds(const uint32_t *__restrict__ gs, int64_t n,
+                                               const uint32_t *__restrict__ off, int32_t nc,
+                                               uint32_t *__restrict__ rb) {
+    const int c = blockIdx.x * CB + threadIdx.x;
+    if (c > nc) return;
+    rb[c] = (uint32_t)dev::lower_bound(gs, 0, n, off[c]);
+}
+
+// U at the last left of each contig with lefts
+__global__ __launch_bounds__(CB) void k_last(const uint32_t *__restrict__ lb,
+                                             const uint32_t *__restrict__ U, int32_t nc,
+                                             uint32_t *__restrict__ last) {
+    const int c = blockIdx.x * CB + threadIdx.x;
+    if (c >= nc) return;
+    last[c] = lb[c + 1] > lb[c] ? U[lb[c + 1] - 1] : 0u;
+}
+
+// jag[k] = R[k].end when R[k-1] (same contig) ends later, else NONE
+__global__ __launch_bounds__(CB) void k_jags(const uint32_t *__restrict__ gs,
+                                             const uint32_t *__restrict__ ge, int64_t n,
+                                             const uint32_t *__restrict__ off, int32_t nc,
+                                             uint32_t *__restrict__ jag) {
+    __shared__ uint32_t s_off[OCAP];
+    if (nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= nc; i += CB) s_off[i] = off[i];
+    __syncthreads();
+    const uint32_t *o = nc + 1 <= OCAP ? s_off : off;
+    const int64_t k = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (k >= n) return;
+    uint32_t v = NONE;
+    if (k > 0) {
+        const int c = contig_of(o, nc, gs[k]);
+        if (gs[k - 1] >= o[c] && ge[k - 1] > ge[k]) v = ge[k];
+    }
+    jag[k] = v;
+}
+
+// one block-min / block-max level: 64 inputs per output, one wave each
+template <bool MIN>
+__global__ __launch_bounds__(CB) void k_level(const uint32_t *__restrict__ v, int64_t n,
+                                              uint32_t *__restrict__ out, int64_t m) {
+    const int64_t b = (int64_t)blockIdx.x * (CB / 64) + threadIdx.x / 64;
+    if (b >= m) return;
+    const int64_t i = b * 64 + dev::lane_id();
+    uint32_t x = i < n ? v[i] : (MIN ? NONE : 0u);
+    x = MIN ? dev::wave_reduce_min(x) : dev::wave_reduce_max(x);
+    if (dev::lane_id() == 0) out[b] = x;
+}
+
+// per left: A (first right starting at or after L.end) and N (the left's
+// own stop at or after A)
+__global__ __launch_bounds__(CB) void k_stops(Lefts L, Rights R, uint32_t *__restrict__ Aout,
+                                              uint32_t *__restrict__ Nout) {
+    __shared__ uint32_t s_off[OCAP];
+    if (L.nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
+    __syncthreads();
+    const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (i >= L.n) return;
+    const uint32_t ls = L.gs[i], le = L.ge[i];
+    const int c = contig_of(o, L.nc, ls);
+    const int64_t lo = L.rb[c], hi = L.rb[c + 1];
+    const int64_t a = dev::lower_bound(R.gs, lo, hi, le);
+    int64_t nn;
+    if (a == hi)
+        nn = hi;
+    else if (a > lo && udist(ls, le, R.gs[a - 1], R.ge[a - 1]) < udist(ls, le, R.gs[a], R.ge[a]))
+        nn = a;
+    else
+        nn = dev::upper_bound(R.gs, a, hi, R.gs[a]);
+    Aout[i] = (uint32_t)a;
+    Nout[i] = (uint32_t)nn;
+}
+
+// per left: the first active jag in [max(U_{i-1}, r0 + 1), A_i); the
+// smallest such left of each contig (and its jag) is kept per contig
+__global__ __launch_bounds__(CB) void k_stuck(Lefts L, Rights R, const uint32_t *__restrict__ A,
+                                              const uint32_t *__restrict__ U,
+                                              unsigned long long *__restrict__ stuck) {
+    __shared__ uint32_t s_off[OCAP];
+    if (L.nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
+    __syncthreads();
+    const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (i >= L.n) return;
+    const uint32_t ls = L.gs[i];
+    const int c = contig_of(o, L.nc, ls);
+    const int64_t r0 = L.rb[c];
+    const int64_t lo = max((int64_t)(i > 0 ? U[i - 1] : 0u), r0 + 1);
+    const int64_t a = A[i];
+    if (lo >= a) return;
+    const int64_t k = first_hit<true>(R.jag, R.jmin1, R.jmin2, lo, a, ls);
+    if (k < a) atomicMin(&stuck[c], ((unsigned long long)i << 32) | (unsigned long long)k);
+}
+
+struct State {
+    const uint32_t *A, *U;
+    const unsigned long long *stuck;
+    const uint8_t *live;
+};
+
+__device__ __forceinline__ uint32_t pointer_of(const State &s, int c, int64_t i) {
+    const unsigned long long st = s.stuck[c];
+    if (st != ~0ull && (uint64_t)i >= (st >> 32)) return (uint32_t)(st & 0xffffffffu);
+    return s.U[i];
+}
+
+// F_i(x): first k in [x, j) with dist(L, R[k]) <= D, else x.  Below A that
+// is R.end >= L.start + 1 - D; from A on it is R.start <= L.end + D - 1,
+// which holds for a prefix of [A, j) (starts ascend), so only A is tested.
+__device__ __forceinline__ int64_t near_from(const Rights &R, uint32_t ls, uint32_t le,
+                                             uint32_t D, int64_t a, int64_t j, int64_t x,
+                                             bool fresh) {
+    const int64_t T = (int64_t)ls + 1 - (int64_t)D;
+    const int64_t hi = min(a, j);
+    if (x < hi) {
+        int64_t k;
+        if (T <= 0)
+            k = x;
+        else if (fresh)  // prefix max of ends: exact from the contig start
+            k = dev::lower_bound(R.pmax, x, hi, (uint64_t)T);
+        else
+            k = first_hit<false>(R.ge, R.gmax1, R.gmax2, x, hi, (uint64_t)T);
+        if (k < hi) return k;
+    }
+    const int64_t k = max(x, a);
+    if (k < j && (int64_t)R.gs[k] <= (int64_t)le + (int64_t)D - 1) return k;
+    return x;
+}
+
+// per left: j, D and the fresh cache head F_i(r0)
+__global__ __launch_bounds__(CB) void k_fresh(Lefts L, Rights R, State s,
+                                              uint32_t *__restrict__ jp, uint32_t *__restrict__ dd,
+                                              uint32_t *__restrict__ P) {
+    __shared__ uint32_t s_off[OCAP];
+    if (L.nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
+    __syncthreads();
+    const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (i >= L.n) return;
+    const uint32_t ls = L.gs[i], le = L.ge[i];
+    const int c = contig_of(o, L.nc, ls);
+    const int64_t r0 = L.rb[c];
+    const int64_t j = pointer_of(s, c, i);
+    jp[i] = (uint32_t)j;
+    if (!s.live[c] || j <= r0) {
+        dd[i] = NONE;
+        P[i] = (uint32_t)r0;
+        return;
+    }
+    const uint32_t D = udist(ls, le, R.gs[j - 1], R.ge[j - 1]);
+    dd[i] = D;
+    P[i] = (uint32_t)near_from(R, ls, le, D, s.A[i], j, r0, true);
+}
+
+// one round of p_i <- max(p_i, F_i(p_{i-1}))
+__global__ __launch_bounds__(CB) void k_prune_round(Lefts L, Rights R, State s,
+                                                    const uint32_t *__restrict__ jp,
+                                                    const uint32_t *__restrict__ dd,
+                                                    const uint32_t *__restrict__ pin,
+                                                    uint32_t *__restrict__ pout,
+                                                    unsigned int *__restrict__ changed) {
+    __shared__ uint32_t s_off[OCAP];
+    if (L.nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
+    __syncthreads();
+    const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (i >= L.n) return;
+    const uint32_t cur = pin[i];
+    uint32_t nv = cur;
+    const uint32_t D = dd[i];
+    if (D != NONE) {
+        const uint32_t ls = L.gs[i], le = L.ge[i];
+        const int c = contig_of(o, L.nc, ls);
+        const int64_t r0 = L.rb[c];
+        const int64_t x = max((int64_t)(i > 0 ? pin[i - 1] : 0u), r0);
+        const int64_t f = near_from(R, ls, le, D, s.A[i], jp[i], x, false);
+        nv = (uint32_t)max((int64_t)cur, f);
+    }
+    pout[i] = nv;
+    if (nv != cur) atomicOr(changed, 1u);
+}
+
+// output count per left: k in [p, j) with dist == D
+__global__ __launch_bounds__(CB) void k_count(Lefts L, Rights R, const uint32_t *__restrict__ jp,
+                                              const uint32_t *__restrict__ pp,
+                                              const uint32_t *__restrict__ dd,
+                                              uint64_t *__restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (i >= L.n) return;
+    const uint32_t D = dd[i];
+    uint64_t m = 0;
+    if (D != NONE) {
+        const uint32_t ls = L.gs[i], le = L.ge[i];
+        for (int64_t k = pp[i], j = jp[i]; k < j; ++k) m += udist(ls, le, R.gs[k], R.ge[k]) == D;
+    }
+    cnt[i] = m;
+}
+
+// records [first, first + count) of the output order, or their checksum
+template <bool CKSUM>
+__global__ __launch_bounds__(CB) void k_emit(Lefts L, Rights R, const uint32_t *__restrict__ jp,
+                                             const uint32_t *__restrict__ pp,
+                                             const uint32_t *__restrict__ dd,
+                                             const uint64_t *__restrict__ off, int64_t first,
+                                             int64_t count, lime_pair *__restrict__ out,
+                                             unsigned long long *__restrict__ ck) {
+    __shared__ uint32_t s_off[OCAP];
+    if (L.nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
+    __syncthreads();
+    const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    uint64_t hs = 0, hx = 0;
+    if (i < L.n && dd[i] != NONE) {
+        const uint32_t D = dd[i];
+        int64_t pos = (int64_t)off[i];
+        const int64_t end = (int64_t)off[i + 1];
+        if (CKSUM || (end > first && pos < first + count)) {
+            const uint32_t ls = L.gs[i], le = L.ge[i];
+            const int c = contig_of(o, L.nc, ls);
+            const uint32_t s0 = ls - o[c], e0 = le - o[c], ar = L.row[i];
+            for (int64_t k = pp[i], j = jp[i]; k < j && pos < end; ++k) {
+                if (udist(ls, le, R.gs[k], R.ge[k]) != D) continue;
+                if (CKSUM) {
+                    const uint64_t h = dev::pair_hash(s0, e0, ar, R.row[k]);
+                    hs += h;
+                    hx ^= h;
+                } else if (pos >= first && pos < first + count) {
+                    out[pos - first] = lime_pair{s0, e0, ar, R.row[k]};
+                }
+                ++pos;
+            }
+        }
+    }
+    if (CKSUM) {
+        hs = dev::wave_reduce_sum(hs);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) hx ^= __shfl_xor(hx, d, 64);
+        if (dev::lane_id() == 0) {
+            atomicAdd(&ck[0], (unsigned long long)hs);
+            atomicXor(&ck[1], (unsigned long long)hx);
+        }
+    }
+}
+
+}  // namespace
+
+void closest_free(ClosestPlan *pl) {
+    if (!pl) return;
+    lime_ctx *ctx = pl->ctx;
+    release(ctx, pl->jp);
+    release(ctx, pl->pp);
+    release(ctx, pl->dd);
+    release(ctx, pl->off);
+    release(ctx, pl->rb);
+    delete pl;
+}
+
+int64_t closest_total(const ClosestPlan *pl) { return pl->total; }
+int closest_rounds(const ClosestPlan *pl) { return pl->rounds; }
+
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan **out) {
+    const int64_t nl = A->n, nr = B->n;
+    const int32_t nc = A->n_contigs;
+    if (nl >= (int64_t)NONE || nr >= (int64_t)NONE)
+        return fail(LIME_ERR_RANGE, "closest supports fewer than 2^32 - 1 rows per set");
+    ClosestPlan *pl = new ClosestPlan();
+    pl->ctx = ctx;
+    pl->A = A;
+    pl->B = B;
+    pl->nl = nl;
+    auto bail = [&](int rc) {
+        closest_free(pl);
+        return rc;
+    };
+    int rc;
+#define CL_TRY(x)                    \
+    if ((rc = (x)) != LIME_OK) {     \
+        return bail(rc);             \
+    }
+    CL_TRY(alloc(ctx, &pl->rb, (size_t)nc + 1));
+    CL_TRY(alloc(ctx, &pl->jp, (size_t)std::max<int64_t>(nl, 1)));
+    CL_TRY(alloc(ctx, &pl->pp, (size_t)std::max<int64_t>(nl, 1)));
+    CL_TRY(alloc(ctx, &pl->dd, (size_t)std::max<int64_t>(nl, 1)));
+    CL_TRY(alloc(ctx, &pl->off, (size_t)nl + 1));
+    if (nl == 0) {
+        LIME_HIP(hipMemsetAsync(pl->off, 0, sizeof(uint64_t), S(ctx)));
+        *out = pl;
+        return LIME_OK;
+    }
+    hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), B->gs, nr,
+                       B->d_off, nc, pl->rb);
+    LIME_HIP(hipGetLastError());
+    CL_TRY(build_prefix_max(ctx, B));
+    // right-side search levels
+    const int64_t m1 = (nr + 63) / 64, m2 = (m1 + 63) / 64;
+    uint32_t *jag, *jmin1, *jmin2, *gmax1, *gmax2;
+    CL_TRY(alloc(ctx, &jag, (size_t)std::max<int64_t>(nr, 1)));
+    CL_TRY(alloc(ctx, &jmin1, (size_t)std::max<int64_t>(m1, 1)));
+    CL_TRY(alloc(ctx, &jmin2, (size_t)std::max<int64_t>(m2, 1)));
+    CL_TRY(alloc(ctx, &gmax1, (size_t)std::max<int64_t>(m1, 1)));
+    CL_TRY(alloc(ctx, &gmax2, (size_t)std::max<int64_t>(m2, 1)));
+    if (nr > 0) {
+        hipLaunchKernelGGL(k_jags, dim3(blocks_for(nr, CB)), dim3(CB), 0, S(ctx), B->gs, B->ge,
+                           nr, B->d_off, nc, jag);
+        hipLaunchKernelGGL(k_level<true>, dim3(blocks_for(m1, CB / 64)), dim3(CB), 0, S(ctx),
+                           (const uint32_t *)jag, nr, jmin1, m1);
+        hipLaunchKernelGGL(k_level<true>, dim3(blocks_for(m2, CB / 64)), dim3(CB), 0, S(ctx),
+                           (const uint32_t *)jmin1, m1, jmin2, m2);
+        hipLaunchKernelGGL(k_level<false>, dim3(blocks_for(m1, CB / 64)), dim3(CB), 0, S(ctx),
+                           B->ge, nr, gmax1, m1);
+        hipLaunchKernelGGL(k_level<false>, dim3(blocks_for(m2, CB / 64)), dim3(CB), 0, S(ctx),
+                           (const uint32_t *)gmax1, m1, gmax2, m2);
+        LIME_HIP(hipGetLastError());
+    }
+    Rights R{B->gs, B->ge, B->row, B->pmax, jag, jmin1, jmin2, gmax1, gmax2, nr};
+    Lefts L{A->gs, A->ge, A->row, nl, A->d_off, nc, pl->rb};
+    // right pointer: stops, prefix max, stuck positions
+    uint32_t *Aa, *Nn, *U, *P, *p2;
+    unsigned long long *stuck;
+    uint8_t *live;
+    unsigned int *changed;
+    CL_TRY(alloc(ctx, &Aa, (size_t)nl));
+    CL_TRY(alloc(ctx, &Nn, (size_t)nl));
+    CL_TRY(alloc(ctx, &U, (size_t)nl));
+    CL_TRY(alloc(ctx, &P, (size_t)nl));
+    CL_TRY(alloc(ctx, &p2, (size_t)nl));
+    CL_TRY(alloc(ctx, &stuck, (size_t)nc));
+    CL_TRY(alloc(ctx, &live, (size_t)nc));
+    CL_TRY(alloc(ctx, &changed, 1));
+    const unsigned gl = blocks_for(nl, CB);
+    hipLaunchKernelGGL(k_stops, dim3(gl), dim3(CB), 0, S(ctx), L, R, Aa, Nn);
+    LIME_HIP(hipGetLastError());
+    CL_TRY(prefix_max_u32(ctx, Nn, U, nl));
+    LIME_HIP(hipMemsetAsync(stuck, 0xff, sizeof(unsigned long long) * (size_t)nc, S(ctx)));
+    hipLaunchKernelGGL(k_stuck, dim3(gl), dim3(CB), 0, S(ctx), L, R, (const uint32_t *)Aa,
+                       (const uint32_t *)U, stuck);
+    LIME_HIP(hipGetLastError());
+    // contig liveness (host, <= n_contigs steps): the sweep enters the next
+    // left contig only from the end of this contig's rights, and only if no
+    // rights lie on the contigs in between
+    {
+        uint32_t *lbd, *lastU;
+        CL_TRY(alloc(ctx, &lbd, (size_t)nc + 1));
+        CL_TRY(alloc(ctx, &lastU, (size_t)nc));
+        hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), A->gs,
+                           nl, A->d_off, nc, lbd);
+        hipLaunchKernelGGL(k_last, dim3(blocks_for(nc, CB)), dim3(CB), 0, S(ctx),
+                           (const uint32_t *)lbd, (const uint32_t *)U, nc, lastU);
+        LIME_HIP(hipGetLastError());
+        std::vector<uint32_t> rb(nc + 1), lb(nc + 1), lu(nc);
+        std::vector<unsigned long long> st(nc);
+        CL_TRY(read_back(ctx, rb.data(), pl->rb, sizeof(uint32_t) * (nc + 1)));
+        CL_TRY(read_back(ctx, lb.data(), lbd, sizeof(uint32_t) * (nc + 1)));
+        CL_TRY(read_back(ctx, lu.data(), lastU, sizeof(uint32_t) * nc));
+        CL_TRY(read_back(ctx, st.data(), stuck, sizeof(unsigned long long) * nc));
+        release(ctx, lbd);
+        release(ctx, lastU);
+        std::vector<uint8_t> lv(nc, 0);
+        bool alive = true, first = true;
+        for (int32_t c = 0; c < nc; ++c) {
+            if (lb[c + 1] <= lb[c]) continue;  // no lefts on c
+            if (first) {  // the sweep starts at right row 0
+                alive = rb[c] == 0;
+                first = false;
+            }
+            lv[c] = alive ? 1 : 0;
+            if (!alive) continue;
+            const uint64_t last = lb[c + 1] - 1;
+            const uint32_t jl =
+                (st[c] != ~0ull && last >= (st[c] >> 32)) ? (uint32_t)(st[c] & 0xffffffffu) : lu[c];
+            // the next left contig is entered from the end of c's rights only,
+            // and only if no rights lie on the contigs in between
+            alive = jl == rb[c + 1];
+            int32_t cn = c + 1;
+            while (cn < nc && lb[cn + 1] <= lb[cn]) ++cn;
+            if (alive && cn < nc) alive = rb[c + 1] == rb[cn];
+        }
+        LIME_HIP(hipMemcpyAsync(live, lv.data(), (size_t)nc, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipStreamSynchronize(S(ctx)));
+    }
+    State s{Aa, U, stuck, live};
+    hipLaunchKernelGGL(k_fresh, dim3(gl), dim3(CB), 0, S(ctx), L, R, s, pl->jp, pl->dd, P);
+    LIME_HIP(hipGetLastError());
+    // cache head: prefix max of the fresh heads, then rounds to the fixed point
+    CL_TRY(prefix_max_u32(ctx, P, pl->pp, nl));
+    uint32_t *cur = pl->pp, *nxt = p2;
+    for (int64_t r = 0; r <= nl; ++r) {
+        LIME_HIP(hipMemsetAsync(changed, 0, sizeof(unsigned int), S(ctx)));
+        hipLaunchKernelGGL(k_prune_round, dim3(gl), dim3(CB), 0, S(ctx), L, R, s,
+                           (const uint32_t *)pl->jp, (const uint32_t *)pl->dd,
+                           (const uint32_t *)cur, nxt, changed);
+        LIME_HIP(hipGetLastError());
+        unsigned int ch = 0;
+        LIME_TRY(read_back(ctx, &ch, changed, sizeof(ch)));
+        std::swap(cur, nxt);
+        ++pl->rounds;
+        if (!ch) break;
+    }
+    if (cur != pl->pp)
+        LIME_HIP(hipMemcpyAsync(pl->pp, cur, sizeof(uint32_t) * (size_t)nl,
+                                hipMemcpyDeviceToDevice, S(ctx)));
+    // output counts and offsets
+    uint64_t *cnt, *tot;
+    CL_TRY(alloc(ctx, &cnt, (size_t)nl));
+    CL_TRY(alloc(ctx, &tot, 1));
+    hipLaunchKernelGGL(k_count, dim3(gl), dim3(CB), 0, S(ctx), L, R, (const uint32_t *)pl->jp,
+                       (const uint32_t *)pl->pp, (const uint32_t *)pl->dd, cnt);
+    LIME_HIP(hipGetLastError());
+    CL_TRY(scan_exclusive_u64(ctx, cnt, pl->off, nl, tot));
+    LIME_HIP(hipMemcpyAsync(pl->off + nl, tot, sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                            S(ctx)));
+    uint64_t total = 0;
+    LIME_TRY(read_back(ctx, &total, tot, sizeof(total)));
+    pl->total = (int64_t)total;
+    for (void *q : {(void *)jag, (void *)jmin1, (void *)jmin2, (void *)gmax1, (void *)gmax2,
+                    (void *)Aa, (void *)Nn, (void *)U, (void *)P, (void *)p2, (void *)stuck,
+                    (void *)live, (void *)changed, (void *)cnt, (void *)tot})
+        ctx->pool.put(q);
+#undef CL_TRY
+    *out = pl;
+    return LIME_OK;
+}
+
+int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out) {
+    lime_ctx *ctx = pl->ctx;
+    if (first < 0 || count < 0 || first + count > pl->total)
+        return fail(LIME_ERR_ARG, "fill range outside the plan");
+    if (count == 0 || pl->nl == 0) return LIME_OK;
+    const lime_set *A = pl->A, *B = pl->B;
+    Rights R{B->gs, B->ge, B->row, B->pmax, nullptr, nullptr, nullptr, nullptr, nullptr, B->n};
+    Lefts L{A->gs, A->ge, A->row, pl->nl, A->d_off, A->n_contigs, pl->rb};
+    hipLaunchKernelGGL(k_emit<false>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0, S(ctx), L, R,
+                       (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+                       (const uint32_t *)pl->dd, (const uint64_t *)pl->off, first, count, d_out,
+                       nullptr);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
+int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr) {
+    lime_ctx *ctx = pl->ctx;
+    unsigned long long *ck;
+    LIME_TRY(alloc(ctx, &ck, 2));
+    LIME_HIP(hipMemsetAsync(ck, 0, 2 * sizeof(unsigned long long), S(ctx)));
+    if (pl->nl > 0) {
+        const lime_set *A = pl->A, *B = pl->B;
+        Rights R{B->gs, B->ge, B->row, B->pmax, nullptr, nullptr, nullptr, nullptr, nullptr,
+                 B->n};
+        Lefts L{A->gs, A->ge, A->row, pl->nl, A->d_off, A->n_contigs, pl->rb};
+        hipLaunchKernelGGL(k_emit<true>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0, S(ctx), L,
+                           R, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+                           (const uint32_t *)pl->dd, (const uint64_t *)pl->off, (int64_t)0,
+                           pl->total, (lime_pair *)nullptr, ck);
+        LIME_HIP(hipGetLastError());
+    }
+    unsigned long long h[2];
+    LIME_TRY(read_back(ctx, h, ck, sizeof(h)));
+    release(ctx, ck);
+    *sum = h[0];
+    *xr = h[1];
+    return LIME_OK;
+}
+
+}  // namespace lime

@@ -85,6 +85,7 @@ struct lime_set {
     // row; the set is sorted by (gs, ge, strand) and merge breaks runs at
     // strand changes (the reference fold's overlaps test)
     int8_t *strand_in = nullptr;
+    bool strand_uniform = false;  // every row has the same strand code
     // binned sets (bitset painting from unsorted rows): only the gs digits
     // at shifts >= min_shift are sorted, i.e. rows grouped by gs >> min_shift
     int min_shift = 0;
@@ -151,6 +152,8 @@ int scan_exclusive_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t
 int scan_exclusive_u64(lime_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n,
                        uint64_t *total_dev);
 int build_prefix_max(lime_ctx *ctx, const lime_set *set);
+// inclusive prefix max of a u32 array (out may alias in)
+int prefix_max_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n);
 
 }  // namespace lime
 

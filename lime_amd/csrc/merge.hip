@@ -383,20 +383,23 @@ int tile_prefix(lime_ctx *ctx, const uint32_t *ge, int64_t n, uint32_t **tpre_ou
 
 }  // namespace
 
+int prefix_max_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n) {
+    if (n <= 0) return LIME_OK;
+    uint32_t *tpre;
+    LIME_TRY(tile_prefix(ctx, in, n, &tpre));
+    const int64_t nt = (n + MTILE - 1) / MTILE;
+    hipLaunchKernelGGL(k_prefix_max, dim3((unsigned)nt), dim3(MB), 0, S(ctx), in, n,
+                       (const uint32_t *)tpre, out);
+    LIME_HIP(hipGetLastError());
+    release(ctx, tpre);
+    return LIME_OK;
+}
+
 int build_prefix_max(lime_ctx *ctx, const lime_set *set) {
     if (set->pmax) return LIME_OK;
-    const int64_t n = set->n;
     uint32_t *pm;
-    LIME_TRY(alloc(ctx, &pm, (size_t)n));
-    if (n > 0) {
-        uint32_t *tpre;
-        LIME_TRY(tile_prefix(ctx, set->ge, n, &tpre));
-        const int64_t nt = (n + MTILE - 1) / MTILE;
-        hipLaunchKernelGGL(k_prefix_max, dim3((unsigned)nt), dim3(MB), 0, S(ctx), set->ge, n,
-                           (const uint32_t *)tpre, pm);
-        LIME_HIP(hipGetLastError());
-        release(ctx, tpre);
-    }
+    LIME_TRY(alloc(ctx, &pm, (size_t)set->n));
+    LIME_TRY(prefix_max_u32(ctx, set->ge, pm, set->n));
     set->pmax = pm;
     return LIME_OK;
 }

@@ -44,16 +44,18 @@ struct SetStats {
 };
 
 // Pass kinds: an 8-bit digit of gs (M_GS); the zero-width bit (M_NZ, 0 =
-// zero width); an 8-bit digit of ge (M_GE); the strand code of the row
-// (M_ST).  Stranded sets sort by (gs, ge, strand) -- RegionOrdering -- with
-// passes ST, GE x4, GS x4; plain sets by (gs, zero-width first) with NZ?, GS.
+// zero width); an 8-bit digit of the width ge - gs (M_GE: among equal gs,
+// width order is end order); the strand code of the row (M_ST).  Stranded
+// sets sort by (gs, ge, strand) -- RegionOrdering -- with passes ST (skipped
+// when every row has one strand), GE x ceil(bits(max width) / 8), GS; plain
+// sets by (gs, zero-width first) with NZ?, GS.
 enum { M_GS = 0, M_NZ = 1, M_GE = 2, M_ST = 3 };
 
 template <int M>
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, uint32_t r, int shift,
                                              const int8_t *st) {
     if (M == M_NZ) return e > k ? 1u : 0u;
-    if (M == M_GE) return (e >> shift) & (RBINS - 1);
+    if (M == M_GE) return ((e - k) >> shift) & (RBINS - 1);
     // strand codes 0 independent, 1 forward, 2 reverse, 3 unknown sort by
     // bdg-formats' enum ordinal: FORWARD, REVERSE, INDEPENDENT, UNKNOWN
     if (M == M_ST) return (0xd2u >> (2 * ((uint32_t)(uint8_t)st[r] & 3u))) & 3u;
@@ -618,10 +620,9 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         if (stranded) {
             // RegionOrdering (start, end, strand): strand, then ge, then gs.
             // The strand pass runs first, while row i is still input row i.
-            const uint32_t span = set->off.empty() ? 0xffffffffu : set->off.back();
-            const int ebits = span ? 32 - __builtin_clz(span) : 1;
-            passes.push_back({M_ST, 0});
-            for (int sh = 0; sh < ebits; sh += 8) passes.push_back({M_GE, sh});
+            const int wbits = h.max_width ? 32 - __builtin_clz(h.max_width) : 0;
+            if (!set->strand_uniform) passes.push_back({M_ST, 0});
+            for (int sh = 0; sh < wbits; sh += 8) passes.push_back({M_GE, sh});
         } else if (set->has_zero_width && set->min_shift == 0) {
             passes.push_back({M_NZ, 0});
         }

@@ -311,6 +311,14 @@ class Context:
                                             d_end, C.byref(h)))
         return IntervalSet(self, h, space)
 
+    def set_from_device_stranded(self, space, n, d_contig, d_start, d_end, d_strand=None):
+        """device rows in full RegionOrdering (int8 strand codes in HBM, or
+        None = every row independent)"""
+        h = vp()
+        check(_lib().lime_set_create_device_stranded(self._h, space.handle, int(n), d_contig,
+                                                     d_start, d_end, d_strand, C.byref(h)))
+        return IntervalSet(self, h, space)
+
     def set_from_global(self, space, n, d_gs, d_ge, d_row):
         """rows already in the space's global coordinates (u32 device arrays)"""
         h = vp()
@@ -332,6 +340,14 @@ class Context:
         h, n = vp(), i64()
         check(_lib().lime_window_count(self._h, a._h, b._h, int(distance), C.byref(h),
                                        C.byref(n)))
+        return Pairs(self, h, n.value, keep=(a, b))
+
+    def closest(self, a, b):
+        """SingleClosest (Closest.scala:34-214) on one partition: for each
+        left row, the cached right rows at the current closest's distance.
+        Both sets must come from set_from_host_stranded (RegionOrdering)."""
+        h, n = vp(), i64()
+        check(_lib().lime_closest_count(self._h, a._h, b._h, 0, C.byref(h), C.byref(n)))
         return Pairs(self, h, n.value, keep=(a, b))
 
     def parse_bed(self, text):

@@ -14,6 +14,8 @@ lime-core/src/main/scala/org/bdgenomics/lime/set_theory/:
         -> [(ReferenceRegion, [])]                 Complement.scala:131-134
     DistributedWindow(leftRdd, rightRdd, partitionMap, threshold=1000).compute()
         -> [(ReferenceRegion, (T, U))]             Window.scala:71-95
+    SingleClosest(leftRdd, rightRdd, partitionMap).compute()
+        -> [(ReferenceRegion, (T, U))]             Closest.scala:34-214
     UnstrandedCluster / StrandedCluster / ...WithMinimumOverlap(rddToCompute,
                           partitionMap, threshold=0).compute()
         -> [(ReferenceRegion, [T])]                Cluster.scala:38-121
@@ -189,6 +191,35 @@ class DistributedWindow(_Op):
         lrank, rrank = _sorted_rank(lr), _sorted_rank(rr)
         out.sort(key=lambda t: (lrank[t[0]], rrank[t[1]]))
         return [(lr[a], (lv[a], rv[b])) for a, b in out]
+
+
+class SingleClosest(_Op):
+    """Closest.scala:34-214 (the CLI's closest): for each left row, in
+    RegionOrdering, the cached right rows at the same unstrandedDistance as
+    the sweep's currentClosest -> [(leftRegion, (T, U))].  One stranded set
+    per side (the order includes strand; the distance ignores it), run as the
+    reference's sweep runs on one partition."""
+
+    def __init__(self, leftRdd, rightRdd, partitionMap=None, threshold=0, ctx=None):
+        super().__init__(ctx)
+        self.left, self.right = list(leftRdd), list(rightRdd)
+        self.partitionMap, self.threshold = partitionMap, int(threshold)
+
+    def compute(self):
+        lr, lv = _rows(self.left)
+        rr, rv = _rows(self.right)
+        space = _space_for(lr, rr)
+        codes = lambda regs: np.array([_STRAND_CODE[r.strand] for r in regs], np.int8)
+        A = self.ctx.set_from_host_stranded(space, *_arrays(space, lr, range(len(lr))),
+                                            codes(lr))
+        B = self.ctx.set_from_host_stranded(space, *_arrays(space, rr, range(len(rr))),
+                                            codes(rr))
+        plan = self.ctx.closest(A, B)
+        out = [(lr[p["a_row"]], (lv[p["a_row"]], rv[p["b_row"]])) for p in plan.fill_host()]
+        plan.close()
+        A.close()
+        B.close()
+        return out
 
 
 class DistributedSubtract(_Op):

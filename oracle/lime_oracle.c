@@ -25,6 +25,9 @@
  *     called without threshold -> 0, quirk Q6), Merge.scala:8-31.
  *   - window: Window.scala:51-95 (cache predicates and processHits) over the
  *     same sweep, with ADAM's isNearby / distance (gap + 1) restated.
+ *   - closest: Closest.scala:10-268 (SingleClosest, SingleClosestSingleOverlap)
+ *     with its mutable currentClosest over the same sweep, pinned by the
+ *     arrays of ClosestSuite.scala:21-45,64-85.
  *   - complement: Complement.scala:11-128 as pinned by ComplementSuite.scala
  *     (canonical P=1-independent form): gaps of
  *     merge(A) per genome contig in String order, zero-width gaps dropped,
@@ -247,6 +250,102 @@ int64_t lo_window(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_
         for (int64_t k = cache.head; k < cache.tail; ++k) {
             const lo_region *r = cache.v[k];
             if (lo_nearby(cur, r, d)) lo_emit(&out, cur->contig, cur->start, cur->end, cur->row, r->row);
+        }
+    }
+    free(cache.v);
+    free(L);
+    free(R);
+    return out.count;
+}
+
+/* --------------------------------------------------------------- closest */
+
+#define LO_CLOSEST 0        /* SingleClosest (Closest.scala:34-214), the CLI's op */
+#define LO_CLOSEST_SINGLE 1 /* SingleClosestSingleOverlap (Closest.scala:216-268) */
+#define LO_NONE INT64_MAX   /* Option.None (different reference names) */
+
+/* ADAM unstrandedDistance (3rd-party, restated like distance above but
+ * strand-blind): None across contigs, 0 if covering, else gap + 1. */
+static int64_t lo_udist(const lo_region *a, const lo_region *o) {
+    if (a->contig != o->contig) return LO_NONE;
+    if (lo_covers(a, o)) return 0;
+    return o->start >= a->end ? o->start - a->end + 1 : a->start - o->end + 1;
+}
+/* ADAM coversBy: the covered length when covering, else None (restated as
+ * the overlap length, like overlapsBy in Appendix A.2; the suite's arrays do
+ * not tell it apart from other readings). */
+static int64_t lo_covers_by(const lo_region *a, const lo_region *o) {
+    if (!lo_covers(a, o)) return LO_NONE;
+    int64_t e = a->end < o->end ? a->end : o->end;
+    int64_t s = a->start > o->start ? a->start : o->start;
+    return e - s;
+}
+static int64_t lo_or(int64_t v, int64_t dflt) { return v == LO_NONE ? dflt : v; }
+
+/* Closest.scala, over the SetTheory.scala:131-187 sweep with its mutable
+ * currentClosest (:12, initially ReferenceRegion("", 0, 0): contig -1 here).
+ *   advance (:179-192 / :251-267) sets currentClosest = candidate on success;
+ *   prune   (:160-169 / :230-241) with the Q8 "index <= 0 -> trim nothing";
+ *   processHits (:202-213): every cached R with unstrandedDistance(L, R)
+ *   .contains(unstrandedDistance(L, C).getOrElse(Long.MaxValue)), emitted as
+ *   (L, (L.value, R.value)) in cache order.
+ * One partition holding every row (P = 1), as for the other ops. */
+int64_t lo_closest(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
+                   const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
+                   const int64_t *re, const int8_t *rstr, int mode, int64_t cap, int32_t *oc,
+                   int64_t *os, int64_t *oe, int64_t *olrow, int64_t *orrow) {
+    lo_region *L = lo_load(nl, lc, ls, le, lstr);
+    lo_region *R = lo_load(nr, rc, rs, re, rstr);
+    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+    lo_cache cache = {0};
+    lo_region dummy = {-1, 0, 0, 0, -1};
+    const lo_region *C = &dummy;
+    int64_t rpos = 0;
+    for (int64_t i = 0; i < nl; ++i) {
+        const lo_region *u = &L[i];
+        /* advanceCache */
+        while (rpos < nr) {
+            const lo_region *c = &R[rpos];
+            int adv;
+            if (c->contig != u->contig)
+                adv = 0;
+            else if (u->contig != C->contig)
+                adv = 1;
+            else if (mode == LO_CLOSEST)
+                adv = lo_udist(u, c) <= lo_or(lo_udist(u, C), INT64_MAX);
+            else
+                adv = (lo_covers(u, c) && lo_covers_by(u, c) >= lo_or(lo_covers_by(u, C), 0)) ||
+                      (!lo_covers(u, c) && lo_udist(u, c) <= lo_or(lo_udist(u, C), INT64_MAX));
+            if (!adv) break;
+            C = c;
+            cache_push(&cache, &R[rpos++]);
+        }
+        /* pruneCache */
+        int64_t index = -1;
+        for (int64_t k = cache.head; k < cache.tail; ++k) {
+            const lo_region *c = cache.v[k];
+            int prune;
+            if (c->contig != u->contig)
+                prune = 1;
+            else {
+                prune = lo_udist(u, c) > lo_or(lo_udist(u, C), 0);
+                if (mode == LO_CLOSEST_SINGLE)
+                    prune = prune || (lo_covers(u, c) &&
+                                      lo_covers_by(u, c) < lo_or(lo_covers_by(u, C), INT64_MAX));
+            }
+            if (!prune) {
+                index = k - cache.head;
+                break;
+            }
+        }
+        if (index > 0) cache.head += index;
+        /* processHits */
+        int64_t target = lo_or(lo_udist(u, C), INT64_MAX);
+        for (int64_t k = cache.head; k < cache.tail; ++k) {
+            const lo_region *r = cache.v[k];
+            int64_t d = lo_udist(u, r);
+            if (d != LO_NONE && d == target)
+                lo_emit(&out, u->contig, u->start, u->end, u->row, r->row);
         }
     }
     free(cache.v);

@@ -43,6 +43,9 @@ def lib():
                                               P(i64)]
         L.lo_window.restype = i64
         L.lo_window.argtypes = pair_args + [i64, P(i32), P(i64), P(i64), P(i64), P(i64)]
+        L.lo_closest.restype = i64
+        L.lo_closest.argtypes = pair_args[:-1] + [C.c_int, i64, P(i32), P(i64), P(i64),
+                                                  P(i64), P(i64)]
         L.lo_merge.restype = i64
         L.lo_merge.argtypes = [i64, P(i32), P(i64), P(i64), P(i8), i64, P(i32), P(i64), P(i64),
                                P(i8), P(i64)]
@@ -103,6 +106,24 @@ def window(a, b, distance=1000):
     n = L.lo_window(*args, 0, None, None, None, None, None)
     o = _out(n)
     L.lo_window(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))])
+    return _result(o)
+
+
+CLOSEST, CLOSEST_SINGLE = 0, 1
+
+
+def closest(a, b, mode=CLOSEST):
+    """Closest.scala's SingleClosest (mode 0) / SingleClosestSingleOverlap
+    (mode 1) over the sweep, restated (lo_closest): records carry a's own
+    region; reference emission order."""
+    L = lib()
+    na, ac, as_, ae, ast = _in(*a)
+    nb, bc, bs, be, bst = _in(*b)
+    args = [na, _p(ac, i32), _p(as_, i64), _p(ae, i64), _p(ast, i8), nb, _p(bc, i32),
+            _p(bs, i64), _p(be, i64), _p(bst, i8), int(mode)]
+    n = L.lo_closest(*args, 0, None, None, None, None, None)
+    o = _out(n)
+    L.lo_closest(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))])
     return _result(o)
 
 

@@ -31,6 +31,10 @@ def main():
         "merge_count": 1,
         # WindowSuite.scala:22-31: (left, right) region pairs, bedtools window
         "window": [r for r in zip(*[iter(regions("WindowSuite.scala"))] * 2)],
+        # ClosestSuite.scala:21-45 (SingleClosest) then :64-85
+        # (SingleClosestSingleOverlap): (left, right) region pairs
+        "closest": [r for r in zip(*[iter(regions("ClosestSuite.scala")[:48])] * 2)],
+        "closest_single_overlap": [r for r in zip(*[iter(regions("ClosestSuite.scala")[48:])] * 2)],
         # full truth for intersect_with_overlap_00 x _01 (left sorted order,
         # then right order), derived by hand from the fixture rows
         "intersection_full": [

@@ -22,7 +22,8 @@ def g(name):
 def test_usage_and_version():
     r = run()
     assert r.returncode == 0 and "Choose one of the following commands" in r.stdout
-    for cmd in ("complement", "intersect", "merge", "subtract", "sort", "window", "cluster"):
+    for cmd in ("complement", "intersect", "merge", "subtract", "sort", "window", "cluster",
+                "closest"):
         assert cmd in r.stdout
     r = run("-version")
     assert r.returncode == 0 and r.stdout.startswith("Version 0")
@@ -86,3 +87,15 @@ def test_cli_cluster():
     out = lines(run("cluster", g("cpg_20merge.bed")))
     assert len(out) == 1 and out[0][3] == "20"
     assert out[0][:3] == ["chr1", "28735", "29810"]
+
+
+@pytest.mark.gpu
+def test_cli_closest():
+    # ClosestSuite.scala:8-49 through the CLI (cli/Closest.scala: SingleClosest
+    # on stranded keys; the fixtures carry no strand): all 24 pairs in order
+    out = lines(run("closest", g("intersect_with_overlap_00.bed"),
+                    g("intersect_with_overlap_01.bed")))
+    right = {n: [c, int(s), int(e)] for c, s, e, n in
+             (ln.rstrip("\n").split("\t")[:4] for ln in open(g("intersect_with_overlap_01.bed")))}
+    got = [[[c, int(s), int(e)], right[r]] for c, s, e, _, r in out]
+    assert got == [list(map(list, p)) for p in expected()["closest"]]

@@ -58,6 +58,7 @@ namespace {
 constexpr int CB = 256;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int OCAP = 4096;  // contig offsets staged in LDS
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int contig_of(const uint32_t *off, int32_t nc, uint32_t g) {
     int lo = 0, hi = nc;  // largest c with off[c] <= g
@@ -308,63 +309,89 @@ __global__ __launch_bounds__(CB) void k_prune_round(Lefts L, Rights R, State s,
     if (nv != cur) atomicOr(changed, 1u);
 }
 
-// output count per left: k in [p, j) with dist == D
-__global__ __launch_bounds__(CB) void k_count(Lefts L, Rights R, const uint32_t *__restrict__ jp,
-                                              const uint32_t *__restrict__ pp,
-                                              const uint32_t *__restrict__ dd,
-                                              uint64_t *__restrict__ cnt) {
-    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
-    if (i >= L.n) return;
-    const uint32_t D = dd[i];
-    uint64_t m = 0;
-    if (D != NONE) {
-        const uint32_t ls = L.gs[i], le = L.ge[i];
-        for (int64_t k = pp[i], j = jp[i]; k < j; ++k) m += udist(ls, le, R.gs[k], R.ge[k]) == D;
-    }
-    cnt[i] = m;
-}
+// Output pass, one wave per 64 consecutive lefts: for each left of the group
+// in turn the wave tests 64 candidates of [p, j) at once (coalesced loads of
+// the right rows), so matches come out as contiguous runs -- counted
+// (SCAN_COUNT), written as 16-B records at their output offsets (SCAN_FILL,
+// only those inside [first, first + count)) or hashed (SCAN_SUM).
+enum { SCAN_COUNT = 0, SCAN_FILL = 1, SCAN_SUM = 2 };
 
-// records [first, first + count) of the output order, or their checksum
-template <bool CKSUM>
-__global__ __launch_bounds__(CB) void k_emit(Lefts L, Rights R, const uint32_t *__restrict__ jp,
+template <int MODE>
+__global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, const uint32_t *__restrict__ jp,
                                              const uint32_t *__restrict__ pp,
                                              const uint32_t *__restrict__ dd,
                                              const uint64_t *__restrict__ off, int64_t first,
-                                             int64_t count, lime_pair *__restrict__ out,
+                                             int64_t count, uint64_t *__restrict__ cnt,
+                                             lime_pair *__restrict__ out,
                                              unsigned long long *__restrict__ ck) {
     __shared__ uint32_t s_off[OCAP];
     if (L.nc + 1 <= OCAP)
         for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
     __syncthreads();
     const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
-    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
-    uint64_t hs = 0, hx = 0;
-    if (i < L.n && dd[i] != NONE) {
-        const uint32_t D = dd[i];
-        int64_t pos = (int64_t)off[i];
-        const int64_t end = (int64_t)off[i + 1];
-        if (CKSUM || (end > first && pos < first + count)) {
-            const uint32_t ls = L.gs[i], le = L.ge[i];
+    const int lane = dev::lane_id();
+    const int64_t i = ((int64_t)blockIdx.x * (CB / 64) + threadIdx.x / 64) * 64 + lane;
+    uint32_t ls = 0, le = 0, D = NONE, p = 0, j = 0, s0 = 0, e0 = 0, ar = 0;
+    uint64_t pos0 = 0;
+    bool valid = i < L.n && dd[i] != NONE;
+    if (valid) {
+        ls = L.gs[i];
+        le = L.ge[i];
+        D = dd[i];
+        p = pp[i];
+        j = jp[i];
+        if (MODE != SCAN_COUNT) {
             const int c = contig_of(o, L.nc, ls);
-            const uint32_t s0 = ls - o[c], e0 = le - o[c], ar = L.row[i];
-            for (int64_t k = pp[i], j = jp[i]; k < j && pos < end; ++k) {
-                if (udist(ls, le, R.gs[k], R.ge[k]) != D) continue;
-                if (CKSUM) {
-                    const uint64_t h = dev::pair_hash(s0, e0, ar, R.row[k]);
-                    hs += h;
-                    hx ^= h;
-                } else if (pos >= first && pos < first + count) {
-                    out[pos - first] = lime_pair{s0, e0, ar, R.row[k]};
-                }
-                ++pos;
-            }
+            s0 = ls - o[c];
+            e0 = le - o[c];
+            ar = L.row[i];
+            pos0 = off[i];
+            if (MODE == SCAN_FILL)
+                valid = off[i + 1] > (uint64_t)first && pos0 < (uint64_t)(first + count);
         }
     }
-    if (CKSUM) {
+    uint64_t mine = 0, hs = 0, hx = 0;
+    const uint64_t below = dev::lanemask_lt();
+    for (uint64_t todo = __ballot(valid); todo; todo &= todo - 1) {
+        const int l = __builtin_ctzll(todo);
+        const uint32_t bls = __shfl(ls, l), ble = __shfl(le, l), bD = __shfl(D, l);
+        const uint32_t bj = __shfl(j, l);
+        uint32_t bs0 = 0, be0 = 0, bar = 0;
+        uint64_t pos = 0;
+        if (MODE != SCAN_COUNT) {
+            bs0 = __shfl(s0, l);
+            be0 = __shfl(e0, l);
+            bar = __shfl(ar, l);
+            pos = __shfl(pos0, l);
+        }
+        uint64_t total = 0;
+        for (int64_t k0 = __shfl(p, l); k0 < (int64_t)bj; k0 += 64) {
+            const int64_t k = k0 + lane;
+            const bool m = k < (int64_t)bj && udist(bls, ble, R.gs[k], R.ge[k]) == bD;
+            const uint64_t bm = __ballot(m);
+            if (MODE == SCAN_FILL && m) {
+                const int64_t idx = (int64_t)(pos + __popcll(bm & below)) - first;
+                if (idx >= 0 && idx < count) {
+                    u32x4 v = {bs0, be0, bar, R.row[k]};
+                    *reinterpret_cast<u32x4 *>(out + idx) = v;
+                }
+            }
+            if (MODE == SCAN_SUM && m) {
+                const uint64_t h = dev::pair_hash(bs0, be0, bar, R.row[k]);
+                hs += h;
+                hx ^= h;
+            }
+            pos += __popcll(bm);
+            total += __popcll(bm);
+        }
+        if (lane == l) mine = total;
+    }
+    if (MODE == SCAN_COUNT && i < L.n) cnt[i] = valid ? mine : 0;
+    if (MODE == SCAN_SUM) {
         hs = dev::wave_reduce_sum(hs);
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) hx ^= __shfl_xor(hx, d, 64);
-        if (dev::lane_id() == 0) {
+        if (lane == 0) {
             atomicAdd(&ck[0], (unsigned long long)hs);
             atomicXor(&ck[1], (unsigned long long)hx);
         }
@@ -532,8 +559,10 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     uint64_t *cnt, *tot;
     CL_TRY(alloc(ctx, &cnt, (size_t)nl));
     CL_TRY(alloc(ctx, &tot, 1));
-    hipLaunchKernelGGL(k_count, dim3(gl), dim3(CB), 0, S(ctx), L, R, (const uint32_t *)pl->jp,
-                       (const uint32_t *)pl->pp, (const uint32_t *)pl->dd, cnt);
+    hipLaunchKernelGGL(k_scan<SCAN_COUNT>, dim3(gl), dim3(CB), 0, S(ctx), L, R,
+                       (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+                       (const uint32_t *)pl->dd, (const uint64_t *)nullptr, (int64_t)0,
+                       (int64_t)0, cnt, (lime_pair *)nullptr, (unsigned long long *)nullptr);
     LIME_HIP(hipGetLastError());
     CL_TRY(scan_exclusive_u64(ctx, cnt, pl->off, nl, tot));
     LIME_HIP(hipMemcpyAsync(pl->off + nl, tot, sizeof(uint64_t), hipMemcpyDeviceToDevice,
@@ -558,10 +587,10 @@ int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out
     const lime_set *A = pl->A, *B = pl->B;
     Rights R{B->gs, B->ge, B->row, B->pmax, nullptr, nullptr, nullptr, nullptr, nullptr, B->n};
     Lefts L{A->gs, A->ge, A->row, pl->nl, A->d_off, A->n_contigs, pl->rb};
-    hipLaunchKernelGGL(k_emit<false>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0, S(ctx), L, R,
-                       (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
-                       (const uint32_t *)pl->dd, (const uint64_t *)pl->off, first, count, d_out,
-                       nullptr);
+    hipLaunchKernelGGL(k_scan<SCAN_FILL>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0, S(ctx), L,
+                       R, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+                       (const uint32_t *)pl->dd, (const uint64_t *)pl->off, first, count,
+                       (uint64_t *)nullptr, d_out, (unsigned long long *)nullptr);
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
@@ -576,10 +605,10 @@ int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr) {
         Rights R{B->gs, B->ge, B->row, B->pmax, nullptr, nullptr, nullptr, nullptr, nullptr,
                  B->n};
         Lefts L{A->gs, A->ge, A->row, pl->nl, A->d_off, A->n_contigs, pl->rb};
-        hipLaunchKernelGGL(k_emit<true>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0, S(ctx), L,
-                           R, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+        hipLaunchKernelGGL(k_scan<SCAN_SUM>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0,
+                           S(ctx), L, R, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
                            (const uint32_t *)pl->dd, (const uint64_t *)pl->off, (int64_t)0,
-                           pl->total, (lime_pair *)nullptr, ck);
+                           pl->total, (uint64_t *)nullptr, (lime_pair *)nullptr, ck);
         LIME_HIP(hipGetLastError());
     }
     unsigned long long h[2];

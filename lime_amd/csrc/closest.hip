@@ -40,6 +40,9 @@
 
 namespace lime {
 
+int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const uint32_t *d_ge,
+                    const uint32_t *d_row, const uint32_t *d_len);
+
 struct ClosestPlan {
     lime_ctx *ctx = nullptr;
     const lime_set *A = nullptr, *B = nullptr;
@@ -49,6 +52,9 @@ struct ClosestPlan {
     uint32_t *dd = nullptr;    // per left: D (0xffffffff: no output)
     uint64_t *off = nullptr;   // per left: exclusive output offsets
     uint32_t *rb = nullptr;    // n_contigs + 1 right contig bounds
+    uint32_t *aa = nullptr;    // per left: A, the first right starting at or after its end
+    uint32_t *eg = nullptr;    // the rights' ends, ascending (end index) ...
+    uint32_t *ek = nullptr;    // ... and the right index of each, ascending among equal ends
     int64_t total = 0;
     int rounds = 0;            // cache-head rounds until the fixed point
 };
@@ -128,6 +134,11 @@ __global__ __launch_bounds__(CB) void k_bounds(const uint32_t *__restrict__ gs, 
     const int c = blockIdx.x * CB + threadIdx.x;
     if (c > nc) return;
     rb[c] = (uint32_t)dev::lower_bound(gs, 0, n, off[c]);
+}
+
+__global__ __launch_bounds__(CB) void k_iota(uint32_t *__restrict__ v, int64_t n) {
+    const int64_t k = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (k < n) v[k] = (uint32_t)k;
 }
 
 // U at the last left of each contig with lefts
@@ -309,15 +320,29 @@ __global__ __launch_bounds__(CB) void k_prune_round(Lefts L, Rights R, State s,
     if (nv != cur) atomicOr(changed, 1u);
 }
 
-// Output pass, one wave per 64 consecutive lefts: for each left of the group
-// in turn the wave tests 64 candidates of [p, j) at once (coalesced loads of
-// the right rows), so matches come out as contiguous runs -- counted
-// (SCAN_COUNT), written as 16-B records at their output offsets (SCAN_FILL,
-// only those inside [first, first + count)) or hashed (SCAN_SUM).
+// Output pass.  A match is k in [p, j) with dist(L, R[k]) == D.
+//  D > 0: below A that means R[k].end == L.start + 1 - D exactly, above A
+//    R[k].start == L.end + D - 1 exactly: one run of the end index (rights by
+//    end, index ascending) and one run of the starts, each cut to its index
+//    range by binary search -- no scan.  Before-side matches (k < A) precede
+//    after-side ones, so index order is kept.
+//  D == 0 (L covered by the current closest): the covering rights of
+//    [p, min(A, j)); one wave per 64 consecutive lefts tests 64 candidates at
+//    once (coalesced loads), so matches come out as contiguous runs.
+// Matches are counted (SCAN_COUNT), written as 16-B records at their output
+// offsets (SCAN_FILL, only those inside [first, first + count)) or hashed
+// (SCAN_SUM).
 enum { SCAN_COUNT = 0, SCAN_FILL = 1, SCAN_SUM = 2 };
 
+struct EndIndex {
+    const uint32_t *eg, *ek;  // ends ascending, right index ascending among equal ends
+    const uint32_t *aa;       // per left A
+    int64_t n;
+};
+
 template <int MODE>
-__global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, const uint32_t *__restrict__ jp,
+__global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, EndIndex E,
+                                             const uint32_t *__restrict__ jp,
                                              const uint32_t *__restrict__ pp,
                                              const uint32_t *__restrict__ dd,
                                              const uint64_t *__restrict__ off, int64_t first,
@@ -351,11 +376,46 @@ __global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, const uint32_t *
         }
     }
     uint64_t mine = 0, hs = 0, hx = 0;
+    uint32_t a = 0;
+    if (valid) a = E.aa[i];
+    if (valid && D > 0) {
+        // before-side run: rights ending exactly at T with index in [p, min(A, j))
+        uint64_t pos = pos0;
+        auto emit = [&](int64_t k) {
+            if (MODE == SCAN_FILL && (int64_t)pos >= first && (int64_t)pos < first + count) {
+                u32x4 v = {s0, e0, ar, R.row[k]};
+                *reinterpret_cast<u32x4 *>(out + (pos - first)) = v;
+            }
+            if (MODE == SCAN_SUM) {
+                const uint64_t h = dev::pair_hash(s0, e0, ar, R.row[k]);
+                hs += h;
+                hx ^= h;
+            }
+            ++pos;
+            ++mine;
+        };
+        const int64_t T = (int64_t)ls + 1 - (int64_t)D;
+        const int64_t hb = min((int64_t)a, (int64_t)j);
+        if (T >= 0 && (int64_t)p < hb) {
+            const int64_t e0r = dev::lower_bound(E.eg, 0, E.n, (uint64_t)T);
+            const int64_t e1r = dev::upper_bound(E.eg, e0r, E.n, (uint64_t)T);
+            for (int64_t e = dev::lower_bound(E.ek, e0r, e1r, p); e < e1r && (int64_t)E.ek[e] < hb;
+                 ++e)
+                emit(E.ek[e]);
+        }
+        // after-side run: rights starting exactly at V with index in [max(p, A), j)
+        const int64_t V = (int64_t)le + (int64_t)D - 1;
+        const int64_t lo = max((int64_t)p, (int64_t)a);
+        if (V <= (int64_t)NONE && lo < (int64_t)j)
+            for (int64_t k = dev::lower_bound(R.gs, lo, (int64_t)j, (uint64_t)V);
+                 k < (int64_t)j && R.gs[k] == (uint32_t)V; ++k)
+                emit(k);
+    }
     const uint64_t below = dev::lanemask_lt();
-    for (uint64_t todo = __ballot(valid); todo; todo &= todo - 1) {
+    for (uint64_t todo = __ballot(valid && D == 0); todo; todo &= todo - 1) {
         const int l = __builtin_ctzll(todo);
         const uint32_t bls = __shfl(ls, l), ble = __shfl(le, l), bD = __shfl(D, l);
-        const uint32_t bj = __shfl(j, l);
+        const uint32_t bj = min(__shfl(j, l), __shfl(a, l));  // covering rights lie below A
         uint32_t bs0 = 0, be0 = 0, bar = 0;
         uint64_t pos = 0;
         if (MODE != SCAN_COUNT) {
@@ -408,6 +468,9 @@ void closest_free(ClosestPlan *pl) {
     release(ctx, pl->dd);
     release(ctx, pl->off);
     release(ctx, pl->rb);
+    release(ctx, pl->aa);
+    release(ctx, pl->eg);
+    release(ctx, pl->ek);
     delete pl;
 }
 
@@ -534,6 +597,30 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
         LIME_HIP(hipMemcpyAsync(live, lv.data(), (size_t)nc, hipMemcpyHostToDevice, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));
     }
+    pl->aa = Aa;
+    // end index for the exact-distance lookups of the output pass
+    CL_TRY(alloc(ctx, &pl->eg, (size_t)std::max<int64_t>(nr, 1)));
+    CL_TRY(alloc(ctx, &pl->ek, (size_t)std::max<int64_t>(nr, 1)));
+    if (nr > 0) {
+        uint32_t *idx;
+        CL_TRY(alloc(ctx, &idx, (size_t)nr));
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for(nr, CB)), dim3(CB), 0, S(ctx), idx, nr);
+        LIME_HIP(hipGetLastError());
+        lime_set es;  // (ge, ge, k) sorted by ge; ties keep k ascending
+        es.ctx = ctx;
+        es.n = nr;
+        es.d_off = B->d_off;
+        es.n_contigs = nc;
+        es.off = B->off;
+        es.len = B->len;
+        CL_TRY(sort_set_global(ctx, &es, B->ge, B->ge, idx, nullptr));
+        release(ctx, pl->eg);
+        release(ctx, pl->ek);
+        pl->eg = es.gs;
+        pl->ek = es.row;
+        release(ctx, es.ge);
+        release(ctx, idx);
+    }
     State s{Aa, U, stuck, live};
     hipLaunchKernelGGL(k_fresh, dim3(gl), dim3(CB), 0, S(ctx), L, R, s, pl->jp, pl->dd, P);
     LIME_HIP(hipGetLastError());
@@ -559,7 +646,8 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     uint64_t *cnt, *tot;
     CL_TRY(alloc(ctx, &cnt, (size_t)nl));
     CL_TRY(alloc(ctx, &tot, 1));
-    hipLaunchKernelGGL(k_scan<SCAN_COUNT>, dim3(gl), dim3(CB), 0, S(ctx), L, R,
+    const EndIndex E{pl->eg, pl->ek, pl->aa, nr};
+    hipLaunchKernelGGL(k_scan<SCAN_COUNT>, dim3(gl), dim3(CB), 0, S(ctx), L, R, E,
                        (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
                        (const uint32_t *)pl->dd, (const uint64_t *)nullptr, (int64_t)0,
                        (int64_t)0, cnt, (lime_pair *)nullptr, (unsigned long long *)nullptr);
@@ -571,7 +659,7 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     LIME_TRY(read_back(ctx, &total, tot, sizeof(total)));
     pl->total = (int64_t)total;
     for (void *q : {(void *)jag, (void *)jmin1, (void *)jmin2, (void *)gmax1, (void *)gmax2,
-                    (void *)Aa, (void *)Nn, (void *)U, (void *)P, (void *)p2, (void *)stuck,
+                    (void *)Nn, (void *)U, (void *)P, (void *)p2, (void *)stuck,
                     (void *)live, (void *)changed, (void *)cnt, (void *)tot})
         ctx->pool.put(q);
 #undef CL_TRY
@@ -587,8 +675,9 @@ int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out
     const lime_set *A = pl->A, *B = pl->B;
     Rights R{B->gs, B->ge, B->row, B->pmax, nullptr, nullptr, nullptr, nullptr, nullptr, B->n};
     Lefts L{A->gs, A->ge, A->row, pl->nl, A->d_off, A->n_contigs, pl->rb};
+    const EndIndex E{pl->eg, pl->ek, pl->aa, B->n};
     hipLaunchKernelGGL(k_scan<SCAN_FILL>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0, S(ctx), L,
-                       R, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+                       R, E, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
                        (const uint32_t *)pl->dd, (const uint64_t *)pl->off, first, count,
                        (uint64_t *)nullptr, d_out, (unsigned long long *)nullptr);
     LIME_HIP(hipGetLastError());
@@ -605,8 +694,9 @@ int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr) {
         Rights R{B->gs, B->ge, B->row, B->pmax, nullptr, nullptr, nullptr, nullptr, nullptr,
                  B->n};
         Lefts L{A->gs, A->ge, A->row, pl->nl, A->d_off, A->n_contigs, pl->rb};
+        const EndIndex E{pl->eg, pl->ek, pl->aa, B->n};
         hipLaunchKernelGGL(k_scan<SCAN_SUM>, dim3(blocks_for(pl->nl, CB)), dim3(CB), 0,
-                           S(ctx), L, R, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
+                           S(ctx), L, R, E, (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
                            (const uint32_t *)pl->dd, (const uint64_t *)pl->off, (int64_t)0,
                            pl->total, (uint64_t *)nullptr, (lime_pair *)nullptr, ck);
         LIME_HIP(hipGetLastError());

@@ -623,7 +623,8 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             const int wbits = h.max_width ? 32 - __builtin_clz(h.max_width) : 0;
             if (!set->strand_uniform) passes.push_back({M_ST, 0});
             for (int sh = 0; sh < wbits; sh += 8) passes.push_back({M_GE, sh});
-        } else if (set->has_zero_width && set->min_shift == 0) {
+        } else if (set->has_zero_width && set->max_width > 0 && set->min_shift == 0) {
+            // (all rows zero-width: the bit is constant, no pass)
             passes.push_back({M_NZ, 0});
         }
         for (int sh = 0; sh < bits; sh += 8)

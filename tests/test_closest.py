@@ -326,3 +326,26 @@ def test_gpu_device_stranded_sets(ctx):
     p = plan.fill_host()
     assert p["a_row"].tolist() == exp["a_row"].tolist()
     assert p["b_row"].tolist() == exp["b_row"].tolist()
+
+
+@pytest.mark.gpu
+def test_gpu_c2_density(ctx):
+    # C2's density (depth ~82, len U[50,5000]) on hg38/100 with 2 x 1e6 rows:
+    # count and order-free checksum of ~2.5e7 records == oracle
+    from lime_amd import Space, synth
+    lens = np.array(list(synth.HG38.values())) // 100
+    sp = Space(list(synth.HG38.keys()), lens.tolist())
+    A = synth.uniform(lens, 1_000_000, 0xA, 50, 5000)
+    B = synth.uniform(lens, 1_000_000, 0xB, 50, 5000)
+    # synth indexes contigs in HG38 order; the space numbers them in Java
+    # String order, which both sides must share (it orders the sweep)
+    m = np.array([sp.index[nm] for nm in synth.HG38], np.int32)
+    A = (m[A[0]], np.asarray(A[1], np.int64), np.asarray(A[2], np.int64))
+    B = (m[B[0]], np.asarray(B[1], np.int64), np.asarray(B[2], np.int64))
+    z = np.zeros(1_000_000, np.int8)
+    a = ctx.set_from_host_stranded(sp, *A, z)
+    b = ctx.set_from_host_stranded(sp, *B, z)
+    plan = ctx.closest(a, b)
+    exp = oracle.closest((*A, z), (*B, z))
+    assert plan.n == len(exp["start"]) > 1_000_000
+    assert plan.checksum() == oracle.checksum_pairs(exp)

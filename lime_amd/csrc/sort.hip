@@ -95,19 +95,6 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t ntiles) {
     return x * q + (x < r ? x : r) + i;
 }
 
-// per-wave digit histogram of this wave's rows into hist[w][*]
-template <int M>
-__device__ __forceinline__ void wave_hist(uint32_t (*hist)[RBINS], int w, const uint32_t *vk,
-                                          const uint32_t *ve, const uint32_t *vr,
-                                          const bool *valid, int shift, const int8_t *st) {
-#pragma unroll
-    for (int k = 0; k < RITEMS; ++k) {
-        uint32_t d = digit_of<M>(vk[k], ve[k], vr[k], shift, st);
-        uint64_t m = match_digit<M>(d, valid[k]);
-        if (valid[k] && (m & dev::lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
-    }
-}
-
 __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *counts,
                                            uint32_t ntiles) {
     for (int d = threadIdx.x; d < RBINS; d += RB) {
@@ -273,7 +260,9 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     }
     }
     __syncthreads();
-    wave_hist<M_GS>(hist, w, vk, ve, vk, valid, 0, nullptr);
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (valid[k]) atomicAdd(&hist[w][vk[k] & (RBINS - 1)], 1u);
     err = dev::wave_reduce_or(err);
     mx = dev::wave_reduce_max(mx);
     mnw = dev::wave_reduce_min(mnw);
@@ -380,7 +369,11 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
         }
     }
     __syncthreads();
-    wave_hist<M>(hist, w, vk, ve, vr, valid, shift, st);
+    // LDS atomics, not the scatter's 8 ballots per row: a histogram needs no
+    // ranks (190 -> 104 us per 1e8-row pass)
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (valid[k]) atomicAdd(&hist[w][digit_of<M>(vk[k], ve[k], vr[k], shift, st)], 1u);
     __syncthreads();
     flush_hist(hist, counts, ntiles);
 }

@@ -477,25 +477,28 @@ void closest_free(ClosestPlan *pl) {
 int64_t closest_total(const ClosestPlan *pl) { return pl->total; }
 int closest_rounds(const ClosestPlan *pl) { return pl->rounds; }
 
-int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan **out) {
+namespace {
+
+// Scratch buffers of one plan build, returned to the pool however it ends.
+struct Scratch {
+    lime_ctx *ctx;
+    std::vector<void *> held;
+    template <typename T>
+    int get(T **p, size_t n) {
+        LIME_TRY(alloc(ctx, p, n));
+        held.push_back(*p);
+        return LIME_OK;
+    }
+    ~Scratch() {
+        for (void *q : held) ctx->pool.put(q);
+    }
+};
+
+int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan *pl) {
     const int64_t nl = A->n, nr = B->n;
     const int32_t nc = A->n_contigs;
-    if (nl >= (int64_t)NONE || nr >= (int64_t)NONE)
-        return fail(LIME_ERR_RANGE, "closest supports fewer than 2^32 - 1 rows per set");
-    ClosestPlan *pl = new ClosestPlan();
-    pl->ctx = ctx;
-    pl->A = A;
-    pl->B = B;
-    pl->nl = nl;
-    auto bail = [&](int rc) {
-        closest_free(pl);
-        return rc;
-    };
-    int rc;
-#define CL_TRY(x)                    \
-    if ((rc = (x)) != LIME_OK) {     \
-        return bail(rc);             \
-    }
+    Scratch sc{ctx, {}};
+#define CL_TRY LIME_TRY
     CL_TRY(alloc(ctx, &pl->rb, (size_t)nc + 1));
     CL_TRY(alloc(ctx, &pl->jp, (size_t)std::max<int64_t>(nl, 1)));
     CL_TRY(alloc(ctx, &pl->pp, (size_t)std::max<int64_t>(nl, 1)));
@@ -503,7 +506,6 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     CL_TRY(alloc(ctx, &pl->off, (size_t)nl + 1));
     if (nl == 0) {
         LIME_HIP(hipMemsetAsync(pl->off, 0, sizeof(uint64_t), S(ctx)));
-        *out = pl;
         return LIME_OK;
     }
     hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), B->gs, nr,
@@ -513,11 +515,11 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     // right-side search levels
     const int64_t m1 = (nr + 63) / 64, m2 = (m1 + 63) / 64;
     uint32_t *jag, *jmin1, *jmin2, *gmax1, *gmax2;
-    CL_TRY(alloc(ctx, &jag, (size_t)std::max<int64_t>(nr, 1)));
-    CL_TRY(alloc(ctx, &jmin1, (size_t)std::max<int64_t>(m1, 1)));
-    CL_TRY(alloc(ctx, &jmin2, (size_t)std::max<int64_t>(m2, 1)));
-    CL_TRY(alloc(ctx, &gmax1, (size_t)std::max<int64_t>(m1, 1)));
-    CL_TRY(alloc(ctx, &gmax2, (size_t)std::max<int64_t>(m2, 1)));
+    CL_TRY(sc.get(&jag, (size_t)std::max<int64_t>(nr, 1)));
+    CL_TRY(sc.get(&jmin1, (size_t)std::max<int64_t>(m1, 1)));
+    CL_TRY(sc.get(&jmin2, (size_t)std::max<int64_t>(m2, 1)));
+    CL_TRY(sc.get(&gmax1, (size_t)std::max<int64_t>(m1, 1)));
+    CL_TRY(sc.get(&gmax2, (size_t)std::max<int64_t>(m2, 1)));
     if (nr > 0) {
         hipLaunchKernelGGL(k_jags, dim3(blocks_for(nr, CB)), dim3(CB), 0, S(ctx), B->gs, B->ge,
                            nr, B->d_off, nc, jag);
@@ -538,14 +540,15 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     unsigned long long *stuck;
     uint8_t *live;
     unsigned int *changed;
-    CL_TRY(alloc(ctx, &Aa, (size_t)nl));
-    CL_TRY(alloc(ctx, &Nn, (size_t)nl));
-    CL_TRY(alloc(ctx, &U, (size_t)nl));
-    CL_TRY(alloc(ctx, &P, (size_t)nl));
-    CL_TRY(alloc(ctx, &p2, (size_t)nl));
-    CL_TRY(alloc(ctx, &stuck, (size_t)nc));
-    CL_TRY(alloc(ctx, &live, (size_t)nc));
-    CL_TRY(alloc(ctx, &changed, 1));
+    CL_TRY(alloc(ctx, &pl->aa, (size_t)nl));
+    Aa = pl->aa;
+    CL_TRY(sc.get(&Nn, (size_t)nl));
+    CL_TRY(sc.get(&U, (size_t)nl));
+    CL_TRY(sc.get(&P, (size_t)nl));
+    CL_TRY(sc.get(&p2, (size_t)nl));
+    CL_TRY(sc.get(&stuck, (size_t)nc));
+    CL_TRY(sc.get(&live, (size_t)nc));
+    CL_TRY(sc.get(&changed, 1));
     const unsigned gl = blocks_for(nl, CB);
     hipLaunchKernelGGL(k_stops, dim3(gl), dim3(CB), 0, S(ctx), L, R, Aa, Nn);
     LIME_HIP(hipGetLastError());
@@ -559,8 +562,8 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     // rights lie on the contigs in between
     {
         uint32_t *lbd, *lastU;
-        CL_TRY(alloc(ctx, &lbd, (size_t)nc + 1));
-        CL_TRY(alloc(ctx, &lastU, (size_t)nc));
+        CL_TRY(sc.get(&lbd, (size_t)nc + 1));
+        CL_TRY(sc.get(&lastU, (size_t)nc));
         hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), A->gs,
                            nl, A->d_off, nc, lbd);
         hipLaunchKernelGGL(k_last, dim3(blocks_for(nc, CB)), dim3(CB), 0, S(ctx),
@@ -572,8 +575,6 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
         CL_TRY(read_back(ctx, lb.data(), lbd, sizeof(uint32_t) * (nc + 1)));
         CL_TRY(read_back(ctx, lu.data(), lastU, sizeof(uint32_t) * nc));
         CL_TRY(read_back(ctx, st.data(), stuck, sizeof(unsigned long long) * nc));
-        release(ctx, lbd);
-        release(ctx, lastU);
         std::vector<uint8_t> lv(nc, 0);
         bool alive = true, first = true;
         for (int32_t c = 0; c < nc; ++c) {
@@ -597,13 +598,12 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
         LIME_HIP(hipMemcpyAsync(live, lv.data(), (size_t)nc, hipMemcpyHostToDevice, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));
     }
-    pl->aa = Aa;
     // end index for the exact-distance lookups of the output pass
     CL_TRY(alloc(ctx, &pl->eg, (size_t)std::max<int64_t>(nr, 1)));
     CL_TRY(alloc(ctx, &pl->ek, (size_t)std::max<int64_t>(nr, 1)));
     if (nr > 0) {
         uint32_t *idx;
-        CL_TRY(alloc(ctx, &idx, (size_t)nr));
+        CL_TRY(sc.get(&idx, (size_t)nr));
         hipLaunchKernelGGL(k_iota, dim3(blocks_for(nr, CB)), dim3(CB), 0, S(ctx), idx, nr);
         LIME_HIP(hipGetLastError());
         lime_set es;  // (ge, ge, k) sorted by ge; ties keep k ascending
@@ -619,7 +619,6 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
         pl->eg = es.gs;
         pl->ek = es.row;
         release(ctx, es.ge);
-        release(ctx, idx);
     }
     State s{Aa, U, stuck, live};
     hipLaunchKernelGGL(k_fresh, dim3(gl), dim3(CB), 0, S(ctx), L, R, s, pl->jp, pl->dd, P);
@@ -644,8 +643,8 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
                                 hipMemcpyDeviceToDevice, S(ctx)));
     // output counts and offsets
     uint64_t *cnt, *tot;
-    CL_TRY(alloc(ctx, &cnt, (size_t)nl));
-    CL_TRY(alloc(ctx, &tot, 1));
+    CL_TRY(sc.get(&cnt, (size_t)nl));
+    CL_TRY(sc.get(&tot, 1));
     const EndIndex E{pl->eg, pl->ek, pl->aa, nr};
     hipLaunchKernelGGL(k_scan<SCAN_COUNT>, dim3(gl), dim3(CB), 0, S(ctx), L, R, E,
                        (const uint32_t *)pl->jp, (const uint32_t *)pl->pp,
@@ -658,11 +657,25 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     uint64_t total = 0;
     LIME_TRY(read_back(ctx, &total, tot, sizeof(total)));
     pl->total = (int64_t)total;
-    for (void *q : {(void *)jag, (void *)jmin1, (void *)jmin2, (void *)gmax1, (void *)gmax2,
-                    (void *)Nn, (void *)U, (void *)P, (void *)p2, (void *)stuck,
-                    (void *)live, (void *)changed, (void *)cnt, (void *)tot})
-        ctx->pool.put(q);
 #undef CL_TRY
+    return LIME_OK;
+}
+
+}  // namespace
+
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan **out) {
+    if (A->n >= (int64_t)NONE || B->n >= (int64_t)NONE)
+        return fail(LIME_ERR_RANGE, "closest supports fewer than 2^32 - 1 rows per set");
+    ClosestPlan *pl = new ClosestPlan();
+    pl->ctx = ctx;
+    pl->A = A;
+    pl->B = B;
+    pl->nl = A->n;
+    const int rc = plan_body(ctx, A, B, pl);
+    if (rc != LIME_OK) {
+        closest_free(pl);
+        return rc;
+    }
     *out = pl;
     return LIME_OK;
 }

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                 if (g1 >= span) err |= 4u;
                 gs[i] = g0;
                 ge[i] = g1;
-                row[i] = end[i];
+                if (row) row[i] = end[i];
                 mx = g0 > mx ? g0 : mx;
                 const uint32_t wd = g1 - g0;
                 mnw = wd < mnw ? wd : mnw;
@@ -218,7 +218,9 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
             }
             g4[q] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
             h4[q] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
-            r4[q] = make_uint4((uint32_t)i0, (uint32_t)i0 + 1, (uint32_t)i0 + 2, (uint32_t)i0 + 3);
+            if (row)
+                r4[q] = make_uint4((uint32_t)i0, (uint32_t)i0 + 1, (uint32_t)i0 + 2,
+                                   (uint32_t)i0 + 3);
         }
 #pragma unroll
         for (int k = 0; k < RITEMS; ++k) valid[k] = true;
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
             }
             gs[i] = g0;
             ge[i] = g1;
-            row[i] = (uint32_t)i;
+            if (row) row[i] = (uint32_t)i;
             mx = g0 > mx ? g0 : mx;
             const uint32_t wd = g1 - g0;
             mnw = wd < mnw ? wd : mnw;
@@ -411,6 +413,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS], pd[RITEMS];
     // 32-bit offsets from per-wave base pointers keep address math scalar
     const int lim = (int)min((int64_t)WITEMS, n - base);  // valid rows of this wave
+    // row_in == nullptr (GS passes only): the set keeps no row ids
+    const bool rows = row_in != nullptr;
     const uint32_t *kin = key_in + base, *ein = ge_in + base, *rin = row_in + base;
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
@@ -418,7 +422,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         const bool valid = o < lim;
         vk[k] = valid ? kin[o] : 0u;
         ve[k] = valid ? ein[o] : 0u;
-        vr[k] = valid ? rin[o] : 0u;
+        vr[k] = valid && rows ? rin[o] : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -496,6 +500,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
         ge_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
     }
+    if (!rows) return;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
@@ -566,7 +571,10 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     SetStats *part, *st;
     LIME_TRY(alloc(ctx, &k0, (size_t)n));
     LIME_TRY(alloc(ctx, &e0, (size_t)n));
-    LIME_TRY(alloc(ctx, &r0, (size_t)n));
+    // binned sets (bitset painting) keep no row ids: 8 B per row per pass
+    const bool keep_rows = set->min_shift == 0;
+    r0 = nullptr;
+    if (keep_rows) LIME_TRY(alloc(ctx, &r0, (size_t)n));
     LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * (ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &st, 1));
@@ -604,10 +612,10 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     // (a binned set whose keys all share one bin needs no pass)
     if (n > 1 && (h.unsorted || stranded) &&
         !(set->min_shift > 0 && (h.max_gs >> set->min_shift) == 0)) {
-        uint32_t *k1, *e1, *r1;
+        uint32_t *k1, *e1, *r1 = nullptr;
         LIME_TRY(alloc(ctx, &k1, (size_t)n));
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
-        LIME_TRY(alloc(ctx, &r1, (size_t)n));
+        if (keep_rows) LIME_TRY(alloc(ctx, &r1, (size_t)n));
         const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
         std::vector<std::pair<int, int>> passes;  // (mode, shift), least significant first
         if (stranded) {

@@ -119,7 +119,8 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              int64_t n, uint32_t *__restrict__ gs,
                                              uint32_t *__restrict__ ge, uint32_t *__restrict__ row,
                                              SetStats *__restrict__ part,
-                                             uint32_t *__restrict__ counts, uint32_t ntiles) {
+                                             uint32_t *__restrict__ counts, uint32_t ntiles,
+                                             int hshift) {
     __shared__ uint32_t hist[RWAVES][RBINS];
     __shared__ SetStats ws[RWAVES];
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
-        if (valid[k]) atomicAdd(&hist[w][vk[k] & (RBINS - 1)], 1u);
+        if (valid[k]) atomicAdd(&hist[w][(vk[k] >> hshift) & (RBINS - 1)], 1u);
     err = dev::wave_reduce_or(err);
     mx = dev::wave_reduce_max(mx);
     mnw = dev::wave_reduce_min(mnw);
@@ -583,11 +584,11 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         if (global)
             hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start,
                                d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0,
-                               e0, r0, part, mat, ntiles);
+                               e0, r0, part, mat, ntiles, set->min_shift);
         else
             hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
                                d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, r0, part, mat, ntiles);
+                               set->n_contigs, n, k0, e0, r0, part, mat, ntiles, set->min_shift);
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());
@@ -630,8 +631,8 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         }
         for (int sh = 0; sh < bits; sh += 8)
             if (sh >= set->min_shift) passes.push_back({M_GS, sh});
-        // k_prep already histogrammed digit 0 of gs in the prep layout
-        bool have = passes.front().first == M_GS && passes.front().second == 0;
+        // k_prep already histogrammed the gs digit at min_shift
+        bool have = passes.front().first == M_GS && passes.front().second == set->min_shift;
         for (auto &p : passes) {
             LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
                                 e1, r1, mat, ntiles));

@@ -462,24 +462,40 @@ __global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, EndIndex E,
             pos = __shfl(pos0, l);
         }
         uint64_t total = 0;
-        for (int64_t k0 = __shfl(p, l); k0 < (int64_t)bj; k0 += 64) {
-            const int64_t k = k0 + lane;
-            const bool m = k < (int64_t)bj && udist(bls, ble, R.gs[k], R.ge[k]) == bD;
+        // software-pipelined: the next chunk's coordinates and payload rows
+        // are loaded while this chunk is tested and stored
+        int64_t k0 = __shfl(p, l);
+        uint32_t cs = 0, ce = 0, cr = 0;
+        auto fetch = [&](int64_t kk, uint32_t &fs, uint32_t &fe, uint32_t &fr) {
+            if (kk < (int64_t)bj) {
+                fs = R.gs[kk];
+                fe = R.ge[kk];
+                if (MODE != SCAN_COUNT) fr = R.row[kk];
+            }
+        };
+        fetch(k0 + lane, cs, ce, cr);
+        for (; k0 < (int64_t)bj; k0 += 64) {
+            uint32_t ns = 0, ne = 0, nr = 0;
+            fetch(k0 + 64 + lane, ns, ne, nr);
+            const bool m = k0 + lane < (int64_t)bj && udist(bls, ble, cs, ce) == bD;
             const uint64_t bm = __ballot(m);
             if (MODE == SCAN_FILL && m) {
                 const int64_t idx = (int64_t)(pos + __popcll(bm & below)) - first;
                 if (idx >= 0 && idx < count) {
-                    u32x4 v = {bs0, be0, bar, R.row[k]};
+                    u32x4 v = {bs0, be0, bar, cr};
                     *reinterpret_cast<u32x4 *>(out + idx) = v;
                 }
             }
             if (MODE == SCAN_SUM && m) {
-                const uint64_t h = dev::pair_hash(bs0, be0, bar, R.row[k]);
+                const uint64_t h = dev::pair_hash(bs0, be0, bar, cr);
                 hs += h;
                 hx ^= h;
             }
             pos += __popcll(bm);
             total += __popcll(bm);
+            cs = ns;
+            ce = ne;
+            cr = nr;
         }
         if (lane == l) mine = total;
     }

@@ -1,5 +1,5 @@
-"""Supplementary benchmark lines for BASELINE.json configs C3, C4 and C5
-(bench.py measures the headline config C2).  Single GPU; one JSON line each.
+"""Supplementary benchmark lines for BASELINE.json configs C3, C4 and C5 and
+the 8(f) rows (bench.py measures the headline config C2).  Single GPU; one JSON line each.
 
   C3  merge of 5e8 ChIP-seq-like pile-ups (2e6 centres, N(0,150) offsets,
       len U[150,600], seeds 0xC / 0xD): sort + merge with run ids.
@@ -16,6 +16,10 @@
   bed BED text parse on the device (lime_bed_parse_device, 8(f) row 1):
       1e7 BED6 lines over hg38 (host text, H2D inside the call); unit:
       lines/s, with the host reader (lime_bed_read, 1 thread) beside it
+  window   DistributedWindow, distance 1000, on C2's inputs (8(f) row 3):
+      sort + window join, every record filled through a 32 GiB buffer
+  closest  SingleClosest on C2's inputs (8(f) row 4): RegionOrdering sort +
+      plan + fill
 
 Inputs are generated on the device (counter-based RNG) outside the timed
 region; every step starts from unsorted rows in HBM.
@@ -34,7 +38,8 @@ HBM = 8000.0
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c4", "c5", "bed", "closest"], required=True)
+    p.add_argument("--workload", required=True,
+                   choices=["c3", "c4", "c5", "bed", "closest", "window"])
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scale", type=float, default=1.0, help="row-count scale (testing)")
@@ -131,6 +136,40 @@ def main():
             return {"bitset_build_ms (bin + paint)": t1.elapsed_time(t2),
                     "extract_ms": ms, "complement_runs": nc, "difference_runs": nd}, \
                 {"kernel": "bitset extraction (k_ev_count, k_ev_write)", "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+    elif a.workload == "window":
+        # DistributedWindow (distance 1000) on C2's inputs: every pair within
+        # 1000 bases, 16-B records chunked through a reusable 32 GiB buffer
+        ia = gen(int(1e8 * a.scale), 0xA, 50, 5000)
+        ib = gen(int(1e8 * a.scale), 0xB, 50, 5000)
+        n = ia[0]
+        chunk = 1 << 31
+        buf = torch.empty((chunk, 4), dtype=torch.int32, device=dev)
+
+        def step(rec):
+            t0 = ev()
+            SA, SB = mkset(ia), mkset(ib)
+            t1 = ev()
+            plan = ctx.window(SA, SB, 1000)
+            t2 = ev()
+            for f in range(0, plan.n, chunk):
+                plan.fill_device(f, min(chunk, plan.n - f), buf.data_ptr())
+            t3 = ev()
+            rec.append((t0, t1, t2, t3, plan.n))
+            plan.close()
+            SA.close()
+            SB.close()
+        units, unit = 2 * n, "intervals/s"
+        desc = f"window (distance 1000): sort + window join of 2 x {n} intervals, uniform " \
+               "over hg38, len U[50,5000] (C2's inputs)"
+
+        def roof(rec):
+            t0, t1, t2, t3, k = rec[-1]
+            ms = t2.elapsed_time(t3)
+            b = 16 * k  # the fill's records
+            return {"sort_ms": t0.elapsed_time(t1), "plan_ms": t1.elapsed_time(t2),
+                    "fill_ms": ms, "pairs": k}, \
+                {"kernel": "k_fill (window records, all launches)", "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "closest":
         # SingleClosest on C2's inputs: sets sorted in full RegionOrdering

@@ -21,18 +21,27 @@ int fail(int code, const std::string &msg) {
 
 void *Pool::get(size_t bytes) {
     bytes = (bytes + 255) & ~(size_t)255;
-    auto it = free_blocks.find(bytes);
-    if (it != free_blocks.end()) {
-        void *p = it->second;
+    const hipStream_t cur = stream ? *stream : nullptr;
+    auto range = free_blocks.equal_range(bytes);
+    for (auto it = range.first; it != range.second; ++it) {
+        Block &b = it->second;
+        // same stream: stream order protects the reuse; another stream: the
+        // releasing stream's work must be done
+        if (b.s != cur && b.ev && hipEventQuery(b.ev) != hipSuccess) continue;
+        void *p = b.p;
+        if (b.ev) spare_events.push_back(b.ev);
         free_blocks.erase(it);
         live[p] = bytes;
         return p;
     }
     void *p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) {
-        // give cached blocks back and retry once
-        for (auto &kv : free_blocks) hipFree(kv.second);
-        for (auto &kv : free_blocks) held -= (int64_t)kv.first;
+        // give cached blocks back and retry once (hipFree waits for the device)
+        for (auto &kv : free_blocks) {
+            hipFree(kv.second.p);
+            if (kv.second.ev) spare_events.push_back(kv.second.ev);
+            held -= (int64_t)kv.first;
+        }
         free_blocks.clear();
         (void)hipGetLastError();
         if (hipMalloc(&p, bytes) != hipSuccess) {
@@ -47,14 +56,32 @@ void *Pool::get(size_t bytes) {
 void Pool::put(void *p) {
     auto it = live.find(p);
     if (it == live.end()) return;
-    free_blocks.emplace(it->second, p);
+    Block b{p, stream ? *stream : nullptr, nullptr};
+    if (multi_stream) {
+        if (!spare_events.empty()) {
+            b.ev = spare_events.back();
+            spare_events.pop_back();
+        } else if (hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            b.ev = nullptr;
+            b.s = nullptr;  // no event: treat as foreign to every stream...
+        }
+        if (b.ev && hipEventRecord(b.ev, b.s) != hipSuccess) (void)hipGetLastError();
+        if (!b.ev) hipStreamSynchronize(stream ? *stream : nullptr);  // ...and drain instead
+    }
+    free_blocks.emplace(it->second, b);
     live.erase(it);
 }
 void Pool::release_all() {
-    for (auto &kv : free_blocks) hipFree(kv.second);
+    for (auto &kv : free_blocks) {
+        hipFree(kv.second.p);
+        if (kv.second.ev) hipEventDestroy(kv.second.ev);
+    }
     for (auto &kv : live) hipFree(kv.first);
+    for (hipEvent_t e : spare_events) hipEventDestroy(e);
     free_blocks.clear();
     live.clear();
+    spare_events.clear();
     held = 0;
 }
 
@@ -244,6 +271,7 @@ int lime_ctx_create(int device, lime_ctx **out) {
         return fail(LIME_ERR_DEVICE, "stream / pinned buffer creation failed");
     }
     c->stream = c->own_stream;
+    c->pool.stream = &c->stream;
     *out = c;
     return LIME_OK;
 }
@@ -261,7 +289,16 @@ int lime_ctx_destroy(lime_ctx *ctx) {
 
 int lime_ctx_set_stream(lime_ctx *ctx, void *stream) {
     if (!ctx) return fail(LIME_ERR_ARG, "ctx is null");
-    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->own_stream;
+    // Work of this context on a second stream: from now on releases are
+    // ordered by events.  The blocks cached so far carry none, so the old
+    // stream is drained once here.
+    const bool used = !ctx->pool.live.empty() || !ctx->pool.free_blocks.empty();
+    if (s != ctx->stream && used && !ctx->pool.multi_stream) {
+        LIME_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->pool.multi_stream = true;
+    }
+    ctx->stream = s;
     return LIME_OK;
 }
 

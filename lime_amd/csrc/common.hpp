@@ -35,9 +35,23 @@ int fail(int code, const std::string &msg);
 // ------------------------------------------------------------- device pool
 // Grow-only caching allocator: blocks are recycled by exact (rounded) size so
 // that repeated operator calls of the same shape never hit hipMalloc.
+// Caching device allocator of one context.  A released block is reused at
+// once by work on the stream that released it (stream order).  Once the
+// context has run on more than one stream (lime_ctx_set_stream), each release
+// also records an event, and work on another stream takes the block only
+// after that event has completed -- so e.g. the next batch's sort can run on
+// a second stream while this batch's fill streams, sharing one pool.
 struct Pool {
-    std::multimap<size_t, void *> free_blocks;
+    struct Block {
+        void *p;
+        hipStream_t s;   // stream current at release
+        hipEvent_t ev;   // completion of the releasing stream's work (or null)
+    };
+    std::multimap<size_t, Block> free_blocks;
     std::map<void *, size_t> live;
+    std::vector<hipEvent_t> spare_events;
+    const hipStream_t *stream = nullptr;  // the owning context's current stream
+    bool multi_stream = false;
     int64_t held = 0;
     void *get(size_t bytes);
     void put(void *p);

@@ -179,6 +179,7 @@ int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64
 
 /* ------------------------------------------------------------------ closest */
 #define LIME_CLOSEST 0 /* SingleClosest (lime-core Closest.scala:34-214), the CLI's op */
+#define LIME_CLOSEST_SINGLE_OVERLAP 1 /* SingleClosestSingleOverlap (Closest.scala:216-268) */
 
 /* SingleClosest(left = a, right = b, partitionMap).compute() (Closest.scala
  * :34-214, CLI cli/Closest.scala:45-58) as the reference's sweep computes it on

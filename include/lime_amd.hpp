@@ -311,11 +311,11 @@ class DistributedWindow {
 // the sweep's currentClosest, keyed by the left region; the reference's sweep
 // on one partition (lime_closest_count).  Rows of every strand go into one
 // stranded set per side (the order includes strand, the distance ignores it).
-template <typename T, typename U>
-class SingleClosest {
+template <typename T, typename U, int MODE = LIME_CLOSEST>
+class ClosestOp {
    public:
-    SingleClosest(RDD<T> left, RDD<U> right, PartitionMap partitionMap = {},
-                  Engine &eng = Engine::thread_default())
+    ClosestOp(RDD<T> left, RDD<U> right, PartitionMap partitionMap = {},
+              Engine &eng = Engine::thread_default())
         : left_(std::move(left)), right_(std::move(right)), pm_(std::move(partitionMap)),
           eng_(eng) {}
 
@@ -329,7 +329,7 @@ class SingleClosest {
         detail::upload(eng_.ctx(), *sp, right_, ra, B, true);
         lime_pairs *plan = nullptr;
         int64_t n = 0;
-        check(lime_closest_count(eng_.ctx(), A.h, B.h, LIME_CLOSEST, &plan, &n));
+        check(lime_closest_count(eng_.ctx(), A.h, B.h, MODE, &plan, &n));
         std::vector<lime_pair> p((size_t)n);
         int rc = lime_intersect_fill_host(plan, 0, n, p.data());
         lime_pairs_destroy(plan);
@@ -347,6 +347,11 @@ class SingleClosest {
     PartitionMap pm_;
     Engine &eng_;
 };
+template <typename T, typename U>
+using SingleClosest = ClosestOp<T, U, LIME_CLOSEST>;
+// Closest.scala:216-268 (the suite's variant: covered lengths compared too)
+template <typename T, typename U>
+using SingleClosestSingleOverlap = ClosestOp<T, U, LIME_CLOSEST_SINGLE_OVERLAP>;
 
 template <class T, class U>
 class DistributedIntersection {

@@ -108,7 +108,8 @@ int format_bed(lime_ctx *ctx, const std::vector<uint32_t> &off,
                const uint32_t *ge, const uint32_t *extra, char *out, int64_t cap,
                int64_t *total_len);
 struct ClosestPlan;
-int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan **out);
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode,
+                 ClosestPlan **out);
 int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
 int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr);
 void closest_free(ClosestPlan *pl);
@@ -593,14 +594,14 @@ int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int 
                        lime_pairs **plan, int64_t *n_pairs) {
     if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad closest arguments");
     if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
-    if (mode != LIME_CLOSEST)
-        return fail(LIME_ERR_ARG, "closest mode must be LIME_CLOSEST (SingleClosest)");
+    if (mode != LIME_CLOSEST && mode != LIME_CLOSEST_SINGLE_OVERLAP)
+        return fail(LIME_ERR_ARG, "closest mode must be LIME_CLOSEST or LIME_CLOSEST_SINGLE_OVERLAP");
     if (!a->strand_in || !b->strand_in || a->min_shift || b->min_shift)
         return fail(LIME_ERR_ARG,
                     "closest needs sets in full RegionOrdering (lime_set_create_host_stranded)");
     hipSetDevice(ctx->device);
     ClosestPlan *cl = nullptr;
-    LIME_TRY(closest_plan(ctx, a, b, &cl));
+    LIME_TRY(closest_plan(ctx, a, b, mode, &cl));
     lime_pairs *p = new lime_pairs{nullptr, ctx};
     p->closest = cl;
     *plan = p;

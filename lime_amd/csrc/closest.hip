@@ -354,6 +354,97 @@ __global__ __launch_bounds__(CB) void k_prune_round(Lefts L, Rights R, State s,
     if (nv != cur) atomicOr(changed, 1u);
 }
 
+// SingleClosestSingleOverlap (Closest.scala:216-268): its advance also stops
+// inside the covering zone where the covered length drops, and its prune
+// drops covering rows shorter than a covering current closest.  Those stops
+// depend on each left, so its (j, p) chain is run in order -- one wave per
+// contig, the wave testing 64 candidates per step -- and the output pass is
+// the shared one.  (Used by the reference's suite only; its CLI runs
+// SingleClosest.)
+__device__ __forceinline__ bool covers(uint32_t ls, uint32_t le, uint32_t rs, uint32_t re) {
+    return le > rs && ls < re;
+}
+__device__ __forceinline__ uint32_t cover_len(uint32_t ls, uint32_t le, uint32_t rs, uint32_t re) {
+    return min(le, re) - max(ls, rs);
+}
+
+__global__ __launch_bounds__(64) void k_seq_single(Lefts L, Rights R,
+                                                   const uint32_t *__restrict__ lb,
+                                                   uint32_t *__restrict__ jp,
+                                                   uint32_t *__restrict__ pp,
+                                                   uint32_t *__restrict__ dd) {
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t i0 = lb[c], i1 = lb[c + 1];
+    const int64_t r0 = L.rb[c], r1 = L.rb[c + 1];
+    int64_t j = r0, p = r0;
+    for (int64_t i = i0; i < i1; ++i) {
+        const uint32_t ls = L.gs[i], le = L.ge[i];
+        // advanceCache (:251-267): C = R[k-1]; the contig's first row always
+        // advances (the current closest lies on another contig)
+        for (;;) {
+            const int64_t k = j + lane;
+            bool stop = k >= r1;
+            if (!stop && k > r0) {
+                const uint32_t cs = R.gs[k], ce = R.ge[k], ps = R.gs[k - 1], pe = R.ge[k - 1];
+                bool adv;
+                if (covers(ls, le, cs, ce))
+                    adv = !covers(ls, le, ps, pe) ||
+                          cover_len(ls, le, cs, ce) >= cover_len(ls, le, ps, pe);
+                else
+                    adv = udist(ls, le, cs, ce) <= udist(ls, le, ps, pe);
+                stop = !adv;
+            }
+            const uint64_t b = __ballot(stop);
+            if (b) {
+                j += __builtin_ctzll(b);
+                break;
+            }
+            j += 64;
+        }
+        // pruneCache (:230-241) with SetTheory.scala:131-141's index rule
+        uint32_t D = NONE;
+        if (j > r0) {
+            const uint32_t Cs = R.gs[j - 1], Ce = R.ge[j - 1];
+            D = udist(ls, le, Cs, Ce);
+            const bool cc = covers(ls, le, Cs, Ce);
+            const uint32_t cbC = cc ? cover_len(ls, le, Cs, Ce) : NONE;
+            for (int64_t q = p; q < j; q += 64) {
+                const int64_t k = q + lane;
+                bool keep = false;
+                if (k < j) {
+                    const uint32_t rs = R.gs[k], re = R.ge[k];
+                    const bool cv = covers(ls, le, rs, re);
+                    keep = !((cv && cover_len(ls, le, rs, re) < cbC) || udist(ls, le, rs, re) > D);
+                }
+                const uint64_t b = __ballot(keep);
+                if (b) {
+                    p = q + __builtin_ctzll(b);
+                    break;
+                }
+            }
+        }
+        if (lane == 0) {
+            jp[i] = (uint32_t)j;
+            pp[i] = (uint32_t)p;
+            dd[i] = D;
+        }
+    }
+}
+
+// lefts of contigs the sweep never enters: no output
+__global__ __launch_bounds__(CB) void k_kill(Lefts L, const uint8_t *__restrict__ live,
+                                             uint32_t *__restrict__ dd) {
+    __shared__ uint32_t s_off[OCAP];
+    if (L.nc + 1 <= OCAP)
+        for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
+    __syncthreads();
+    const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
+    const int64_t i = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (i >= L.n) return;
+    if (!live[contig_of(o, L.nc, L.gs[i])]) dd[i] = NONE;
+}
+
 // Output pass.  A match is k in [p, j) with dist(L, R[k]) == D.
 //  D > 0: below A that means R[k].end == L.start + 1 - D exactly, above A
 //    R[k].start == L.end + D - 1 exactly: one run of the end index (rights by
@@ -548,7 +639,7 @@ struct Scratch {
     }
 };
 
-int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan *pl) {
+int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, ClosestPlan *pl) {
     const int64_t nl = A->n, nr = B->n;
     const int32_t nc = A->n_contigs;
     Scratch sc{ctx, {}};
@@ -617,22 +708,31 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan *
     const unsigned gl = blocks_for(nl, CB);
     hipLaunchKernelGGL(k_stops, dim3(gl), dim3(CB), 0, S(ctx), L, R, Aa, Nn);
     LIME_HIP(hipGetLastError());
-    CL_TRY(prefix_max_u32(ctx, Nn, U, nl));
     LIME_HIP(hipMemsetAsync(stuck, 0xff, sizeof(unsigned long long) * (size_t)nc, S(ctx)));
-    hipLaunchKernelGGL(k_stuck, dim3(gl), dim3(CB), 0, S(ctx), L, R, (const uint32_t *)Aa,
-                       (const uint32_t *)U, stuck);
+    uint32_t *lbd;
+    CL_TRY(sc.get(&lbd, (size_t)nc + 1));
+    hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), A->gs, nl,
+                       A->d_off, nc, lbd);
+    LIME_HIP(hipGetLastError());
+    if (mode == 0) {
+        CL_TRY(prefix_max_u32(ctx, Nn, U, nl));
+        hipLaunchKernelGGL(k_stuck, dim3(gl), dim3(CB), 0, S(ctx), L, R, (const uint32_t *)Aa,
+                           (const uint32_t *)U, stuck);
+    } else {
+        // the chain in order, one wave per contig; exit pointers from jp
+        hipLaunchKernelGGL(k_seq_single, dim3(nc), dim3(64), 0, S(ctx), L, R,
+                           (const uint32_t *)lbd, pl->jp, pl->pp, pl->dd);
+    }
     LIME_HIP(hipGetLastError());
     // contig liveness (host, <= n_contigs steps): the sweep enters the next
     // left contig only from the end of this contig's rights, and only if no
     // rights lie on the contigs in between
     {
-        uint32_t *lbd, *lastU;
-        CL_TRY(sc.get(&lbd, (size_t)nc + 1));
+        uint32_t *lastU;
         CL_TRY(sc.get(&lastU, (size_t)nc));
-        hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), A->gs,
-                           nl, A->d_off, nc, lbd);
         hipLaunchKernelGGL(k_last, dim3(blocks_for(nc, CB)), dim3(CB), 0, S(ctx),
-                           (const uint32_t *)lbd, (const uint32_t *)U, nc, lastU);
+                           (const uint32_t *)lbd, (const uint32_t *)(mode == 0 ? U : pl->jp), nc,
+                           lastU);
         LIME_HIP(hipGetLastError());
         std::vector<uint32_t> rb(nc + 1), lb(nc + 1), lu(nc);
         std::vector<unsigned long long> st(nc);
@@ -690,12 +790,18 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan *
         LIME_HIP(hipGetLastError());
     }
     State s{Aa, U, stuck, live};
-    hipLaunchKernelGGL(k_fresh, dim3(gl), dim3(CB), 0, S(ctx), L, R, s, pl->jp, pl->dd, P);
-    LIME_HIP(hipGetLastError());
-    // cache head: prefix max of the fresh heads, then rounds to the fixed point
-    CL_TRY(prefix_max_u32(ctx, P, pl->pp, nl));
+    if (mode != 0) {
+        hipLaunchKernelGGL(k_kill, dim3(gl), dim3(CB), 0, S(ctx), L, (const uint8_t *)live,
+                           pl->dd);
+        LIME_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_fresh, dim3(gl), dim3(CB), 0, S(ctx), L, R, s, pl->jp, pl->dd, P);
+        LIME_HIP(hipGetLastError());
+        // cache head: prefix max of the fresh heads, then rounds to the fixed point
+        CL_TRY(prefix_max_u32(ctx, P, pl->pp, nl));
+    }
     uint32_t *cur = pl->pp, *nxt = p2;
-    for (int64_t r = 0; r <= nl; ++r) {
+    for (int64_t r = 0; mode == 0 && r <= nl; ++r) {
         LIME_HIP(hipMemsetAsync(changed, 0, sizeof(unsigned int), S(ctx)));
         hipLaunchKernelGGL(k_prune_round, dim3(gl), dim3(CB), 0, S(ctx), L, R, s,
                            (const uint32_t *)pl->jp, (const uint32_t *)pl->dd,
@@ -732,7 +838,8 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan *
 
 }  // namespace
 
-int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPlan **out) {
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode,
+                 ClosestPlan **out) {
     if (A->n >= (int64_t)NONE || B->n >= (int64_t)NONE)
         return fail(LIME_ERR_RANGE, "closest supports fewer than 2^32 - 1 rows per set");
     ClosestPlan *pl = new ClosestPlan();
@@ -740,7 +847,7 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, ClosestPla
     pl->A = A;
     pl->B = B;
     pl->nl = A->n;
-    const int rc = plan_body(ctx, A, B, pl);
+    const int rc = plan_body(ctx, A, B, mode, pl);
     if (rc != LIME_OK) {
         closest_free(pl);
         return rc;

@@ -342,12 +342,15 @@ class Context:
                                        C.byref(n)))
         return Pairs(self, h, n.value, keep=(a, b))
 
-    def closest(self, a, b):
-        """SingleClosest (Closest.scala:34-214) on one partition: for each
-        left row, the cached right rows at the current closest's distance.
-        Both sets must come from set_from_host_stranded (RegionOrdering)."""
+    def closest(self, a, b, mode=0):
+        """SingleClosest (mode 0, Closest.scala:34-214) or
+        SingleClosestSingleOverlap (mode 1, :216-268) on one partition: for
+        each left row, the cached right rows at the current closest's
+        distance.  Both sets must be in RegionOrdering (set_from_host_stranded
+        / set_from_device_stranded)."""
         h, n = vp(), i64()
-        check(_lib().lime_closest_count(self._h, a._h, b._h, 0, C.byref(h), C.byref(n)))
+        check(_lib().lime_closest_count(self._h, a._h, b._h, int(mode), C.byref(h),
+                                        C.byref(n)))
         return Pairs(self, h, n.value, keep=(a, b))
 
     def parse_bed(self, text):

@@ -14,8 +14,9 @@ lime-core/src/main/scala/org/bdgenomics/lime/set_theory/:
         -> [(ReferenceRegion, [])]                 Complement.scala:131-134
     DistributedWindow(leftRdd, rightRdd, partitionMap, threshold=1000).compute()
         -> [(ReferenceRegion, (T, U))]             Window.scala:71-95
-    SingleClosest(leftRdd, rightRdd, partitionMap).compute()
-        -> [(ReferenceRegion, (T, U))]             Closest.scala:34-214
+    SingleClosest / SingleClosestSingleOverlap(leftRdd, rightRdd,
+                  partitionMap).compute()
+        -> [(ReferenceRegion, (T, U))]             Closest.scala:34-268
     UnstrandedCluster / StrandedCluster / ...WithMinimumOverlap(rddToCompute,
                           partitionMap, threshold=0).compute()
         -> [(ReferenceRegion, [T])]                Cluster.scala:38-121
@@ -200,6 +201,8 @@ class SingleClosest(_Op):
     per side (the order includes strand; the distance ignores it), run as the
     reference's sweep runs on one partition."""
 
+    MODE = 0
+
     def __init__(self, leftRdd, rightRdd, partitionMap=None, threshold=0, ctx=None):
         super().__init__(ctx)
         self.left, self.right = list(leftRdd), list(rightRdd)
@@ -214,12 +217,18 @@ class SingleClosest(_Op):
                                             codes(lr))
         B = self.ctx.set_from_host_stranded(space, *_arrays(space, rr, range(len(rr))),
                                             codes(rr))
-        plan = self.ctx.closest(A, B)
+        plan = self.ctx.closest(A, B, self.MODE)
         out = [(lr[p["a_row"]], (lv[p["a_row"]], rv[p["b_row"]])) for p in plan.fill_host()]
         plan.close()
         A.close()
         B.close()
         return out
+
+
+class SingleClosestSingleOverlap(SingleClosest):
+    """Closest.scala:216-268: SingleClosest whose advance and prune also
+    compare covered lengths (the suite's second variant)."""
+    MODE = 1
 
 
 class DistributedSubtract(_Op):

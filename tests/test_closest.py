@@ -224,11 +224,11 @@ def _space(nc, ln):
     return Space([f"chr{i + 1}" for i in range(nc)], [ln] * nc)
 
 
-def _gpu_vs_oracle(ctx, sp, A, sa, B, sb):
+def _gpu_vs_oracle(ctx, sp, A, sa, B, sb, mode=0):
     a = ctx.set_from_host_stranded(sp, *A, sa)
     b = ctx.set_from_host_stranded(sp, *B, sb)
-    plan = ctx.closest(a, b)
-    exp = oracle.closest((*A, sa), (*B, sb))
+    plan = ctx.closest(a, b, mode)
+    exp = oracle.closest((*A, sa), (*B, sb), mode)
     assert plan.n == len(exp["start"])
     p = plan.fill_host()
     assert p["a_row"].tolist() == exp["a_row"].tolist()
@@ -349,3 +349,33 @@ def test_gpu_c2_density(ctx):
     exp = oracle.closest((*A, z), (*B, z))
     assert plan.n == len(exp["start"]) > 1_000_000
     assert plan.checksum() == oracle.checksum_pairs(exp)
+
+
+# ------------------------------------------- SingleClosestSingleOverlap (mode 1)
+@pytest.mark.gpu
+def test_gpu_suite_single_overlap(ctx):
+    from lime_amd.set_theory import ReferenceRegion, SingleClosestSingleOverlap
+
+    def keyed(name):
+        chrom, s, e, nm = read_bed_py(os.path.join(GOLDEN, name))
+        return [(ReferenceRegion.unstranded(c, x, y), (c, x, y)) for c, x, y in zip(chrom, s, e)]
+    out = SingleClosestSingleOverlap(keyed("intersect_with_overlap_00.bed"),
+                                     keyed("intersect_with_overlap_01.bed"), None,
+                                     ctx=ctx).compute()
+    got = [[[r.referenceName, r.start, r.end], [v[1][0], int(v[1][1]), int(v[1][2])]]
+           for r, v in out]
+    assert got == [list(map(list, p)) for p in expected()["closest_single_overlap"]]
+
+
+@pytest.mark.gpu
+def test_gpu_single_overlap_random(ctx):
+    for seed in range(300):
+        nc, A, sa, B, sb = _case(seed)
+        _gpu_vs_oracle(ctx, _space(nc, 6000), A, sa, B, sb, mode=1)
+    for seed, n, ml in [(5, 20000, 300), (6, 20000, 3000), (7, 100000, 5000)]:
+        rng = np.random.default_rng(seed)
+        A, B = random_sets(rng, n, n, n_contigs=3, contig_len=40 * n, max_len=ml,
+                           zero_frac=0.05, dup_frac=0.05, book_frac=0.05)
+        sa = rng.integers(0, 4, n).astype(np.int8)
+        sb = rng.integers(0, 4, n).astype(np.int8)
+        assert _gpu_vs_oracle(ctx, _space(3, 40 * n), A, sa, B, sb, mode=1) > 0

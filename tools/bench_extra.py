@@ -20,6 +20,8 @@ the 8(f) rows (bench.py measures the headline config C2).  Single GPU; one JSON 
       sort + window join, every record filled through a 32 GiB buffer
   closest  SingleClosest on C2's inputs (8(f) row 4): RegionOrdering sort +
       plan + fill
+  closest_single  SingleClosestSingleOverlap (sequential chain per contig) on
+      1/100 of C2's rows
 
 Inputs are generated on the device (counter-based RNG) outside the timed
 region; every step starts from unsorted rows in HBM.
@@ -39,7 +41,7 @@ HBM = 8000.0
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", required=True,
-                   choices=["c3", "c4", "c5", "bed", "closest", "window"])
+                   choices=["c3", "c4", "c5", "bed", "closest", "closest_single", "window"])
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scale", type=float, default=1.0, help="row-count scale (testing)")
@@ -171,10 +173,14 @@ def main():
                     "fill_ms": ms, "pairs": k}, \
                 {"kernel": "k_fill (window records, all launches)", "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
-    elif a.workload == "closest":
-        # SingleClosest on C2's inputs: sets sorted in full RegionOrdering
-        ia = gen(int(1e8 * a.scale), 0xA, 50, 5000)
-        ib = gen(int(1e8 * a.scale), 0xB, 50, 5000)
+    elif a.workload in ("closest", "closest_single"):
+        # SingleClosest on C2's inputs: sets sorted in full RegionOrdering.
+        # closest_single: SingleClosestSingleOverlap, whose (j, p) chain runs
+        # in order (one wave per contig): C2's density on 1/100 of the rows
+        mode = 1 if a.workload == "closest_single" else 0
+        sc = a.scale * (0.01 if mode else 1.0)
+        ia = gen(int(1e8 * sc), 0xA, 50, 5000)
+        ib = gen(int(1e8 * sc), 0xB, 50, 5000)
         n = ia[0]
 
         def sset(x):
@@ -186,7 +192,7 @@ def main():
             t0 = ev()
             SA, SB = sset(ia), sset(ib)
             t1 = ev()
-            plan = ctx.closest(SA, SB)
+            plan = ctx.closest(SA, SB, mode)
             out = torch.empty((max(plan.n, 1), 4), dtype=torch.int32, device=dev)
             t2 = ev()
             plan.fill_device(0, plan.n, out.data_ptr())
@@ -196,8 +202,9 @@ def main():
             SA.close()
             SB.close()
         units, unit = 2 * n, "intervals/s"
-        desc = f"closest (SingleClosest): sort (RegionOrdering) + closest of 2 x {n} " \
-               "intervals, uniform over hg38, len U[50,5000] (C2's inputs)"
+        desc = f"closest ({'SingleClosestSingleOverlap' if mode else 'SingleClosest'}): sort " \
+               f"(RegionOrdering) + closest of 2 x {n} intervals, uniform over hg38, " \
+               "len U[50,5000]" + (" (1/100 of C2's rows)" if mode else " (C2's inputs)")
 
         def roof(rec):
             t0, t1, t2, t3, k = rec[-1]

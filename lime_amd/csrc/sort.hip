@@ -50,6 +50,9 @@ struct SetStats {
 // when every row has one strand), GE x ceil(bits(max width) / 8), GS; plain
 // sets by (gs, zero-width first) with NZ?, GS.
 enum { M_GS = 0, M_NZ = 1, M_GE = 2, M_ST = 3 };
+// where a pass's row ids come from: none kept (binned sets), loaded, or the
+// identity (the first pass of a set built from caller rows: row = position)
+enum { ROWS_NONE = 0, ROWS_LOAD = 1, ROWS_IDENT = 2 };
 
 template <int M>
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, uint32_t r, int shift,
@@ -86,6 +89,11 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
         m &= bit ? bb : ~bb;
     }
     return m;
+}
+
+__global__ __launch_bounds__(256) void k_rows_iota(uint32_t *__restrict__ r, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) r[i] = (uint32_t)i;
 }
 
 // bijective blockIdx -> tile map giving each XCD (blockIdx % 8) a contiguous
@@ -329,7 +337,8 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
                                              const uint32_t *__restrict__ ge,
                                              const uint32_t *__restrict__ row, int64_t n, int shift,
                                              const int8_t *__restrict__ st,
-                                             uint32_t *__restrict__ counts, uint32_t ntiles) {
+                                             uint32_t *__restrict__ counts, uint32_t ntiles,
+                                             int rows) {
     __shared__ uint32_t hist[RWAVES][RBINS];
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
@@ -352,7 +361,10 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
             } else {
                 ve[4 * k] = ve[4 * k + 1] = ve[4 * k + 2] = ve[4 * k + 3] = 0u;
             }
-            if (M == M_ST) {
+            if (M == M_ST && rows == ROWS_IDENT) {
+                const uint32_t r = (uint32_t)(base + 4 * (k * 64 + lane));
+                vr[4 * k] = r, vr[4 * k + 1] = r + 1, vr[4 * k + 2] = r + 2, vr[4 * k + 3] = r + 3;
+            } else if (M == M_ST) {
                 const uint4 u = r4[k * 64 + lane];
                 vr[4 * k] = u.x, vr[4 * k + 1] = u.y, vr[4 * k + 2] = u.z, vr[4 * k + 3] = u.w;
             } else {
@@ -368,7 +380,7 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
             valid[k] = i < n;
             vk[k] = valid[k] ? key[i] : 0u;
             ve[k] = (NEED_E && valid[k]) ? ge[i] : 0u;
-            vr[k] = (M == M_ST && valid[k]) ? row[i] : 0u;
+            vr[k] = (M == M_ST && valid[k]) ? (rows == ROWS_IDENT ? (uint32_t)i : row[i]) : 0u;
         }
     }
     __syncthreads();
@@ -381,7 +393,7 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     flush_hist(hist, counts, ntiles);
 }
 
-template <int M>
+template <int M, int ROWS>
 // 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
 __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
                                                 const uint32_t *__restrict__ ge_in,
@@ -414,8 +426,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS], pd[RITEMS];
     // 32-bit offsets from per-wave base pointers keep address math scalar
     const int lim = (int)min((int64_t)WITEMS, n - base);  // valid rows of this wave
-    // row_in == nullptr (GS passes only): the set keeps no row ids
-    const bool rows = row_in != nullptr;
+    // ROWS_NONE (GS passes of binned sets): no row ids are kept;
+    // ROWS_IDENT (first pass over caller rows): row id = position
     const uint32_t *kin = key_in + base, *ein = ge_in + base, *rin = row_in + base;
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
@@ -423,7 +435,11 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         const bool valid = o < lim;
         vk[k] = valid ? kin[o] : 0u;
         ve[k] = valid ? ein[o] : 0u;
-        vr[k] = valid && rows ? rin[o] : 0u;
+        // (GS passes write identity rows straight from the position below,
+        // keeping vr out of the registers of that path)
+        vr[k] = ROWS == ROWS_IDENT && M != M_GS ? (uint32_t)(base + o)
+                : ROWS == ROWS_LOAD             ? (valid ? rin[o] : 0u)
+                                                : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -501,11 +517,12 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
         ge_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
     }
-    if (!rows) return;
+    if (ROWS == ROWS_NONE) return;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
-        if (lp[k] != 0xffffffffu) se[lp[k]] = vr[k];
+        if (lp[k] != 0xffffffffu)
+            se[lp[k]] = ROWS == ROWS_IDENT ? (uint32_t)(base + k * 64 + lane) : vr[k];
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
         const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
@@ -516,32 +533,39 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
 template <int M>
 void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                  const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
-                 uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int &rc) {
+                 uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows, int &rc) {
     if (!have_hist)
         hipLaunchKernelGGL(k_hist<M>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n, shift, st,
-                           mat, ntiles);
+                           mat, ntiles, rows);
     if ((rc = scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr)) != LIME_OK)
         return;
-    hipLaunchKernelGGL(k_scatter<M>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n, shift, st,
-                       (const uint32_t *)mat, ntiles, k1, e1, r1);
+    if (rows == ROWS_IDENT)
+        hipLaunchKernelGGL((k_scatter<M, ROWS_IDENT>), dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0,
+                           r0, n, shift, st, (const uint32_t *)mat, ntiles, k1, e1, r1);
+    else if (rows == ROWS_LOAD)
+        hipLaunchKernelGGL((k_scatter<M, ROWS_LOAD>), dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0,
+                           r0, n, shift, st, (const uint32_t *)mat, ntiles, k1, e1, r1);
+    else if (M == M_GS)  // binned sets: GS passes only
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_NONE>), dim3(ntiles), dim3(RB), 0, S(ctx), k0,
+                           e0, r0, n, shift, st, (const uint32_t *)mat, ntiles, k1, e1, r1);
 }
 
 int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
-               uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles) {
+               uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows) {
     int rc = LIME_OK;
     switch (mode) {
         case M_NZ:
-            launch_pass<M_NZ>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            launch_pass<M_NZ>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
             break;
         case M_GE:
-            launch_pass<M_GE>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            launch_pass<M_GE>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
             break;
         case M_ST:
-            launch_pass<M_ST>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            launch_pass<M_ST>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
             break;
         default:
-            launch_pass<M_GS>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rc);
+            launch_pass<M_GS>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
     }
     if (rc != LIME_OK) return rc;
     LIME_HIP(hipGetLastError());
@@ -588,7 +612,8 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         else
             hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
                                d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, r0, part, mat, ntiles, set->min_shift);
+                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
+                               set->min_shift);  // rows = positions: made by the first pass
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());
@@ -631,12 +656,15 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         }
         for (int sh = 0; sh < bits; sh += 8)
             if (sh >= set->min_shift) passes.push_back({M_GS, sh});
+        // caller rows: the first pass writes row = position (k_prep did not)
+        int rows = !keep_rows ? ROWS_NONE : global ? ROWS_LOAD : ROWS_IDENT;
         // k_prep already histogrammed the gs digit at min_shift
         bool have = passes.front().first == M_GS && passes.front().second == set->min_shift;
         for (auto &p : passes) {
             LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
-                                e1, r1, mat, ntiles));
+                                e1, r1, mat, ntiles, rows));
             have = false;
+            if (rows == ROWS_IDENT) rows = ROWS_LOAD;
             std::swap(k0, k1);
             std::swap(e0, e1);
             std::swap(r0, r1);
@@ -644,6 +672,11 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         release(ctx, k1);
         release(ctx, e1);
         release(ctx, r1);
+    } else if (keep_rows && !global && n > 0) {
+        // already in order: the row ids are the positions
+        hipLaunchKernelGGL(k_rows_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(ctx),
+                           r0, n);
+        LIME_HIP(hipGetLastError());
     }
     release(ctx, mat);
     set->gs = k0;

@@ -267,6 +267,100 @@ __global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w,
     if (dev::lane_id() == 0) atomicAdd(out, (unsigned long long)c);
 }
 
+// Single pass (count + write) when the run count has a known bound: tiles
+// in ticket order, the event offset of a tile by decoupled look-back over
+// the per-tile status words (flag in bits 62-63, value below), and events
+// past the capacity only counted (the caller then falls back to two passes).
+constexpr uint64_t EV_AGG = 1ull << 62, EV_INC = 2ull << 62, EV_VAL = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict__ status,
+                                                 unsigned int *__restrict__ ticket,
+                                                 int64_t cap_events, uint32_t *__restrict__ rgs,
+                                                 uint32_t *__restrict__ rge,
+                                                 unsigned long long *__restrict__ total) {
+    __shared__ unsigned long long img[BT + 1];
+    __shared__ uint32_t s_pad[MAXPAD];
+    __shared__ int s_npad;
+    __shared__ uint32_t scratch[BB / 64 + 1];
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_excl;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const int64_t w0 = (int64_t)tile * BT;
+    stage_tile(a, w0, img, s_pad, &s_npad);
+    const int q0 = threadIdx.x * BW;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < BW; ++k) {
+        uint64_t st, en;
+        events_of(img[q0 + k + 1], img[q0 + k], st, en);
+        c += __popcll(st) + __popcll(en);
+    }
+    uint32_t tot;
+    const uint32_t mine = dev::block_exclusive_sum<BB>(c, scratch, &tot);
+    if (threadIdx.x < 64) {  // one wave publishes and looks back
+        const int lane = dev::lane_id();
+        if (tile == 0) {
+            if (lane == 0) {
+                __hip_atomic_store(status, EV_INC | tot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                s_excl = 0;
+            }
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(status + tile, EV_AGG | tot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t acc = 0;
+            for (int64_t base = (int64_t)tile - 1; base >= 0; base -= 64) {
+                const int64_t t = base - lane;
+                uint64_t v = EV_INC;  // before tile 0: the inclusive identity
+                if (t >= 0) {
+                    v = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    while ((v >> 62) == 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        v = __hip_atomic_load(status + t, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                const uint64_t inc = __ballot((v >> 62) == 2);
+                uint64_t val = v & EV_VAL;
+                if (inc && lane > __builtin_ctzll(inc)) val = 0;
+                acc += dev::wave_reduce_sum(val);
+                if (inc) break;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(status + tile, EV_INC | (acc + tot), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                s_excl = acc;
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t excl = s_excl;
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = excl + tot;
+    uint64_t ev = excl + mine;
+#pragma unroll
+    for (int k = 0; k < BW; ++k) {
+        uint64_t st, en;
+        events_of(img[q0 + k + 1], img[q0 + k], st, en);
+        uint64_t all = st | en;
+        const uint32_t base = (uint32_t)((w0 + q0 + k) * 64);
+        while (all) {
+            const int b = __builtin_ctzll(all);
+            all &= all - 1;
+            if ((int64_t)ev < cap_events) {
+                const uint32_t p = base + (uint32_t)b;
+                if (ev & 1u)
+                    rge[ev >> 1] = p;
+                else
+                    rgs[ev >> 1] = p;
+            }
+            ++ev;
+        }
+    }
+}
+
 }  // namespace
 
 int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
@@ -275,6 +369,7 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     lime_result runs;
     runs.ctx = ctx;
     LIME_TRY(merge_runs(ctx, a, &runs, false));
+    bs->runs_bound = runs.n;
     const int64_t span = (int64_t)a->off[a->n_contigs];
     bs->span = span;
     bs->n_words = (span + 63) / 64;
@@ -292,6 +387,7 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
 // bits of a BINNED set (min_shift == 16): no merge, no full sort
 int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     const int64_t span = (int64_t)a->off[a->n_contigs];
+    bs->runs_bound = a->n;  // the union of n rows has at most n runs
     bs->span = span;
     bs->n_words = (span + 63) / 64;
     LIME_TRY(alloc(ctx, &bs->words, (size_t)bs->n_words));
@@ -329,10 +425,66 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     for (int c = 0; c < a->n_contigs; ++c) pad[c] = a->off[c + 1] - 1;
     uint32_t *d_pad;
     LIME_TRY(alloc(ctx, &d_pad, pad.size() + 1));
-    if (!pad.empty())
-        LIME_HIP(hipMemcpy(d_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
+    if (!pad.empty()) {
+        LIME_HIP(hipMemcpyAsync(d_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipStreamSynchronize(S(ctx)));
+    }
     oa.pad = d_pad;
     const int64_t nt = (a->n_words + BT - 1) / BT;
+    // bound on the result's runs: each run starts at a run start of one
+    // operand (AND / ANDN also at a run end of B); NOT adds one gap per contig
+    bool known = true;
+    int64_t sum = 0;
+    for (int i = 0; i < k; ++i) {
+        known = known && sets[i]->runs_bound >= 0;
+        sum += sets[i]->runs_bound;
+    }
+    const int64_t bound = op == 1 ? a->runs_bound + a->n_contigs + 1 : sum + 1;
+    if (known && nt > 0 && bound < (int64_t)0x7fffffff) {
+        uint64_t *status;
+        unsigned int *ticket;
+        unsigned long long *tot64;
+        LIME_TRY(alloc(ctx, &status, (size_t)nt));
+        LIME_TRY(alloc(ctx, &ticket, 1));
+        LIME_TRY(alloc(ctx, &tot64, 1));
+        LIME_TRY(alloc(ctx, &res->gs, (size_t)bound));
+        LIME_TRY(alloc(ctx, &res->ge, (size_t)bound));
+        LIME_HIP(hipMemsetAsync(status, 0, sizeof(uint64_t) * (size_t)nt, S(ctx)));
+        LIME_HIP(hipMemsetAsync(ticket, 0, sizeof(unsigned int), S(ctx)));
+        hipLaunchKernelGGL(k_ev_fused, dim3((unsigned)nt), dim3(BB), 0, S(ctx), oa, status,
+                           ticket, 2 * bound, res->gs, res->ge, tot64);
+        LIME_HIP(hipGetLastError());
+        unsigned long long nev = 0;
+        LIME_TRY(read_back(ctx, &nev, tot64, sizeof(nev)));
+        release(ctx, status);
+        release(ctx, ticket);
+        release(ctx, tot64);
+        if ((int64_t)nev <= 2 * bound) {
+            release(ctx, d_pad);
+            if (nev & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
+            const int64_t nr = (int64_t)nev / 2;
+            if (nr < bound / 2) {  // keep the result's memory to its size
+                uint32_t *gs, *ge;
+                LIME_TRY(alloc(ctx, &gs, (size_t)nr));
+                LIME_TRY(alloc(ctx, &ge, (size_t)nr));
+                if (nr > 0) {
+                    LIME_HIP(hipMemcpyAsync(gs, res->gs, 4 * (size_t)nr, hipMemcpyDeviceToDevice,
+                                            S(ctx)));
+                    LIME_HIP(hipMemcpyAsync(ge, res->ge, 4 * (size_t)nr, hipMemcpyDeviceToDevice,
+                                            S(ctx)));
+                }
+                release(ctx, res->gs);
+                release(ctx, res->ge);
+                res->gs = gs;
+                res->ge = ge;
+            }
+            res->n = nr;
+            return LIME_OK;
+        }
+        // the bound did not hold (it always should): count first, then write
+        release(ctx, res->gs);
+        release(ctx, res->ge);
+    }
     uint32_t *tcnt, *toff, *total;
     LIME_TRY(alloc(ctx, &tcnt, (size_t)nt));
     LIME_TRY(alloc(ctx, &toff, (size_t)nt));

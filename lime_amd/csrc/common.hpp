@@ -123,6 +123,7 @@ struct lime_bitset {
     lime_ctx *ctx = nullptr;
     uint64_t *words = nullptr;
     int64_t n_words = 0;
+    int64_t runs_bound = -1;  // upper bound on its runs (rows painted), -1 unknown
     int64_t span = 0;
     uint32_t *d_off = nullptr;
     int32_t n_contigs = 0;

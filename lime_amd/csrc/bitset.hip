@@ -85,21 +85,30 @@ __device__ __forceinline__ void paint_lds(unsigned long long *img, uint64_t s, u
     }
 }
 
+// first row of every paint tile (4 bins), searched once per tile up front
+// instead of by each painting block (27 dependent loads on its critical path)
+__global__ __launch_bounds__(BB) void k_tile_starts(const uint32_t *__restrict__ gs, int64_t n,
+                                                    int64_t nt, uint32_t *__restrict__ tstart) {
+    const int64_t t = (int64_t)blockIdx.x * BB + threadIdx.x;
+    if (t > nt) return;
+    const uint64_t bin = ((uint64_t)t * BT * 64) >> BINSH;
+    tstart[t] = (uint32_t)(bin > 0xffffffffull ? n : lb_bin(gs, n, (uint32_t)bin));
+}
+
 __global__ __launch_bounds__(BB) void k_paint_rows(const uint32_t *__restrict__ gs,
-                                                   const uint32_t *__restrict__ ge, int64_t n,
+                                                   const uint32_t *__restrict__ ge,
+                                                   const uint32_t *__restrict__ tstart, int64_t n,
                                                    uint64_t *__restrict__ words, int64_t n_words,
                                                    uint64_t *__restrict__ cross,
                                                    unsigned int *__restrict__ ncross) {
     static_assert((int64_t)BT * 64 == (1ll << (BINSH + 2)), "tile = 4 bins");
     __shared__ unsigned long long img[BT];
-    __shared__ int64_t s_r[2];
     const int64_t w0 = (int64_t)blockIdx.x * BT;
     const uint64_t blo = (uint64_t)w0 * 64, bhi = blo + (uint64_t)BT * 64;
     for (int i = threadIdx.x; i < BT; i += BB) img[i] = 0ull;
-    if (threadIdx.x == 0) s_r[0] = lb_bin(gs, n, (uint32_t)(blo >> BINSH));
-    if (threadIdx.x == 64) s_r[1] = bhi >> BINSH > 0xffffffffull ? n : lb_bin(gs, n, (uint32_t)(bhi >> BINSH));
+    const int64_t r0 = tstart[blockIdx.x], r1 = tstart[blockIdx.x + 1];
     __syncthreads();
-    for (int64_t r = s_r[0] + threadIdx.x; r < s_r[1]; r += BB) {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += BB) {
         const uint64_t g0 = gs[r], g1 = ge[r];
         if (g1 <= g0) continue;
         paint_lds(img, g0 - blo, min(g1, bhi) - blo);
@@ -397,9 +406,14 @@ int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     LIME_TRY(alloc(ctx, &cross, (size_t)std::max<int64_t>(a->n, 1)));
     LIME_TRY(alloc(ctx, &ncross, 1));
     LIME_HIP(hipMemsetAsync(ncross, 0, sizeof(unsigned int), S(ctx)));
-    if (nt > 0)
+    uint32_t *tstart;
+    LIME_TRY(alloc(ctx, &tstart, (size_t)nt + 1));
+    if (nt > 0) {
+        hipLaunchKernelGGL(k_tile_starts, dim3(blocks_for(nt + 1, BB)), dim3(BB), 0, S(ctx),
+                           a->gs, a->n, nt, tstart);
         hipLaunchKernelGGL(k_paint_rows, dim3((unsigned)nt), dim3(BB), 0, S(ctx), a->gs, a->ge,
-                           a->n, bs->words, bs->n_words, cross, ncross);
+                           (const uint32_t *)tstart, a->n, bs->words, bs->n_words, cross, ncross);
+    }
     if (a->n > 0)
         hipLaunchKernelGGL(k_paint_cross, dim3(std::min<unsigned>(blocks_for(a->n, BB), 2048u)),
                            dim3(BB), 0, S(ctx),
@@ -407,6 +421,7 @@ int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     LIME_HIP(hipGetLastError());
     release(ctx, cross);
     release(ctx, ncross);
+    release(ctx, tstart);
     return LIME_OK;
 }
 

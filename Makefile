@@ -45,7 +45,7 @@ $(LIB): $(HIP_OBJS) $(CPP_OBJS)
 
 $(ORACLE): oracle/lime_oracle.c
 	@mkdir -p oracle/build
-	$(CC) -O2 -fPIC -shared -std=c99 -o $@ $<
+	$(CC) -O2 -fPIC -shared -std=c99 -pthread -o $@ $<
 
 $(CLI): lime_amd/cli/lime_submit.cpp include/lime_amd.hpp include/lime_amd.h $(LIB)
 	@mkdir -p bin

@@ -132,7 +132,7 @@ int lime_set_create_global(lime_ctx *ctx, const lime_space *space, int64_t n,
                            const uint32_t *d_row, lime_set **out);
 int lime_set_destroy(lime_set *set);
 int64_t lime_set_size(const lime_set *set);
-/* first sorted row with gstart >= gkey (-1 on error) */
+/* first sorted row with gstart >= gkey; on error -(LIME_ERR_*) */
 int64_t lime_set_lower_bound(const lime_set *set, uint32_t gkey);
 /* device-to-device copy of sorted rows [first, first + count) */
 int lime_set_copy_rows_device(const lime_set *set, int64_t first, int64_t count, uint32_t *d_gstart,
@@ -211,6 +211,14 @@ int lime_result_device_arrays(const lime_result *res, const uint32_t **gstart,
 int lime_result_copy_range(const lime_result *res, int64_t first, int64_t count, uint32_t *gstart,
                            uint32_t *gend);
 int lime_result_destroy(lime_result *res);
+/* Order-independent checksum of a result on the device (verification at
+ * scale): reg = sum / xor over regions of
+ * mix64(lime_pair_hash(start, end, a_row, b_row) + contig) with contig-local
+ * start / end and 0xffffffff for an absent row; grp (merge results, else 0) =
+ * sum / xor over input rows r of mix64(r << 32 | run of r), the Iterable[T]
+ * grouping.  grp_sum / grp_xor may be NULL. */
+int lime_result_checksum(const lime_result *res, uint64_t *reg_sum, uint64_t *reg_xor,
+                         uint64_t *grp_sum, uint64_t *grp_xor);
 /* BED writer on the device (the output side of loadBed, SURVEY.md 8(f) row
  * 1): the rows of a sorted set (in sorted order) or of a result, as
  * "chrom<TAB>start<TAB>end\n" lines in contig-local coordinates, into a

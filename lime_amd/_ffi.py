@@ -88,6 +88,7 @@ SIGNATURES = {
     "lime_result_run_of_row": (C.c_int, [vp, P(i64)]),
     "lime_result_device_arrays": (C.c_int, [vp, pp, pp]),
     "lime_result_destroy": (C.c_int, [vp]),
+    "lime_result_checksum": (C.c_int, [vp, P(u64), P(u64), P(u64), P(u64)]),
     "lime_bitset_from_set": (C.c_int, [vp, vp, pp]),
     "lime_bitset_from_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_bitset_runs": (C.c_int, [vp, C.c_int, vp, vp, pp, P(i64)]),

@@ -138,6 +138,67 @@ __global__ void k_set_lower_bound(const uint32_t *gs, int64_t n, uint32_t key, i
     if (threadIdx.x == 0) *out = dev::lower_bound(gs, 0, n, key);
 }
 
+// Order-independent checksum of a result (SURVEY.md 8(d) "Verification at
+// scale"), restated by the oracle (oracle.result_checksum / lo_merge_mt):
+//   regions   sum / xor over regions of mix64(pair_hash(s, e, a, b) + contig),
+//             (s, e) contig-local, a / b the rows or 0xffffffff if absent
+//   grouping  (merge) sum / xor over sorted rows j of
+//             mix64(row_j << 32 | run_of_sorted_j)
+__global__ __launch_bounds__(256) void k_result_checksum(
+    const uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge,
+    const uint32_t *__restrict__ ar, const uint32_t *__restrict__ br, int64_t n,
+    const uint32_t *__restrict__ off, int32_t nc, const uint32_t *__restrict__ row,
+    const uint32_t *__restrict__ rid, int64_t nrows, unsigned long long *__restrict__ out) {
+    uint64_t rs = 0, rx = 0, gsum = 0, gx = 0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = gs[i];
+        const int64_t c = dev::upper_bound(off, 0, (int64_t)nc, g) - 1;
+        const uint32_t o = off[c < 0 ? 0 : c];
+        const uint64_t h = dev::mix64(dev::pair_hash(g - o, ge[i] - o, ar ? ar[i] : 0xffffffffu,
+                                                     br ? br[i] : 0xffffffffu) +
+                                      (uint64_t)c);
+        rs += h;
+        rx ^= h;
+    }
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; rid && j < nrows; j += stride) {
+        const uint64_t h = dev::mix64(((uint64_t)row[j] << 32) | rid[j]);
+        gsum += h;
+        gx ^= h;
+    }
+    rs = dev::wave_reduce_sum(rs);
+    gsum = dev::wave_reduce_sum(gsum);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        rx ^= __shfl_xor(rx, d, 64);
+        gx ^= __shfl_xor(gx, d, 64);
+    }
+    if (dev::lane_id() == 0) {
+        atomicAdd(&out[0], (unsigned long long)rs);
+        atomicXor(&out[1], (unsigned long long)rx);
+        atomicAdd(&out[2], (unsigned long long)gsum);
+        atomicXor(&out[3], (unsigned long long)gx);
+    }
+}
+
+// RAII release of a pool block on every return path
+template <typename T>
+struct PoolGuard {
+    lime_ctx *ctx;
+    T *&p;
+    ~PoolGuard() { release(ctx, p); }
+};
+
+// every set / bitset an operator reads must belong to the operator's context:
+// its arrays live in that context's pool and device (a foreign set
+// could otherwise be read on another device, or have lazily built state
+// allocated from, and freed into, the wrong pool)
+static int same_ctx(lime_ctx *ctx, const lime_set *s) {
+    if (s && s->ctx != ctx)
+        return fail(LIME_ERR_ARG, "set belongs to another context (one context per thread)");
+    return LIME_OK;
+}
+
 static int32_t contig_of(const std::vector<uint32_t> &off, int32_t nc, uint32_t g) {
     // largest c in [0, nc) with off[c] <= g
     auto it = std::upper_bound(off.begin(), off.begin() + nc, g);
@@ -482,16 +543,19 @@ int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const
 }
 
 int64_t lime_set_lower_bound(const lime_set *s, uint32_t gkey) {
-    if (!s) return fail(LIME_ERR_ARG, "set is null"), -1;
+    if (!s) return -(int64_t)fail(LIME_ERR_ARG, "set is null");
     lime_ctx *ctx = s->ctx;
     hipSetDevice(ctx->device);
-    int64_t *d;
-    if (alloc(ctx, &d, 1)) return -1;
+    int64_t *d = nullptr;
+    if (int rc = alloc(ctx, &d, 1)) return -(int64_t)rc;
+    PoolGuard<int64_t> guard{ctx, d};
     hipLaunchKernelGGL(k_set_lower_bound, dim3(1), dim3(64), 0, S(ctx), (const uint32_t *)s->gs,
                        s->n, gkey, d);
+    if (hipError_t e = hipGetLastError())
+        return -(int64_t)fail(LIME_ERR_DEVICE, std::string("lower_bound launch: ") +
+                                                   hipGetErrorString(e));
     int64_t h = -1;
-    if (hipGetLastError() != hipSuccess || read_back(ctx, &h, d, 8)) h = -1;
-    release(ctx, d);
+    if (int rc = read_back(ctx, &h, d, 8)) return -(int64_t)rc;
     return h;
 }
 
@@ -568,6 +632,8 @@ int lime_intersect_count_owned(lime_ctx *ctx, const lime_set *a, const lime_set 
     if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad intersect arguments");
     if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
     if (a_owned > a->n || b_owned > b->n) return fail(LIME_ERR_ARG, "owned rows exceed set size");
+    LIME_TRY(same_ctx(ctx, a));
+    LIME_TRY(same_ctx(ctx, b));
     hipSetDevice(ctx->device);
     PairsPlan *pl = nullptr;
     LIME_TRY(intersect_plan(ctx, a, b, threshold, a_owned, b_owned, &pl));
@@ -582,6 +648,8 @@ int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64
     if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad window arguments");
     if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
     if (distance < 0) return fail(LIME_ERR_ARG, "window distance must be >= 0");
+    LIME_TRY(same_ctx(ctx, a));
+    LIME_TRY(same_ctx(ctx, b));
     hipSetDevice(ctx->device);
     PairsPlan *pl = nullptr;
     LIME_TRY(window_plan(ctx, a, b, distance, &pl));
@@ -599,6 +667,8 @@ int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int 
     if (!a->strand_in || !b->strand_in || a->min_shift || b->min_shift)
         return fail(LIME_ERR_ARG,
                     "closest needs sets in full RegionOrdering (lime_set_create_host_stranded)");
+    LIME_TRY(same_ctx(ctx, a));
+    LIME_TRY(same_ctx(ctx, b));
     hipSetDevice(ctx->device);
     ClosestPlan *cl = nullptr;
     LIME_TRY(closest_plan(ctx, a, b, mode, &cl));
@@ -620,8 +690,9 @@ int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lim
     lime_ctx *ctx = plan->ctx;
     hipSetDevice(ctx->device);
     const int64_t chunk = 1 << 24;
-    lime_pair *stage;
+    lime_pair *stage = nullptr;
     LIME_TRY(alloc(ctx, &stage, (size_t)std::min(chunk, std::max(count, (int64_t)1))));
+    PoolGuard<lime_pair> guard{ctx, stage};  // released on every return path
     for (int64_t f = 0; f < count; f += chunk) {
         const int64_t c = std::min(chunk, count - f);
         LIME_TRY(pairs_fill(plan, first + f, c, stage));
@@ -629,7 +700,6 @@ int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lim
                                 hipMemcpyDeviceToHost, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));
     }
-    release(ctx, stage);
     return LIME_OK;
 }
 
@@ -653,6 +723,7 @@ int lime_pairs_destroy(lime_pairs *plan) {
 // ----------------------------------------------------------------- results
 int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs) {
     if (!ctx || !a || !out) return fail(LIME_ERR_ARG, "bad merge arguments");
+    LIME_TRY(same_ctx(ctx, a));
     hipSetDevice(ctx->device);
     lime_result *r = new_result(ctx, a);
     r->src = a;
@@ -672,6 +743,8 @@ int lime_subtract(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t t
     if (mode != LIME_SUBTRACT_LIME && mode != LIME_SUBTRACT_SET)
         return fail(LIME_ERR_ARG, "unknown subtract mode");
     if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
+    LIME_TRY(same_ctx(ctx, a));
+    LIME_TRY(same_ctx(ctx, b));
     hipSetDevice(ctx->device);
     lime_result *r = new_result(ctx, a);
     int rc = subtract_run(ctx, a, b, threshold, mode, r);
@@ -689,6 +762,7 @@ int lime_complement(lime_ctx *ctx, const lime_space *genome, const lime_set *a, 
     if (!ctx || !genome || !a || !out) return fail(LIME_ERR_ARG, "bad complement arguments");
     if (genome->n != a->n_contigs || genome->off != a->off)
         return fail(LIME_ERR_CONTIG, "set was not created in the genome's coordinate space");
+    LIME_TRY(same_ctx(ctx, a));
     hipSetDevice(ctx->device);
     lime_result runs;
     runs.ctx = ctx;
@@ -779,6 +853,42 @@ int lime_result_device_arrays(const lime_result *r, const uint32_t **gs, const u
     return LIME_OK;
 }
 
+int lime_result_checksum(const lime_result *r, uint64_t *reg_sum, uint64_t *reg_xor,
+                         uint64_t *grp_sum, uint64_t *grp_xor) {
+    if (!r || !reg_sum || !reg_xor) return fail(LIME_ERR_ARG, "bad checksum arguments");
+    lime_ctx *ctx = r->ctx;
+    hipSetDevice(ctx->device);
+    uint32_t *d_off = nullptr;
+    unsigned long long *d_out = nullptr;
+    LIME_TRY(alloc(ctx, &d_off, (size_t)r->n_contigs + 1));
+    PoolGuard<uint32_t> g1{ctx, d_off};
+    LIME_TRY(alloc(ctx, &d_out, 4));
+    PoolGuard<unsigned long long> g2{ctx, d_out};
+    LIME_HIP(hipMemcpyAsync(d_off, r->off.data(), 4 * ((size_t)r->n_contigs + 1),
+                            hipMemcpyHostToDevice, S(ctx)));
+    LIME_HIP(hipMemsetAsync(d_out, 0, 32, S(ctx)));
+    const bool grp = r->run_of_sorted && r->src;
+    const int64_t nrows = grp ? r->src->n : 0;
+    const int64_t work = std::max<int64_t>(std::max<int64_t>(r->n, nrows), 1);
+    const unsigned grid = std::min<unsigned>(blocks_for(work, 256), 4096u);
+    hipLaunchKernelGGL(k_result_checksum, dim3(grid), dim3(256), 0, S(ctx),
+                       (const uint32_t *)r->gs, (const uint32_t *)r->ge,
+                       (const uint32_t *)r->a_row, (const uint32_t *)r->b_row, r->n,
+                       (const uint32_t *)d_off, r->n_contigs,
+                       grp ? (const uint32_t *)r->src->row : nullptr,
+                       grp ? (const uint32_t *)r->run_of_sorted : nullptr, nrows, d_out);
+    LIME_HIP(hipGetLastError());
+    // (hipMemcpy from pageable memory would not order against the stream: the
+    // pinned-scratch read_back does)
+    uint64_t h[4];
+    LIME_TRY(read_back(ctx, h, d_out, 32));
+    *reg_sum = h[0];
+    *reg_xor = h[1];
+    if (grp_sum) *grp_sum = h[2];
+    if (grp_xor) *grp_xor = h[3];
+    return LIME_OK;
+}
+
 int lime_result_destroy(lime_result *r) {
     if (!r) return LIME_OK;
     lime_ctx *ctx = r->ctx;
@@ -794,6 +904,7 @@ int lime_result_destroy(lime_result *r) {
 // ------------------------------------------------------------------ bitset
 int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out) {
     if (!ctx || !a || !out) return fail(LIME_ERR_ARG, "bad bitset arguments");
+    LIME_TRY(same_ctx(ctx, a));
     hipSetDevice(ctx->device);
     lime_bitset *bs = new lime_bitset();
     bs->ctx = ctx;
@@ -847,6 +958,8 @@ int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bit
     if (!ctx || !a || !out || op < 0 || op > 3 || ((op == 2 || op == 3) && !b))
         return fail(LIME_ERR_ARG, "bad bitset op arguments");
     if (b && (b->off != a->off)) return fail(LIME_ERR_ARG, "bitsets over different spaces");
+    if (a->ctx != ctx || (b && b->ctx != ctx))
+        return fail(LIME_ERR_ARG, "bitset belongs to another context (one context per thread)");
     hipSetDevice(ctx->device);
     const lime_bitset *sets[2] = {a, b};
     lime_result *r = bitset_result(ctx, a);
@@ -863,8 +976,12 @@ int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bit
 int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, lime_result **out,
                          int64_t *n) {
     if (!ctx || k < 1 || !sets || !out) return fail(LIME_ERR_ARG, "bad bitset and arguments");
-    for (int i = 1; i < k; ++i)
+    for (int i = 0; i < k; ++i) {
+        if (!sets[i]) return fail(LIME_ERR_ARG, "bitset is null");
         if (sets[i]->off != sets[0]->off) return fail(LIME_ERR_ARG, "bitsets over different spaces");
+        if (sets[i]->ctx != ctx)
+            return fail(LIME_ERR_ARG, "bitset belongs to another context (one context per thread)");
+    }
     hipSetDevice(ctx->device);
     lime_result *r = bitset_result(ctx, sets[0]);
     int rc = bitset_runs(ctx, 4, k, sets, r);
@@ -878,7 +995,7 @@ int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, l
 }
 
 int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a) {
-    if (!ctx || !a) return -1;
+    if (!ctx || !a || a->ctx != ctx) return -1;
     hipSetDevice(ctx->device);
     return bitset_popcount(ctx, a);
 }

@@ -54,6 +54,8 @@ struct PairsPlan {
     int64_t reach = -1;
 };
 
+void intersect_free(PairsPlan *pl);
+
 namespace {
 
 constexpr int IB = 256;
@@ -201,7 +203,8 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
                                               const uint32_t *__restrict__ win,
                                               uint32_t *__restrict__ olo,
                                               uint32_t *__restrict__ ocnt,
-                                              uint64_t *__restrict__ tcnt) {
+                                              uint64_t *__restrict__ tcnt,
+                                              uint32_t *__restrict__ oflow) {
     __shared__ uint32_t wgs[WCAP];
     __shared__ uint64_t red[IB / 64];
     __shared__ uint32_t scratch[IB / 64 + 1];
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
         }
     }
     uint32_t cv[OPT];
-    uint32_t csum = 0;
+    uint64_t csum = 0;  // 4 owners can exceed 2^32 candidates (deep pile-ups)
 #pragma unroll
     for (int k = 0; k < OPT; ++k) {
         const int64_t j = o0 + threadIdx.x * OPT + k;
@@ -290,10 +293,13 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
         lov[k] = lo;
         csum += cv[k];
     }
+    // tile-local offsets are u32 (the fill stages them as such): a tile with
+    // 2^32 or more pairs is flagged below and the plan fails with
+    // LIME_ERR_OVERFLOW instead of wrapping
     uint32_t run = 0;
     if (OFFS) {
         uint32_t tot;
-        run = dev::block_exclusive_sum<IB>(csum, scratch, &tot);
+        run = dev::block_exclusive_sum<IB>((uint32_t)csum, scratch, &tot);
     }
     // blocked -> lane-consecutive through LDS (the window image is dead
     // now), so the olo / ocnt stores are coalesced whatever owner0's alignment
@@ -322,6 +328,7 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
         uint64_t s = 0;
         for (int i = 0; i < IB / 64; ++i) s += red[i];
         tcnt[sa.tile0 + t] = s;
+        if (s > 0xffffffffull && oflow) atomicOr(oflow, 1u);
     }
 }
 
@@ -857,10 +864,13 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
         (rc = alloc(ctx, &pl->ocnt, (size_t)(a_own + b_own))) ||
         (rc = alloc(ctx, &pl->toff, (size_t)nt)) || (rc = alloc(ctx, &pl->win, (size_t)2 * nt)) ||
         (rc = alloc(ctx, &pl->tseg, (size_t)nt)) ||
-        (rc = alloc(ctx, &tcnt, (size_t)nt)) || (rc = alloc(ctx, &total, 1))) {
+        (rc = alloc(ctx, &tcnt, (size_t)nt)) || (rc = alloc(ctx, &total, 2))) {
         delete pl;
         return rc;
     }
+    // total[1]: overflow flag of the u32 tile-local offsets
+    uint32_t *oflow = reinterpret_cast<uint32_t *>(total + 1);
+    LIME_HIP(hipMemsetAsync(total + 1, 0, sizeof(uint64_t), S(ctx)));
     if (A->n > 0 && B->n > 0) {
         for (int st = 0; st < 2; ++st) {
             const lime_set *O = st == 0 ? A : B;
@@ -877,11 +887,11 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
             if (pl->filtered)
                 hipLaunchKernelGGL((k_count<true, false>), dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
                                    pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
-                                   tcnt);
+                                   tcnt, oflow);
             else
                 hipLaunchKernelGGL((k_count<false, true>), dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa,
                                    pl->tp, threshold, (const uint32_t *)pl->win, pl->olo, pl->ocnt,
-                                   tcnt);
+                                   tcnt, oflow);
             LIME_HIP(hipGetLastError());
         }
     } else {
@@ -891,11 +901,16 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
                                 S(ctx)));
     }
     LIME_TRY(scan_exclusive_u64(ctx, tcnt, pl->toff, nt, total));
-    uint64_t tot = 0;
-    LIME_TRY(read_back(ctx, &tot, total, sizeof(tot)));
+    uint64_t tot[2] = {0, 0};
+    LIME_TRY(read_back(ctx, tot, total, sizeof(tot)));
     release(ctx, tcnt);
     release(ctx, total);
-    pl->total = (int64_t)tot;
+    if (tot[1]) {
+        intersect_free(pl);
+        return fail(LIME_ERR_OVERFLOW,
+                    "a tile of 1024 owner rows has 2^32 or more candidate pairs (pile-up)");
+    }
+    pl->total = (int64_t)tot[0];
     *out = pl;
     return LIME_OK;
 }
@@ -921,7 +936,7 @@ int owner_ranges(lime_ctx *ctx, const lime_set *O, const lime_set *P, int st, in
                        win, (const uint32_t *)nullptr, 0, (uint32_t *)nullptr);
     hipLaunchKernelGGL((k_count<false, false>), dim3((unsigned)ntl), dim3(IB), 0, S(ctx), sa, tp,
                        threshold,
-                       (const uint32_t *)win, olo, ocnt, tcnt);
+                       (const uint32_t *)win, olo, ocnt, tcnt, (uint32_t *)nullptr);
     LIME_HIP(hipGetLastError());
     release(ctx, win);
     release(ctx, tcnt);

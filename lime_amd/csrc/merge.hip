@@ -395,11 +395,16 @@ int prefix_max_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n) 
     return LIME_OK;
 }
 
+// Lazily built state of a const set: built from and owned by the SET's
+// context (operators already reject sets of another context), under that
+// context's lock so two calls cannot both build it.
 int build_prefix_max(lime_ctx *ctx, const lime_set *set) {
+    if (set->ctx != ctx) return fail(LIME_ERR_ARG, "set belongs to another context");
+    std::lock_guard<std::mutex> lock(set->ctx->mu);
     if (set->pmax) return LIME_OK;
     uint32_t *pm;
-    LIME_TRY(alloc(ctx, &pm, (size_t)set->n));
-    LIME_TRY(prefix_max_u32(ctx, set->ge, pm, set->n));
+    LIME_TRY(alloc(set->ctx, &pm, (size_t)set->n));
+    LIME_TRY(prefix_max_u32(set->ctx, set->ge, pm, set->n));
     set->pmax = pm;
     return LIME_OK;
 }

@@ -122,7 +122,7 @@ class IntervalSet:
         """first sorted row with global start >= gkey"""
         r = _lib().lime_set_lower_bound(self._h, int(gkey))
         if r < 0:
-            check(_ffi.LIME_ERR_ARG if r == -1 else int(r))
+            check(int(-r))
         return int(r)
 
     def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
@@ -172,6 +172,13 @@ class Result:
     def to_bed(self):
         """the result's regions as BED3 text, formatted on the device"""
         return _format_bed(_lib().lime_result_format_bed, self._h, self.space)
+
+    def checksum(self):
+        """(reg_sum, reg_xor, grp_sum, grp_xor): order-independent checksums of
+        the regions and (merge) of the row -> run grouping, on the device"""
+        v = [u64() for _ in range(4)]
+        check(_lib().lime_result_checksum(self._h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
     def run_of_row(self, n_rows):
         out = np.zeros(n_rows, dtype=np.int64)

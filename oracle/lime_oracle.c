@@ -40,6 +40,8 @@
  * Output arrays use the two-call protocol: each op returns the exact output
  * count and writes min(count, cap) records, so callers ask with cap = 0 first.
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -113,9 +115,32 @@ typedef struct {
     int64_t count, cap;
     int32_t *contig;
     int64_t *start, *end, *lrow, *rrow;
+    /* hash: also fold lo_pair_hash(start, end, lrow, rrow) into (hsum, hxor),
+     * the order-independent checksum of SURVEY.md 8(d); grow: the arrays are
+     * owned and doubled on demand (the contig-sharded drivers below) */
+    int hash, grow;
+    uint64_t hsum, hxor;
 } lo_out;
 
+uint64_t lo_pair_hash(uint32_t start, uint32_t end, uint32_t a, uint32_t b);
+
+static void lo_out_grow(lo_out *o) {
+    int64_t cap = o->cap ? 2 * o->cap : 1024;
+    o->contig = (int32_t *)realloc(o->contig, sizeof(int32_t) * (size_t)cap);
+    o->start = (int64_t *)realloc(o->start, sizeof(int64_t) * (size_t)cap);
+    o->end = (int64_t *)realloc(o->end, sizeof(int64_t) * (size_t)cap);
+    o->lrow = (int64_t *)realloc(o->lrow, sizeof(int64_t) * (size_t)cap);
+    o->rrow = (int64_t *)realloc(o->rrow, sizeof(int64_t) * (size_t)cap);
+    o->cap = cap;
+}
+
 static void lo_emit(lo_out *o, int32_t c, int64_t s, int64_t e, int64_t lr, int64_t rr) {
+    if (o->hash) {
+        uint64_t h = lo_pair_hash((uint32_t)s, (uint32_t)e, (uint32_t)lr, (uint32_t)rr);
+        o->hsum += h;
+        o->hxor ^= h;
+    }
+    if (o->grow && o->count == o->cap) lo_out_grow(o);
     if (o->count < o->cap) {
         int64_t k = o->count;
         if (o->contig) o->contig[k] = c;
@@ -180,13 +205,8 @@ static void advance_cache(lo_cache *c, const lo_region *right, int64_t nr, int64
 /* Intersection.scala:58-69 processHits: every cached R with
  * overlapsBy(L, R) >= threshold, in cache order, emits
  * (L.intersection(R), (L.value, R.value)). */
-int64_t lo_intersect(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
-                     const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
-                     const int64_t *re, const int8_t *rstr, int64_t threshold, int64_t cap,
-                     int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow, int64_t *orrow) {
-    lo_region *L = lo_load(nl, lc, ls, le, lstr);
-    lo_region *R = lo_load(nr, rc, rs, re, rstr);
-    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+static void lo_intersect_sorted(const lo_region *L, int64_t nl, const lo_region *R, int64_t nr,
+                                int64_t threshold, lo_out *o) {
     lo_cache cache = {0};
     int64_t rpos = 0;
     for (int64_t i = 0; i < nl; ++i) { /* SetTheory.scala:181-186 */
@@ -198,11 +218,21 @@ int64_t lo_intersect(int64_t nl, const int32_t *lc, const int64_t *ls, const int
             if (lo_overlaps_by_at_least(cur, r, threshold)) {
                 int64_t s = cur->start > r->start ? cur->start : r->start;
                 int64_t e = cur->end < r->end ? cur->end : r->end;
-                lo_emit(&out, cur->contig, s, e, cur->row, r->row);
+                lo_emit(o, cur->contig, s, e, cur->row, r->row);
             }
         }
     }
     free(cache.v);
+}
+
+int64_t lo_intersect(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
+                     const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
+                     const int64_t *re, const int8_t *rstr, int64_t threshold, int64_t cap,
+                     int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow, int64_t *orrow) {
+    lo_region *L = lo_load(nl, lc, ls, le, lstr);
+    lo_region *R = lo_load(nr, rc, rs, re, rstr);
+    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+    lo_intersect_sorted(L, nl, R, nr, threshold, &out);
     free(L);
     free(R);
     return out.count;
@@ -457,10 +487,8 @@ int64_t lo_subtract(int64_t nl, const int32_t *lc, const int64_t *ls, const int6
  * condition(head, next) = head.overlaps(next) (threshold not passed -> 0);
  * primitive = hull.  run_of_row[row] receives the index of the run the input
  * row was folded into (the Iterable[T] grouping). */
-int64_t lo_merge(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e,
-                 const int8_t *strand, int64_t cap, int32_t *oc, int64_t *os, int64_t *oe,
-                 int8_t *ostrand, int64_t *run_of_row) {
-    lo_region *A = lo_load(n, c, s, e, strand);
+static int64_t lo_merge_sorted(const lo_region *A, int64_t n, int64_t cap, int32_t *oc,
+                               int64_t *os, int64_t *oe, int8_t *ostrand, int64_t *run_of_row) {
     int64_t count = 0;
     lo_region head;
     for (int64_t i = 0; i < n; ++i) {
@@ -488,6 +516,14 @@ int64_t lo_merge(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e
         if (oe) oe[count - 1] = head.end;
         if (ostrand) ostrand[count - 1] = head.strand;
     }
+    return count;
+}
+
+int64_t lo_merge(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e,
+                 const int8_t *strand, int64_t cap, int32_t *oc, int64_t *os, int64_t *oe,
+                 int8_t *ostrand, int64_t *run_of_row) {
+    lo_region *A = lo_load(n, c, s, e, strand);
+    int64_t count = lo_merge_sorted(A, n, cap, oc, os, oe, ostrand, run_of_row);
     free(A);
     return count;
 }
@@ -551,4 +587,248 @@ uint64_t lo_pair_hash(uint32_t start, uint32_t end, uint32_t a, uint32_t b) {
     uint64_t x = ((uint64_t)start << 32) | end;
     uint64_t y = ((uint64_t)a << 32) | b;
     return lo_mix64(x ^ lo_mix64(y));
+}
+
+/* ------------------------------------------- contig-sharded drivers (MT) */
+
+/* The reference runs one Spark task per range partition; every op here is
+ * contig-local (no predicate holds across reference names), so sharding the
+ * rows by contig and running the same per-partition code (lo_intersect_sorted,
+ * lo_merge_sorted) on each contig in its own thread gives exactly the P = 1
+ * result, with outputs concatenated in contig (String) order.  These drivers
+ * take the device's u32 contig-local coordinates so that full-size inputs
+ * (1e8-5e8 rows) need no int64 copy; rows keep their input index.  They
+ * serve the size-independent parity checks of SURVEY.md 8(d) ("Verification
+ * at scale": count plus order-independent checksum) and the CPU baseline. */
+
+typedef struct {
+    int64_t n;
+    const int32_t *c;
+    const uint32_t *s, *e;
+    int64_t *off; /* n_contigs + 1: rows of contig k are idx[off[k] .. off[k+1]) */
+    int64_t *idx;
+} lo_groups;
+
+static void lo_group(lo_groups *g, int32_t nc, int64_t n, const int32_t *c, const uint32_t *s,
+                     const uint32_t *e) {
+    g->n = n;
+    g->c = c;
+    g->s = s;
+    g->e = e;
+    g->off = (int64_t *)calloc((size_t)nc + 2, sizeof(int64_t));
+    g->idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    for (int64_t i = 0; i < n; ++i) g->off[c[i] + 1]++;
+    for (int32_t k = 0; k < nc; ++k) g->off[k + 1] += g->off[k];
+    int64_t *pos = (int64_t *)malloc(sizeof(int64_t) * ((size_t)nc + 1));
+    memcpy(pos, g->off, sizeof(int64_t) * ((size_t)nc + 1));
+    for (int64_t i = 0; i < n; ++i) g->idx[pos[c[i]]++] = i;
+    free(pos);
+}
+
+static void lo_ungroup(lo_groups *g) {
+    free(g->off);
+    free(g->idx);
+}
+
+/* the rows of contig k as sorted regions (RegionOrdering, ties by row) */
+static lo_region *lo_load_group(const lo_groups *g, int32_t k, int64_t *n_out) {
+    const int64_t a = g->off[k], b = g->off[k + 1];
+    lo_region *r = (lo_region *)malloc(sizeof(lo_region) * (size_t)(b > a ? b - a : 1));
+    for (int64_t j = a; j < b; ++j) {
+        const int64_t i = g->idx[j];
+        lo_region *x = &r[j - a];
+        x->contig = k;
+        x->start = g->s[i];
+        x->end = g->e[i];
+        x->strand = 0;
+        x->row = i;
+    }
+    qsort(r, (size_t)(b - a), sizeof(lo_region), lo_qsort_cmp);
+    *n_out = b - a;
+    return r;
+}
+
+typedef struct {
+    int op; /* 0 intersect, 1 merge */
+    int32_t nc;
+    lo_groups L, R;
+    int64_t threshold;
+    int keep;            /* buffer the records (else count + checksum only) */
+    int32_t *order;      /* contigs, largest first */
+    int next;            /* work-queue head (atomic) */
+    lo_out *res;         /* per contig */
+    int64_t *run_of_row; /* merge: local run id per input row */
+} lo_mt;
+
+static void *lo_mt_worker(void *arg) {
+    lo_mt *m = (lo_mt *)arg;
+    for (;;) {
+        const int q = __sync_fetch_and_add(&m->next, 1);
+        if (q >= m->nc) break;
+        const int32_t k = m->order[q];
+        lo_out *o = &m->res[k];
+        int64_t nl = 0, nr = 0;
+        lo_region *L = lo_load_group(&m->L, k, &nl);
+        if (m->op == 0) {
+            lo_region *R = lo_load_group(&m->R, k, &nr);
+            o->hash = 1;
+            o->grow = m->keep;
+            lo_intersect_sorted(L, nl, R, nr, m->threshold, o);
+            free(R);
+        } else {
+            /* at most one run per row: the buffers are sized by the rows */
+            o->cap = nl;
+            o->start = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nl > 0 ? nl : 1));
+            o->end = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nl > 0 ? nl : 1));
+            o->count = lo_merge_sorted(L, nl, nl, NULL, o->start, o->end, NULL, m->run_of_row);
+        }
+        free(L);
+    }
+    return NULL;
+}
+
+static void lo_mt_run(lo_mt *m, int nthreads) {
+    /* contigs largest first, so the long shards start early */
+    m->order = (int32_t *)malloc(sizeof(int32_t) * (size_t)(m->nc > 0 ? m->nc : 1));
+    for (int32_t k = 0; k < m->nc; ++k) m->order[k] = k;
+    for (int32_t a = 1; a < m->nc; ++a) { /* insertion sort: nc is small */
+        const int32_t k = m->order[a];
+        const int64_t w = (m->L.off[k + 1] - m->L.off[k]) + (m->op == 0 ? m->R.off[k + 1] - m->R.off[k] : 0);
+        int32_t b = a - 1;
+        while (b >= 0) {
+            const int32_t j = m->order[b];
+            const int64_t wj = (m->L.off[j + 1] - m->L.off[j]) +
+                               (m->op == 0 ? m->R.off[j + 1] - m->R.off[j] : 0);
+            if (wj >= w) break;
+            m->order[b + 1] = j;
+            --b;
+        }
+        m->order[b + 1] = k;
+    }
+    m->next = 0;
+    m->res = (lo_out *)calloc((size_t)(m->nc > 0 ? m->nc : 1), sizeof(lo_out));
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    int started = 0;
+    for (int t = 1; t < nthreads; ++t)
+        if (pthread_create(&th[started], NULL, lo_mt_worker, m) == 0) ++started;
+    lo_mt_worker(m);
+    for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+    free(m->order);
+}
+
+static void lo_out_free(lo_out *o) {
+    free(o->contig);
+    free(o->start);
+    free(o->end);
+    free(o->lrow);
+    free(o->rrow);
+}
+
+/* intersect (Intersection.scala:58-69 over the SetTheory.scala:131-187 sweep)
+ * sharded by contig over `nthreads` threads.  Returns the pair count; *sum /
+ * *xr receive the order-independent checksum (sum and xor of lo_pair_hash of
+ * (start, end, a_row, b_row), contig-local start / end as the engine hashes
+ * them).  With cap >= count the records are also written in the reference's
+ * P = 1 emission order. */
+int64_t lo_intersect_mt(int32_t n_contigs, int64_t nl, const int32_t *lc, const uint32_t *ls,
+                        const uint32_t *le, int64_t nr, const int32_t *rc, const uint32_t *rs,
+                        const uint32_t *re, int64_t threshold, int nthreads, int64_t cap,
+                        int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow, int64_t *orrow,
+                        uint64_t *sum, uint64_t *xr) {
+    for (int64_t i = 0; i < nl; ++i)
+        if (lc[i] < 0 || lc[i] >= n_contigs) return -1;
+    for (int64_t i = 0; i < nr; ++i)
+        if (rc[i] < 0 || rc[i] >= n_contigs) return -1;
+    lo_mt m;
+    memset(&m, 0, sizeof(m));
+    m.op = 0;
+    m.nc = n_contigs;
+    m.threshold = threshold;
+    m.keep = cap > 0;
+    lo_group(&m.L, n_contigs, nl, lc, ls, le);
+    lo_group(&m.R, n_contigs, nr, rc, rs, re);
+    lo_mt_run(&m, nthreads);
+    int64_t total = 0;
+    uint64_t hs = 0, hx = 0;
+    for (int32_t k = 0; k < n_contigs; ++k) {
+        total += m.res[k].count;
+        hs += m.res[k].hsum;
+        hx ^= m.res[k].hxor;
+    }
+    if (cap >= total) {
+        int64_t at = 0;
+        for (int32_t k = 0; k < n_contigs; ++k) {
+            const lo_out *o = &m.res[k];
+            for (int64_t j = 0; j < o->count; ++j, ++at) {
+                if (oc) oc[at] = o->contig[j];
+                if (os) os[at] = o->start[j];
+                if (oe) oe[at] = o->end[j];
+                if (olrow) olrow[at] = o->lrow[j];
+                if (orrow) orrow[at] = o->rrow[j];
+            }
+        }
+    }
+    for (int32_t k = 0; k < n_contigs; ++k) lo_out_free(&m.res[k]);
+    free(m.res);
+    lo_ungroup(&m.L);
+    lo_ungroup(&m.R);
+    if (sum) *sum = hs;
+    if (xr) *xr = hx;
+    return total;
+}
+
+/* merge (SetTheory.scala:208-225 + Merge.scala) sharded by contig.  Returns
+ * the run count; with cap >= count writes the runs in order.  run_of_row
+ * (optional, n entries) receives every input row's global run index, and
+ * (*gsum, *gxr) the checksum of that grouping: sum / xor over rows r of
+ * mix64(r << 32 | run_of_row[r]) -- the Iterable[T] of every run. */
+static uint64_t lo_mix64(uint64_t z);
+
+int64_t lo_merge_mt(int32_t n_contigs, int64_t n, const int32_t *c, const uint32_t *s,
+                    const uint32_t *e, int nthreads, int64_t cap, int32_t *oc, int64_t *os,
+                    int64_t *oe, int64_t *run_of_row, uint64_t *gsum, uint64_t *gxr) {
+    for (int64_t i = 0; i < n; ++i)
+        if (c[i] < 0 || c[i] >= n_contigs) return -1;
+    lo_mt m;
+    memset(&m, 0, sizeof(m));
+    m.op = 1;
+    m.nc = n_contigs;
+    int64_t *rid = run_of_row ? run_of_row : (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    m.run_of_row = rid;
+    lo_group(&m.L, n_contigs, n, c, s, e);
+    lo_mt_run(&m, nthreads);
+    int64_t *base = (int64_t *)malloc(sizeof(int64_t) * ((size_t)n_contigs + 1));
+    int64_t total = 0;
+    for (int32_t k = 0; k < n_contigs; ++k) {
+        base[k] = total;
+        total += m.res[k].count;
+    }
+    uint64_t hs = 0, hx = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        rid[i] += base[c[i]];
+        const uint64_t h = lo_mix64(((uint64_t)i << 32) | (uint64_t)(uint32_t)rid[i]);
+        hs += h;
+        hx ^= h;
+    }
+    if (cap >= total) {
+        for (int32_t k = 0; k < n_contigs; ++k) {
+            const lo_out *o = &m.res[k];
+            for (int64_t j = 0; j < o->count; ++j) {
+                const int64_t at = base[k] + j;
+                if (oc) oc[at] = k;
+                if (os) os[at] = o->start[j];
+                if (oe) oe[at] = o->end[j];
+            }
+        }
+    }
+    for (int32_t k = 0; k < n_contigs; ++k) lo_out_free(&m.res[k]);
+    free(m.res);
+    free(base);
+    lo_ungroup(&m.L);
+    if (!run_of_row) free(rid);
+    if (gsum) *gsum = hs;
+    if (gxr) *gxr = hx;
+    return total;
 }

@@ -27,7 +27,8 @@ SUB_LIME, SUB_SET = 0, 1
 def build():
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c99", "-o", LIB, SRC])
+        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c99", "-pthread", "-o", LIB,
+                               SRC])
 
 
 def lib():
@@ -52,6 +53,14 @@ def lib():
         L.lo_complement.restype = i64
         L.lo_complement.argtypes = [i64, P(i32), P(i64), P(i64), i32, P(i64), i64, P(i32),
                                     P(i64), P(i64)]
+        u32p, u64p = P(C.c_uint32), P(C.c_uint64)
+        L.lo_intersect_mt.restype = i64
+        L.lo_intersect_mt.argtypes = [i32, i64, P(i32), u32p, u32p, i64, P(i32), u32p, u32p, i64,
+                                      C.c_int, i64, P(i32), P(i64), P(i64), P(i64), P(i64), u64p,
+                                      u64p]
+        L.lo_merge_mt.restype = i64
+        L.lo_merge_mt.argtypes = [i32, i64, P(i32), u32p, u32p, C.c_int, i64, P(i32), P(i64),
+                                  P(i64), P(i64), u64p, u64p]
         L.lo_pair_hash.restype = C.c_uint64
         L.lo_pair_hash.argtypes = [C.c_uint32] * 4
         _lib = L
@@ -184,3 +193,74 @@ def checksum_pairs(res):
         tot = int(np.sum(h, dtype=np.uint64))
     xr = int(np.bitwise_xor.reduce(h)) if len(h) else 0
     return tot, xr
+
+
+def threads():
+    """Host threads for the contig-sharded drivers: OMP_NUM_THREADS (16 on the
+    GPU box), at most os.cpu_count()."""
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1, 64))
+
+
+def _in32(contig, start, end):
+    c = np.ascontiguousarray(contig, dtype=np.int32)
+    s = np.ascontiguousarray(start, dtype=np.uint32)
+    e = np.ascontiguousarray(end, dtype=np.uint32)
+    return len(c), c, s, e
+
+
+def intersect_mt(n_contigs, a, b, threshold=0, records=False, nthreads=None):
+    """Contig-sharded intersect (lo_intersect_mt): the P = 1 result computed
+    one contig per thread.  Returns {"n", "sum", "xor"} and, with
+    records=True, the pair arrays in the reference's emission order."""
+    L = lib()
+    na, ac, as_, ae = _in32(*a)
+    nb, bc, bs, be = _in32(*b)
+    u32p = P(C.c_uint32)
+    sm, xr = C.c_uint64(), C.c_uint64()
+    args = [int(n_contigs), na, _p(ac, i32), as_.ctypes.data_as(u32p), ae.ctypes.data_as(u32p),
+            nb, _p(bc, i32), bs.ctypes.data_as(u32p), be.ctypes.data_as(u32p), int(threshold),
+            int(nthreads or threads())]
+    n = L.lo_intersect_mt(*args, 0, None, None, None, None, None, C.byref(sm), C.byref(xr))
+    if n < 0:
+        raise KeyError("contig id outside [0, n_contigs)")
+    out = {"n": int(n), "sum": sm.value, "xor": xr.value}
+    if records:
+        o = _out(n)
+        L.lo_intersect_mt(*args, n, *[_p(x, t) for x, t in zip(o, (i32, i64, i64, i64, i64))],
+                          C.byref(sm), C.byref(xr))
+        out.update(_result(o))
+    return out
+
+
+def merge_mt(n_contigs, a, run_of_row=False, nthreads=None):
+    """Contig-sharded merge (lo_merge_mt): runs in order plus the checksum of
+    the run id of every input row ({"grp_sum", "grp_xor"})."""
+    L = lib()
+    n, c, s, e = _in32(*a)
+    u32p = P(C.c_uint32)
+    gs, gx = C.c_uint64(), C.c_uint64()
+    rid = np.zeros(n, np.int64) if run_of_row else None
+    args = [int(n_contigs), n, _p(c, i32), s.ctypes.data_as(u32p), e.ctypes.data_as(u32p),
+            int(nthreads or threads())]
+    # runs <= rows: size the buffers by the rows, one call
+    oc, os_, oe = np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.int64)
+    k = L.lo_merge_mt(*args, n, _p(oc, i32), _p(os_, i64), _p(oe, i64), _p(rid, i64),
+                      C.byref(gs), C.byref(gx))
+    if k < 0:
+        raise KeyError("contig id outside [0, n_contigs)")
+    out = {"contig": oc[:k], "start": os_[:k], "end": oe[:k], "grp_sum": gs.value,
+           "grp_xor": gx.value}
+    if run_of_row:
+        out["run_of_row"] = rid
+    return out
+
+
+def grouping_checksum(run_of_row):
+    """sum / xor over rows r of mix64(r << 32 | run_of_row[r]) (lo_merge_mt's
+    grouping checksum, restated in numpy for small cases)."""
+    from lime_amd.synth import mix64
+    r = np.arange(len(run_of_row), dtype=np.uint64)
+    h = mix64((r << np.uint64(32)) | np.asarray(run_of_row, dtype=np.uint64))
+    with np.errstate(over="ignore"):
+        tot = int(np.sum(h, dtype=np.uint64))
+    return tot, (int(np.bitwise_xor.reduce(h)) if len(h) else 0)

@@ -312,3 +312,44 @@ def test_zero_width_edges():
     res = oracle.intersect(L, R2)
     assert list(zip(res["start"].tolist(), res["end"].tolist(), res["b_row"].tolist())) == \
         [(4, 4, 1)]
+
+
+# ------------------------------------------- contig-sharded drivers (MT)
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_mt_drivers_equal_single_partition(seed):
+    # lo_intersect_mt / lo_merge_mt shard by contig over threads; every op is
+    # contig-local, so they must reproduce the P = 1 restatement exactly
+    # (records in order, checksums, run ids)
+    from tests.util import random_sets
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 4000, 3000, n_contigs=5, contig_len=30000, max_len=400,
+                       zero_frac=0.1, dup_frac=0.05, book_frac=0.1)
+    for t in (0, 1, 30, -3):
+        e = oracle.intersect(A, B, t)
+        m = oracle.intersect_mt(5, A, B, t, records=True, nthreads=4)
+        assert m["n"] == len(e["start"])
+        for k in ("contig", "start", "end", "a_row", "b_row"):
+            assert (m[k] == e[k]).all(), k
+        assert (m["sum"], m["xor"]) == oracle.checksum_pairs(e)
+        assert oracle.intersect_mt(5, A, B, t, nthreads=3)["sum"] == m["sum"]
+    em = oracle.merge(A)
+    mm = oracle.merge_mt(5, A, run_of_row=True, nthreads=4)
+    for k in ("contig", "start", "end", "run_of_row"):
+        assert (np.asarray(mm[k]) == np.asarray(em[k])).all(), k
+    assert (mm["grp_sum"], mm["grp_xor"]) == oracle.grouping_checksum(em["run_of_row"])
+
+
+def test_mt_drivers_on_reference_fixtures(golden):
+    # the IntersectionSuite / MergeSuite inputs through the sharded drivers
+    from tests.util import expected, ranked, read_bed_py
+    a = read_bed_py(os.path.join(golden, "intersect_with_overlap_00.bed"))
+    b = read_bed_py(os.path.join(golden, "intersect_with_overlap_01.bed"))
+    rk = ranked(a[0] + b[0])
+    A = (np.array([rk[c] for c in a[0]], np.int32), a[1], a[2])
+    B = (np.array([rk[c] for c in b[0]], np.int32), b[1], b[2])
+    m = oracle.intersect_mt(len(rk), A, B, records=True, nthreads=2)
+    assert [[c, int(s), int(e)] for c, s, e in
+            zip(["chr1"] * m["n"], m["start"], m["end"])] == expected()["intersection_full"]
+    c = read_bed_py(os.path.join(golden, "cpg_20merge.bed"))
+    mm = oracle.merge_mt(1, (np.zeros(len(c[1]), np.int32), c[1], c[2]))
+    assert list(zip(mm["start"], mm["end"])) == [(28735, 30000)]

@@ -153,7 +153,7 @@ def test_c1_cli_against_oracle(tmp_path):
     want = sorted((inv[int(c)], int(s), int(e), A[3][a], B[3][b]) for c, s, e, a, b in
                   zip(exp["contig"], exp["start"], exp["end"], exp["a_row"], exp["b_row"]))
     got = sorted((c, int(s), int(e), na, nb) for c, s, e, na, nb in run_cli("intersect", pa, pb))
-    assert len(want) > 100 and got == want
+    assert len(want) > 20 and got == want  # ~72 expected: 1e4 x 1e4 x ~2.1 kb / 2.9 Gb
     # merge (cli/Merge.scala:36-44) and subtract (DistributedSubtract)
     m = oracle.merge(ia)
     got = [(c, int(s), int(e)) for c, s, e, _ in run_cli("merge", pa)]

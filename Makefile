@@ -15,7 +15,7 @@ OBJDIR   = build/obj
 HIP_SRCS = $(SRC)/capi.hip $(SRC)/scan.hip $(SRC)/sort.hip $(SRC)/merge.hip \
            $(SRC)/intersect.hip $(SRC)/subtract.hip $(SRC)/complement.hip \
            $(SRC)/bitset.hip $(SRC)/synth.hip $(SRC)/bedparse.hip \
-           $(SRC)/bedwrite.hip $(SRC)/closest.hip
+           $(SRC)/bedwrite.hip $(SRC)/closest.hip $(SRC)/route.hip
 HIP_OBJS = $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 CPP_OBJS = $(OBJDIR)/bed.o
 LIB      = lime_amd/liblime_amd.so

@@ -239,6 +239,15 @@ int lime_bitset_from_device(lime_ctx *ctx, const lime_space *space, int64_t n,
                             const int32_t *d_contig, const uint32_t *d_start,
                             const uint32_t *d_end, lime_bitset **out);
 int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out);
+/* A coordinate shard's bitset: global bits [lo, hi) of the space only
+ * (lo % 64 == 0), from device rows in GLOBAL coordinates (gstart, gend, e.g.
+ * the rows lime_route_rows delivered to this shard), clipped to the window.
+ * Ops combine bitsets of the same window; their runs are in global
+ * coordinates (SURVEY.md 8(e) "Bitset ops": clip at shard bounds, no halo). */
+int lime_bitset_from_global(lime_ctx *ctx, const lime_space *space, int64_t lo, int64_t hi,
+                            int64_t n, const uint32_t *d_gstart, const uint32_t *d_gend,
+                            lime_bitset **out);
+int lime_bitset_window(const lime_bitset *bs, int64_t *lo, int64_t *n_words);
 /* op: 0 = a, 1 = not a (within contigs), 2 = a and b, 3 = a and not b */
 int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bitset *b,
                      lime_result **out, int64_t *n_runs);
@@ -247,6 +256,24 @@ int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, l
                          int64_t *n_runs);
 int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
 int lime_bitset_destroy(lime_bitset *bs);
+
+/* ------------------------------------------------------ range sharding */
+/* Route unsorted device rows to coordinate shards (the
+ * Spark shuffles of ADAM repartitionAndSort, cli/Intersection.scala:42-43,
+ * and OverlapBasedSetTheory.scala:75-84 with Partitioners.scala:10-20's
+ * explicit-destination partitioner).  Shard r owns global coordinates
+ * [splits[r], splits[r+1]) (host array, n_shards + 1 entries, splits[0] = 0,
+ * splits[n_shards] = span, n_shards <= 64).  d_contig == NULL: d_start /
+ * d_end are already global.  clip = 0: every row goes to the shard of its
+ * start, whole; clip = 1: to every shard it overlaps, clipped to it.
+ * counts[r] receives the rows for shard r; when their total is <= cap the
+ * rows are also written grouped by shard (shard order, input order within a
+ * shard) as global (d_gs, d_ge) and row id row_base + input index (d_row may
+ * be NULL).  Validation and error codes as lime_set_create_device. */
+int lime_route_rows(lime_ctx *ctx, const lime_space *space, int64_t n, const int32_t *d_contig,
+                    const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base,
+                    int32_t n_shards, const uint32_t *splits, int clip, int64_t cap,
+                    uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts);
 
 /* ------------------------------------------------------ synthetic inputs */
 /* Counter-based generators (splitmix64 keyed by (seed, row)) identical to
@@ -257,6 +284,15 @@ int lime_synth_uniform(lime_ctx *ctx, const lime_space *space, int64_t n, uint64
 int lime_synth_pileup(lime_ctx *ctx, const lime_space *space, int64_t n, uint64_t seed,
                       int64_t n_centres, uint32_t sigma, uint32_t len_lo, uint32_t len_hi,
                       int32_t *d_contig, uint32_t *d_start, uint32_t *d_end);
+/* Rows [first, first + n) of the same sequences (a rank's slice of one
+ * input: every shard count sees the same rows). */
+int lime_synth_uniform_rows(lime_ctx *ctx, const lime_space *space, int64_t first, int64_t n,
+                            uint64_t seed, uint32_t len_lo, uint32_t len_hi, int32_t *d_contig,
+                            uint32_t *d_start, uint32_t *d_end);
+int lime_synth_pileup_rows(lime_ctx *ctx, const lime_space *space, int64_t first, int64_t n,
+                           uint64_t seed, int64_t n_centres, uint32_t sigma, uint32_t len_lo,
+                           uint32_t len_hi, int32_t *d_contig, uint32_t *d_start,
+                           uint32_t *d_end);
 
 /* ------------------------------------------------------ host-only helpers */
 /* rank_out[i] = position of names[i] in Java String order of the distinct

@@ -91,12 +91,18 @@ SIGNATURES = {
     "lime_result_checksum": (C.c_int, [vp, P(u64), P(u64), P(u64), P(u64)]),
     "lime_bitset_from_set": (C.c_int, [vp, vp, pp]),
     "lime_bitset_from_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
+    "lime_bitset_from_global": (C.c_int, [vp, vp, i64, i64, i64, vp, vp, pp]),
+    "lime_bitset_window": (C.c_int, [vp, P(i64), P(i64)]),
+    "lime_route_rows": (C.c_int, [vp, vp, i64, vp, vp, vp, u32, i32, P(u32), C.c_int, i64, vp,
+                                  vp, vp, P(i64)]),
     "lime_bitset_runs": (C.c_int, [vp, C.c_int, vp, vp, pp, P(i64)]),
     "lime_bitset_and_runs": (C.c_int, [vp, C.c_int, P(vp), pp, P(i64)]),
     "lime_bitset_popcount": (i64, [vp, vp]),
     "lime_bitset_destroy": (C.c_int, [vp]),
     "lime_synth_uniform": (C.c_int, [vp, vp, i64, u64, u32, u32, vp, vp, vp]),
     "lime_synth_pileup": (C.c_int, [vp, vp, i64, u64, i64, u32, u32, u32, vp, vp, vp]),
+    "lime_synth_uniform_rows": (C.c_int, [vp, vp, i64, i64, u64, u32, u32, vp, vp, vp]),
+    "lime_synth_pileup_rows": (C.c_int, [vp, vp, i64, i64, u64, i64, u32, u32, u32, vp, vp, vp]),
     "lime_contig_rank": (C.c_int, [i32, P(C.c_char_p), P(i32)]),
     "lime_bed_read": (C.c_int, [C.c_char_p, pp]),
     "lime_bed_rows": (i64, [vp]),

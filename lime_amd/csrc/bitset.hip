@@ -8,6 +8,7 @@
 //               workgroup: the tile's runs (two binary searches) are OR-ed
 //               into an LDS image, which is then stored once, coalesced --
 //               every word written exactly once, no memset, no global atomics
+//   k_bin_*     unsorted rows -> bits without a sort (below)
 //   k_ev_count  per 4096-word tile: events (run starts + run ends) of
 //               op(words) where op = A | ~A | A&B | A&~B | AND of k sets;
 //               operands are combined while loading (coalesced) into LDS
@@ -57,68 +58,6 @@ __global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
     for (int i = threadIdx.x; i < cnt; i += BB) words[w0 + i] = img[i];
 }
 
-// Binned rows -> bits: rows grouped by gs >> 16 (two radix passes instead of
-// a full sort + merge).  A tile (4096 words = 2^18 bases = 4 bins) paints
-// the rows that START in it into its LDS image (clipped at the tile end) and
-// stores it once; the remainders of rows reaching past the tile are queued
-// and OR-ed into global words by k_paint_cross after every tile is stored.
-constexpr int BINSH = 16;
-__device__ __forceinline__ int64_t lb_bin(const uint32_t *gs, int64_t n, uint32_t bin) {
-    int64_t lo = 0, hi = n;  // first row with (gs >> BINSH) >= bin
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((gs[mid] >> BINSH) < bin)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ void paint_lds(unsigned long long *img, uint64_t s, uint64_t e) {
-    const uint64_t a = s >> 6, b = (e - 1) >> 6;
-    for (uint64_t w = a; w <= b; ++w) {
-        const uint64_t lo = w == a ? (s & 63) : 0;
-        const uint64_t hi = w == b ? ((e - 1) & 63) : 63;
-        const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
-        atomicOr(&img[w], (unsigned long long)m);
-    }
-}
-
-// first row of every paint tile (4 bins), searched once per tile up front
-// instead of by each painting block (27 dependent loads on its critical path)
-__global__ __launch_bounds__(BB) void k_tile_starts(const uint32_t *__restrict__ gs, int64_t n,
-                                                    int64_t nt, uint32_t *__restrict__ tstart) {
-    const int64_t t = (int64_t)blockIdx.x * BB + threadIdx.x;
-    if (t > nt) return;
-    const uint64_t bin = ((uint64_t)t * BT * 64) >> BINSH;
-    tstart[t] = (uint32_t)(bin > 0xffffffffull ? n : lb_bin(gs, n, (uint32_t)bin));
-}
-
-__global__ __launch_bounds__(BB) void k_paint_rows(const uint32_t *__restrict__ gs,
-                                                   const uint32_t *__restrict__ ge,
-                                                   const uint32_t *__restrict__ tstart, int64_t n,
-                                                   uint64_t *__restrict__ words, int64_t n_words,
-                                                   uint64_t *__restrict__ cross,
-                                                   unsigned int *__restrict__ ncross) {
-    static_assert((int64_t)BT * 64 == (1ll << (BINSH + 2)), "tile = 4 bins");
-    __shared__ unsigned long long img[BT];
-    const int64_t w0 = (int64_t)blockIdx.x * BT;
-    const uint64_t blo = (uint64_t)w0 * 64, bhi = blo + (uint64_t)BT * 64;
-    for (int i = threadIdx.x; i < BT; i += BB) img[i] = 0ull;
-    const int64_t r0 = tstart[blockIdx.x], r1 = tstart[blockIdx.x + 1];
-    __syncthreads();
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += BB) {
-        const uint64_t g0 = gs[r], g1 = ge[r];
-        if (g1 <= g0) continue;
-        paint_lds(img, g0 - blo, min(g1, bhi) - blo);
-        if (g1 > bhi) cross[atomicAdd(ncross, 1u)] = (bhi << 32) | g1;  // remainder [bhi, g1)
-    }
-    __syncthreads();
-    const int cnt = (int)min((int64_t)BT, n_words - w0);
-    for (int i = threadIdx.x; i < cnt; i += BB) words[w0 + i] = img[i];
-}
-
 // bits [s, e) of global words (after every tile is stored)
 __device__ __forceinline__ void paint_global(uint64_t *words, uint64_t s, uint64_t e) {
     const uint64_t a = s >> 6, b = (e - 1) >> 6;
@@ -141,11 +80,376 @@ __global__ __launch_bounds__(BB) void k_paint_cross(const uint64_t *__restrict__
         paint_global(words, cross[i] >> 32, cross[i] & 0xffffffffull);
 }
 
+// ------------------------------------------------- rows -> bits, no sort
+// Unsorted rows are binned by a two-level counting scatter, then each
+// 2^PSH-base paint tile ORs its rows into an LDS image and stores it once:
+//   k_bin_count  per chunk of rows (one block, looping): LDS histogram of the
+//                rows' paint tiles -> per-bin counts into column `chunk` of
+//                the bin-major matrix mat[bin][chunk], tile totals by atomics
+//   scan x2      (bin, chunk) segment starts; paint tile starts
+//   k_bin_write  the chunks again: per 8192-row step the rows are ranked per
+//                bin (LDS atomics), staged in LDS in bin order, and stored as
+//                runs, one u32 each (offset in bin << LENB | length); longer
+//                rows and rows crossing the bin end leave their remainder to
+//                the cross list (k_paint_cross)
+//   k_bin_split  one block per bin: its rows to its PSUB paint tiles (wave-
+//                aggregated LDS cursors: 8 destinations, coalesced runs),
+//                re-packed relative to the tile, tile-crossing remainders to
+//                the cross list
+//   k_paint_bins one block per paint tile: its rows OR-ed into a 64 KiB LDS
+//                image, stored once (every word written exactly once)
+// Why two levels: a one-level scatter to 5,900 paint tiles (hg38) keeps
+// (destinations x resident blocks) lines open per XCD, far beyond its 4 MiB
+// L2, and wrote 3.9x its bytes (profiles/round2_c5_pmc_onelevel.txt); 737
+// bins x one block per CU fit.  Staging the step in LDS (runs per bin) beat
+// direct per-row stores 0.90 vs 1.38 ms per 1.25e8 rows.
+// HBM per row: 8 B (count) + 12 B + 4 B (write) + 4 B + 4 B (split) + 4 B
+// (paint), + G/8 bits.
+constexpr int BSH = 22;                  // bin = 2^22 bases
+constexpr int PSH = 19;                  // paint tile = 2^19 bases = 8192 words (64 KiB)
+constexpr int PSUB = 1 << (BSH - PSH);   // paint tiles per bin
+constexpr int TWORDS = 1 << (PSH - 6);
+constexpr int LENB = 32 - BSH;           // packed length bits (bin slab)
+constexpr uint32_t LMAX = (1u << LENB) - 1;
+constexpr int PLENB = 32 - PSH;          // packed length bits (tile slab)
+constexpr int NBMAX = 1 << (32 - BSH);   // bins (span < 2^32)
+constexpr int NTMAX = NBMAX * PSUB;      // paint tiles
+constexpr int BINB = 1024;               // count / split block
+constexpr int WRB = 512;                 // write block (<= 256 VGPRs: no spills)
+constexpr int PAINTB = 512;
+
+struct BinArgs {
+    const int32_t *contig;     // null: start / end are global coordinates
+    const uint32_t *start, *end;
+    const uint32_t *off, *len;
+    int32_t nc;
+    int64_t n;
+    uint64_t lo, hi;           // the bitset covers global bits [lo, hi), lo % 64 == 0
+    uint64_t span;
+    int nb;                    // bins
+    int64_t chunk_rows;        // R (multiple of STEP)
+    uint32_t nchunks;
+    uint32_t *mat;             // nb * nchunks + 1 (counts, then scanned starts)
+    uint32_t *ttot;            // nb * PSUB + 1 tile totals, then scanned starts
+    uint32_t *slab;            // n packed rows, bin order
+    uint32_t *slab2;           // n packed rows, paint tile order
+    uint64_t *cross;           // remainders (s << 32 | e) in window bits, capacity n
+    unsigned int *ncross;
+    unsigned int *err;         // bit0 contig, bit1 end < start, bit2 end > length
+};
+
+// global start of a row (0 for an invalid contig); every pass derives a
+// row's bin and tile from it alone, so they always agree
+__device__ __forceinline__ uint64_t row_gs(const BinArgs &a, int32_t c, uint32_t s) {
+    if (!a.contig) return s;
+    return (c >= 0 && c < a.nc) ? (uint64_t)a.off[c] + s : 0ull;
+}
+// bit g of the space -> bit of the bitset's window (clamped into it)
+__device__ __forceinline__ uint64_t local_bit(const BinArgs &a, uint64_t g) {
+    return (g < a.lo ? a.lo : (g > a.hi ? a.hi : g)) - a.lo;
+}
+__device__ __forceinline__ int bin_of(const BinArgs &a, uint64_t l) {
+    const uint64_t t = l >> BSH;
+    return t < (uint64_t)a.nb ? (int)t : a.nb - 1;
+}
+// paint tile of a window bit, consistent with bin_of
+__device__ __forceinline__ int ptile_of(const BinArgs &a, uint64_t l) {
+    const int b = bin_of(a, l);
+    const uint64_t q = (l - ((uint64_t)b << BSH)) >> PSH;
+    return b * PSUB + (q < PSUB ? (int)q : PSUB - 1);
+}
+// bijective block -> chunk map: each XCD (blockIdx % 8) takes a contiguous
+// range of chunks (speed only)
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t bid, uint32_t nch) {
+    const uint32_t q = nch / 8, r = nch % 8, x = bid % 8, i = bid / 8;
+    return x * q + (x < r ? x : r) + i;
+}
+
+// A step = 16 rows per lane: four groups of 4 consecutive rows, the groups
+// BINB * 4 rows apart, so every load is a lane-consecutive 16-B access and a
+// step keeps 8-12 loads in flight per lane.
+constexpr int SROWS = 16;
+constexpr int STEP = SROWS * BINB;    // rows per count step
+constexpr int WSTEP = SROWS * WRB;    // rows per write step
+
+template <bool END, int NT = BINB>
+__device__ __forceinline__ void load_step(const BinArgs &a, int64_t base, int64_t lim,
+                                          int32_t (&c)[SROWS], uint32_t (&s)[SROWS],
+                                          uint32_t (&e)[SROWS], uint32_t &valid) {
+    valid = 0;
+#pragma unroll
+    for (int q = 0; q < SROWS / 4; ++q) {
+        const int64_t i0 = base + (int64_t)q * 4 * NT + 4 * threadIdx.x;
+        if (i0 + 4 <= lim) {
+            const int4 cv =
+                a.contig ? *reinterpret_cast<const int4 *>(a.contig + i0) : int4{0, 0, 0, 0};
+            const uint4 sv = *reinterpret_cast<const uint4 *>(a.start + i0);
+            c[4 * q] = cv.x, c[4 * q + 1] = cv.y, c[4 * q + 2] = cv.z, c[4 * q + 3] = cv.w;
+            s[4 * q] = sv.x, s[4 * q + 1] = sv.y, s[4 * q + 2] = sv.z, s[4 * q + 3] = sv.w;
+            if (END) {
+                const uint4 ev = *reinterpret_cast<const uint4 *>(a.end + i0);
+                e[4 * q] = ev.x, e[4 * q + 1] = ev.y, e[4 * q + 2] = ev.z, e[4 * q + 3] = ev.w;
+            }
+            valid |= 0xfu << (4 * q);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool v = i0 + j < lim;
+                c[4 * q + j] = v && a.contig ? a.contig[i0 + j] : 0;
+                s[4 * q + j] = v ? a.start[i0 + j] : 0u;
+                if (END) e[4 * q + j] = v ? a.end[i0 + j] : 0u;
+                if (v) valid |= 1u << (4 * q + j);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
+    __shared__ uint32_t hist[NTMAX];
+    const int nt = a.nb * PSUB;
+    for (int i = threadIdx.x; i < nt; i += BINB) hist[i] = 0;
+    __syncthreads();
+    const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
+    const int64_t r0 = (int64_t)ch * a.chunk_rows;
+    const int64_t r1 = min(a.n, r0 + a.chunk_rows);
+    for (int64_t base = r0; base < r1; base += STEP) {
+        int32_t c[SROWS];
+        uint32_t s[SROWS], e[SROWS];
+        uint32_t valid;
+        load_step<false>(a, base, r1, c, s, e, valid);
+#pragma unroll
+        for (int k = 0; k < SROWS; ++k)
+            if (valid & (1u << k))
+                atomicAdd(&hist[ptile_of(a, local_bit(a, row_gs(a, c[k], s[k])))], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < a.nb; b += BINB) {
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < PSUB; ++q) sum += hist[b * PSUB + q];
+        a.mat[(int64_t)b * a.nchunks + ch] = sum;
+    }
+    for (int t = threadIdx.x; t < nt; t += BINB)
+        if (hist[t]) atomicAdd(&a.ttot[t], hist[t]);
+}
+
+__global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
+    __shared__ uint32_t stage[WSTEP];
+    __shared__ uint16_t sbin[WSTEP];
+    __shared__ uint32_t hist[NBMAX], soff[NBMAX], cur[NBMAX];
+    __shared__ uint32_t scratch[WRB / 64 + 1];
+    const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
+    for (int t = threadIdx.x; t < NBMAX; t += WRB) {
+        cur[t] = t < a.nb ? a.mat[(int64_t)t * a.nchunks + ch] : 0u;
+        hist[t] = 0;
+    }
+    __syncthreads();
+    const int64_t r0 = (int64_t)ch * a.chunk_rows;
+    const int64_t r1 = min(a.n, r0 + a.chunk_rows);
+    uint32_t err = 0;
+    int32_t c[SROWS];
+    uint32_t s[SROWS], e[SROWS];
+    uint32_t valid = 0;
+    if (r0 < r1) load_step<true, WRB>(a, r0, r1, c, s, e, valid);
+    for (int64_t base = r0; base < r1; base += WSTEP) {
+        uint32_t tb[SROWS], pk[SROWS];
+#pragma unroll
+        for (int k = 0; k < SROWS; ++k) {
+            const int32_t cc = c[k];
+            const uint64_t gs = row_gs(a, cc, s[k]);
+            uint64_t ge = gs;
+            if (!(valid & (1u << k))) {
+            } else if (!a.contig) {
+                if (e[k] < s[k]) err |= 2u;
+                else if (e[k] > a.span) err |= 4u;
+                else ge = e[k];
+            } else if (cc < 0 || cc >= a.nc) {
+                err |= 1u;
+            } else if (e[k] < s[k]) {
+                err |= 2u;
+            } else if (e[k] > a.len[cc]) {
+                err |= 4u;
+            } else {
+                ge = (uint64_t)a.off[cc] + e[k];
+            }
+            // the row's part inside the window, in window bits
+            const uint64_t g0 = local_bit(a, gs), g1 = local_bit(a, ge);
+            const int t = bin_of(a, g0);
+            // in-bin piece [g0, g0 + l), l <= LMAX; the rest: cross list
+            const uint64_t tend = ((uint64_t)t + 1) << BSH;
+            uint64_t l = g1 > g0 ? g1 - g0 : 0;
+            if (l > LMAX) l = LMAX;
+            if (g0 + l > tend) l = tend > g0 ? tend - g0 : 0;
+            tb[k] = (uint32_t)t;
+            pk[k] = ((uint32_t)(g0 - ((uint64_t)t << BSH)) << LENB) | (uint32_t)l;
+            if ((valid & (1u << k)) && g1 > g0 + l)
+                a.cross[atomicAdd(a.ncross, 1u)] = ((g0 + l) << 32) | g1;
+        }
+        const uint32_t vnow = valid;
+        // the next step's rows: their loads stay in flight across this step's
+        // barriers (plain loads survive __syncthreads)
+        if (base + WSTEP < r1) load_step<true, WRB>(a, base + WSTEP, r1, c, s, e, valid);
+        // rank per bin (16 independent LDS atomics), then bin offsets in the
+        // step (one scan over <= 1024 bins), then stage in bin order
+        uint32_t rk[SROWS];
+#pragma unroll
+        for (int k = 0; k < SROWS; ++k)
+            if (vnow & (1u << k)) rk[k] = atomicAdd(&hist[tb[k]], 1u);
+        __syncthreads();
+        {
+            // bins 2t, 2t + 1 per thread (NBMAX = 2 * WRB)
+            const int t = 2 * threadIdx.x;
+            const uint32_t h0 = hist[t], h1 = hist[t + 1];
+            uint32_t tot;
+            const uint32_t o = dev::block_exclusive_sum<WRB>(h0 + h1, scratch, &tot);
+            soff[t] = o;
+            soff[t + 1] = o + h0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SROWS; ++k)
+            if (vnow & (1u << k)) {
+                const uint32_t j = soff[tb[k]] + rk[k];
+                stage[j] = pk[k];
+                sbin[j] = (uint16_t)tb[k];
+            }
+        __syncthreads();
+        // runs of a bin are consecutive: lane-consecutive stores
+        const int cnt = (int)min((int64_t)WSTEP, r1 - base);
+        for (int j = threadIdx.x; j < cnt; j += WRB) {
+            const uint32_t t = sbin[j];
+            a.slab[cur[t] + (uint32_t)j - soff[t]] = stage[j];
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < NBMAX; t += WRB) {
+            cur[t] += hist[t];
+            hist[t] = 0;
+        }
+        __syncthreads();
+    }
+    err = dev::wave_reduce_or(err);
+    if (err && dev::lane_id() == 0) atomicOr(a.err, err);
+}
+
+// one block per bin: its rows -> its PSUB paint tiles.  Slot claims per wave
+// and step: lane j = 8 k + d counts the rows of slot k bound for tile d (64
+// ballots), a prefix over k gives each (k, d) its offset among the wave's
+// claims for d, and ONE LDS atomic instruction (lanes 56..63) reserves all
+// of them -- no chain of returning atomics per row.
+static_assert(PSUB == 8, "claims: 8 slots x 8 destinations = one wave");
+static_assert(NBMAX == 2 * WRB, "write-pass bin scan: two bins per thread");
+__global__ __launch_bounds__(BINB) void k_bin_split(BinArgs a) {
+    __shared__ uint32_t cur[PSUB];
+    const int b = blockIdx.x;
+    if (threadIdx.x < PSUB) cur[threadIdx.x] = a.ttot[b * PSUB + threadIdx.x];
+    const uint32_t r0 = a.mat[(int64_t)b * a.nchunks], r1 = a.mat[(int64_t)(b + 1) * a.nchunks];
+    __syncthreads();
+    const int lane = dev::lane_id();
+    const uint64_t bin0 = (uint64_t)b << BSH;
+    const uint64_t lt = dev::lanemask_lt();
+    constexpr int PV = 8;
+    // rows of a wave per step: 64 lanes x PV slots, lane-consecutive per slot
+    const int wv = threadIdx.x / 64, nwv = BINB / 64;
+    for (uint32_t rb = r0 + (uint32_t)wv * 64 * PV; rb < r1; rb += (uint32_t)nwv * 64 * PV) {
+        uint32_t pv[PV];
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const uint32_t r = rb + k * 64 + lane;
+            pv[k] = r < r1 ? a.slab[r] : 0u;
+        }
+        uint32_t q[PV], rk[PV], val[PV];
+        uint32_t myc = 0;  // lane 8 k + d: rows of slot k bound for tile d
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const bool v = rb + k * 64 + lane < r1;
+            const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
+            q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
+            const uint32_t qend = (q[k] + 1) << PSH;
+            const uint32_t l2 = o + l > qend ? qend - o : l;  // clipped at the tile end
+            if (v && l2 < l)  // remainder [o + l2, o + l) into the next tile(s)
+                a.cross[atomicAdd(a.ncross, 1u)] = ((bin0 + o + l2) << 32) | (bin0 + o + l);
+            val[k] = ((o - (q[k] << PSH)) << PLENB) | l2;
+            rk[k] = 0;
+#pragma unroll
+            for (int d = 0; d < PSUB; ++d) {
+                const uint64_t m = __ballot(q[k] == (uint32_t)d);
+                if (q[k] == (uint32_t)d) rk[k] = (uint32_t)__popcll(m & lt);
+                if (lane == k * PSUB + d) myc = (uint32_t)__popcll(m);
+            }
+        }
+        // exclusive prefix of myc over k for each d (lanes d, d + 8, ...)
+        uint32_t pre = myc;
+#pragma unroll
+        for (int sh = PSUB; sh < 64; sh <<= 1) {
+            const uint32_t o = __shfl_up(pre, sh, 64);
+            if (lane >= sh) pre += o;
+        }
+        pre -= myc;
+        uint32_t base = 0;
+        if (lane >= 64 - PSUB) base = atomicAdd(&cur[lane - (64 - PSUB)], pre + myc);
+        base = __shfl(base, 64 - PSUB + (lane & (PSUB - 1)), 64);
+        const uint32_t off = base + pre;  // first slot of (k = lane / 8, d = lane % 8)
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const uint32_t o = __shfl(off, k * PSUB + (int)(q[k] & (PSUB - 1)), 64);
+            if (q[k] < PSUB) a.slab2[o + rk[k]] = val[k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(PAINTB) void k_paint_bins(const uint32_t *__restrict__ slab2,
+                                                       const uint32_t *__restrict__ tstart,
+                                                       uint64_t *__restrict__ words,
+                                                       int64_t n_words) {
+    __shared__ unsigned long long img[TWORDS];
+    const int t = blockIdx.x;
+    for (int i = threadIdx.x; i < TWORDS; i += PAINTB) img[i] = 0ull;
+    const uint32_t r0 = tstart[t], r1 = tstart[t + 1];
+    __syncthreads();
+    // 8 independent loads per lane per step, then their paints
+    constexpr int PV = 8;
+    for (uint32_t rb = r0; rb < r1; rb += PV * PAINTB) {
+        uint32_t pv[PV];
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const uint32_t r = rb + k * PAINTB + threadIdx.x;
+            pv[k] = r < r1 ? slab2[r] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const uint32_t l = pv[k] & ((1u << PLENB) - 1);
+            if (l == 0) continue;
+            const uint32_t s0 = pv[k] >> PLENB, e0 = s0 + l;  // bits [s0, e0) of the tile
+            const uint32_t wa = s0 >> 6, wb = (e0 - 1) >> 6;
+            for (uint32_t w = wa; w <= wb; ++w) {
+                const uint32_t lo = w == wa ? (s0 & 63) : 0;
+                const uint32_t hi = w == wb ? ((e0 - 1) & 63) : 63;
+                const uint64_t mk = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
+                if (mk == ~0ull)
+                    img[w] = mk;  // whole word: a plain store is idempotent with the ORs
+                else
+                    atomicOr(&img[w], (unsigned long long)mk);
+            }
+        }
+    }
+    __syncthreads();
+    const int64_t w0 = (int64_t)t * TWORDS;
+    const int cnt = (int)max((int64_t)0, min((int64_t)TWORDS, n_words - w0));
+    // 16-B stores: two words per lane
+    for (int i = 2 * threadIdx.x; i < cnt; i += 2 * PAINTB) {
+        if (i + 1 < cnt)
+            *reinterpret_cast<ulonglong2 *>(words + w0 + i) = make_ulonglong2(img[i], img[i + 1]);
+        else
+            words[w0 + i] = img[i];
+    }
+}
+
 struct OpArgs {
     const uint64_t *w[MAXK];
     int k;
     int op;  // 0 a, 1 not a, 2 a & b, 3 a & ~b, 4 and of k
     int64_t n_words;
+    int64_t word0;        // global index of word 0 (a shard's window)
     int64_t span;
     const uint32_t *pad;  // pad bit position of every contig (sorted), nc entries
     int32_t nc;
@@ -176,7 +480,7 @@ __device__ __forceinline__ void events_of(uint64_t x, uint64_t prev, uint64_t &s
 __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned long long *img,
                                            uint32_t *s_pad, int *s_npad) {
     if (a.op == 1 && threadIdx.x == 0) {
-        const int64_t lo = (w0 > 0 ? w0 - 1 : 0) * 64, hi = (w0 + BT) * 64;
+        const int64_t lo = (a.word0 + (w0 > 0 ? w0 - 1 : 0)) * 64, hi = (a.word0 + w0 + BT) * 64;
         int64_t c = dev::lower_bound(a.pad, 0, (int64_t)a.nc, (uint32_t)min(lo, (int64_t)0xffffffff));
         int np = 0;
         for (; c < a.nc && (int64_t)a.pad[c] < hi && np < MAXPAD; ++c) s_pad[np++] = a.pad[c];
@@ -189,7 +493,7 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
         if (w >= 0 && w < a.n_words) {
             x = op_raw(a, w);
             if (a.op == 1) {
-                const int64_t b0 = w * 64;
+                const int64_t b0 = (a.word0 + w) * 64;
                 if (b0 + 64 > a.span) {
                     const int64_t keep = a.span - b0;
                     x &= keep <= 0 ? 0ull : (keep >= 64 ? ~0ull : ((1ull << keep) - 1));
@@ -253,7 +557,7 @@ __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__res
         uint64_t st, en;
         events_of(img[q0 + k + 1], img[q0 + k], st, en);
         uint64_t all = st | en;
-        const uint32_t base = (uint32_t)((w0 + q0 + k) * 64);
+        const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
         while (all) {
             const int b = __builtin_ctzll(all);
             all &= all - 1;
@@ -354,7 +658,7 @@ __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict_
         uint64_t st, en;
         events_of(img[q0 + k + 1], img[q0 + k], st, en);
         uint64_t all = st | en;
-        const uint32_t base = (uint32_t)((w0 + q0 + k) * 64);
+        const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
         while (all) {
             const int b = __builtin_ctzll(all);
             all &= all - 1;
@@ -381,6 +685,7 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     bs->runs_bound = runs.n;
     const int64_t span = (int64_t)a->off[a->n_contigs];
     bs->span = span;
+    bs->hi_bit = span;
     bs->n_words = (span + 63) / 64;
     LIME_TRY(alloc(ctx, &bs->words, (size_t)bs->n_words));
     const int64_t nt = (bs->n_words + BT - 1) / BT;
@@ -393,35 +698,91 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     return LIME_OK;
 }
 
-// bits of a BINNED set (min_shift == 16): no merge, no full sort
-int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
-    const int64_t span = (int64_t)a->off[a->n_contigs];
-    bs->runs_bound = a->n;  // the union of n rows has at most n runs
+// bits straight from UNSORTED device rows (k_bin_count / k_bin_write /
+// k_paint_bins / k_paint_cross): no sort, no merge
+// window [lo, hi) of the space's global bits (lo % 64 == 0): the whole
+// space, or a coordinate shard's range (rows clipped to it)
+int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                      const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
+                      const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs) {
+    const int64_t span = sp->span;
+    const int64_t width = hi - lo;
+    bs->runs_bound = n;  // the union of n rows has at most n runs
     bs->span = span;
-    bs->n_words = (span + 63) / 64;
-    LIME_TRY(alloc(ctx, &bs->words, (size_t)bs->n_words));
-    const int64_t nt = (bs->n_words + BT - 1) / BT;
+    bs->word0 = lo / 64;
+    bs->hi_bit = hi;
+    bs->n_words = (width + 63) / 64;
+    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
+    const int nb = (int)std::max<int64_t>((width + (1ll << BSH) - 1) >> BSH, 1);
+    const int nt = nb * PSUB;
+    // chunk: ~2 chunks per CU, 1..16 steps of 16 rows per lane
+    int64_t R = (n + 511) / 512;
+    R = std::min<int64_t>(std::max<int64_t>(R, STEP), 16 * (int64_t)STEP);
+    R = (R + STEP - 1) / STEP * STEP;
+    const uint32_t nch = (uint32_t)std::max<int64_t>((n + R - 1) / R, 1);
+    const int64_t mlen = (int64_t)nb * nch + 1;
+    uint32_t *mat, *ttot, *slab, *slab2;
     uint64_t *cross;
-    unsigned int *ncross;
-    LIME_TRY(alloc(ctx, &cross, (size_t)std::max<int64_t>(a->n, 1)));
-    LIME_TRY(alloc(ctx, &ncross, 1));
-    LIME_HIP(hipMemsetAsync(ncross, 0, sizeof(unsigned int), S(ctx)));
-    uint32_t *tstart;
-    LIME_TRY(alloc(ctx, &tstart, (size_t)nt + 1));
-    if (nt > 0) {
-        hipLaunchKernelGGL(k_tile_starts, dim3(blocks_for(nt + 1, BB)), dim3(BB), 0, S(ctx),
-                           a->gs, a->n, nt, tstart);
-        hipLaunchKernelGGL(k_paint_rows, dim3((unsigned)nt), dim3(BB), 0, S(ctx), a->gs, a->ge,
-                           (const uint32_t *)tstart, a->n, bs->words, bs->n_words, cross, ncross);
+    unsigned int *flags;  // [0] ncross, [1] err
+    LIME_TRY(alloc(ctx, &mat, (size_t)mlen));
+    PoolGuard<uint32_t> g0{ctx, mat};
+    LIME_TRY(alloc(ctx, &ttot, (size_t)nt + 1));
+    PoolGuard<uint32_t> g1{ctx, ttot};
+    LIME_TRY(alloc(ctx, &slab, (size_t)std::max<int64_t>(n, 1)));
+    PoolGuard<uint32_t> g3{ctx, slab};
+    LIME_TRY(alloc(ctx, &slab2, (size_t)std::max<int64_t>(n, 1)));
+    PoolGuard<uint32_t> g6{ctx, slab2};
+    LIME_TRY(alloc(ctx, &cross, (size_t)std::max<int64_t>(n, 1)));
+    PoolGuard<uint64_t> g4{ctx, cross};
+    LIME_TRY(alloc(ctx, &flags, 2));
+    PoolGuard<unsigned int> g5{ctx, flags};
+    LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
+    LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
+    if (n == 0)
+        LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
+    else  // the total's slot (k_bin_count writes the nb * nch counts before it)
+        LIME_HIP(hipMemsetAsync(mat + mlen - 1, 0, 4, S(ctx)));
+    BinArgs a;
+    a.contig = d_contig;
+    a.start = d_start;
+    a.end = d_end;
+    a.off = d_off;
+    a.len = d_len;
+    a.nc = sp->n;
+    a.n = n;
+    a.lo = (uint64_t)lo;
+    a.hi = (uint64_t)hi;
+    a.span = (uint64_t)span;
+    a.nb = nb;
+    a.chunk_rows = R;
+    a.nchunks = nch;
+    a.mat = mat;
+    a.ttot = ttot;
+    a.slab = slab;
+    a.slab2 = slab2;
+    a.cross = cross;
+    a.ncross = flags;
+    a.err = flags + 1;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_bin_count, dim3(nch), dim3(BINB), 0, S(ctx), a);
+        // (the extra last entries receive the totals)
+        LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
+        LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
+        hipLaunchKernelGGL(k_bin_write, dim3(nch), dim3(WRB), 0, S(ctx), a);
+        hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(BINB), 0, S(ctx), a);
     }
-    if (a->n > 0)
-        hipLaunchKernelGGL(k_paint_cross, dim3(std::min<unsigned>(blocks_for(a->n, BB), 2048u)),
-                           dim3(BB), 0, S(ctx),
-                           (const uint64_t *)cross, (const unsigned int *)ncross, bs->words);
+    hipLaunchKernelGGL(k_paint_bins, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx),
+                       (const uint32_t *)slab2, (const uint32_t *)ttot, bs->words, bs->n_words);
+    if (n > 0)
+        hipLaunchKernelGGL(k_paint_cross, dim3(std::min<unsigned>(blocks_for(n, BB), 2048u)),
+                           dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+                           (const unsigned int *)flags, bs->words);
     LIME_HIP(hipGetLastError());
-    release(ctx, cross);
-    release(ctx, ncross);
-    release(ctx, tstart);
+    unsigned int h[2] = {0, 0};
+    LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
+    if (h[1] & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
+    if (h[1] & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
+    if (h[1] & 4u) return fail(LIME_ERR_RANGE, "interval end beyond its contig length");
     return LIME_OK;
 }
 
@@ -433,7 +794,8 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     oa.k = k;
     oa.op = op;
     oa.n_words = a->n_words;
-    oa.span = a->span;
+    oa.word0 = a->word0;
+    oa.span = a->hi_bit;  // NOT clears every bit past the window
     oa.nc = a->n_contigs;
     // pad positions: off[c+1] - 1
     std::vector<uint32_t> pad(a->n_contigs);
@@ -445,7 +807,16 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
         LIME_HIP(hipStreamSynchronize(S(ctx)));
     }
     oa.pad = d_pad;
-    const int64_t nt = (a->n_words + BT - 1) / BT;
+    // tiles cover one word past the last: a run reaching the window's end
+    // closes there (a shard window may end on any word)
+    const int64_t nt = a->n_words == 0 ? 0 : a->n_words / BT + 1;
+    if (nt == 0) {  // an empty window (e.g. a zero-width shard): no runs
+        release(ctx, d_pad);
+        LIME_TRY(alloc(ctx, &res->gs, 1));
+        LIME_TRY(alloc(ctx, &res->ge, 1));
+        res->n = 0;
+        return LIME_OK;
+    }
     // bound on the result's runs: each run starts at a run start of one
     // operand (AND / ANDN also at a run end of B); NOT adds one gap per contig
     bool known = true;

@@ -124,12 +124,18 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
 int complement_run(lime_ctx *ctx, const lime_result *runs, const uint32_t *d_off,
                    const uint32_t *d_len, int32_t nc, lime_result *res);
 int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
-int bitset_build_binned(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
+int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                      const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
+                      const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs);
+int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+               const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
+               const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
+               uint32_t *d_row, int64_t *counts);
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
-int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t n, uint64_t seed, uint32_t lo,
-          uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig, uint32_t *d_start,
-          uint32_t *d_end);
+int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t first, int64_t n, uint64_t seed,
+          uint32_t lo, uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig,
+          uint32_t *d_start, uint32_t *d_end);
 
 int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const uint32_t *d_ge,
                     const uint32_t *d_row, const uint32_t *d_len);
@@ -180,14 +186,6 @@ __global__ __launch_bounds__(256) void k_result_checksum(
         atomicXor(&out[3], (unsigned long long)gx);
     }
 }
-
-// RAII release of a pool block on every return path
-template <typename T>
-struct PoolGuard {
-    lime_ctx *ctx;
-    T *&p;
-    ~PoolGuard() { release(ctx, p); }
-};
 
 // every set / bitset an operator reads must belong to the operator's context:
 // its arrays live in that context's pool and device (a foreign set
@@ -927,22 +925,68 @@ int lime_bitset_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
         return fail(LIME_ERR_ARG, "bad bitset arguments");
     if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
     hipSetDevice(ctx->device);
-    // rows grouped by 65536-base bin (two radix passes), then painted
-    lime_set *tmp = nullptr;
-    LIME_TRY(create_from_device(ctx, sp, n, d_contig, d_start, d_end, &tmp, nullptr, 16));
+    // rows binned by tile in one counting scatter, painted tile by tile
+    uint32_t *d_off = nullptr, *d_len = nullptr;
+    LIME_TRY(upload_space(ctx, sp, &d_off, &d_len));
+    PoolGuard<uint32_t> g0{ctx, d_off};
+    PoolGuard<uint32_t> g1{ctx, d_len};
     lime_bitset *bs = new lime_bitset();
     bs->ctx = ctx;
-    bs->n_contigs = tmp->n_contigs;
-    bs->off = tmp->off;
-    bs->len = tmp->len;
-    int rc = bitset_build_binned(ctx, tmp, bs);
-    lime_set_destroy(tmp);
+    bs->n_contigs = sp->n;
+    bs->off = sp->off;
+    bs->len = sp->len;
+    int rc = bitset_build_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, 0, sp->span,
+                               bs);
     if (rc != LIME_OK) {
+        release(ctx, bs->words);
         delete bs;
         return rc;
     }
     *out = bs;
     return LIME_OK;
+}
+
+int lime_bitset_from_global(lime_ctx *ctx, const lime_space *sp, int64_t lo, int64_t hi,
+                            int64_t n, const uint32_t *d_gs, const uint32_t *d_ge,
+                            lime_bitset **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_gs || !d_ge)))
+        return fail(LIME_ERR_ARG, "bad bitset arguments");
+    if (lo < 0 || hi < lo || hi > sp->span || lo % 64 != 0)
+        return fail(LIME_ERR_ARG, "window must satisfy 0 <= lo <= hi <= span, lo % 64 == 0");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    lime_bitset *bs = new lime_bitset();
+    bs->ctx = ctx;
+    bs->n_contigs = sp->n;
+    bs->off = sp->off;
+    bs->len = sp->len;
+    int rc = bitset_build_rows(ctx, sp, n, nullptr, d_gs, d_ge, nullptr, nullptr, lo, hi, bs);
+    if (rc != LIME_OK) {
+        release(ctx, bs->words);
+        delete bs;
+        return rc;
+    }
+    *out = bs;
+    return LIME_OK;
+}
+
+int lime_bitset_window(const lime_bitset *bs, int64_t *lo, int64_t *n_words) {
+    if (!bs) return fail(LIME_ERR_ARG, "bitset is null");
+    if (lo) *lo = bs->word0 * 64;
+    if (n_words) *n_words = bs->n_words;
+    return LIME_OK;
+}
+
+int lime_route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                    const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base,
+                    int32_t n_shards, const uint32_t *splits, int clip, int64_t cap,
+                    uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts) {
+    if (!ctx || !sp || !splits || !counts || n < 0 || (n > 0 && (!d_start || !d_end)))
+        return fail(LIME_ERR_ARG, "bad route arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one call");
+    hipSetDevice(ctx->device);
+    return route_rows(ctx, sp, n, d_contig, d_start, d_end, row_base, n_shards, splits, clip, cap,
+                      d_gs, d_ge, d_row, counts);
 }
 
 static lime_result *bitset_result(lime_ctx *ctx, const lime_bitset *b) {
@@ -957,7 +1001,8 @@ int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bit
                      lime_result **out, int64_t *n) {
     if (!ctx || !a || !out || op < 0 || op > 3 || ((op == 2 || op == 3) && !b))
         return fail(LIME_ERR_ARG, "bad bitset op arguments");
-    if (b && (b->off != a->off)) return fail(LIME_ERR_ARG, "bitsets over different spaces");
+    if (b && (b->off != a->off || b->word0 != a->word0 || b->n_words != a->n_words))
+        return fail(LIME_ERR_ARG, "bitsets over different spaces / windows");
     if (a->ctx != ctx || (b && b->ctx != ctx))
         return fail(LIME_ERR_ARG, "bitset belongs to another context (one context per thread)");
     hipSetDevice(ctx->device);
@@ -978,7 +1023,9 @@ int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, l
     if (!ctx || k < 1 || !sets || !out) return fail(LIME_ERR_ARG, "bad bitset and arguments");
     for (int i = 0; i < k; ++i) {
         if (!sets[i]) return fail(LIME_ERR_ARG, "bitset is null");
-        if (sets[i]->off != sets[0]->off) return fail(LIME_ERR_ARG, "bitsets over different spaces");
+        if (sets[i]->off != sets[0]->off || sets[i]->word0 != sets[0]->word0 ||
+            sets[i]->n_words != sets[0]->n_words)
+            return fail(LIME_ERR_ARG, "bitsets over different spaces / windows");
         if (sets[i]->ctx != ctx)
             return fail(LIME_ERR_ARG, "bitset belongs to another context (one context per thread)");
     }
@@ -1013,7 +1060,15 @@ int lime_synth_uniform(lime_ctx *ctx, const lime_space *sp, int64_t n, uint64_t 
                        uint32_t *d_end) {
     if (!ctx || !sp) return fail(LIME_ERR_ARG, "bad synth arguments");
     hipSetDevice(ctx->device);
-    return synth(ctx, sp, 0, n, seed, lo, hi, 0, 0, d_contig, d_start, d_end);
+    return synth(ctx, sp, 0, 0, n, seed, lo, hi, 0, 0, d_contig, d_start, d_end);
+}
+
+int lime_synth_uniform_rows(lime_ctx *ctx, const lime_space *sp, int64_t first, int64_t n,
+                            uint64_t seed, uint32_t lo, uint32_t hi, int32_t *d_contig,
+                            uint32_t *d_start, uint32_t *d_end) {
+    if (!ctx || !sp) return fail(LIME_ERR_ARG, "bad synth arguments");
+    hipSetDevice(ctx->device);
+    return synth(ctx, sp, 0, first, n, seed, lo, hi, 0, 0, d_contig, d_start, d_end);
 }
 
 int lime_synth_pileup(lime_ctx *ctx, const lime_space *sp, int64_t n, uint64_t seed,
@@ -1021,7 +1076,15 @@ int lime_synth_pileup(lime_ctx *ctx, const lime_space *sp, int64_t n, uint64_t s
                       int32_t *d_contig, uint32_t *d_start, uint32_t *d_end) {
     if (!ctx || !sp) return fail(LIME_ERR_ARG, "bad synth arguments");
     hipSetDevice(ctx->device);
-    return synth(ctx, sp, 1, n, seed, lo, hi, n_centres, sigma, d_contig, d_start, d_end);
+    return synth(ctx, sp, 1, 0, n, seed, lo, hi, n_centres, sigma, d_contig, d_start, d_end);
+}
+
+int lime_synth_pileup_rows(lime_ctx *ctx, const lime_space *sp, int64_t first, int64_t n,
+                           uint64_t seed, int64_t n_centres, uint32_t sigma, uint32_t lo,
+                           uint32_t hi, int32_t *d_contig, uint32_t *d_start, uint32_t *d_end) {
+    if (!ctx || !sp) return fail(LIME_ERR_ARG, "bad synth arguments");
+    hipSetDevice(ctx->device);
+    return synth(ctx, sp, 1, first, n, seed, lo, hi, n_centres, sigma, d_contig, d_start, d_end);
 }
 
 // ----------------------------------------------------------- host helpers

@@ -124,6 +124,8 @@ struct lime_bitset {
     uint64_t *words = nullptr;
     int64_t n_words = 0;
     int64_t runs_bound = -1;  // upper bound on its runs (rows painted), -1 unknown
+    int64_t word0 = 0;        // global index of words[0] (a coordinate shard's window)
+    int64_t hi_bit = 0;       // end of the window (global bits): bits >= hi_bit are outside
     int64_t span = 0;
     uint32_t *d_off = nullptr;
     int32_t n_contigs = 0;
@@ -149,6 +151,14 @@ inline void release(lime_ctx *c, T *&p) {
     if (p) c->pool.put(reinterpret_cast<void *>(p));
     p = nullptr;
 }
+
+// RAII release of a pool block on every return path
+template <typename T>
+struct PoolGuard {
+    lime_ctx *ctx;
+    T *&p;
+    ~PoolGuard() { release(ctx, p); }
+};
 
 // read a device scalar back to the host (synchronises the context stream)
 int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes);

@@ -1,0 +1,235 @@
+// route.hip -- range sharding of unsorted rows over coordinate shards
+// (SURVEY.md 8(e)): the device half of the Spark shuffles that move every
+// record to the partition owning it (ADAM repartitionAndSort at
+// cli/Intersection.scala:42-43; OverlapBasedSetTheory.scala:75-84 with the
+// explicit-destination ReferenceRegionRangePartitioner of
+// util/Partitioners.scala:10-20).
+//
+// Shard r owns global coordinates [split[r], split[r + 1]).  A row goes to
+// the shard owning its start (pairwise ops and merge: the owner of a row is
+// the shard of its start) or, clipped, to every shard it overlaps (bit-per-
+// base algebra, where clipping at shard bounds is exact).  The rows leave
+// grouped by destination, each destination's rows in input order, as
+// global-coordinate (gs, ge, row) arrays ready for one all_to_all per array.
+//
+//   k_route_count  per 1024-row block: pieces per destination -> column b of
+//                  the destination-major count matrix mat[d][b]
+//   scan           every (destination, block) segment's start
+//   k_route_write  pieces at their slots: per destination a block scan over
+//                  the threads keeps input order (deterministic output)
+#include "common.hpp"
+
+namespace lime {
+namespace {
+
+constexpr int RT = 256;
+constexpr int RPT = 4;           // rows per thread
+constexpr int RBLK = RT * RPT;   // rows per block
+constexpr int MAXSH = 64;
+
+struct RouteArgs {
+    const int32_t *contig;  // contig-local rows; null: start / end are global
+    const uint32_t *start, *end;
+    const uint32_t *off, *len;
+    int32_t nc;
+    int64_t n;
+    uint32_t span;
+    const uint32_t *split;  // nsh + 1 global bounds
+    int nsh;
+    int clip;
+    uint32_t row_base;
+    uint32_t *mat;  // nsh * nblk + 1
+    uint32_t nblk;
+    uint32_t *gs, *ge, *row;
+    unsigned int *err;  // bit0 contig, bit1 end < start, bit2 end > length / span
+};
+
+// global [g0, g1) of row i (validated; invalid rows become [0, 0) and raise err)
+__device__ __forceinline__ void route_row(const RouteArgs &a, int64_t i, uint32_t &g0, uint32_t &g1,
+                                          uint32_t &err) {
+    g0 = g1 = 0;
+    const uint32_t s = a.start[i], e = a.end[i];
+    if (!a.contig) {
+        if (e < s) err |= 2u;
+        else if (e > a.span) err |= 4u;
+        else g0 = s, g1 = e;
+        return;
+    }
+    const int32_t c = a.contig[i];
+    if (c < 0 || c >= a.nc) err |= 1u;
+    else if (e < s) err |= 2u;
+    else if (e > a.len[c]) err |= 4u;
+    else g0 = a.off[c] + s, g1 = a.off[c] + e;
+}
+
+// largest r with split[r] <= g (split in LDS, nsh <= 64)
+__device__ __forceinline__ int owner_of(const uint32_t *sp, int nsh, uint32_t g) {
+    int lo = 0, hi = nsh;  // answer in [lo, hi)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (sp[mid] <= g)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// destinations [d0, d1] of a row
+__device__ __forceinline__ void dests(const RouteArgs &a, const uint32_t *sp, uint32_t g0,
+                                      uint32_t g1, int &d0, int &d1) {
+    d0 = owner_of(sp, a.nsh, g0);
+    d1 = (a.clip && g1 > g0) ? owner_of(sp, a.nsh, g1 - 1) : d0;
+}
+
+__global__ __launch_bounds__(RT) void k_route_count(RouteArgs a) {
+    __shared__ uint32_t sp[MAXSH + 1];
+    __shared__ uint32_t cnt[MAXSH];
+    for (int i = threadIdx.x; i <= a.nsh; i += RT) sp[i] = a.split[i];
+    for (int i = threadIdx.x; i < a.nsh; i += RT) cnt[i] = 0;
+    __syncthreads();
+    uint32_t err = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int64_t i = (int64_t)blockIdx.x * RBLK + k * RT + threadIdx.x;
+        if (i >= a.n) continue;
+        uint32_t g0, g1;
+        route_row(a, i, g0, g1, err);
+        int d0, d1;
+        dests(a, sp, g0, g1, d0, d1);
+        for (int d = d0; d <= d1; ++d) atomicAdd(&cnt[d], 1u);
+    }
+    err = dev::wave_reduce_or(err);
+    if (err && dev::lane_id() == 0) atomicOr(a.err, err);
+    __syncthreads();
+    for (int d = threadIdx.x; d < a.nsh; d += RT) a.mat[(int64_t)d * a.nblk + blockIdx.x] = cnt[d];
+}
+
+__global__ __launch_bounds__(RT) void k_route_write(RouteArgs a) {
+    __shared__ uint32_t sp[MAXSH + 1];
+    __shared__ uint32_t scratch[RT / 64 + 1];
+    for (int i = threadIdx.x; i <= a.nsh; i += RT) sp[i] = a.split[i];
+    __syncthreads();
+    // rows of this thread: blocked (k * RT + t keeps loads coalesced; the
+    // order within a destination is the thread-major order below)
+    uint32_t g0[RPT], g1[RPT];
+    int d0[RPT], d1[RPT];
+    uint32_t err = 0;
+    int dmin = MAXSH, dmax = -1;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int64_t i = (int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k;
+        d0[k] = 0, d1[k] = -1;
+        if (i >= a.n) continue;
+        route_row(a, i, g0[k], g1[k], err);
+        dests(a, sp, g0[k], g1[k], d0[k], d1[k]);
+        dmin = min(dmin, d0[k]);
+        dmax = max(dmax, d1[k]);
+    }
+    // per destination: offset of this thread's pieces = block scan
+    for (int d = 0; d < a.nsh; ++d) {
+        uint32_t c = 0;
+        if (d >= dmin && d <= dmax)
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) c += (d >= d0[k] && d <= d1[k]);
+        uint32_t tot;
+        uint32_t pos = a.mat[(int64_t)d * a.nblk + blockIdx.x] +
+                       dev::block_exclusive_sum<RT>(c, scratch, &tot);
+        if (c == 0) continue;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            if (d < d0[k] || d > d1[k]) continue;
+            const uint32_t lo = sp[d], hi = sp[d + 1];
+            a.gs[pos] = a.clip ? max(g0[k], lo) : g0[k];
+            a.ge[pos] = a.clip && g1[k] > g0[k] ? min(g1[k], hi) : g1[k];
+            if (a.row)
+                a.row[pos] = a.row_base + (uint32_t)((int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k);
+            ++pos;
+        }
+    }
+}
+
+__global__ void k_route_totals(const uint32_t *__restrict__ mat, uint32_t nblk, int nsh,
+                               int64_t *__restrict__ out) {
+    const int d = threadIdx.x;
+    if (d <= nsh) out[d] = mat[(int64_t)d * nblk];
+}
+
+}  // namespace
+
+int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+               const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
+               const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
+               uint32_t *d_row, int64_t *counts) {
+    if (nsh < 1 || nsh > MAXSH) return fail(LIME_ERR_ARG, "1 to 64 shards");
+    if (splits[0] != 0 || (int64_t)splits[nsh] != sp->span)
+        return fail(LIME_ERR_ARG, "splits must start at 0 and end at the span");
+    for (int r = 0; r < nsh; ++r)
+        if (splits[r + 1] < splits[r]) return fail(LIME_ERR_ARG, "splits must be non-decreasing");
+    const uint32_t nblk = (uint32_t)std::max<int64_t>((n + RBLK - 1) / RBLK, 1);
+    const int64_t mlen = (int64_t)nsh * nblk + 1;
+    uint32_t *mat = nullptr, *d_split = nullptr, *d_off = nullptr, *d_len = nullptr;
+    unsigned int *err = nullptr;
+    int64_t *tot = nullptr;
+    LIME_TRY(alloc(ctx, &mat, (size_t)mlen));
+    PoolGuard<uint32_t> g0{ctx, mat};
+    LIME_TRY(alloc(ctx, &d_split, (size_t)nsh + 1));
+    PoolGuard<uint32_t> g1{ctx, d_split};
+    LIME_TRY(alloc(ctx, &d_off, (size_t)sp->n + 1));
+    PoolGuard<uint32_t> g2{ctx, d_off};
+    LIME_TRY(alloc(ctx, &d_len, (size_t)sp->n + 1));
+    PoolGuard<uint32_t> g3{ctx, d_len};
+    LIME_TRY(alloc(ctx, &err, 1));
+    PoolGuard<unsigned int> g4{ctx, err};
+    LIME_TRY(alloc(ctx, &tot, (size_t)nsh + 1));
+    PoolGuard<int64_t> g5{ctx, tot};
+    std::vector<uint32_t> len32(sp->n + 1, 0);
+    for (int c = 0; c < sp->n; ++c) len32[c] = (uint32_t)sp->len[c];
+    LIME_HIP(hipMemcpyAsync(d_split, splits, 4 * ((size_t)nsh + 1), hipMemcpyHostToDevice, S(ctx)));
+    LIME_HIP(hipMemcpyAsync(d_off, sp->off.data(), 4 * ((size_t)sp->n + 1), hipMemcpyHostToDevice,
+                            S(ctx)));
+    LIME_HIP(hipMemcpyAsync(d_len, len32.data(), 4 * ((size_t)sp->n + 1), hipMemcpyHostToDevice,
+                            S(ctx)));
+    LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
+    LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
+    RouteArgs a;
+    a.contig = d_contig;
+    a.start = d_start;
+    a.end = d_end;
+    a.off = d_off;
+    a.len = d_len;
+    a.nc = sp->n;
+    a.n = n;
+    a.span = (uint32_t)sp->span;
+    a.split = d_split;
+    a.nsh = nsh;
+    a.clip = clip;
+    a.row_base = row_base;
+    a.mat = mat;
+    a.nblk = nblk;
+    a.gs = d_gs;
+    a.ge = d_ge;
+    a.row = d_row;
+    a.err = err;
+    if (n > 0) hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(RT), 0, S(ctx), a);
+    LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
+    hipLaunchKernelGGL(k_route_totals, dim3(1), dim3(MAXSH + 1), 0, S(ctx), (const uint32_t *)mat,
+                       nblk, nsh, tot);
+    LIME_HIP(hipGetLastError());
+    // the destination starts (and the total) + the error flags: one read-back
+    std::vector<int64_t> h((size_t)nsh + 1);
+    LIME_TRY(read_back(ctx, h.data(), tot, 8 * ((size_t)nsh + 1)));
+    unsigned int herr = 0;
+    LIME_TRY(read_back(ctx, &herr, err, 4));
+    if (herr & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
+    if (herr & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
+    if (herr & 4u) return fail(LIME_ERR_RANGE, "interval end beyond its contig / the span");
+    // (h[nsh] is mat's last entry: the total, the scan's exclusive sum)
+    for (int d = 0; d < nsh; ++d) counts[d] = h[d + 1] - h[d];
+    if (h[nsh] > cap || n == 0) return LIME_OK;  // counts only
+    hipLaunchKernelGGL(k_route_write, dim3(nblk), dim3(RT), 0, S(ctx), a);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
+}  // namespace lime

@@ -29,6 +29,7 @@ struct SynthArgs {
     int32_t nc;
     uint64_t G;
     int64_t n;
+    int64_t first;  // rows [first, first + n) of the generator's sequence
     uint64_t seed;
     uint32_t len_lo, len_hi;
     int64_t n_centres;
@@ -51,8 +52,9 @@ __device__ __forceinline__ void place(const SynthArgs &a, int64_t i, uint64_t po
 __global__ __launch_bounds__(256) void k_uniform(SynthArgs a) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t pos = mulhi(rng(a.seed, i, 0), a.G);
-        const uint64_t l = a.len_lo + mulhi(rng(a.seed, i, 1), (uint64_t)(a.len_hi - a.len_lo) + 1);
+        const uint64_t r = (uint64_t)(a.first + i);
+        const uint64_t pos = mulhi(rng(a.seed, r, 0), a.G);
+        const uint64_t l = a.len_lo + mulhi(rng(a.seed, r, 1), (uint64_t)(a.len_hi - a.len_lo) + 1);
         place(a, i, pos, l);
     }
 }
@@ -61,12 +63,13 @@ __global__ __launch_bounds__(256) void k_pileup(SynthArgs a) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t s1 = a.seed + 1;
-        const uint64_t k = mulhi(rng(s1, i, 0), (uint64_t)a.n_centres);
+        const uint64_t r = (uint64_t)(a.first + i);
+        const uint64_t k = mulhi(rng(s1, r, 0), (uint64_t)a.n_centres);
         const uint64_t cpos = mulhi(rng(a.seed, k, 0), a.G);
         int64_t sum = 0;
 #pragma unroll
         for (int q = 1; q <= 3; ++q) {
-            uint64_t x = rng(s1, i, q);
+            uint64_t x = rng(s1, r, q);
 #pragma unroll
             for (int h = 0; h < 4; ++h) sum += (int64_t)((x >> (16 * h)) & 0xffff);
         }
@@ -74,17 +77,18 @@ __global__ __launch_bounds__(256) void k_pileup(SynthArgs a) {
         int64_t p = (int64_t)cpos + off;
         if (p < 0) p = 0;
         if (p >= (int64_t)a.G) p = (int64_t)a.G - 1;
-        const uint64_t l = a.len_lo + mulhi(rng(s1, i, 4), (uint64_t)(a.len_hi - a.len_lo) + 1);
+        const uint64_t l = a.len_lo + mulhi(rng(s1, r, 4), (uint64_t)(a.len_hi - a.len_lo) + 1);
         place(a, i, (uint64_t)p, l);
     }
 }
 
 }  // namespace
 
-int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t n, uint64_t seed, uint32_t lo,
-          uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig, uint32_t *d_start,
-          uint32_t *d_end) {
+int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t first, int64_t n, uint64_t seed,
+          uint32_t lo, uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig,
+          uint32_t *d_start, uint32_t *d_end) {
     if (n <= 0) return LIME_OK;
+    if (first < 0) return fail(LIME_ERR_ARG, "negative first row");
     if (hi < lo) return fail(LIME_ERR_ARG, "len_hi < len_lo");
     std::vector<uint64_t> base(sp->n + 1), len(sp->n);
     base[0] = 0;
@@ -104,6 +108,7 @@ int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t n, uint64_t see
     a.nc = sp->n;
     a.G = base[sp->n];
     a.n = n;
+    a.first = first;
     a.seed = seed;
     a.len_lo = lo;
     a.len_hi = hi;

@@ -180,3 +180,95 @@ def merge_carry(run_gs, run_ge=None, group=None, k=256, device=None):
         if not again:
             return drops[me], ext.get(me)
         k *= 2
+
+
+# ------------------------------------------------------ device exchanges
+def coord_splits(span, world, align=None):
+    """Equal coordinate ranges with inner bounds rounded to `align` (a
+    multiple of 64: the bitset's word; by default the bitset build's 2^22-base
+    bin, or a smaller power of two for small spans, so that no shard is
+    rounded away); last = span."""
+    if align is None:
+        align = 1 << 22
+        while align > 64 and align * 4 * world > span:
+            align >>= 1
+    cuts = [0]
+    for r in range(1, world):
+        c = (span * r // world) // align * align
+        cuts.append(min(max(c, cuts[-1]), span))
+    return cuts + [int(span)]
+
+
+def exchange(tensors, counts, group=None, comm_device=None):
+    """Variable all_to_all of 1-D tensors whose rows are grouped by destination
+    (counts[q] rows to rank q, the same for every tensor).  The tensors stay
+    on their device for RCCL (backend "nccl": xGMI peer traffic, no host
+    copy); with comm_device = cpu (gloo) they are staged through the host.
+    Returns (received tensors on the input device, received counts)."""
+    w, _ = _ws(group)
+    dev = tensors[0].device
+    cd = comm_device if comm_device is not None else dev
+    sc = torch.tensor(counts, dtype=torch.int64, device=cd)
+    rc = torch.empty(w, dtype=torch.int64, device=cd)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcounts = rc.tolist()
+    out = []
+    for t in tensors:
+        src = t[:sum(counts)].to(cd)
+        r = torch.empty(sum(rcounts), dtype=t.dtype, device=cd)
+        dist.all_to_all_single(r, src, output_split_sizes=rcounts,
+                               input_split_sizes=list(counts), group=group)
+        out.append(r.to(dev))
+    return out, rcounts
+
+
+def allgatherv(t, group=None, comm_device=None):
+    """all_gather of a variable number of rows per rank (RCCL has no
+    allgatherv): counts by one all_gather, rows by one padded all_gather,
+    returned concatenated in rank order on t's device (used only
+    when a caller needs the whole ordered list, the CLIs' collect())."""
+    w, _ = _ws(group)
+    dev = t.device
+    cd = comm_device if comm_device is not None else dev
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=cd)
+    ns = torch.empty(w, dtype=torch.int64, device=cd)
+    dist.all_gather_into_tensor(ns, n, group=group)
+    ns = ns.tolist()
+    m = max(ns) if ns else 0
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=cd)
+    pad[:t.shape[0]] = t.to(cd)
+    allp = torch.empty((w * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=cd)
+    dist.all_gather_into_tensor(allp, pad, group=group)
+    parts = [allp[r * m:r * m + ns[r]] for r in range(w)]
+    return torch.cat(parts).to(dev), ns
+
+
+def bitset_carry(n_runs, first_start, first_end, last_end, group=None, device=None):
+    """Runs of bit-per-base results split at shard bounds: a run ending exactly
+    where the next non-empty shard's first run starts is ONE run of the
+    single-device result (base-level runs are maximal).  One all_gather of
+    (n, first start, first end, last end) per shard; returns (drop_first,
+    new_last_end or None) for this shard: drop its first run, and/or extend
+    its last run, so that the shards' runs concatenate to the unsharded
+    result.  A shard whose only run is absorbed passes the run on."""
+    w, me = _ws(group)
+    dev = device if device is not None else "cpu"
+    h = torch.tensor([n_runs, first_start, first_end, last_end], dtype=torch.int64, device=dev)
+    allh = torch.empty(4 * w, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allh, h, group=group)
+    info = allh.view(w, 4).cpu().tolist()
+    owner, cend = -1, -1
+    drops, ext = [0] * w, {}
+    for r in range(w):
+        n, fs, fe, le = info[r]
+        if n == 0:
+            continue
+        if owner >= 0 and fs == cend:
+            drops[r] = 1
+            if n == 1:
+                ext[owner] = le
+                cend = le
+                continue
+            ext[owner] = fe
+        owner, cend = r, le
+    return drops[me], ext.get(me)

@@ -253,6 +253,12 @@ class Bitset:
     def popcount(self):
         return int(_lib().lime_bitset_popcount(self.ctx.handle, self._h))
 
+    def window(self):
+        """(lo, n_words): the global bits this bitset covers start at lo"""
+        lo, nw = i64(), i64()
+        check(_lib().lime_bitset_window(self._h, C.byref(lo), C.byref(nw)))
+        return lo.value, nw.value
+
     def close(self):
         if self._h and self.ctx.handle:  # a closed context already freed its pool
             _lib().lime_bitset_destroy(self._h)
@@ -395,6 +401,28 @@ class Context:
                                              vp(d_start), vp(d_end), C.byref(h)))
         return Bitset(self, h, space)
 
+    def bitset_from_global(self, space, lo, hi, n, d_gs, d_ge):
+        """a coordinate shard's bitset: global bits [lo, hi) from device rows in
+        global coordinates (clipped to the window)"""
+        h = vp()
+        check(_lib().lime_bitset_from_global(self._h, space.handle, int(lo), int(hi), int(n),
+                                             vp(d_gs), vp(d_ge), C.byref(h)))
+        return Bitset(self, h, space)
+
+    def route_rows(self, space, n, d_contig, d_start, d_end, splits, clip=False, cap=-1,
+                   d_gs=None, d_ge=None, d_row=None, row_base=0):
+        """Rows -> coordinate shards (lime_route_rows): returns the per-shard
+        counts; when their total <= cap the rows are written, grouped by
+        shard, to d_gs / d_ge (global) and d_row (row_base + input index).
+        d_contig None: d_start / d_end are already global."""
+        k = len(splits) - 1
+        sp = (C.c_uint32 * (k + 1))(*[int(x) for x in splits])
+        counts = (i64 * k)()
+        check(_lib().lime_route_rows(self._h, space.handle, int(n), vp(d_contig), vp(d_start),
+                                     vp(d_end), int(row_base) & 0xFFFFFFFF, k, sp, int(bool(clip)),
+                                     int(cap), vp(d_gs), vp(d_ge), vp(d_row), counts))
+        return list(counts)
+
     def bitset_runs(self, op, a, b=None):
         h, n = vp(), i64()
         check(_lib().lime_bitset_runs(self._h, int(op), a._h, b._h if b is not None else None,
@@ -411,6 +439,12 @@ class Context:
     def synth_uniform(self, space, n, seed, len_lo, len_hi, d_contig, d_start, d_end):
         check(_lib().lime_synth_uniform(self._h, space.handle, int(n), int(seed), int(len_lo),
                                         int(len_hi), d_contig, d_start, d_end))
+
+    def synth_uniform_rows(self, space, first, n, seed, len_lo, len_hi, d_contig, d_start,
+                           d_end):
+        """rows [first, first + n) of lime_synth_uniform's sequence"""
+        check(_lib().lime_synth_uniform_rows(self._h, space.handle, int(first), int(n), int(seed),
+                                             int(len_lo), int(len_hi), d_contig, d_start, d_end))
 
     def synth_pileup(self, space, n, seed, n_centres, sigma, len_lo, len_hi, d_contig, d_start,
                      d_end):

@@ -115,3 +115,106 @@ class ShardStep:
             if E is not S:
                 E.close()
         return out
+
+
+class ShardedAnd:
+    """BASELINE C5: k-way intersection over bit-per-base sets, range-sharded.
+
+    Shard r (one rank per GPU) owns global coordinates [splits[r],
+    splits[r+1]) (lime_amd.dist.coord_splits).  Per input set every rank
+    routes its slice of unsorted rows to the shards they overlap, clipped at
+    the shard bounds (lime_route_rows, clip = 1: exact for base-level
+    algebra, no halo); one all_to_all moves them (RCCL over
+    xGMI, device buffers); each shard paints the rows it received into a
+    bitset over its window (lime_bitset_from_global) and ANDs the k bitsets
+    (lime_bitset_and_runs).  Runs are in global coordinates; the one
+    boundary fix-up (a run ending exactly at a shard bound continues in the
+    next shard) is dist.bitset_carry, one all_gather of 4 numbers per shard.
+    The runs stay sharded; run(gather=True) adds the emulated allgatherv.
+    Same code at world size 1 (no collective is issued then).
+
+    Reference analogue: the range partitioning + replication of
+    OverlapBasedSetTheory.scala:74-84 (here each right record is clipped, not
+    replicated) and SURVEY.md Appendix A.4 (N-way = fold of intersect over
+    merged operands, per base).
+    """
+
+    def __init__(self, ctx, space, splits=None, group=None, comm_device=None,
+                 shared_stream=False):
+        self.ctx, self.space, self.group = ctx, space, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.splits = splits or ld.coord_splits(space.span, self.world)
+        self.lo, self.hi = self.splits[self.rank], self.splits[self.rank + 1]
+        self.dev = torch.device("cuda", ctx.device)
+        self.comm = comm_device
+        # the engine shares torch's current stream (bench): stream order
+        # covers the collectives; otherwise drain around them
+        self.shared = shared_stream
+        self.moved = 0  # rows received from other shards (diagnostics)
+
+    def _sync(self):
+        if not self.shared:
+            self.ctx.synchronize()
+            torch.cuda.current_stream(self.dev).synchronize()
+
+    def bitset(self, n, d_contig, d_start, d_end):
+        """this shard's bitset of one set, from this rank's slice of its rows"""
+        ctx, sp = self.ctx, self.space
+        if self.world == 1:
+            return ctx.bitset_from_device(sp, n, d_contig, d_start, d_end)
+        cap = n + 4096
+        gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
+                                cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
+        if sum(counts) > cap:  # many rows cross shard bounds: exact size
+            cap = sum(counts)
+            gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
+            ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
+            counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
+                                    cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
+        self._sync()
+        (rgs, rge), rc = ld.exchange([gs, ge], counts, self.group, self.comm)
+        self._sync()
+        self.moved += sum(rc) - rc[self.rank]
+        m = sum(rc)
+        return ctx.bitset_from_global(sp, self.lo, self.hi, m, rgs.data_ptr(), rge.data_ptr())
+
+    def run(self, inputs, gather=False):
+        """inputs: [(n, d_contig, d_start, d_end)] per set (this rank's rows,
+        device pointers).  Returns a dict: the shard's AND result (global
+        coordinates), the carry (drop_first, new_last_end), the total run
+        count of the unsharded result and, with gather=True, every run as an
+        int64 [m, 2] tensor (global start, end) in order."""
+        bits = [self.bitset(*x) for x in inputs]
+        res = self.ctx.bitset_and(bits)
+        for b in bits:
+            b.close()
+        n = res.n
+        drop, ext = 0, None
+        total = n
+        if self.world > 1:
+            fs = fe = le = -1
+            if n:
+                gs0, ge0 = res.copy_range(0, 1)
+                fs, fe = int(gs0[0]), int(ge0[0])
+                _, gel = res.copy_range(n - 1, 1)
+                le = int(gel[0])
+            drop, ext = ld.bitset_carry(n, fs, fe, le, self.group, self.comm or self.dev)
+            cd = self.comm or self.dev
+            t = torch.tensor([n - drop], dtype=torch.int64, device=cd)
+            dist.all_reduce(t, group=self.group)
+            total = int(t.item())
+        out = {"result": res, "drop": drop, "extend": ext, "runs_total": total,
+               "window": (self.lo, self.hi)}
+        if gather:
+            gs, ge = res.copy_range(0, n) if n else (np.zeros(0, np.uint32),) * 2
+            runs = np.stack([gs.astype(np.int64), ge.astype(np.int64)], axis=1)[drop:]
+            if ext is not None and len(runs):
+                runs[-1, 1] = ext
+            t = torch.from_numpy(np.ascontiguousarray(runs))
+            if self.world > 1:
+                t, _ = ld.allgatherv(t.to(self.comm or self.dev), self.group, self.comm)
+            out["runs"] = t.cpu()
+        return out

@@ -117,3 +117,96 @@ def test_sharded_intersect_and_merge(world, mode):
     assert len(pairs) == len(set(pairs))  # shard outputs are disjoint
     m = oracle.merge((z, gA, eA))
     assert runs == list(zip(m["start"].tolist(), m["end"].tolist()))
+
+
+# ------------------------------------------- bitset sharding (C5 host logic)
+def _runs_of(bits, lo):
+    """runs of a 0/1 array as (global start, end)"""
+    d = np.diff(np.concatenate([[0], bits.astype(np.int8), [0]]))
+    s, e = np.flatnonzero(d == 1), np.flatnonzero(d == -1)
+    return np.stack([s + lo, e + lo], axis=1).astype(np.int64)
+
+
+def _and_sets(span, k, n, seed, maxlen):
+    """k sets of n rows; every 50th row is long (up to 40 shard-widths of
+    64), so runs cross and swallow whole shards"""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(k):
+        g = rng.integers(0, span - 20 * maxlen, n)
+        ln = rng.integers(0, maxlen, n)
+        ln[::50] = rng.integers(maxlen, 20 * maxlen, len(ln[::50]))
+        out.append((g, g + ln))
+    return out
+
+
+def _bits_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        span, k, n = 50_000, 3, 400
+        sets = _and_sets(span, k, n, 7, 300)
+        splits = ld.coord_splits(span, world, align=64)
+        lo, hi = splits[rank], splits[rank + 1]
+        acc = np.ones(hi - lo, bool)
+        for g, e in sets:
+            # this rank's slice of the rows, clipped and routed (the device
+            # router's rule, restated), moved by the product exchange
+            sl = slice(rank * n // world, (rank + 1) * n // world)
+            pieces = [[] for _ in range(world)]
+            for a, b in zip(g[sl], e[sl]):
+                for r in range(world):
+                    s_, e_ = max(a, splits[r]), min(b, splits[r + 1])
+                    if e_ > s_:
+                        pieces[r].append((s_, e_))
+            counts = [len(p) for p in pieces]
+            flat = [x for p in pieces for x in p] or [(0, 0)]
+            gs = torch.tensor([x[0] for x in flat], dtype=torch.int32)
+            ge = torch.tensor([x[1] for x in flat], dtype=torch.int32)
+            (rgs, rge), rc = ld.exchange([gs, ge], counts)
+            cov = np.zeros(hi - lo, bool)
+            for a, b in zip(rgs.tolist(), rge.tolist()):
+                assert lo <= a and b <= hi
+                cov[a - lo:b - lo] = True
+            acc &= cov
+        runs = _runs_of(acc, lo)
+        n_r = len(runs)
+        fs, fe, le = (int(runs[0, 0]), int(runs[0, 1]), int(runs[-1, 1])) if n_r else (-1, -1, -1)
+        drop, ext = ld.bitset_carry(n_r, fs, fe, le)
+        mine = runs[drop:].copy()
+        if ext is not None and len(mine):
+            mine[-1, 1] = ext
+        allr, _ = ld.allgatherv(torch.from_numpy(mine))
+        q.put((rank, allr.numpy().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_bitset_and_carry(world):
+    # shard-count invariance of the C5 boundary logic: rows clipped at shard
+    # bounds, per-shard AND, book-ended runs re-joined by bitset_carry, the
+    # emulated allgatherv == the unsharded per-base AND
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bits_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    span, k, n = 50_000, 3, 400
+    acc = np.ones(span, bool)
+    for g, e in _and_sets(span, k, n, 7, 300):
+        cov = np.zeros(span, bool)
+        for a, b in zip(g, e):
+            cov[a:b] = True
+        acc &= cov
+    want = _runs_of(acc, 0).tolist()
+    assert len(want) > 30
+    for _, got in res:
+        assert got == want  # every rank holds the whole ordered list

@@ -117,3 +117,88 @@ def test_sharded_engine_matches_single_shard(world):
         runs = sum((r[2][k] for r in res), [])
         assert [tuple(map(int, t)) for t in runs] == \
             list(zip(m["contig"].tolist(), m["start"].tolist(), m["end"].tolist()))
+
+
+# ------------------------------------------------------------ sharded C5
+C5_LENS = [3_000_000, 2_000_000, 2_500_000]
+C5_K, C5_N = 4, 120_000  # rows per set (all ranks together), len U[10, 400]
+
+
+def _c5_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        import lime_amd
+        from lime_amd.sharded import ShardedAnd
+        ctx = lime_amd.Context(0)
+        sp = lime_amd.Space(NAMES, C5_LENS)
+        # this rank's slice of every set: rows [first, first + m) of the
+        # counter-based generator, unsorted, on the device
+        first, last = rank * C5_N // world, (rank + 1) * C5_N // world
+        m = last - first
+        inputs, keep = [], []
+        for i in range(C5_K):
+            c = torch.empty(m, dtype=torch.int32, device="cuda")
+            s = torch.empty(m, dtype=torch.int32, device="cuda")
+            e = torch.empty(m, dtype=torch.int32, device="cuda")
+            ctx.synth_uniform_rows(sp, first, m, 0x70 + i, 10, 400, c.data_ptr(), s.data_ptr(),
+                                   e.data_ptr())
+            keep.append((c, s, e))
+            inputs.append((m, c.data_ptr(), s.data_ptr(), e.data_ptr()))
+        ctx.synchronize()
+        step = ShardedAnd(ctx, sp, comm_device=torch.device("cpu"))
+        out = step.run(inputs, gather=True)
+        q.put((rank, out["runs"].numpy().tolist(), out["runs_total"], step.moved,
+               [int(x) for x in sp.offsets]))
+        out["result"].close()
+        ctx.close()
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc(), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_sharded_c5_matches_single_shard_oracle(world):
+    # BASELINE C5's sharded path (route + clip + all_to_all + windowed
+    # bitsets + AND + boundary carry + allgatherv) with `world` ranks sharing
+    # the GPU (gloo), against the oracle fold of intersect over the merged
+    # operands (coalesced book-ended runs)
+    from lime_amd import synth
+    from oracle import oracle
+    from tests.test_gpu_configs import coalesce, fold_and
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_c5_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    errs = [r[2] for r in res if r[1] == "error"]
+    assert not errs, errs[0]
+    for p in ps:
+        assert p.exitcode == 0
+    off = np.array(res[0][4])
+    merged = []
+    for i in range(C5_K):
+        X = synth.uniform(C5_LENS, C5_N, 0x70 + i, 10, 400)
+        merged.append(oracle.merge_mt(len(C5_LENS), X))
+    exp = fold_and(len(C5_LENS), merged)
+    want = coalesce(exp["contig"], exp["start"], exp["end"])
+    for r in res:
+        runs = np.array(r[1], dtype=np.int64).reshape(-1, 2)
+        # global -> (contig, local)
+        c = np.searchsorted(off, runs[:, 0], side="right") - 1
+        got = coalesce(c, runs[:, 0] - off[c], runs[:, 1] - off[c])
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y)
+        assert r[2] == len(runs)
+    if world > 1:
+        assert sum(r[3] for r in res) > 0  # rows really moved between shards

@@ -1,23 +1,34 @@
-"""bench.py -- BASELINE.json's metric on its N=1 configuration (C2).
+"""bench.py -- BASELINE.json's metric on its configurations.
 
-One step = the whole operator pipeline over one batch of synthetic input
-already resident in HBM (unsorted, as loaded):
-  device radix sort of A and B  ->  intersect count pass  ->  fill of every
-  qualifying pair (16-B records, chunked through a reusable output buffer)
-  ->  merge(A), merge(B)  (runs + run id of every row).
+--workload c2 (default; the headline metric "intervals/sec for pairwise
+intersect+merge"): one step = the whole operator pipeline over one batch of
+synthetic input already resident in HBM (unsorted, as loaded):
+  N = 1:  device radix sort of A and B -> intersect count pass -> fill of
+          every qualifying pair (16-B records, chunked through a reusable
+          output buffer) -> merge(A), merge(B) (runs + run id of every row).
+  N > 1:  ONE C2 input (the same 2 x 1e8 rows) range-sharded over the N
+          ranks (strong scaling): every rank starts from its 1/N slice of the
+          unsorted rows; route to owner shards (device counting scatter +
+          all_to_all over RCCL) -> sort -> local merges -> device halo
+          exchange -> owned intersect count + fill -> merge carry
+          (lime_amd.sharded.ShardStep).
 C2 = 2 x 1e8 intervals, uniform starts over hg38 primary, lengths U[50,5000]
-(~1.63e10 pairs per step).  value = intervals processed per second by the
-whole job (sum over ranks).
+(~1.63e10 pairs per step).
 
-Multi-GPU (torchrun, one rank per GPU): every rank owns one coordinate shard
--- its own copy of the hg38 space with its own seeds -- and runs the same
-per-GPU workload (weak scaling); shards are independent, so the data path has
-no collective; a barrier brackets the timed region and the time is the max
-over ranks.
+--workload c5: BASELINE C5, the 8-way intersection of 8 x 1.25e8 rows (len
+U[10,40], seeds 0x50..0x57) over hg38: every rank holds its 1/N slice of every
+set; rows routed to the shard(s) they overlap, clipped (exact for per-base
+algebra), bit-per-base sets painted per shard window, AND-ed, runs extracted,
+boundary carry (lime_amd.sharded.ShardedAnd; no collective at N = 1).
 
-Also reported: roofline of the dominant kernel (k_fill, HBM-bound) from HIP
-events on the launch stream, and a CPU baseline (the oracle's restatement of
-lime's sweep-line, 1 thread) on a bounded sample, rank 0 / N=1 only.
+value = intervals processed per second by the whole job; the time is the
+max over ranks of the timed region, bracketed by barriers.
+
+Also reported: the roofline of the dominant kernel (c2: k_fill, HBM-bound,
+HIP events on the launch stream; c5: the whole step against its
+algorithmic bytes 12 B per row + 8 bitsets of G/8) and a CPU baseline (the
+oracle's restatement of lime's algorithm on a bounded sample), rank 0 /
+N = 1 only.
 """
 import argparse
 import json
@@ -36,7 +47,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rows", type=int, default=100_000_000, help="rows per set (C2: 1e8)")
+    p.add_argument("--workload", default="c2", choices=["c2", "c5"])
+    p.add_argument("--rows", type=int, default=None,
+                   help="rows per set (C2: 1e8; C5: 1.25e8, 8 sets)")
     p.add_argument("--chunk", type=int, default=1 << 31, help="pairs per output chunk")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -155,6 +168,37 @@ def cpu_baseline_threaded(L, ac, as_, ae, bc, bs, be, reps):
             "max_share": max(load) / max(1, sum(load))}
 
 
+def c5_cpu_baseline(scale, per_full, k=8, reps=3):
+    """lime's fold of intersect over merged operands
+    restated in C (oracle/lime_oracle.c, contig-sharded threads), on C5's
+    density over hg38/scale with per/scale rows per set; sort included."""
+    import numpy as np
+
+    from lime_amd import synth
+    from oracle import oracle
+    lens = np.array(list(synth.HG38.values())) // scale
+    n = per_full // scale
+    sets = [synth.uniform(lens, n, 0x50 + i, 10, 40) for i in range(k)]
+    nc = len(lens)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        merged = [oracle.merge_mt(nc, X) for X in sets]
+        cur = merged[0]
+        for m in merged[1:]:
+            ix = oracle.intersect_mt(nc, (cur["contig"], cur["start"], cur["end"]),
+                                     (m["contig"], m["start"], m["end"]), records=True)
+            cur = {q: ix[q] for q in ("contig", "start", "end")}
+        times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    thr = oracle.threads()
+    return {"value": k * n / t, "unit": "intervals/s", "cores": thr, "kind": "port",
+            "sample": f"C5 density on hg38/{scale}: {k} x {n} rows, merge of every set then "
+                      f"the fold of intersect over the merged operands (Appendix A.4), median "
+                      f"of {reps}; restated in C (oracle/lime_oracle.c), {thr} threads sharded "
+                      "by contig; every merge sorts its input inside the timed region"}
+
+
 def main():
     args = parse()
     import torch
@@ -164,11 +208,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; --dist-backend gloo lets several ranks share one GPU
-    # (rehearsal of the multi-GPU path on a 1-GPU box, boundary records on CPU)
+    # (rehearsal of the multi-GPU path on a 1-GPU box, rows staged on the host)
     gpu = local % max(torch.cuda.device_count(), 1)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
-    comm_dev = dev
+    comm_dev = None  # RCCL: device buffers
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -181,34 +225,73 @@ def main():
 
     ctx = lime_amd.Context(dev.index)
     # one non-default stream shared by torch and the engine: the HIP events
-    # below are recorded on the stream the kernels are launched on
+    # below are recorded on the stream the kernels are launched on, and the
+    # collectives are stream-ordered with the engine's kernels
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     space = lime_amd.Space(list(synth.HG38.keys()), list(synth.HG38.values()))
-    n = args.rows
-    seed_a, seed_b = 0xA + 0x100 * rank, 0xB + 0x100 * rank
-
-    def gen(seed):
-        c = torch.empty(n, dtype=torch.int32, device=dev)
-        s = torch.empty(n, dtype=torch.int32, device=dev)
-        e = torch.empty(n, dtype=torch.int32, device=dev)
-        ctx.synth_uniform(space, n, seed, 50, 5000, c.data_ptr(), s.data_ptr(), e.data_ptr())
-        return c, s, e
-    A_in, B_in = gen(seed_a), gen(seed_b)
-    buf = torch.empty((args.chunk, 4), dtype=torch.int32, device=dev)
-    torch.cuda.synchronize(dev)
-
-    fills = []  # (start event, end event, pairs) of every fill launch
 
     def ev():
         e = torch.cuda.Event(enable_timing=True)
         e.record(stream)
         return e
 
-    def fill_all(plan, halos=None):
-        for f in range(0, plan.n, args.chunk):
-            k = min(args.chunk, plan.n - f)
+    if args.workload == "c5":
+        run = bench_c5(args, ctx, space, dev, world, rank, comm_dev, ev)
+    else:
+        run = bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev)
+    step, finish = run
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i == args.steps - 1)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=comm_dev or dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    line = finish(dt)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
+    import torch
+    n = args.rows or 100_000_000
+    seed_a, seed_b = 0xA, 0xB
+    # this rank's slice of the one C2 input (all of it at N = 1)
+    first, last = rank * n // world, (rank + 1) * n // world
+    m = last - first
+
+    def gen(seed):
+        c = torch.empty(m, dtype=torch.int32, device=dev)
+        s = torch.empty(m, dtype=torch.int32, device=dev)
+        e = torch.empty(m, dtype=torch.int32, device=dev)
+        ctx.synth_uniform_rows(space, first, m, seed, 50, 5000, c.data_ptr(), s.data_ptr(),
+                               e.data_ptr())
+        return c, s, e
+    A_in, B_in = gen(seed_a), gen(seed_b)
+    chunk = args.chunk if world == 1 else min(args.chunk, max(1, 4 * (1 << 31) // world))
+    buf = torch.empty((chunk, 4), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    fills = []  # (start event, end event, pairs of the launch, pairs of the plan)
+    state = {"phases": None, "npairs": 0, "nruns": 0, "halo": (0, 0), "routed": 0}
+
+    def fill_all(plan):
+        for f in range(0, plan.n, chunk):
+            k = min(chunk, plan.n - f)
             e0 = ev()
             plan.fill_device(f, k, buf.data_ptr())
             fills.append((e0, ev(), k, plan.n))
@@ -216,24 +299,28 @@ def main():
     shard = None
     if world > 1:
         from lime_amd.sharded import ShardStep
-        # rank r owns the r-th copy of the genome on one virtual coordinate
-        # line: offset r * span; boundary exchange + merge carry over RCCL
-        shard = ShardStep(ctx, space, offset=rank * space.span, comm_device=comm_dev)
+        shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
 
-    def step(phases=None):
-        t = [ev()] if phases is not None else None
-        A = ctx.set_from_device(space, n, *(x.data_ptr() for x in A_in))
-        B = ctx.set_from_device(space, n, *(x.data_ptr() for x in B_in))
-        if t is not None:
-            t.append(ev())
+    def step(last_step):
+        t = [ev()] if last_step else None
         if shard is not None:
+            A = shard.load(m, *(x.data_ptr() for x in A_in), row_base=first)
+            B = shard.load(m, *(x.data_ptr() for x in B_in), row_base=first)
+            if t is not None:
+                t.append(ev())
             out = shard.run(A, B, on_pairs=fill_all)
             for h in (out["merge_a"], out["merge_b"], A, B):
                 h.close()
             if t is not None:
-                t += [ev(), ev(), ev()]
-                phases.append(t)
-            return out["pairs"], out["runs_a"] + out["runs_b"]
+                t.append(ev())
+                state["phases"] = t
+                state["halo"] = out["halo"]
+            state["npairs"], state["nruns"] = out["pairs"], out["runs_a"] + out["runs_b"]
+            return
+        A = ctx.set_from_device(space, m, *(x.data_ptr() for x in A_in))
+        B = ctx.set_from_device(space, m, *(x.data_ptr() for x in B_in))
+        if t is not None:
+            t.append(ev())
         plan = ctx.intersect(A, B)
         if t is not None:
             t.append(ev())
@@ -243,83 +330,134 @@ def main():
         ma, mb = ctx.merge(A), ctx.merge(B)
         if t is not None:
             t.append(ev())
-            phases.append(t)
-        npairs, nruns = plan.n, ma.n + mb.n
+            state["phases"] = t
+        state["npairs"], state["nruns"] = plan.n, ma.n + mb.n
         for h in (plan, ma, mb, A, B):
             h.close()
-        return npairs, nruns
 
-    for _ in range(args.warmup):
-        step()
-    fills.clear()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    phases = []
-    for i in range(args.steps):
-        npairs, nruns = step(phases if i == args.steps - 1 else None)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=comm_dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    ms = dt / args.steps * 1e3
-    value = world * 2 * n / (dt / args.steps)
-
-    # roofline of the dominant kernel (fill): algorithmic bytes per launch =
-    # 16 B per pair written + 20 B per owner row consumed (lo, count, start,
-    # end, row), prorated to the pairs of the launch
-    fill_ms = [a.elapsed_time(b) for a, b, _, _ in fills]
-    fill_bytes = [16 * k + 20 * (2 * n) * k / tot for _, _, k, tot in fills]
-    avg_ms = sum(fill_ms) / len(fill_ms)
-    avg_b = sum(fill_bytes) / len(fill_bytes)
-    achieved = avg_b / (avg_ms * 1e-3) / 1e9
-    p = phases[-1]
-    if world > 1:
-        breakdown = {"sort_ms": p[0].elapsed_time(p[1]),
-                     "merge_halo_intersect_fill_carry_ms": p[1].elapsed_time(p[2]),
-                     "fill_ms": sum(fill_ms[-(-npairs // args.chunk):])}
-    else:
-        breakdown = {"sort_ms": p[0].elapsed_time(p[1]), "count_ms": p[1].elapsed_time(p[2]),
-                     "fill_ms": p[2].elapsed_time(p[3]), "merge_ms": p[3].elapsed_time(p[4])}
-
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "fill_pmc.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_scale, n)
-
-    if rank == 0:
-        line = {
+    def finish(dt):
+        import torch.distributed as dist
+        ms = dt / args.steps * 1e3
+        value = 2 * n / (dt / args.steps)
+        timed = fills[-args.steps * max(1, -(-state["npairs"] // chunk)):] if fills else []
+        fill_ms = [a.elapsed_time(b) for a, b, _, _ in timed]
+        # algorithmic bytes per launch: 16 B per pair written + 20 B per owner
+        # row consumed (lo, count, start, end, row), prorated to the launch
+        own = 2 * m
+        fill_bytes = [16 * k + 20 * own * k / tot for _, _, k, tot in timed]
+        avg_ms = sum(fill_ms) / max(len(fill_ms), 1)
+        avg_b = sum(fill_bytes) / max(len(fill_bytes), 1)
+        achieved = avg_b / (avg_ms * 1e-3) / 1e9 if avg_ms else 0.0
+        p = state["phases"]
+        if world > 1:
+            breakdown = {"route_sort_ms": p[0].elapsed_time(p[1]),
+                         "merge_halo_count_fill_carry_ms": p[1].elapsed_time(p[2]),
+                         "fill_ms": sum(fill_ms[-max(1, -(-state["npairs"] // chunk)):]),
+                         "halo_rows": list(state["halo"]), "rows_routed_in": shard.routed}
+        else:
+            breakdown = {"sort_ms": p[0].elapsed_time(p[1]), "count_ms": p[1].elapsed_time(p[2]),
+                         "fill_ms": p[2].elapsed_time(p[3]), "merge_ms": p[3].elapsed_time(p[4])}
+        npairs, nruns = state["npairs"], state["nruns"]
+        if world > 1:
+            tt = torch.tensor([npairs, nruns], dtype=torch.int64, device=comm_dev or dev)
+            dist.all_reduce(tt)
+            npairs, nruns = (int(x) for x in tt.tolist())
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "fill_pmc.json")
+        if os.path.exists(pmc) and world == 1:
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_scale, n)
+        return {
             "metric": "intervals/sec for pairwise intersect+merge at 1/2/4/8 GPUs; "
                       "% of HBM peak GB/s",
             "value": value, "unit": "intervals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (counter-based splitmix64, seeds 0xA/0xB per shard)",
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (counter-based splitmix64, seeds 0xA/0xB; rank r generates "
+                    "rows [r n/N, (r+1) n/N) of the one input)",
             "config": {"workload": "C2: sort + intersect + merge(A), merge(B); 2 x 1e8 "
-                                   "intervals per GPU, uniform over hg38, len U[50,5000]",
+                                   "intervals, uniform over hg38, len U[50,5000]"
+                                   + (", one genome range-sharded over the ranks"
+                                      if world > 1 else ""),
                        "rows_per_set": n, "pairs_per_step": npairs, "runs_per_step": nruns,
-                       "output_chunk_pairs": args.chunk, "parallelism": f"range-shard x{world}"},
+                       "output_chunk_pairs": chunk,
+                       "parallelism": f"range-shard x{world}" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_fill<false>", "avg_launch_ms": avg_ms,
-                         "alg_bytes_per_launch": avg_b, "launches": len(fills)},
+                         "alg_bytes_per_launch": avg_b, "launches": len(timed)},
             "breakdown_ms": breakdown,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return step, finish
+
+
+def bench_c5(args, ctx, space, dev, world, rank, comm_dev, ev):
+    import torch
+
+    from lime_amd.sharded import ShardedAnd
+    k = 8
+    per = args.rows or 125_000_000
+    first, last = rank * per // world, (rank + 1) * per // world
+    m = last - first
+    ins = []
+    for i in range(k):
+        c = torch.empty(m, dtype=torch.int32, device=dev)
+        s = torch.empty(m, dtype=torch.int32, device=dev)
+        e = torch.empty(m, dtype=torch.int32, device=dev)
+        ctx.synth_uniform_rows(space, first, m, 0x50 + i, 10, 40, c.data_ptr(), s.data_ptr(),
+                               e.data_ptr())
+        ins.append((c, s, e))
+    torch.cuda.synchronize(dev)
+    op = ShardedAnd(ctx, space, comm_device=comm_dev, shared_stream=True)
+    state = {"t": None, "runs": 0}
+
+    def step(last_step):
+        t0 = ev() if last_step else None
+        out = op.run([(m, *(x.data_ptr() for x in X)) for X in ins])
+        if last_step:
+            state["t"] = (t0, ev())
+        state["runs"] = out["runs_total"]
+        out["result"].close()
+
+    def finish(dt):
+        ms = dt / args.steps * 1e3
+        G = int(sum(synth_lengths()))
+        W = (space.span + 63) // 64 * 8
+        alg = 12 * k * per + k * W  # rows read once + k bitsets (G/8 each)
+        achieved = alg / world / (ms * 1e-3) / 1e9
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = c5_cpu_baseline(100, per)
+        return {
+            "metric": "intervals/sec for 8-way intersection (BASELINE C5); % of HBM peak GB/s",
+            "value": k * per / (dt / args.steps), "unit": "intervals/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (counter-based splitmix64, seeds 0x50..0x57; rank r generates "
+                    "rows [r n/N, (r+1) n/N) of every set)",
+            "config": {"workload": f"C5: {k}-way intersection, {k} x {per} rows, len U[10,40], "
+                                   "hg38, bit-per-base path" +
+                                   (", range-sharded with clipped rows" if world > 1 else ""),
+                       "sets": k, "rows_per_set": per, "runs_per_step": state["runs"],
+                       "genome_bases": G,
+                       "parallelism": f"range-shard x{world}" if world > 1 else "1 GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "whole C5 step (route, bin, paint, AND, extract) per GPU",
+                         "alg_bytes_per_step_per_gpu": alg / world,
+                         "step_ms_hip_events": state["t"][0].elapsed_time(state["t"][1])},
+            "cpu_baseline": cpu,
+        }
+    return step, finish
+
+
+def synth_lengths():
+    from lime_amd import synth
+    return list(synth.HG38.values())
 
 
 if __name__ == "__main__":

@@ -1,12 +1,12 @@
-"""Range-sharded operator step: one engine context per rank (one GPU per
-process), rows exchanged with torch.distributed (RCCL over xGMI on MI355X,
-gloo in CPU-side tests).  See lime_amd.dist for the protocol.
+"""Range-sharded operator steps: one engine context per rank (one GPU per
+process), rows exchanged with torch.distributed (RCCL over xGMI on MI355X;
+gloo, staged through the host, in CPU-side tests and one-GPU rehearsals).
+See lime_amd.dist for the protocol.
 
-Coordinates: every rank's engine works in u32 global coordinates of its own
-Space; `offset` places that space in a virtual int64 coordinate line shared
-by all ranks (0 for one genome cut into ranges, r * span when every rank owns
-its own copy of a genome -- the weak-scaling benchmark).  Boundary records
-travel in virtual coordinates.
+One genome is cut into coordinate ranges (dist.even_splits / coord_splits /
+sample_splits); shard r owns the rows whose global start lies in
+[splits[r], splits[r+1]).  Row ids are global (the caller's row_base + input
+index), so every output record names its input rows directly.
 """
 import numpy as np
 import torch
@@ -16,100 +16,128 @@ from . import dist as ld
 
 
 class _EngineRuns:
-    """merge result as seen by lime_amd.dist.merge_carry (virtual coordinates)."""
+    """merge result as seen by lime_amd.dist.merge_carry"""
 
-    def __init__(self, res, offset):
-        self.res, self.off, self.n = res, offset, res.n
+    def __init__(self, res):
+        self.res, self.n = res, res.n
         self.last_end = -1
         if self.n:
             _, ge = res.copy_range(self.n - 1, 1)
-            self.last_end = int(ge[0]) + offset
+            self.last_end = int(ge[0])
 
     def head(self, k):
         gs, ge = self.res.copy_range(0, k)
-        return [int(x) + self.off for x in gs], [int(x) + self.off for x in ge]
+        return [int(x) for x in gs], [int(x) for x in ge]
 
 
 class ShardStep:
-    def __init__(self, ctx, space, offset=0, group=None, comm_device=None):
-        self.ctx, self.space, self.offset, self.group = ctx, space, int(offset), group
+    """Pairwise intersect + merge of both inputs over one range shard.
+
+    load():  this rank's slice of unsorted rows -> the rows this shard owns,
+             sorted (lime_route_rows, clip = 0: a row goes to the shard of its
+             start; one all_to_all per array -- the Spark shuffle of ADAM
+             repartitionAndSort, cli/Intersection.scala:42-43)
+    run():   merge both sets locally; right halo (rows of later shards that
+             start before this shard's max end: the replication of
+             OverlapBasedSetTheory.scala:75-80, bounded by the longest row) by
+             one all_gather of ends + one all_to_all of device rows; intersect
+             with ownership (a pair belongs to the row with the smaller start,
+             ties to a, so shard outputs are disjoint); merge carry (one
+             all_gather replaces SetTheory.scala:236-282's log2(P) rounds).
+    """
+
+    def __init__(self, ctx, space, splits=None, group=None, comm_device=None,
+                 shared_stream=False):
+        self.ctx, self.space, self.group = ctx, space, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.comm = comm_device if comm_device is not None else torch.device("cpu")
+        self.splits = splits or ld.even_splits(space.span, self.world)
+        self.comm = comm_device
         self.dev = torch.device("cuda", ctx.device)
+        self.shared = shared_stream
+        self.routed = 0  # rows received from other ranks by load() (diagnostics)
 
-    # ------------------------------------------------------------- halo
+    def _sync(self):
+        if not self.shared:
+            self.ctx.synchronize()
+            torch.cuda.current_stream(self.dev).synchronize()
+
+    def _i32(self, n):
+        return torch.empty(max(int(n), 1), dtype=torch.int32, device=self.dev)
+
+    # ----------------------------------------------------------- routing
+    def load(self, n, d_contig, d_start, d_end, row_base=0):
+        """-> IntervalSet of the rows this shard owns (global row ids)"""
+        ctx, sp = self.ctx, self.space
+        gs, ge, row = self._i32(n), self._i32(n), self._i32(n)
+        counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=False, cap=n,
+                                d_gs=gs.data_ptr(), d_ge=ge.data_ptr(), d_row=row.data_ptr(),
+                                row_base=row_base)
+        self._sync()
+        (rgs, rge, rrow), rc = ld.exchange([gs, ge, row], counts, self.group, self.comm)
+        self._sync()
+        self.routed += sum(rc) - rc[self.rank]
+        m = sum(rc)
+        return ctx.set_from_global(sp, m, rgs.data_ptr(), rge.data_ptr(), rrow.data_ptr())
+
+    # -------------------------------------------------------------- halo
     def _halo(self, sets, my_end):
-        """right halo of every set: rows of later shards starting before this
-        shard's max end.  Returns [(gs, ge, src_rank, src_row) int64 numpy]."""
+        """right halo of every set, on the device: [(gs, ge, row) int32
+        tensors], each sorted (later shards' prefixes in rank order)"""
         w, me = self.world, self.rank
-        t = torch.tensor([my_end], dtype=torch.int64, device=self.comm)
-        ends = torch.empty(w, dtype=torch.int64, device=self.comm)
-        dist.all_gather_into_tensor(ends, t, group=self.group)
+        cd = self.comm if self.comm is not None else self.dev
+        ends = torch.empty(w, dtype=torch.int64, device=cd)
+        dist.all_gather_into_tensor(ends, torch.tensor([my_end], dtype=torch.int64, device=cd),
+                                    group=self.group)
         ends = ends.tolist()
         out = []
         for S in sets:
-            counts = []
-            for r in range(w):
-                key = ends[r] - self.offset
-                if r < me and key > 0:
-                    counts.append(S.lower_bound(min(key, 0xFFFFFFFF)))
-                else:
-                    counts.append(0)
+            # rows of mine that shard r < me needs: gs < ends[r]
+            counts = [S.lower_bound(min(ends[r], 0xFFFFFFFF)) if r < me and ends[r] > 0 else 0
+                      for r in range(w)]
             c = max(counts) if counts else 0
+            pre = [self._i32(c) for _ in range(3)]
             if c:
-                buf = torch.empty((3, c), dtype=torch.int32, device=self.dev)
-                S.copy_rows_device(0, c, buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr())
-                torch.cuda.synchronize(self.dev)
-                u = buf.to(torch.int64) & 0xFFFFFFFF
-                rows = torch.stack([u[0] + self.offset, u[1] + self.offset, u[2],
-                                    torch.full_like(u[2], me)], dim=1)
-                send = torch.cat([rows[:k] for k in counts]).to(self.comm)
-            else:
-                send = torch.empty((0, 4), dtype=torch.int64, device=self.comm)
-            recv, _ = ld._alltoallv(send, counts, self.group)
-            out.append(recv.cpu().numpy())
+                S.copy_rows_device(0, c, *(t.data_ptr() for t in pre))
+            send = [torch.cat([t[:k] for k in counts]) if sum(counts) else t[:0] for t in pre]
+            self._sync()
+            recv, _ = ld.exchange(send, counts, self.group, self.comm)
+            self._sync()
+            out.append(recv)
         return out
 
     def _extend(self, S, halo):
-        """own sorted rows followed by the halo rows, as one engine set"""
-        n, h = S.n, len(halo)
-        gs = torch.empty(n + h, dtype=torch.int32, device=self.dev)
-        ge = torch.empty(n + h, dtype=torch.int32, device=self.dev)
-        row = torch.empty(n + h, dtype=torch.int32, device=self.dev)
+        """own sorted rows followed by the halo rows (already in order), as
+        one engine set: nothing to sort, k_prep only checks the order"""
+        n, h = S.n, halo[0].numel()
+        gs, ge, row = self._i32(n + h), self._i32(n + h), self._i32(n + h)
         S.copy_rows_device(0, n, gs.data_ptr(), ge.data_ptr(), row.data_ptr())
-        loc = halo[:, :2] - self.offset
-        if loc.min() < 0 or loc.max() >= 2**32:
-            raise ValueError("halo rows outside this shard's coordinate space")
-        tail = np.stack([loc[:, 0], loc[:, 1], n + np.arange(h)]).astype(np.uint32)
-        torch.cuda.synchronize(self.dev)
-        t = torch.from_numpy(tail.view(np.int32)).to(self.dev)
-        gs[n:], ge[n:], row[n:] = t[0], t[1], t[2]
-        torch.cuda.synchronize(self.dev)
-        E = self.ctx.set_from_global(self.space, n + h, gs.data_ptr(), ge.data_ptr(),
-                                     row.data_ptr())
-        return E
+        gs[n:n + h], ge[n:n + h], row[n:n + h] = halo
+        self._sync()
+        return self.ctx.set_from_global(self.space, n + h, gs.data_ptr(), ge.data_ptr(),
+                                        row.data_ptr())
 
-    # ------------------------------------------------------------- step
+    # -------------------------------------------------------------- step
     def run(self, A, B, threshold=0, on_pairs=None):
-        """A, B: this shard's own sorted sets.  Intersect (owned pairs only,
-        emitted through on_pairs(plan, halo_rows)) + merge of A and B with the
-        cross-shard carry.  Returns a dict of counts."""
+        """A, B: this shard's own sorted sets (load()).  Intersect (owned
+        pairs only, handed to on_pairs(plan)) + merge of A and B with the
+        cross-shard carry.  Returns a dict of counts and the merge results."""
         ctx = self.ctx
         ma, mb = ctx.merge(A), ctx.merge(B)
-        ra, rb = _EngineRuns(ma, self.offset), _EngineRuns(mb, self.offset)
+        ra, rb = _EngineRuns(ma), _EngineRuns(mb)
         my_end = max(ra.last_end, rb.last_end)
         halo_a, halo_b = self._halo([A, B], my_end)
-        Ae = self._extend(A, halo_a) if len(halo_a) else A
-        Be = self._extend(B, halo_b) if len(halo_b) else B
+        Ae = self._extend(A, halo_a) if halo_a[0].numel() else A
+        Be = self._extend(B, halo_b) if halo_b[0].numel() else B
         plan = ctx.intersect(Ae, Be, threshold, a_owned=A.n, b_owned=B.n)
         if on_pairs is not None:
-            on_pairs(plan, (halo_a, halo_b))
-        da, ea = ld.merge_carry(ra, group=self.group, device=self.comm)
-        db, eb = ld.merge_carry(rb, group=self.group, device=self.comm)
+            on_pairs(plan)
+        cd = self.comm if self.comm is not None else self.dev
+        da, ea = ld.merge_carry(ra, group=self.group, device=cd)
+        db, eb = ld.merge_carry(rb, group=self.group, device=cd)
         out = {"pairs": plan.n, "runs_a": ma.n - da, "runs_b": mb.n - db,
-               "drop": (da, db), "extend": (ea, eb), "halo": (len(halo_a), len(halo_b)),
-               "merge_a": ma, "merge_b": mb}
+               "drop": (da, db), "extend": (ea, eb),
+               "halo": (halo_a[0].numel(), halo_b[0].numel()), "merge_a": ma, "merge_b": mb}
         plan.close()
         for E, S in ((Ae, A), (Be, B)):
             if E is not S:

@@ -1,8 +1,10 @@
-"""Range-sharded engine path on the GPU: 2 and 3 ranks sharing the one
-MI355X of the test box (gloo carries the boundary records), one genome cut
-into coordinate ranges so that intervals DO cross shard boundaries.  The
-union of the shards' owned pairs and carried merge runs must equal the
-single-shard oracle result."""
+"""Range-sharded engine paths on the GPU: 1-4 ranks sharing the one MI355X
+of the test box (gloo carries the rows, staged through the host), one genome
+cut into coordinate ranges so that intervals DO cross shard boundaries.
+Every rank starts from an arbitrary slice of the unsorted input (the device
+router moves rows to their owner shards).  The union of the shards' owned
+pairs and carried merge runs (C2's path), and the gathered k-way AND runs
+(C5's path), must equal the single-shard oracle result."""
 import os
 import socket
 
@@ -40,34 +42,33 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
     try:
         import lime_amd
-        from lime_amd import dist as ld
         from lime_amd.sharded import ShardStep
         ctx = lime_amd.Context(0)
         sp = lime_amd.Space(NAMES, LENS)
         off = sp.offsets
         A, B = _rows()
-        splits = ld.even_splits(sp.span, world)
+        step = ShardStep(ctx, sp, comm_device=torch.device("cpu"))
 
-        def owned(X):
-            g = off[X[0]] + X[1]
-            return [np.nonzero((g >= splits[r]) & (g < splits[r + 1]))[0] for r in range(world)]
-        own_a, own_b = owned(A), owned(B)
-        ia, ib = own_a[rank], own_b[rank]
-        Aset = ctx.set_from_host(sp, A[0][ia], A[1][ia], A[2][ia])
-        Bset = ctx.set_from_host(sp, B[0][ib], B[1][ib], B[2][ib])
+        def load(X):
+            # this rank's arbitrary slice of the UNSORTED input, on the device;
+            # load() routes it to the owner shards (row ids stay global)
+            n = len(X[0])
+            f, l = rank * n // world, (rank + 1) * n // world
+            t = [torch.from_numpy(np.ascontiguousarray(x[f:l]).astype(np.int32)).cuda()
+                 for x in X]
+            torch.cuda.synchronize()
+            S = step.load(l - f, *(x.data_ptr() for x in t), row_base=f)
+            h = S.to_host()
+            g = off[h["contig"]] + h["start"]
+            assert ((g >= step.splits[rank]) & (g < step.splits[rank + 1])).all()
+            return S
+        Aset, Bset = load(A), load(B)
         got = []
 
-        def on_pairs(plan, halos):
+        def on_pairs(plan):
             p = plan.fill_host()
-            ha, hb = halos
-            for x in p:
-                a, b = int(x["a_row"]), int(x["b_row"])
-                # halo rows: (gs, ge, source row, source rank)
-                ga = ia[a] if a < len(ia) else own_a[int(ha[a - len(ia)][3])][int(ha[a - len(ia)][2])]
-                gb = ib[b] if b < len(ib) else own_b[int(hb[b - len(ib)][3])][int(hb[b - len(ib)][2])]
-                got.append((int(ga), int(gb), int(x["start"]), int(x["end"])))
-        # own rows: srcs as seen by other ranks are (rank, local row) -> own_x[rank][row]
-        step = ShardStep(ctx, sp, offset=0, comm_device=torch.device("cpu"))
+            got.extend(zip(p["a_row"].tolist(), p["b_row"].tolist(), p["start"].tolist(),
+                           p["end"].tolist()))
         out = step.run(Aset, Bset, on_pairs=on_pairs)
         # merged runs after the carry, in local coordinates
         runs = []
@@ -79,11 +80,11 @@ def _worker(rank, world, port, q):
             if e is not None and st:
                 en[-1] = e - off[ct[-1]]
             runs.append(list(zip(ct, st, en)))
-        q.put((rank, got, runs, out["halo"]))
+        q.put((rank, got, runs, out["halo"], step.routed))
         ctx.close()
     except Exception as e:  # report instead of hanging the parent
         import traceback
-        q.put((rank, "error", traceback.format_exc(), None))
+        q.put((rank, "error", traceback.format_exc(), None, None))
         raise
     finally:
         dist.destroy_process_group()
@@ -111,7 +112,8 @@ def test_sharded_engine_matches_single_shard(world):
                       exp["end"].tolist()))
     got = sorted(sum((r[1] for r in res), []))
     assert got == want
-    assert sum(r[3][0] + r[3][1] for r in res) > 0  # boundary rows really moved
+    assert sum(r[3][0] + r[3][1] for r in res) > 0  # boundary rows really moved (halo)
+    assert sum(r[4] for r in res) > 0                 # and the input was routed
     for k, X in ((0, A), (1, B)):
         m = oracle.merge(X)
         runs = sum((r[2][k] for r in res), [])

@@ -72,6 +72,9 @@ class FakePlan:
 class FakeCtx:
     device = 0
 
+    def synchronize(self):
+        pass
+
     def merge(self, S):
         from oracle import oracle
         m = oracle.merge((np.zeros(S.n, np.int32), S.gs, S.ge))
@@ -119,20 +122,17 @@ def _worker(rank, world, port, q):
         own_a, own_b = owned(A), owned(B)
         ia, ib = own_a[rank], own_b[rank]
 
-        def mk(X, idx):
+        def mk(X, idx):  # the shard's own rows, global row ids (as load() delivers them)
             c = X[0][idx]
-            return FakeSet(off[c] + X[1][idx], off[c] + X[2][idx], np.arange(len(idx)))
+            return FakeSet(off[c] + X[1][idx], off[c] + X[2][idx], idx.astype(np.int64))
         Aset, Bset = mk(A, ia), mk(B, ib)
-        step = sharded.ShardStep(FakeCtx(), sp, offset=0, comm_device=torch.device("cpu"))
+        step = sharded.ShardStep(FakeCtx(), sp, splits=splits, comm_device=torch.device("cpu"),
+                                 shared_stream=True)
         step.dev = torch.device("cpu")
         got = []
 
-        def on_pairs(plan, halos):
-            ha, hb = halos
-            for a, b in plan.pairs:
-                ga = ia[a] if a < len(ia) else own_a[int(ha[a - len(ia)][3])][int(ha[a - len(ia)][2])]
-                gb = ib[b] if b < len(ib) else own_b[int(hb[b - len(ib)][3])][int(hb[b - len(ib)][2])]
-                got.append((int(ga), int(gb)))
+        def on_pairs(plan):  # halo rows carry their global ids: pairs name input rows
+            got.extend((int(a), int(b)) for a, b in plan.pairs)
         out = step.run(Aset, Bset, on_pairs=on_pairs)
         runs = []
         for k, res in enumerate((out["merge_a"], out["merge_b"])):

@@ -86,29 +86,7 @@ __device__ __forceinline__ void owner_keys(uint32_t og, uint32_t oe, uint32_t lo
     hi_key = (int64_t)oe - tp + 1;
 }
 
-// 65-ary search by one wave: every step probes 64 evenly spaced rows at once
-// and keeps the gap the key falls in, so a lower_bound over 1e8 rows takes
-// 5 dependent memory round trips instead of 27.  Wave-uniform result.
-__device__ __forceinline__ int64_t wave_lower_bound(const uint32_t *__restrict__ a, int64_t n,
-                                                    int64_t key) {
-    int64_t lo = 0, hi = n;  // answer in [lo, hi]
-    const int lane = dev::lane_id();
-    while (hi - lo > 64) {
-        const int64_t step = (hi - lo + 64) / 65;  // probes lo + step*(l+1) - 1, l < 64
-        const int64_t idx = lo + step * (lane + 1) - 1;
-        const bool less = idx < hi && (int64_t)a[idx] < key;
-        const uint64_t m = __ballot(less);
-        const int c = __popcll(m);  // probes below key (a prefix, a is sorted)
-        const int64_t nlo = c == 0 ? lo : lo + step * c;
-        const int64_t nhi = c == 64 ? hi : min(hi, lo + step * (c + 1) - 1);
-        lo = nlo;
-        hi = nhi;
-    }
-    // final: at most 64 candidates [lo, hi)
-    const int64_t idx = lo + lane;
-    const bool less = idx < hi && (int64_t)a[idx] < key;
-    return lo + __popcll(__ballot(less));
-}
+using dev::wave_lower_bound;
 
 __device__ __forceinline__ uint32_t contig_off(const uint32_t *__restrict__ off, int32_t nc,
                                                uint32_t g) {

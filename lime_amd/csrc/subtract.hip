@@ -10,12 +10,21 @@
 // Mode LIME_SUBTRACT_SET emits L minus the union of the blocks instead.
 //
 // Hits of a left row a in sorted order are
-//   spanning:  j < lo1 with B.ge[j] > thr   (b.s < a.s; thr = a.s, or a.s+t-1)
+//   spanning:  b.s < a.s, B.ge > thr   (thr = a.s, or a.s + t - 1)
 //   inside:    j in [lo1, hi1) (width(b) >= t when t >= 1)
-// where [lo1, hi1) is the intersect stream-0 candidate range, and the first
-// spanning candidate is found by galloping backwards on the inclusive prefix
-// max of B.ge (monotone).  One thread per left row walks its hits twice
-// (count pass, write pass); remnants are written at owner offsets from a scan.
+// where [lo1, hi1) is the intersect stream-0 candidate range.  Every
+// spanning hit contains the point a.s, so they all overlap each other and the
+// fold merges them into ONE block: [start of the first spanning hit, max end
+// of the rows before lo1) -- the first spanning hit by a galloping search of
+// B's inclusive prefix max of ends (monotone), the max end is that prefix
+// max at lo1 - 1.  No walk over the spanning rows: a long B row (a gene body,
+// a segmental duplication) costs every later left row O(log n), not a walk
+// back to it (the O(n_A * n_B) cliff of a per-row backward scan).  The block
+// head is the spanning hit with the smallest (start, end, row): the rows
+// sharing the first hit's start are scanned for it.  The inside hits then
+// continue the fold one by one (work proportional to the hits).
+// One thread per left row, two passes (count, write); the write pass stages
+// a block's records in LDS and stores them lane-consecutively.
 #include "common.hpp"
 
 namespace lime {
@@ -28,6 +37,7 @@ namespace {
 constexpr int SUB_B = 256;
 
 struct SubArgs {
+    const uint32_t *wstart;  // per block: first B row a spanning hit can be (or null)
     const uint32_t *ags, *age, *arow;
     const uint32_t *bgs, *bge, *brow, *bpmax;
     const uint32_t *olo, *ocnt;
@@ -61,32 +71,96 @@ __device__ __forceinline__ int64_t first_spanning(const uint32_t *__restrict__ p
     return lo;
 }
 
+constexpr int SCAP = 512;   // records staged per block in the write pass
+constexpr int BWIN = 1024;  // B rows of a block's hit window staged in LDS
+// (24 KiB of LDS in all: the walk is latency-bound, occupancy is its speed)
+
+// per block: first B row that can span any of the block's left rows: a
+// spanning b starts after a.s - max width(B) (one 65-ary wave search)
+__global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__ ags, int64_t na,
+                                                    const uint32_t *__restrict__ bgs, int64_t nb,
+                                                    uint32_t maxw, int64_t nblk,
+                                                    uint32_t *__restrict__ wstart) {
+    const int64_t b = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    if (b >= nblk) return;
+    const int64_t key = (int64_t)ags[b * SUB_B] - maxw;
+    const int64_t r = dev::wave_lower_bound(bgs, nb, key < 0 ? 0 : key);
+    if (dev::lane_id() == 0) wstart[b] = (uint32_t)r;
+}
+
 template <bool WRITE>
 __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
+    __shared__ uint32_t st_gs[WRITE ? SCAP : 1], st_ge[WRITE ? SCAP : 1];
+    __shared__ uint32_t st_ar[WRITE ? SCAP : 1], st_br[WRITE ? SCAP : 1];
+    __shared__ uint32_t w_gs[BWIN], w_ge[BWIN], w_row[BWIN], w_pm[BWIN];
+    __shared__ uint32_t s_whi[SUB_B / 64];
     const int64_t i = (int64_t)blockIdx.x * SUB_B + threadIdx.x;
-    if (i >= sa.na) return;
-    const uint32_t as = sa.ags[i], ae = sa.age[i], ar = sa.arow[i];
+    // the block's hit window [wlo, whi) of B (spanning and inside hits):
+    // consecutive left rows share most of it, so it is loaded once,
+    // coalesced, into LDS
+    const int64_t wlo = sa.wstart[blockIdx.x];
+    {
+        uint32_t h = 0;
+        if (i < sa.na) h = sa.olo[i] + sa.ocnt[i];
+        h = dev::wave_reduce_max(h);
+        if (dev::lane_id() == 0) s_whi[threadIdx.x / 64] = h;
+    }
+    __syncthreads();
+    int64_t whi = wlo;
+    for (int w = 0; w < SUB_B / 64; ++w) whi = max(whi, (int64_t)s_whi[w]);
+    const bool win = whi - wlo <= BWIN;
+    if (win)
+        for (int64_t k = threadIdx.x; k < whi - wlo; k += SUB_B) {
+            w_gs[k] = sa.bgs[wlo + k];
+            w_ge[k] = sa.bge[wlo + k];
+            w_row[k] = sa.brow[wlo + k];
+            w_pm[k] = sa.bpmax[wlo + k];
+        }
+    __syncthreads();
+    // B's arrays at row j, from the window when staged
+    auto Bgs = [&](int64_t j) { return win ? w_gs[j - wlo] : sa.bgs[j]; };
+    auto Bge = [&](int64_t j) { return win ? w_ge[j - wlo] : sa.bge[j]; };
+    auto Brow = [&](int64_t j) { return win ? w_row[j - wlo] : sa.brow[j]; };
+    // the block's output window (write pass): staged in LDS when it fits
+    int64_t bbase = 0, bend = 0;
+    bool staged = false;
+    if (WRITE) {
+        const int64_t first = (int64_t)blockIdx.x * SUB_B;
+        const int64_t last = min(first + SUB_B, sa.na);
+        bbase = (int64_t)sa.off[first];
+        bend = (int64_t)sa.off[last];
+        staged = bend - bbase <= SCAP;
+    }
+    uint32_t as = 0, ae = 0, ar = 0;
+    if (i < sa.na) as = sa.ags[i], ae = sa.age[i], ar = sa.arow[i];
     const int64_t t = sa.t;
     int64_t pos = 0, end = 0;
-    if (WRITE) {
+    if (WRITE && i < sa.na) {
         pos = (int64_t)sa.off[i];
         end = (int64_t)sa.off[i + 1];
     }
     uint64_t n_out = 0;
     auto emit = [&](uint32_t s, uint32_t e, uint32_t br, int64_t at) {
         if (WRITE) {
-            sa.ogs[at] = s;
-            sa.oge[at] = e;
-            sa.oar[at] = ar;
-            sa.obr[at] = br;
+            if (staged) {
+                const int k = (int)(at - bbase);
+                st_gs[k] = s;
+                st_ge[k] = e;
+                st_ar[k] = ar;
+                st_br[k] = br;
+            } else {
+                sa.ogs[at] = s;
+                sa.oge[at] = e;
+                sa.oar[at] = ar;
+                sa.obr[at] = br;
+            }
         }
     };
     bool any = false;
-    if (!(t >= 1 && (int64_t)(ae - as) < t)) {
+    if (i < sa.na && !(t >= 1 && (int64_t)(ae - as) < t)) {
         const int64_t lo1 = sa.olo[i];
         const int64_t hi1 = lo1 + sa.ocnt[i];
         const uint32_t thr = t <= 0 ? as : (uint32_t)((int64_t)as + t - 1);
-        const int64_t j0 = first_spanning(sa.bpmax, lo1, thr);
         // fold state.  The block's value is its head = first hit in the
         // reference's (start, end, row) order; the device order only ties
         // starts by (zero-width first, row), so among same-start non-empty
@@ -94,15 +168,56 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         uint32_t bs = 0, be = 0, bh = 0, bhe = 0;  // block, head row, head end
         uint64_t cum = 0;  // remnants of finished blocks (lime mode, write order)
         uint32_t setpos = as;
-        for (int64_t j = j0; j < hi1; ++j) {
-            const uint32_t gs = sa.bgs[j], ge = sa.bge[j];
-            bool hit;
-            if (j < lo1)
-                hit = ge > thr;
-            else
-                hit = t >= 1 ? (int64_t)(ge - gs) >= t : true;
-            if (!hit) continue;
-            const uint32_t row = sa.brow[j];
+        // the spanning block (all spanning hits overlap at a.s): the first
+        // spanning row lies in [wlo, lo1) (rows before wlo end before a.s)
+        const uint32_t pm_last = lo1 > 0 ? (win && lo1 - 1 >= wlo ? w_pm[lo1 - 1 - wlo]
+                                                                   : sa.bpmax[lo1 - 1])
+                                         : 0u;
+        if (lo1 > 0 && pm_last > thr) {
+            int64_t j0;
+            if (win) {  // first j in [wlo, lo1) with pmax > thr, in LDS
+                int64_t lo = wlo, hi = lo1 - 1;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (w_pm[mid - wlo] > thr)
+                        hi = mid;
+                    else
+                        lo = mid + 1;
+                }
+                j0 = lo;
+            } else {
+                j0 = first_spanning(sa.bpmax, lo1, thr);
+            }
+            any = true;
+            bs = Bgs(j0);
+            be = pm_last;
+            bh = Brow(j0);
+            bhe = Bge(j0);
+            for (int64_t j = j0 + 1; j < lo1 && Bgs(j) == bs; ++j) {
+                const uint32_t ge = Bge(j), row = Brow(j);
+                if (ge > thr && (ge < bhe || (ge == bhe && row < bh))) {
+                    bh = row;
+                    bhe = ge;
+                }
+            }
+        }
+        // four hits per step: their loads are independent of the fold state
+        for (int64_t j4 = lo1; j4 < hi1; j4 += 4) {
+            uint32_t vg[4], ve[4], vr[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t j = j4 + q;
+                const bool ok = j < hi1;
+                vg[q] = ok ? Bgs(j) : 0u;
+                ve[q] = ok ? Bge(j) : 0u;
+                vr[q] = ok ? Brow(j) : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+            if (j4 + q >= hi1) break;
+            const uint32_t gs = vg[q], ge = ve[q];
+            if (t >= 1 && (int64_t)(ge - gs) < t) continue;
+            const uint32_t row = vr[q];
             if (!any) {  // foldLeft(List(filteredCache.head)): the head seeds the
                 any = true;  // list and is then folded against itself once
                 bs = gs;
@@ -110,36 +225,35 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                 bh = row;
                 bhe = ge;
             }
-            {
-                if (be > gs && bs < ge) {  // block.overlaps(b): hull
-                    if (gs == bs && bhe > bs && (ge < bhe || (ge == bhe && row < bh))) {
-                        bh = row;
-                        bhe = ge;
-                    }
-                    bs = gs < bs ? gs : bs;
-                    be = ge > be ? ge : be;
-                } else {
-                    // close block (bs, be, bh)
-                    if (sa.mode == LIME_SUBTRACT_LIME) {
-                        uint32_t r = (bs > as) + (ae > be);
-                        if (WRITE) {
-                            int64_t at = end - (int64_t)cum - r;
-                            if (bs > as) emit(as, bs, bh, at++);
-                            if (ae > be) emit(be, ae, bh, at++);
-                        }
-                        cum += r;
-                    } else {
-                        if (bs > setpos) {
-                            if (WRITE) emit(setpos, bs, bh, pos + (int64_t)cum);
-                            ++cum;
-                        }
-                        if (be > setpos) setpos = be;
-                    }
-                    bs = gs;
-                    be = ge;
+            if (be > gs && bs < ge) {  // block.overlaps(b): hull
+                if (gs == bs && bhe > bs && (ge < bhe || (ge == bhe && row < bh))) {
                     bh = row;
                     bhe = ge;
                 }
+                bs = gs < bs ? gs : bs;
+                be = ge > be ? ge : be;
+            } else {
+                // close block (bs, be, bh)
+                if (sa.mode == LIME_SUBTRACT_LIME) {
+                    uint32_t r = (bs > as) + (ae > be);
+                    if (WRITE) {
+                        int64_t at = end - (int64_t)cum - r;
+                        if (bs > as) emit(as, bs, bh, at++);
+                        if (ae > be) emit(be, ae, bh, at++);
+                    }
+                    cum += r;
+                } else {
+                    if (bs > setpos) {
+                        if (WRITE) emit(setpos, bs, bh, pos + (int64_t)cum);
+                        ++cum;
+                    }
+                    if (be > setpos) setpos = be;
+                }
+                bs = gs;
+                be = ge;
+                bh = row;
+                bhe = ge;
+            }
             }
         }
         if (any) {  // close the last block
@@ -165,11 +279,24 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             n_out = cum;
         }
     }
-    if (!any) {
+    if (i < sa.na && !any) {
         if (WRITE) emit(as, ae, 0xffffffffu, pos);
         n_out = 1;
     }
-    if (!WRITE) sa.count[i] = n_out;
+    if (!WRITE) {
+        if (i < sa.na) sa.count[i] = n_out;
+        return;
+    }
+    if (staged) {  // the block's records, lane-consecutive
+        __syncthreads();
+        const int cnt = (int)(bend - bbase);
+        for (int k = threadIdx.x; k < cnt; k += SUB_B) {
+            sa.ogs[bbase + k] = st_gs[k];
+            sa.oge[bbase + k] = st_ge[k];
+            sa.oar[bbase + k] = st_ar[k];
+            sa.obr[bbase + k] = st_br[k];
+        }
+    }
 }
 
 }  // namespace
@@ -193,7 +320,17 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     LIME_TRY(alloc(ctx, &cnt, (size_t)na + 1));
     LIME_TRY(alloc(ctx, &off, (size_t)na + 1));
     LIME_TRY(owner_ranges(ctx, A, B, 0, threshold, olo, ocnt));
+    const int64_t nblk = (na + SUB_B - 1) / SUB_B;
+    uint32_t *wstart;
+    LIME_TRY(alloc(ctx, &wstart, (size_t)nblk));
+    PoolGuard<uint32_t> gw{ctx, wstart};
+    if (B->n > 0)
+        hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nblk, 4)), dim3(256), 0, S(ctx), A->gs,
+                           na, B->gs, B->n, B->max_width, nblk, wstart);
+    else
+        LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nblk, S(ctx)));
     SubArgs sa;
+    sa.wstart = wstart;
     sa.ags = A->gs;
     sa.age = A->ge;
     sa.arow = A->row;

@@ -287,6 +287,31 @@ def test_subtract_parity(ctx, mode, seed, t, zero):
         assert list(res[k][og]) == list(exp[k][oe]), k
 
 
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+@pytest.mark.parametrize("seed,t", [(26, 0), (27, 1), (28, 40), (29, -5)])
+def test_subtract_long_right_intervals(ctx, mode, seed, t):
+    # B holds megabase rows (gene bodies, segmental duplications) among short
+    # ones: every later left row has far-back spanning hits.  The engine folds
+    # all spanning hits of a row into one block found by a search (no walk
+    # back over B); it must still equal the reference fold exactly.
+    rng = np.random.default_rng(seed)
+    L = 5_000_000
+    A, B = random_sets(rng, 6000, 4000, n_contigs=2, contig_len=L, max_len=800,
+                       zero_frac=0.05, dup_frac=0.05, book_frac=0.1)
+    k = rng.random(len(B[0])) < 0.01  # ~40 long rows, up to 3 Mb
+    B[1][k] = rng.integers(0, L // 2, k.sum())
+    B[2][k] = np.minimum(B[1][k] + rng.integers(100_000, 3_000_000, k.sum()), L)
+    # spanning hits sharing a start with different ends (head re-pick)
+    B[1][:20], B[2][:20] = B[1][k][0], B[1][k][0] + rng.integers(1, 2_000_000, 20)
+    B[0][:20] = B[0][k][0]
+    sp = space_for(2, L)
+    res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t, mode).to_host()
+    exp = oracle.subtract(A, B, t, mode)
+    og, oe = np.argsort(res["a_row"], kind="stable"), np.argsort(exp["a_row"], kind="stable")
+    for key in ("contig", "start", "end", "a_row", "b_row"):
+        assert list(res[key][og]) == list(exp[key][oe]), key
+
+
 @pytest.mark.parametrize("seed,zero", [(31, 0.0), (32, 0.1)])
 def test_complement_parity(ctx, seed, zero):
     rng = np.random.default_rng(seed)

@@ -16,6 +16,7 @@ the 8(f) rows (bench.py measures the headline config C2).  Single GPU; one JSON 
   bed BED text parse on the device (lime_bed_parse_device, 8(f) row 1):
       1e7 BED6 lines over hg38 (host text, H2D inside the call); unit:
       lines/s, with the host reader (lime_bed_read, 1 thread) beside it
+  subtract DistributedSubtract (lime mode) on C2's inputs: sort + A minus B
   window   DistributedWindow, distance 1000, on C2's inputs (8(f) row 3):
       sort + window join, every record filled through a 32 GiB buffer
   closest  SingleClosest on C2's inputs (8(f) row 4): RegionOrdering sort +
@@ -41,7 +42,8 @@ HBM = 8000.0
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", required=True,
-                   choices=["c3", "c4", "c5", "bed", "closest", "closest_single", "window"])
+                   choices=["c3", "c4", "c5", "bed", "closest", "closest_single", "window",
+                            "subtract"])
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scale", type=float, default=1.0, help="row-count scale (testing)")
@@ -139,6 +141,35 @@ def main():
                     "extract_ms": ms, "complement_runs": nc, "difference_runs": nd}, \
                 {"kernel": "bitset extraction (k_ev_fused: one pass, look-back offsets)",
                  "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+    elif a.workload == "subtract":
+        # DistributedSubtract (lime mode) on C2's inputs: A minus B, every
+        # remnant materialised (contig-local start / end, a_row, b_row)
+        ia = gen(int(1e8 * a.scale), 0xA, 50, 5000)
+        ib = gen(int(1e8 * a.scale), 0xB, 50, 5000)
+        n = ia[0]
+
+        def step(rec):
+            t0 = ev()
+            SA, SB = mkset(ia), mkset(ib)
+            t1 = ev()
+            r = ctx.subtract(SA, SB)
+            t2 = ev()
+            rec.append((t0, t1, t2, r.n))
+            r.close()
+            SA.close()
+            SB.close()
+        units, unit = 2 * n, "intervals/s"
+        desc = f"subtract (lime mode): sort + A minus B of 2 x {n} intervals, uniform over " \
+               "hg38, len U[50,5000] (C2's inputs)"
+
+        def roof(rec):
+            t0, t1, t2, k = rec[-1]
+            ms = t1.elapsed_time(t2)
+            # A rows (gs, ge, row) + B's gs / ge / row / prefix max + 16 B per remnant
+            b = 12 * n + 16 * n + 16 * k
+            return {"sort_ms": t0.elapsed_time(t1), "subtract_ms": ms, "remnants": k}, \
+                {"kernel": "subtract (owner ranges + k_subtract count / write)", "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "window":
         # DistributedWindow (distance 1000) on C2's inputs: every pair within

@@ -134,6 +134,11 @@ int lime_set_destroy(lime_set *set);
 int64_t lime_set_size(const lime_set *set);
 /* first sorted row with gstart >= gkey; on error -(LIME_ERR_*) */
 int64_t lime_set_lower_bound(const lime_set *set, uint32_t gkey);
+/* first sorted row j with max(gend[0..j]) > gkey, i.e. every row from there
+ * on may reach past gkey and none before does (a coordinate shard's rows that
+ * can overlap a later shard: the left halo of pairwise ops); n if none;
+ * on error -(LIME_ERR_*) */
+int64_t lime_set_first_reaching(const lime_set *set, uint32_t gkey);
 /* device-to-device copy of sorted rows [first, first + count) */
 int lime_set_copy_rows_device(const lime_set *set, int64_t first, int64_t count, uint32_t *d_gstart,
                               uint32_t *d_gend, uint32_t *d_row);

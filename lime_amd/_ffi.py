@@ -68,6 +68,7 @@ SIGNATURES = {
     "lime_set_destroy": (C.c_int, [vp]),
     "lime_set_size": (i64, [vp]),
     "lime_set_lower_bound": (i64, [vp, u32]),
+    "lime_set_first_reaching": (i64, [vp, u32]),
     "lime_set_copy_rows_device": (C.c_int, [vp, i64, i64, vp, vp, vp]),
     "lime_result_copy_range": (C.c_int, [vp, i64, i64, P(u32), P(u32)]),
     "lime_set_device_arrays": (C.c_int, [vp, pp, pp, pp]),

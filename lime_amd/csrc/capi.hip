@@ -557,6 +557,30 @@ int64_t lime_set_lower_bound(const lime_set *s, uint32_t gkey) {
     return h;
 }
 
+__global__ void k_first_reaching(const uint32_t *pmax, int64_t n, uint32_t key, int64_t *out) {
+    // first j with pmax[j] > key (pmax non-decreasing); n if none
+    if (threadIdx.x == 0) *out = dev::upper_bound(pmax, 0, n, key);
+}
+
+int64_t lime_set_first_reaching(const lime_set *s, uint32_t gkey) {
+    if (!s) return -(int64_t)fail(LIME_ERR_ARG, "set is null");
+    lime_ctx *ctx = s->ctx;
+    hipSetDevice(ctx->device);
+    if (s->n == 0) return 0;
+    if (int rc = build_prefix_max(ctx, s)) return -(int64_t)rc;
+    int64_t *d = nullptr;
+    if (int rc = alloc(ctx, &d, 1)) return -(int64_t)rc;
+    PoolGuard<int64_t> guard{ctx, d};
+    hipLaunchKernelGGL(k_first_reaching, dim3(1), dim3(64), 0, S(ctx), (const uint32_t *)s->pmax,
+                       s->n, gkey, d);
+    if (hipError_t e = hipGetLastError())
+        return -(int64_t)fail(LIME_ERR_DEVICE, std::string("first_reaching launch: ") +
+                                                   hipGetErrorString(e));
+    int64_t h = -1;
+    if (int rc = read_back(ctx, &h, d, 8)) return -(int64_t)rc;
+    return h;
+}
+
 int lime_set_copy_rows_device(const lime_set *s, int64_t first, int64_t count, uint32_t *d_gs,
                               uint32_t *d_ge, uint32_t *d_row) {
     if (!s || first < 0 || count < 0 || first + count > s->n)

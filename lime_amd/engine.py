@@ -125,6 +125,13 @@ class IntervalSet:
             check(int(-r))
         return int(r)
 
+    def first_reaching(self, gkey):
+        """first sorted row from which rows may end past gkey (none before)"""
+        r = _lib().lime_set_first_reaching(self._h, int(gkey))
+        if r < 0:
+            check(int(-r))
+        return int(r)
+
     def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
         check(_lib().lime_set_copy_rows_device(self._h, int(first), int(count), d_gs, d_ge,
                                                d_row))

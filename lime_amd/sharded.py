@@ -117,6 +117,57 @@ class ShardStep:
         return self.ctx.set_from_global(self.space, n + h, gs.data_ptr(), ge.data_ptr(),
                                         row.data_ptr())
 
+    def _left_halo(self, S):
+        """rows of earlier shards that may reach into this shard: shard q
+        sends shard r > q its sorted rows from the first one whose running max
+        end passes split[r] (a superset of the rows overlapping r's range;
+        extra rows overlap nothing there).  Device rows, in order."""
+        w, me = self.world, self.rank
+        counts, first = [], []
+        for r in range(w):
+            f = S.first_reaching(min(self.splits[r], 0xFFFFFFFF)) if r > me else S.n
+            first.append(f)
+            counts.append(S.n - f)
+        f0 = min(first) if first else S.n
+        c = S.n - f0
+        suf = [self._i32(c) for _ in range(3)]
+        if c:
+            S.copy_rows_device(f0, c, *(t.data_ptr() for t in suf))
+        send = [torch.cat([t[first[r] - f0:] for r in range(w) if counts[r]])
+                if sum(counts) else t[:0] for t in suf]
+        self._sync()
+        recv, _ = ld.exchange(send, counts, self.group, self.comm)
+        self._sync()
+        return recv
+
+    def subtract(self, A, B, threshold=0, mode=0):
+        """DistributedSubtract of this shard's own rows of A: every B row that
+        overlaps one of them -- the left halo (earlier shards' rows reaching
+        in) + own B rows + the right halo -- as one sorted set.  Outputs are
+        disjoint across shards (each A row is subtracted where it is owned)
+        and carry global row ids (Subtract.scala:78-116 over the replication
+        of OverlapBasedSetTheory.scala:75-80)."""
+        my_end = -1
+        if A.n:
+            ma = self.ctx.merge(A)
+            my_end = _EngineRuns(ma).last_end
+            ma.close()
+        left = self._left_halo(B)
+        (right,) = self._halo([B], my_end)
+        n, hl, hr = B.n, left[0].numel(), right[0].numel()
+        if hl or hr:
+            gs, ge, row = self._i32(hl + n + hr), self._i32(hl + n + hr), self._i32(hl + n + hr)
+            gs[:hl], ge[:hl], row[:hl] = left
+            B.copy_rows_device(0, n, gs[hl:].data_ptr(), ge[hl:].data_ptr(), row[hl:].data_ptr())
+            gs[hl + n:hl + n + hr], ge[hl + n:hl + n + hr], row[hl + n:hl + n + hr] = right
+            self._sync()
+            Be = self.ctx.set_from_global(self.space, hl + n + hr, gs.data_ptr(), ge.data_ptr(),
+                                          row.data_ptr())
+        else:
+            Be = B
+        res = self.ctx.subtract(A, Be, threshold, mode)
+        return res, (hl, hr), Be
+
     # -------------------------------------------------------------- step
     def run(self, A, B, threshold=0, on_pairs=None):
         """A, B: this shard's own sorted sets (load()).  Intersect (owned
@@ -145,8 +196,9 @@ class ShardStep:
         return out
 
 
-class ShardedAnd:
-    """BASELINE C5: k-way intersection over bit-per-base sets, range-sharded.
+class ShardedBitset:
+    """Bit-per-base set algebra range-sharded (BASELINE C4 and C5): k-way
+    intersection (C5), complement and difference (C4).
 
     Shard r (one rank per GPU) owns global coordinates [splits[r],
     splits[r+1]) (lime_amd.dist.coord_splits).  Per input set every rank
@@ -209,14 +261,23 @@ class ShardedAnd:
         m = sum(rc)
         return ctx.bitset_from_global(sp, self.lo, self.hi, m, rgs.data_ptr(), rge.data_ptr())
 
-    def run(self, inputs, gather=False):
+    def run(self, inputs, gather=False, op="and"):
         """inputs: [(n, d_contig, d_start, d_end)] per set (this rank's rows,
-        device pointers).  Returns a dict: the shard's AND result (global
+        device pointers); op "and" (k sets: C5), "not" (1 set: complement of
+        its union against the genome), "andnot" (2 sets: per-base
+        difference).  Returns a dict: the shard's result (global
         coordinates), the carry (drop_first, new_last_end), the total run
         count of the unsharded result and, with gather=True, every run as an
         int64 [m, 2] tensor (global start, end) in order."""
         bits = [self.bitset(*x) for x in inputs]
-        res = self.ctx.bitset_and(bits)
+        if op == "and":
+            res = self.ctx.bitset_and(bits)
+        elif op == "not":
+            res = self.ctx.bitset_runs(1, bits[0])
+        elif op == "andnot":
+            res = self.ctx.bitset_runs(3, bits[0], bits[1])
+        else:
+            raise ValueError(f"unknown op {op}")
         for b in bits:
             b.close()
         n = res.n
@@ -246,3 +307,6 @@ class ShardedAnd:
                 t, _ = ld.allgatherv(t.to(self.comm or self.dev), self.group, self.comm)
             out["runs"] = t.cpu()
         return out
+
+
+ShardedAnd = ShardedBitset  # C5's name for it

@@ -204,3 +204,100 @@ def test_sharded_c5_matches_single_shard_oracle(world):
         assert r[2] == len(runs)
     if world > 1:
         assert sum(r[3] for r in res) > 0  # rows really moved between shards
+
+
+# ------------------------------------------- sharded subtract and C4 ops
+def _c4_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        import lime_amd
+        from lime_amd import SUBTRACT_LIME, SUBTRACT_SET
+        from lime_amd.sharded import ShardedBitset, ShardStep
+        ctx = lime_amd.Context(0)
+        sp = lime_amd.Space(NAMES, LENS)
+        A, B = _rows()
+        dev_rows = []
+        for X in (A, B):
+            n = len(X[0])
+            f, l = rank * n // world, (rank + 1) * n // world
+            t = [torch.from_numpy(np.ascontiguousarray(x[f:l]).astype(np.int32)).cuda()
+                 for x in X]
+            dev_rows.append((f, l - f, t))
+        torch.cuda.synchronize()
+        out = {}
+        # subtract (interval path): own A rows against left + own + right B
+        step = ShardStep(ctx, sp, comm_device=torch.device("cpu"))
+        S = [step.load(m, *(x.data_ptr() for x in t), row_base=f) for f, m, t in dev_rows]
+        for mode in (SUBTRACT_LIME, SUBTRACT_SET):
+            for thr in (0, 25):
+                res, halo, Be = step.subtract(S[0], S[1], thr, mode)
+                h = res.to_host()
+                out[("sub", mode, thr)] = (list(zip(h["contig"].tolist(), h["start"].tolist(),
+                                                    h["end"].tolist(), h["a_row"].tolist(),
+                                                    h["b_row"].tolist())), halo)
+                res.close()
+                if Be is not S[1]:
+                    Be.close()
+        # complement (NOT) and difference (AND-NOT) on shard windows
+        bits = ShardedBitset(ctx, sp, comm_device=torch.device("cpu"))
+        inp = [(m, *(x.data_ptr() for x in t)) for f, m, t in dev_rows]
+        for op, args in (("not", inp[:1]), ("andnot", inp)):
+            r = bits.run(args, gather=True, op=op)
+            out[op] = r["runs"].numpy().tolist()
+            r["result"].close()
+        q.put((rank, out, [int(x) for x in sp.offsets]))
+        ctx.close()
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_subtract_and_c4_ops(world):
+    # sharded subtract (both modes, two thresholds) == the oracle on all rows;
+    # sharded complement / difference on shard windows == the oracle's
+    # complement / set-mode subtract of merged runs (per base, coalesced)
+    from lime_amd import SUBTRACT_LIME, SUBTRACT_SET
+    from oracle import oracle
+    from tests.test_gpu_configs import coalesce
+    from tests.util import as_sorted_tuples
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    errs = [r[2] for r in res if r[1] == "error"]
+    assert not errs, errs[0]
+    A, B = _rows()
+    for mode in (SUBTRACT_LIME, SUBTRACT_SET):
+        for thr in (0, 25):
+            got = sorted(sum((r[1][("sub", mode, thr)][0] for r in res), []))
+            assert got == as_sorted_tuples(oracle.subtract(A, B, thr, mode))
+    assert sum(r[1][("sub", SUBTRACT_LIME, 0)][1][0] for r in res) > 0  # left halo moved
+    off = np.array(res[0][2])
+
+    def local(runs):
+        runs = np.array(runs, dtype=np.int64).reshape(-1, 2)
+        c = np.searchsorted(off, runs[:, 0], side="right") - 1
+        return coalesce(c, runs[:, 0] - off[c], runs[:, 1] - off[c])
+    comp = oracle.complement(A, LENS)
+    ma, mb = oracle.merge(A), oracle.merge(B)
+    diff = oracle.subtract((ma["contig"], ma["start"], ma["end"]),
+                           (mb["contig"], mb["start"], mb["end"]), 0, oracle.SUB_SET)
+    for r in res:
+        for op, exp in (("not", comp), ("andnot", diff)):
+            got = local(r[1][op])
+            want = coalesce(exp["contig"], exp["start"], exp["end"])
+            for x, y in zip(got, want):
+                assert np.array_equal(x, y), op

@@ -118,7 +118,10 @@ __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *co
 // GLOBAL: the input is already (gs, ge, row) in global coordinates (rows of
 // sets of this space, e.g. a shard's own rows + its halo); `contig` / `start`
 // / `end` then carry gs / ge / row and only order and span are validated.
-template <bool GLOBAL>
+// WRITE = false (plain caller rows): only validate, gather statistics and
+// histogram -- the first radix pass then reads the caller's rows itself
+// (k_scatter RAW), so gs / ge are never written and read back in between.
+template <bool GLOBAL, bool WRITE = true>
 __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              const uint32_t *__restrict__ start,
                                              const uint32_t *__restrict__ end,
@@ -225,8 +228,10 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                     uns = 1;
                 p0 = a0[j], p1 = a1[j], pok = ok[j];
             }
-            g4[q] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
-            h4[q] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
+            if (WRITE) {
+                g4[q] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
+                h4[q] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
+            }
             if (row)
                 r4[q] = make_uint4((uint32_t)i0, (uint32_t)i0 + 1, (uint32_t)i0 + 2,
                                    (uint32_t)i0 + 3);
@@ -250,8 +255,10 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                 g0 = off[c] + s;
                 g1 = off[c] + e;
             }
-            gs[i] = g0;
-            ge[i] = g1;
+            if (WRITE) {
+                gs[i] = g0;
+                ge[i] = g1;
+            }
             if (row) row[i] = (uint32_t)i;
             mx = g0 > mx ? g0 : mx;
             const uint32_t wd = g1 - g0;
@@ -393,7 +400,9 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     flush_hist(hist, counts, ntiles);
 }
 
-template <int M, int ROWS>
+// RAW (first pass over caller rows only): key_in / ge_in / row_in are the
+// caller's contig / start / end, and (gs, ge) = off[contig] + (start, end)
+template <int M, int ROWS, bool RAW = false>
 // 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
 __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
                                                 const uint32_t *__restrict__ ge_in,
@@ -402,7 +411,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
                                                 const uint32_t *__restrict__ base_mat,
                                                 uint32_t ntiles, uint32_t *__restrict__ key_out,
                                                 uint32_t *__restrict__ ge_out,
-                                                uint32_t *__restrict__ row_out) {
+                                                uint32_t *__restrict__ row_out,
+                                                const uint32_t *__restrict__ off = nullptr) {
     __shared__ uint32_t cnt[RWAVES][RBINS];
     __shared__ uint32_t dstart[RBINS];
     __shared__ uint32_t gbase[RBINS];
@@ -433,12 +443,19 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     for (int k = 0; k < RITEMS; ++k) {
         const int o = k * 64 + lane;
         const bool valid = o < lim;
-        vk[k] = valid ? kin[o] : 0u;
-        ve[k] = valid ? ein[o] : 0u;
+        if (RAW) {  // validated by k_prep: every contig id is in range
+            const uint32_t c = valid ? kin[o] : 0u;
+            const uint32_t base = valid ? off[c] : 0u;
+            vk[k] = valid ? base + ein[o] : 0u;
+            ve[k] = valid ? base + rin[o] : 0u;
+        } else {
+            vk[k] = valid ? kin[o] : 0u;
+            ve[k] = valid ? ein[o] : 0u;
+        }
         // (GS passes write identity rows straight from the position below,
         // keeping vr out of the registers of that path)
         vr[k] = ROWS == ROWS_IDENT && M != M_GS ? (uint32_t)(base + o)
-                : ROWS == ROWS_LOAD             ? (valid ? rin[o] : 0u)
+                : ROWS == ROWS_LOAD && !RAW     ? (valid ? rin[o] : 0u)
                                                 : 0u;
     }
     __syncthreads();
@@ -533,7 +550,17 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
 template <int M>
 void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                  const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
-                 uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows, int &rc) {
+                 uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows, int &rc,
+                 const uint32_t *raw_off = nullptr) {
+    if (raw_off) {  // first gs pass straight from the caller's rows (k_prep's histogram)
+        if ((rc = scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr)) != LIME_OK)
+            return;
+        if (M == M_GS && rows == ROWS_IDENT)
+            hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, true>), dim3(ntiles), dim3(RB), 0,
+                               S(ctx), k0, e0, r0, n, shift, st, (const uint32_t *)mat, ntiles, k1,
+                               e1, r1, raw_off);
+        return;
+    }
     if (!have_hist)
         hipLaunchKernelGGL(k_hist<M>, dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, r0, n, shift, st,
                            mat, ntiles, rows);
@@ -552,8 +579,16 @@ void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint
 
 int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
-               uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows) {
+               uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows,
+               const uint32_t *raw_off = nullptr) {
     int rc = LIME_OK;
+    if (raw_off) {
+        launch_pass<M_GS>(ctx, shift, true, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc,
+                          raw_off);
+        if (rc != LIME_OK) return rc;
+        LIME_HIP(hipGetLastError());
+        return LIME_OK;
+    }
     switch (mode) {
         case M_NZ:
             launch_pass<M_NZ>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
@@ -604,7 +639,22 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &st, 1));
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
-    if (n > 0) {
+    // plain caller rows: validate + histogram only, and let the first radix
+    // pass read the caller's rows (saves writing gs / ge and reading them back)
+    const bool raw_ok = !global && keep_rows && set->strand_in == nullptr && set->min_shift == 0;
+    bool raw = false;
+    if (n > 0 && raw_ok) {
+        hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
+                           d_start, d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n,
+                           k0, e0, nullptr, part, mat, ntiles, 0);
+        hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
+                           (int64_t)ntiles, st);
+        LIME_HIP(hipGetLastError());
+        LIME_TRY(read_back(ctx, &h, st, sizeof(h)));
+        // the fast path needs the first pass to be a gs pass over unsorted rows
+        raw = !h.err && n > 1 && h.unsorted && !(h.has_zero && h.max_width > 0);
+    }
+    if (n > 0 && !raw) {
         if (global)
             hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start,
                                d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0,
@@ -660,9 +710,19 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         int rows = !keep_rows ? ROWS_NONE : global ? ROWS_LOAD : ROWS_IDENT;
         // k_prep already histogrammed the gs digit at min_shift
         bool have = passes.front().first == M_GS && passes.front().second == set->min_shift;
+        bool first = true;
         for (auto &p : passes) {
-            LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
-                                e1, r1, mat, ntiles, rows));
+            if (first && raw) {
+                // the caller's (contig, start, end) in place of (gs, ge, row)
+                LIME_TRY(radix_pass(ctx, p.first, p.second, true, n,
+                                    reinterpret_cast<const uint32_t *>(d_contig), d_start, d_end,
+                                    set->strand_in, k1, e1, r1, mat, ntiles, rows,
+                                    (const uint32_t *)set->d_off));
+            } else {
+                LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in,
+                                    k1, e1, r1, mat, ntiles, rows));
+            }
+            first = false;
             have = false;
             if (rows == ROWS_IDENT) rows = ROWS_LOAD;
             std::swap(k0, k1);

@@ -641,7 +641,12 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
     // plain caller rows: validate + histogram only, and let the first radix
     // pass read the caller's rows (saves writing gs / ge and reading them back)
-    const bool raw_ok = !global && keep_rows && set->strand_in == nullptr && set->min_shift == 0;
+    // Opt-in (LIME_SORT_RAW=1): measured SLOWER on MI355X (C2 sort 5.8 ->
+    // 7.1 ms, C3 13.4 -> 17.2 ms: the first pass's off[contig] gather costs
+    // more than the ~4 B/row it saves), kept for experiments only.
+    static const bool raw_env = getenv("LIME_SORT_RAW") && atoi(getenv("LIME_SORT_RAW")) == 1;
+    const bool raw_ok = raw_env && !global && keep_rows && set->strand_in == nullptr &&
+                        set->min_shift == 0;
     bool raw = false;
     if (n > 0 && raw_ok) {
         hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,

@@ -140,9 +140,23 @@ struct BinArgs {
 
 // global start of a row (0 for an invalid contig); every pass derives a
 // row's bin and tile from it alone, so they always agree
-__device__ __forceinline__ uint64_t row_gs(const BinArgs &a, int32_t c, uint32_t s) {
+__device__ __forceinline__ uint64_t row_gs(const BinArgs &a, const uint32_t *off, int32_t c,
+                                           uint32_t s) {
     if (!a.contig) return s;
-    return (c >= 0 && c < a.nc) ? (uint64_t)a.off[c] + s : 0ull;
+    return (c >= 0 && c < a.nc) ? (uint64_t)off[c] + s : 0ull;
+}
+// the contig table in LDS when it fits (CMAX contigs: every hg assembly's
+// primary contigs), else read through the caches; the row passes gather it
+// once per row, a dependent load the prefetch cannot hide
+constexpr int CMAX = 1024;
+template <bool LC>
+__device__ __forceinline__ void stage_contigs(const BinArgs &a, uint32_t *coff, uint32_t *clen,
+                                              int nt) {
+    if (LC)
+        for (int i = threadIdx.x; i < a.nc; i += nt) {
+            coff[i] = a.off[i];
+            if (clen) clen[i] = a.len[i];
+        }
 }
 // bit g of the space -> bit of the bitset's window (clamped into it)
 __device__ __forceinline__ uint64_t local_bit(const BinArgs &a, uint64_t g) {
@@ -204,10 +218,14 @@ __device__ __forceinline__ void load_step(const BinArgs &a, int64_t base, int64_
     }
 }
 
+template <bool LC>
 __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
     __shared__ uint32_t hist[NTMAX];
+    __shared__ uint32_t coff[LC ? CMAX : 1];
+    const uint32_t *off = LC ? coff : a.off;
     const int nt = a.nb * PSUB;
     for (int i = threadIdx.x; i < nt; i += BINB) hist[i] = 0;
+    stage_contigs<LC>(a, coff, nullptr, BINB);
     __syncthreads();
     const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
     const int64_t r0 = (int64_t)ch * a.chunk_rows;
@@ -220,7 +238,7 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
             if (valid & (1u << k))
-                atomicAdd(&hist[ptile_of(a, local_bit(a, row_gs(a, c[k], s[k])))], 1u);
+                atomicAdd(&hist[ptile_of(a, local_bit(a, row_gs(a, off, c[k], s[k])))], 1u);
     }
     __syncthreads();
     for (int b = threadIdx.x; b < a.nb; b += BINB) {
@@ -233,11 +251,15 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
         if (hist[t]) atomicAdd(&a.ttot[t], hist[t]);
 }
 
+template <bool LC>
 __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
     __shared__ uint32_t stage[WSTEP];
     __shared__ uint16_t sbin[WSTEP];
     __shared__ uint32_t hist[NBMAX], soff[NBMAX], cur[NBMAX];
     __shared__ uint32_t scratch[WRB / 64 + 1];
+    __shared__ uint32_t coff[LC ? CMAX : 1], clen[LC ? CMAX : 1];
+    const uint32_t *off = LC ? coff : a.off, *len = LC ? clen : a.len;
+    stage_contigs<LC>(a, coff, clen, WRB);
     const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
     for (int t = threadIdx.x; t < NBMAX; t += WRB) {
         cur[t] = t < a.nb ? a.mat[(int64_t)t * a.nchunks + ch] : 0u;
@@ -256,7 +278,7 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
 #pragma unroll
         for (int k = 0; k < SROWS; ++k) {
             const int32_t cc = c[k];
-            const uint64_t gs = row_gs(a, cc, s[k]);
+            const uint64_t gs = row_gs(a, off, cc, s[k]);
             uint64_t ge = gs;
             if (!(valid & (1u << k))) {
             } else if (!a.contig) {
@@ -267,10 +289,10 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
                 err |= 1u;
             } else if (e[k] < s[k]) {
                 err |= 2u;
-            } else if (e[k] > a.len[cc]) {
+            } else if (e[k] > len[cc]) {
                 err |= 4u;
             } else {
-                ge = (uint64_t)a.off[cc] + e[k];
+                ge = (uint64_t)off[cc] + e[k];
             }
             // the row's part inside the window, in window bits
             const uint64_t g0 = local_bit(a, gs), g1 = local_bit(a, ge);
@@ -777,12 +799,19 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
     a.cross = cross;
     a.ncross = flags;
     a.err = flags + 1;
+    const bool lc = d_contig != nullptr && sp->n <= CMAX;
     if (n > 0) {
-        hipLaunchKernelGGL(k_bin_count, dim3(nch), dim3(BINB), 0, S(ctx), a);
+        if (lc)
+            hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);
+        else
+            hipLaunchKernelGGL(k_bin_count<false>, dim3(nch), dim3(BINB), 0, S(ctx), a);
         // (the extra last entries receive the totals)
         LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
         LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
-        hipLaunchKernelGGL(k_bin_write, dim3(nch), dim3(WRB), 0, S(ctx), a);
+        if (lc)
+            hipLaunchKernelGGL(k_bin_write<true>, dim3(nch), dim3(WRB), 0, S(ctx), a);
+        else
+            hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
         hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
     }
     hipLaunchKernelGGL(k_paint_bins, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx),

@@ -121,12 +121,15 @@ __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *co
 // WRITE = false (plain caller rows): only validate, gather statistics and
 // histogram -- the first radix pass then reads the caller's rows itself
 // (k_scatter RAW), so gs / ge are never written and read back in between.
-template <bool GLOBAL, bool WRITE = true>
+// LC: the contig table (<= PCMAX contigs) is staged in LDS, so the per-row
+// off / len gathers are LDS reads rather than dependent cache round trips
+constexpr int PCMAX = 1024;
+template <bool GLOBAL, bool WRITE = true, bool LC = false>
 __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              const uint32_t *__restrict__ start,
                                              const uint32_t *__restrict__ end,
-                                             const uint32_t *__restrict__ off,
-                                             const uint32_t *__restrict__ len, int32_t n_contigs,
+                                             const uint32_t *__restrict__ goff,
+                                             const uint32_t *__restrict__ glen, int32_t n_contigs,
                                              int64_t n, uint32_t *__restrict__ gs,
                                              uint32_t *__restrict__ ge, uint32_t *__restrict__ row,
                                              SetStats *__restrict__ part,
@@ -134,7 +137,16 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              int hshift) {
     __shared__ uint32_t hist[RWAVES][RBINS];
     __shared__ SetStats ws[RWAVES];
+    __shared__ uint32_t s_off[LC ? PCMAX : 1], s_len[LC ? PCMAX : 1];
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
+    if (LC) {
+        for (int i = threadIdx.x; i < n_contigs; i += RB) {
+            s_off[i] = goff[i];
+            s_len[i] = glen[i];
+        }
+        __syncthreads();
+    }
+    const uint32_t *off = LC ? s_off : goff, *len = LC ? s_len : glen;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
     uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
@@ -664,11 +676,16 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start,
                                d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0,
                                e0, r0, part, mat, ntiles, set->min_shift);
+        else if (set->n_contigs <= PCMAX)
+            hipLaunchKernelGGL((k_prep<false, true, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                               d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
+                               set->min_shift);  // rows = positions: made by the first pass
         else
             hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
                                d_start, d_end, (const uint32_t *)set->d_off, d_len,
                                set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
-                               set->min_shift);  // rows = positions: made by the first pass
+                               set->min_shift);
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());

@@ -498,3 +498,32 @@ def test_bitset_paths(ctx):
     order = np.lexsort((ix["start"], ix["contig"]))
     exp = coalesce({k: ix[k][order] for k in ("contig", "start", "end")})
     assert got == exp
+
+
+@pytest.mark.parametrize("nc", [200, 1500])
+def test_contig_table_lds_and_global(ctx, nc):
+    # the row passes stage the contig table in LDS up to 1024 contigs and
+    # read it through the caches beyond: both branches == the oracle
+    # (sort prep via set_from_host; bin count / write via bitset_from_device)
+    import torch
+    rng = np.random.default_rng(70 + nc)
+    A, B = random_sets(rng, 40000, 30000, n_contigs=nc, contig_len=5000, max_len=400,
+                       zero_frac=0.02)
+    sp = Space([f"c{i}" for i in range(nc)], [5000] * nc)
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    m = ctx.merge(a).to_host()
+    em = oracle.merge(A)
+    assert m["start"].tolist() == em["start"].tolist() and m["end"].tolist() == em["end"].tolist()
+    assert ctx.intersect(a, b).n == len(oracle.intersect(A, B)["start"])
+    dev = torch.device("cuda", 0)
+    t = [torch.from_numpy(np.ascontiguousarray(x).astype(np.int32)).to(dev) for x in A]
+    torch.cuda.synchronize()
+    bu = ctx.bitset_from_device(sp, len(A[0]), *(x.data_ptr() for x in t))
+    assert bu.popcount() == int((em["end"] - em["start"]).sum())
+    from tests.test_gpu_configs import coalesce  # book-ended runs joined (A.4)
+    comp = ctx.bitset_runs(1, bu).to_host()
+    ec = oracle.complement(A, [5000] * nc)
+    got = coalesce(comp["contig"], comp["start"], comp["end"])
+    exp = coalesce(ec["contig"], ec["start"], ec["end"])
+    for x, y in zip(got, exp):
+        assert x.tolist() == y.tolist()

@@ -237,9 +237,10 @@ int lime_result_format_bed(const lime_result *res, const char *const *names, cha
 
 /* ----------------------------------------------------- bit-per-base path */
 /* The bit-per-base set straight from UNSORTED device rows (u32 contig-local
- * coordinates, as lime_set_create_device): rows are only grouped by
- * 65536-base bin (two radix passes) and painted tile by tile -- no full sort
- * and no merge.  Same bits as lime_bitset_from_set on the sorted set. */
+ * coordinates, as lime_set_create_device): rows are only grouped by 2^22-base
+ * bin and then by 2^19-base paint tile (two counting scatters) and painted
+ * tile by tile -- no sort and no merge.  Same bits as lime_bitset_from_set
+ * on the sorted set. */
 int lime_bitset_from_device(lime_ctx *ctx, const lime_space *space, int64_t n,
                             const int32_t *d_contig, const uint32_t *d_start,
                             const uint32_t *d_end, lime_bitset **out);
@@ -252,6 +253,23 @@ int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out);
 int lime_bitset_from_global(lime_ctx *ctx, const lime_space *space, int64_t lo, int64_t hi,
                             int64_t n, const uint32_t *d_gstart, const uint32_t *d_gend,
                             lime_bitset **out);
+/* The AND of k <= 16 row sets' bits straight from their unsorted device rows
+ * (C5's k-way intersection, SURVEY.md 8(d) and Appendix A.4: the fold of the
+ * reference's pairwise intersect, cli/Intersection.scala:41-54, over merged
+ * operands): every set is binned as above, then one
+ * kernel paints each tile of every set in LDS and ANDs them in registers --
+ * one bitset stored, no per-set bitsets.  n, d_contig, d_start, d_end: k
+ * entries each (host arrays of device pointers).  Same bits as
+ * lime_bitset_and_runs over the k sets' bitsets. */
+int lime_bitset_and_from_device(lime_ctx *ctx, const lime_space *space, int32_t k,
+                                const int64_t *n, const int32_t *const *d_contig,
+                                const uint32_t *const *d_start, const uint32_t *const *d_end,
+                                lime_bitset **out);
+/* The same over a coordinate shard's window [lo, hi) from GLOBAL rows (as
+ * lime_bitset_from_global). */
+int lime_bitset_and_from_global(lime_ctx *ctx, const lime_space *space, int64_t lo, int64_t hi,
+                                int32_t k, const int64_t *n, const uint32_t *const *d_gstart,
+                                const uint32_t *const *d_gend, lime_bitset **out);
 int lime_bitset_window(const lime_bitset *bs, int64_t *lo, int64_t *n_words);
 /* op: 0 = a, 1 = not a (within contigs), 2 = a and b, 3 = a and not b */
 int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bitset *b,

@@ -93,6 +93,9 @@ SIGNATURES = {
     "lime_bitset_from_set": (C.c_int, [vp, vp, pp]),
     "lime_bitset_from_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_bitset_from_global": (C.c_int, [vp, vp, i64, i64, i64, vp, vp, pp]),
+    "lime_bitset_and_from_device": (C.c_int, [vp, vp, C.c_int32, P(i64), P(vp), P(vp), P(vp), pp]),
+    "lime_bitset_and_from_global": (C.c_int, [vp, vp, i64, i64, C.c_int32, P(i64), P(vp), P(vp),
+                                              pp]),
     "lime_bitset_window": (C.c_int, [vp, P(i64), P(i64)]),
     "lime_route_rows": (C.c_int, [vp, vp, i64, vp, vp, vp, u32, i32, P(u32), C.c_int, i64, vp,
                                   vp, vp, P(i64)]),

@@ -124,7 +124,7 @@ struct BinArgs {
     const uint32_t *off, *len;
     int32_t nc;
     int64_t n;
-    uint64_t lo, hi;           // the bitset covers global bits [lo, hi), lo % 64 == 0
+    uint32_t lo, hi;           // the bitset covers global bits [lo, hi), lo % 64 == 0
     uint64_t span;
     int nb;                    // bins
     int64_t chunk_rows;        // R (multiple of STEP)
@@ -139,11 +139,28 @@ struct BinArgs {
 };
 
 // global start of a row (0 for an invalid contig); every pass derives a
-// row's bin and tile from it alone, so they always agree
-__device__ __forceinline__ uint64_t row_gs(const BinArgs &a, const uint32_t *off, int32_t c,
+// row's bin and tile from it alone, so they always agree.  u32 arithmetic
+// (span < 2^32; an invalid row's start may wrap, identically in every pass,
+// and it paints nothing)
+__device__ __forceinline__ uint32_t row_gs(const BinArgs &a, const uint32_t *off, int32_t c,
                                            uint32_t s) {
     if (!a.contig) return s;
-    return (c >= 0 && c < a.nc) ? (uint64_t)off[c] + s : 0ull;
+    return (c >= 0 && c < a.nc) ? off[c] + s : 0u;
+}
+// bit g of the space -> bit of the bitset's window (clamped into it)
+__device__ __forceinline__ uint32_t local_bit(const BinArgs &a, uint32_t g) {
+    return (g < a.lo ? a.lo : (g > a.hi ? a.hi : g)) - a.lo;
+}
+__device__ __forceinline__ int bin_of(const BinArgs &a, uint32_t l) {
+    const uint32_t t = l >> BSH;
+    return t < (uint32_t)a.nb ? (int)t : a.nb - 1;
+}
+// paint tile of a window bit, consistent with bin_of and with the offset
+// k_bin_write packs (clamped into the bin, see there)
+__device__ __forceinline__ int ptile_of(const BinArgs &a, uint32_t l) {
+    const int b = bin_of(a, l);
+    const uint32_t q = (l - ((uint32_t)b << BSH)) >> PSH;
+    return b * PSUB + (q < PSUB ? (int)q : PSUB - 1);
 }
 // the contig table in LDS when it fits (CMAX contigs: every hg assembly's
 // primary contigs), else read through the caches; the row passes gather it
@@ -278,8 +295,8 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
 #pragma unroll
         for (int k = 0; k < SROWS; ++k) {
             const int32_t cc = c[k];
-            const uint64_t gs = row_gs(a, off, cc, s[k]);
-            uint64_t ge = gs;
+            const uint32_t gs = row_gs(a, off, cc, s[k]);
+            uint32_t ge = gs;
             if (!(valid & (1u << k))) {
             } else if (!a.contig) {
                 if (e[k] < s[k]) err |= 2u;
@@ -292,20 +309,22 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
             } else if (e[k] > len[cc]) {
                 err |= 4u;
             } else {
-                ge = (uint64_t)off[cc] + e[k];
+                ge = off[cc] + e[k];
             }
             // the row's part inside the window, in window bits
-            const uint64_t g0 = local_bit(a, gs), g1 = local_bit(a, ge);
+            const uint32_t g0 = local_bit(a, gs), g1 = local_bit(a, ge);
             const int t = bin_of(a, g0);
+            // offset in the bin; a row clamped to the end of a window whose
+            // width is a multiple of 2^BSH sits at 2^BSH: clamp it into the
+            // bin's last tile, where ptile_of counted it (it paints nothing)
+            const uint32_t o = min(g0 - ((uint32_t)t << BSH), (1u << BSH) - 1);
             // in-bin piece [g0, g0 + l), l <= LMAX; the rest: cross list
-            const uint64_t tend = ((uint64_t)t + 1) << BSH;
-            uint64_t l = g1 > g0 ? g1 - g0 : 0;
-            if (l > LMAX) l = LMAX;
-            if (g0 + l > tend) l = tend > g0 ? tend - g0 : 0;
+            uint32_t l = g1 > g0 ? g1 - g0 : 0u;
+            l = min(min(l, LMAX), (1u << BSH) - o);
             tb[k] = (uint32_t)t;
-            pk[k] = ((uint32_t)(g0 - ((uint64_t)t << BSH)) << LENB) | (uint32_t)l;
+            pk[k] = (o << LENB) | l;
             if ((valid & (1u << k)) && g1 > g0 + l)
-                a.cross[atomicAdd(a.ncross, 1u)] = ((g0 + l) << 32) | g1;
+                a.cross[atomicAdd(a.ncross, 1u)] = ((uint64_t)(g0 + l) << 32) | g1;
         }
         const uint32_t vnow = valid;
         // the next step's rows: their loads stay in flight across this step's
@@ -433,6 +452,31 @@ __global__ __launch_bounds__(SPB) void k_bin_split(BinArgs a) {
     }
 }
 
+// bits [s0, e0) of a tile image (LDS); rows within two words (C4/C5's
+// lengths) take a branch-free path: two masked ORs
+__device__ __forceinline__ void paint_lds(unsigned long long *img, uint32_t s0, uint32_t e0) {
+    const uint32_t wa = s0 >> 6, wb = (e0 - 1) >> 6;
+    if (wb - wa <= 1) {
+        const uint64_t head = ~0ull << (s0 & 63), tail = ~0ull >> (63 - ((e0 - 1) & 63));
+        if (wa == wb) {
+            atomicOr(&img[wa], (unsigned long long)(head & tail));
+        } else {
+            atomicOr(&img[wa], (unsigned long long)head);
+            atomicOr(&img[wb], (unsigned long long)tail);
+        }
+        return;
+    }
+    for (uint32_t w = wa; w <= wb; ++w) {
+        const uint32_t lo = w == wa ? (s0 & 63) : 0;
+        const uint32_t hi = w == wb ? ((e0 - 1) & 63) : 63;
+        const uint64_t mk = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
+        if (mk == ~0ull)
+            img[w] = mk;  // whole word: a plain store is idempotent with the ORs
+        else
+            atomicOr(&img[w], (unsigned long long)mk);
+    }
+}
+
 __global__ __launch_bounds__(PAINTB) void k_paint_bins(const uint32_t *__restrict__ slab2,
                                                        const uint32_t *__restrict__ tstart,
                                                        uint64_t *__restrict__ words,
@@ -454,18 +498,7 @@ __global__ __launch_bounds__(PAINTB) void k_paint_bins(const uint32_t *__restric
 #pragma unroll
         for (int k = 0; k < PV; ++k) {
             const uint32_t l = pv[k] & ((1u << PLENB) - 1);
-            if (l == 0) continue;
-            const uint32_t s0 = pv[k] >> PLENB, e0 = s0 + l;  // bits [s0, e0) of the tile
-            const uint32_t wa = s0 >> 6, wb = (e0 - 1) >> 6;
-            for (uint32_t w = wa; w <= wb; ++w) {
-                const uint32_t lo = w == wa ? (s0 & 63) : 0;
-                const uint32_t hi = w == wb ? ((e0 - 1) & 63) : 63;
-                const uint64_t mk = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
-                if (mk == ~0ull)
-                    img[w] = mk;  // whole word: a plain store is idempotent with the ORs
-                else
-                    atomicOr(&img[w], (unsigned long long)mk);
-            }
+            if (l) paint_lds(img, pv[k] >> PLENB, (pv[k] >> PLENB) + l);
         }
     }
     __syncthreads();
@@ -477,6 +510,138 @@ __global__ __launch_bounds__(PAINTB) void k_paint_bins(const uint32_t *__restric
             *reinterpret_cast<ulonglong2 *>(words + w0 + i) = make_ulonglong2(img[i], img[i + 1]);
         else
             words[w0 + i] = img[i];
+    }
+}
+
+// ---------------------------------------- k-way AND straight from rows
+// The C5 shape: k row sets binned as above, then ONE kernel
+// paints every set's rows of a tile into LDS in turn and ANDs the images in
+// registers -- one bitset stored instead of k, and no k-operand re-read.
+// Cross-list pieces (rows longer than a bin piece, pieces crossing a tile)
+// are bucketed by tile first: a piece [s, e) paints its head in tile(s) and
+// its tail in tile(e - 1); the tiles strictly between are wholly covered,
+// which a difference array records (the set then leaves those tiles' AND
+// unchanged).
+__global__ __launch_bounds__(BB) void k_xcount(const uint64_t *__restrict__ cross,
+                                               const unsigned int *__restrict__ ncross,
+                                               uint32_t *__restrict__ xcnt,
+                                               uint32_t *__restrict__ diff) {
+    const int64_t nx = *ncross;
+    for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < nx; i += (int64_t)gridDim.x * BB) {
+        const uint64_t s = cross[i] >> 32, e = cross[i] & 0xffffffffull;
+        const uint32_t t0 = (uint32_t)(s >> PSH), t1 = (uint32_t)((e - 1) >> PSH);
+        atomicAdd(&xcnt[t0], 1u);
+        if (t1 > t0) atomicAdd(&xcnt[t1], 1u);
+        if (t1 > t0 + 1) {
+            atomicAdd(&diff[t0 + 1], 1u);
+            atomicAdd(&diff[t1], 0xffffffffu);  // -1 (the scan is modulo 2^32)
+        }
+    }
+}
+
+__global__ __launch_bounds__(BB) void k_xwrite(const uint64_t *__restrict__ cross,
+                                               const unsigned int *__restrict__ ncross,
+                                               uint32_t *__restrict__ xcur,
+                                               uint2 *__restrict__ xl) {
+    const int64_t nx = *ncross;
+    for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < nx; i += (int64_t)gridDim.x * BB) {
+        const uint64_t s = cross[i] >> 32, e = cross[i] & 0xffffffffull;
+        const uint32_t t0 = (uint32_t)(s >> PSH), t1 = (uint32_t)((e - 1) >> PSH);
+        const uint64_t b0 = (uint64_t)t0 << PSH;
+        const uint64_t h = t1 > t0 ? b0 + (1ull << PSH) : e;  // head [s, h) in tile t0
+        xl[atomicAdd(&xcur[t0], 1u)] = make_uint2((uint32_t)(s - b0), (uint32_t)(h - b0));
+        if (t1 > t0) {
+            const uint64_t b1 = (uint64_t)t1 << PSH;
+            xl[atomicAdd(&xcur[t1], 1u)] = make_uint2(0u, (uint32_t)(e - b1));
+        }
+    }
+}
+
+struct AndArgs {
+    const uint32_t *slab2[MAXK];  // tile-ordered packed rows of set i
+    const uint32_t *tstart[MAXK]; // nt + 1 tile starts
+    const uint2 *xl[MAXK];        // tile-bucketed cross pieces (null: none)
+    const uint32_t *xoff[MAXK];   // nt + 1 bucket starts
+    const uint32_t *full[MAXK];   // nt + 1 exclusive scan of the difference array
+    int k;
+    uint64_t *words;
+    int64_t n_words;
+};
+
+constexpr int AWPT = TWORDS / PAINTB;  // AND words per thread (registers)
+constexpr int APV = 16;                // rows per lane per batch
+// The tile's (set, batch) sequence is software-pipelined: the next batch's
+// loads (possibly the next set's) are issued before the current batch is
+// painted, so they stay in flight across the set's AND barriers.
+__global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
+    __shared__ unsigned long long img[TWORDS];
+    const int t = blockIdx.x;
+    constexpr uint32_t B = APV * PAINTB;
+    uint64_t acc[AWPT];
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
+    // a tile wholly inside one of the set's cross pieces: AND unchanged
+    auto skip = [&](int i) { return a.full[i] && a.full[i][t + 1] != 0u; };
+    auto load = [&](int i, uint32_t rb, uint32_t(&p)[APV]) {
+        const uint32_t r1 = a.tstart[i][t + 1];
+        const uint32_t *slab2 = a.slab2[i];
+#pragma unroll
+        for (int k = 0; k < APV; ++k) {
+            const uint32_t r = rb + k * PAINTB + threadIdx.x;
+            p[k] = r < r1 ? slab2[r] : 0u;
+        }
+    };
+    int i = 0;
+    while (i < a.k && skip(i)) ++i;
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) img[threadIdx.x + j * PAINTB] = 0ull;
+    __syncthreads();
+    uint32_t rb = i < a.k ? a.tstart[i][t] : 0u;
+    uint32_t pv[APV];
+    if (i < a.k) load(i, rb, pv);
+    while (i < a.k) {  // (i, rb) and i2 are uniform over the block
+        int i2 = i;
+        uint32_t rb2 = rb + B;
+        if (rb2 >= a.tstart[i][t + 1]) {
+            i2 = i + 1;
+            while (i2 < a.k && skip(i2)) ++i2;
+            if (i2 < a.k) rb2 = a.tstart[i2][t];
+        }
+        uint32_t pn[APV];
+        if (i2 < a.k) load(i2, rb2, pn);
+#pragma unroll
+        for (int k = 0; k < APV; ++k) {
+            const uint32_t l = pv[k] & ((1u << PLENB) - 1);
+            if (l) paint_lds(img, pv[k] >> PLENB, (pv[k] >> PLENB) + l);
+        }
+        if (i2 != i) {  // set i complete: its cross pieces, then the AND
+            if (a.xl[i]) {
+                const uint32_t x0 = a.xoff[i][t], x1 = a.xoff[i][t + 1];
+                for (uint32_t x = x0 + threadIdx.x; x < x1; x += PAINTB) {
+                    const uint2 p = a.xl[i][x];
+                    if (p.y > p.x) paint_lds(img, p.x, p.y);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < AWPT; ++j) acc[j] &= img[threadIdx.x + j * PAINTB];
+            if (i2 < a.k) {
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < AWPT; ++j) img[threadIdx.x + j * PAINTB] = 0ull;
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < APV; ++k) pv[k] = pn[k];
+        i = i2;
+        rb = rb2;
+    }
+    const int64_t w0 = (int64_t)t * TWORDS;
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) {
+        const int64_t w = w0 + threadIdx.x + j * PAINTB;
+        if (w < a.n_words) a.words[w] = acc[j];
     }
 }
 
@@ -734,22 +899,43 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs) {
     return LIME_OK;
 }
 
-// bits straight from UNSORTED device rows (k_bin_count / k_bin_write /
-// k_paint_bins / k_paint_cross): no sort, no merge
-// window [lo, hi) of the space's global bits (lo % 64 == 0): the whole
-// space, or a coordinate shard's range (rows clipped to it)
-int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
-                      const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
-                      const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs) {
-    const int64_t span = sp->span;
-    const int64_t width = hi - lo;
-    bs->runs_bound = n;  // the union of n rows has at most n runs
-    bs->span = span;
-    bs->word0 = lo / 64;
-    bs->hi_bit = hi;
-    bs->n_words = (width + 63) / 64;
-    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
-    const int nb = (int)std::max<int64_t>((width + (1ll << BSH) - 1) >> BSH, 1);
+namespace {
+// pool blocks released on every return path (a set of PoolGuards)
+struct PoolBag {
+    lime_ctx *ctx;
+    std::vector<void *> ps;
+    template <typename T>
+    int get(T **p, size_t count) {
+        LIME_TRY(alloc(ctx, p, count));
+        ps.push_back((void *)*p);
+        return LIME_OK;
+    }
+    ~PoolBag() {
+        for (void *p : ps) release(ctx, p);
+    }
+};
+
+int rows_error(unsigned int e) {
+    if (e & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
+    if (e & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
+    if (e & 4u) return fail(LIME_ERR_RANGE, "interval end beyond its contig length");
+    return LIME_OK;
+}
+
+int n_bins(int64_t width) {
+    return (int)std::max<int64_t>((width + (1ll << BSH) - 1) >> BSH, 1);
+}
+
+// rows -> their paint tiles' packed rows (slab2, tile order) and the tile
+// starts (ttot, nt + 1 entries); pieces left to the cross list are appended
+// to `cross` (capacity 2 n: a row leaves at most its bin remainder and its
+// tile-crossing remainder), flags[0] counts them and flags[1] collects the
+// row errors.  Enqueued on the context stream only: no host sync.
+int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+             const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
+             const uint32_t *d_len, int64_t lo, int64_t hi, uint32_t *slab2, uint32_t *ttot,
+             uint64_t *cross, unsigned int *flags) {
+    const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
     // chunk: ~2 chunks per CU, 1..16 steps of 16 rows per lane
     int64_t R = (n + 511) / 512;
@@ -757,27 +943,17 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
     R = (R + STEP - 1) / STEP * STEP;
     const uint32_t nch = (uint32_t)std::max<int64_t>((n + R - 1) / R, 1);
     const int64_t mlen = (int64_t)nb * nch + 1;
-    uint32_t *mat, *ttot, *slab, *slab2;
-    uint64_t *cross;
-    unsigned int *flags;  // [0] ncross, [1] err
-    LIME_TRY(alloc(ctx, &mat, (size_t)mlen));
-    PoolGuard<uint32_t> g0{ctx, mat};
-    LIME_TRY(alloc(ctx, &ttot, (size_t)nt + 1));
-    PoolGuard<uint32_t> g1{ctx, ttot};
-    LIME_TRY(alloc(ctx, &slab, (size_t)std::max<int64_t>(n, 1)));
-    PoolGuard<uint32_t> g3{ctx, slab};
-    LIME_TRY(alloc(ctx, &slab2, (size_t)std::max<int64_t>(n, 1)));
-    PoolGuard<uint32_t> g6{ctx, slab2};
-    LIME_TRY(alloc(ctx, &cross, (size_t)std::max<int64_t>(n, 1)));
-    PoolGuard<uint64_t> g4{ctx, cross};
-    LIME_TRY(alloc(ctx, &flags, 2));
-    PoolGuard<unsigned int> g5{ctx, flags};
-    LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
+    PoolBag bag{ctx, {}};
+    uint32_t *mat, *slab;
+    LIME_TRY(bag.get(&mat, (size_t)mlen));
+    LIME_TRY(bag.get(&slab, (size_t)std::max<int64_t>(n, 1)));
     LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
-    if (n == 0)
+    if (n == 0) {
         LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
-    else  // the total's slot (k_bin_count writes the nb * nch counts before it)
-        LIME_HIP(hipMemsetAsync(mat + mlen - 1, 0, 4, S(ctx)));
+        return LIME_OK;
+    }
+    // the total's slot (k_bin_count writes the nb * nch counts before it)
+    LIME_HIP(hipMemsetAsync(mat + mlen - 1, 0, 4, S(ctx)));
     BinArgs a;
     a.contig = d_contig;
     a.start = d_start;
@@ -786,9 +962,9 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
     a.len = d_len;
     a.nc = sp->n;
     a.n = n;
-    a.lo = (uint64_t)lo;
-    a.hi = (uint64_t)hi;
-    a.span = (uint64_t)span;
+    a.lo = (uint32_t)lo;
+    a.hi = (uint32_t)hi;
+    a.span = (uint64_t)sp->span;
     a.nb = nb;
     a.chunk_rows = R;
     a.nchunks = nch;
@@ -800,20 +976,52 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
     a.ncross = flags;
     a.err = flags + 1;
     const bool lc = d_contig != nullptr && sp->n <= CMAX;
-    if (n > 0) {
-        if (lc)
-            hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);
-        else
-            hipLaunchKernelGGL(k_bin_count<false>, dim3(nch), dim3(BINB), 0, S(ctx), a);
-        // (the extra last entries receive the totals)
-        LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
-        LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
-        if (lc)
-            hipLaunchKernelGGL(k_bin_write<true>, dim3(nch), dim3(WRB), 0, S(ctx), a);
-        else
-            hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
-        hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
-    }
+    if (lc)
+        hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);
+    else
+        hipLaunchKernelGGL(k_bin_count<false>, dim3(nch), dim3(BINB), 0, S(ctx), a);
+    // (the extra last entries receive the totals)
+    LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
+    LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
+    if (lc)
+        hipLaunchKernelGGL(k_bin_write<true>, dim3(nch), dim3(WRB), 0, S(ctx), a);
+    else
+        hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
+    hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
+void window_of(lime_bitset *bs, const lime_space *sp, int64_t lo, int64_t hi) {
+    bs->span = sp->span;
+    bs->word0 = lo / 64;
+    bs->hi_bit = hi;
+    bs->n_words = (hi - lo + 63) / 64;
+}
+}  // namespace
+
+// bits straight from UNSORTED device rows (k_bin_count / k_bin_write /
+// k_bin_split / k_paint_bins / k_paint_cross): no sort, no merge.
+// Window [lo, hi) of the space's global bits (lo % 64 == 0): the whole
+// space, or a coordinate shard's range (rows clipped to it)
+int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                      const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
+                      const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs) {
+    window_of(bs, sp, lo, hi);
+    bs->runs_bound = n;  // the union of n rows has at most n runs
+    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
+    const int nt = n_bins(hi - lo) * PSUB;
+    PoolBag bag{ctx, {}};
+    uint32_t *ttot, *slab2;
+    uint64_t *cross;
+    unsigned int *flags;  // [0] ncross, [1] err
+    LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
+    LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n, 1)));
+    LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * n, 1)));
+    LIME_TRY(bag.get(&flags, 2));
+    LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
+    LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, slab2, ttot,
+                      cross, flags));
     hipLaunchKernelGGL(k_paint_bins, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx),
                        (const uint32_t *)slab2, (const uint32_t *)ttot, bs->words, bs->n_words);
     if (n > 0)
@@ -823,9 +1031,76 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
     LIME_HIP(hipGetLastError());
     unsigned int h[2] = {0, 0};
     LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
-    if (h[1] & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
-    if (h[1] & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
-    if (h[1] & 4u) return fail(LIME_ERR_RANGE, "interval end beyond its contig length");
+    return rows_error(h[1]);
+}
+
+// the AND of k row sets' bits over window [lo, hi), straight from their
+// unsorted rows (bin_rows per set, k_paint_and once): rows[i] = (n, contig
+// or null for global rows, start, end)
+int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n,
+                    const int32_t *const *d_contig, const uint32_t *const *d_start,
+                    const uint32_t *const *d_end, const uint32_t *d_off, const uint32_t *d_len,
+                    int64_t lo, int64_t hi, lime_bitset *bs) {
+    if (k < 1 || k > MAXK) return fail(LIME_ERR_ARG, "1 to 16 row sets per AND");
+    window_of(bs, sp, lo, hi);
+    int64_t nmax = 0, bound = 0;
+    for (int i = 0; i < k; ++i) {
+        nmax = std::max(nmax, n[i]);
+        bound += n[i];
+    }
+    bs->runs_bound = bound;  // each AND run starts at a run start of some set
+    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
+    const int nt = n_bins(hi - lo) * PSUB;
+    PoolBag bag{ctx, {}};
+    uint64_t *cross;
+    unsigned int *flags;
+    LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * nmax, 1)));
+    LIME_TRY(bag.get(&flags, 2 * (size_t)k));
+    LIME_HIP(hipMemsetAsync(flags, 0, 8 * (size_t)k, S(ctx)));
+    AndArgs aa;
+    for (int i = 0; i < MAXK; ++i) {
+        aa.slab2[i] = aa.tstart[i] = aa.xoff[i] = aa.full[i] = nullptr;
+        aa.xl[i] = nullptr;
+    }
+    aa.k = k;
+    aa.words = bs->words;
+    aa.n_words = bs->n_words;
+    for (int i = 0; i < k; ++i) {
+        uint32_t *slab2, *ttot;
+        LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
+        LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
+        LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo, hi,
+                          slab2, ttot, cross, flags + 2 * i));
+        aa.slab2[i] = slab2;
+        aa.tstart[i] = ttot;
+        // the cross buffer is reused by the next set: bucket its pieces now
+        unsigned int h[2] = {0, 0};
+        LIME_TRY(read_back(ctx, h, flags + 2 * i, sizeof(h)));
+        LIME_TRY(rows_error(h[1]));
+        if (h[0] == 0) continue;
+        uint32_t *xcnt, *diff, *xcur;
+        uint2 *xl;
+        LIME_TRY(bag.get(&xcnt, (size_t)nt + 1));
+        LIME_TRY(bag.get(&diff, (size_t)nt + 1));
+        LIME_TRY(bag.get(&xcur, (size_t)nt + 1));
+        LIME_TRY(bag.get(&xl, 2 * (size_t)h[0]));
+        LIME_HIP(hipMemsetAsync(xcnt, 0, 4 * ((size_t)nt + 1), S(ctx)));
+        LIME_HIP(hipMemsetAsync(diff, 0, 4 * ((size_t)nt + 1), S(ctx)));
+        const unsigned g = std::min<unsigned>(blocks_for(h[0], BB), 2048u);
+        hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+                           (const unsigned int *)(flags + 2 * i), xcnt, diff);
+        LIME_TRY(scan_exclusive_u32(ctx, xcnt, xcnt, (int64_t)nt + 1, nullptr));
+        LIME_TRY(scan_exclusive_u32(ctx, diff, diff, (int64_t)nt + 1, nullptr));
+        LIME_HIP(hipMemcpyAsync(xcur, xcnt, 4 * ((size_t)nt + 1), hipMemcpyDeviceToDevice, S(ctx)));
+        hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+                           (const unsigned int *)(flags + 2 * i), xcur, xl);
+        LIME_HIP(hipGetLastError());
+        aa.xl[i] = xl;
+        aa.xoff[i] = xcnt;
+        aa.full[i] = diff;
+    }
+    hipLaunchKernelGGL(k_paint_and, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), aa);
+    LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
 

@@ -127,6 +127,10 @@ int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
 int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                       const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
                       const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs);
+int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n,
+                    const int32_t *const *d_contig, const uint32_t *const *d_start,
+                    const uint32_t *const *d_end, const uint32_t *d_off, const uint32_t *d_len,
+                    int64_t lo, int64_t hi, lime_bitset *bs);
 int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
                const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
@@ -992,6 +996,59 @@ int lime_bitset_from_global(lime_ctx *ctx, const lime_space *sp, int64_t lo, int
     }
     *out = bs;
     return LIME_OK;
+}
+
+// k row sets -> the bits of their AND, one fused paint (bitset.hip)
+static int bitset_and_entry(lime_ctx *ctx, const lime_space *sp, int64_t lo, int64_t hi,
+                            int32_t k, const int64_t *n, const int32_t *const *d_contig,
+                            const uint32_t *const *d_start, const uint32_t *const *d_end,
+                            bool global, lime_bitset **out) {
+    if (!ctx || !sp || !out || !n || k < 1 || k > 16 || !d_start || !d_end ||
+        (!global && !d_contig))
+        return fail(LIME_ERR_ARG, "bad bitset and arguments");
+    for (int i = 0; i < k; ++i) {
+        if (n[i] < 0 || (n[i] > 0 && (!d_start[i] || !d_end[i] || (!global && !d_contig[i]))))
+            return fail(LIME_ERR_ARG, "bad bitset and arguments");
+        if (n[i] > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    }
+    hipSetDevice(ctx->device);
+    uint32_t *d_off = nullptr, *d_len = nullptr;
+    if (!global) LIME_TRY(upload_space(ctx, sp, &d_off, &d_len));
+    PoolGuard<uint32_t> g0{ctx, d_off};
+    PoolGuard<uint32_t> g1{ctx, d_len};
+    std::vector<const int32_t *> contig(k, nullptr);
+    if (!global)
+        for (int i = 0; i < k; ++i) contig[i] = d_contig[i];
+    lime_bitset *bs = new lime_bitset();
+    bs->ctx = ctx;
+    bs->n_contigs = sp->n;
+    bs->off = sp->off;
+    bs->len = sp->len;
+    int rc = bitset_and_rows(ctx, sp, k, n, contig.data(), d_start, d_end, d_off, d_len, lo, hi,
+                             bs);
+    if (rc != LIME_OK) {
+        release(ctx, bs->words);
+        delete bs;
+        return rc;
+    }
+    *out = bs;
+    return LIME_OK;
+}
+
+int lime_bitset_and_from_device(lime_ctx *ctx, const lime_space *sp, int32_t k, const int64_t *n,
+                                const int32_t *const *d_contig, const uint32_t *const *d_start,
+                                const uint32_t *const *d_end, lime_bitset **out) {
+    if (!sp) return fail(LIME_ERR_ARG, "bad bitset and arguments");
+    return bitset_and_entry(ctx, sp, 0, sp->span, k, n, d_contig, d_start, d_end, false, out);
+}
+
+int lime_bitset_and_from_global(lime_ctx *ctx, const lime_space *sp, int64_t lo, int64_t hi,
+                                int32_t k, const int64_t *n, const uint32_t *const *d_gstart,
+                                const uint32_t *const *d_gend, lime_bitset **out) {
+    if (!sp) return fail(LIME_ERR_ARG, "bad bitset and arguments");
+    if (lo < 0 || hi < lo || hi > sp->span || lo % 64 != 0)
+        return fail(LIME_ERR_ARG, "window must satisfy 0 <= lo <= hi <= span, lo % 64 == 0");
+    return bitset_and_entry(ctx, sp, lo, hi, k, n, nullptr, d_gstart, d_gend, true, out);
 }
 
 int lime_bitset_window(const lime_bitset *bs, int64_t *lo, int64_t *n_words) {

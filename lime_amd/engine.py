@@ -416,6 +416,28 @@ class Context:
                                              vp(d_gs), vp(d_ge), C.byref(h)))
         return Bitset(self, h, space)
 
+    def bitset_and_from_device(self, space, rows):
+        """the AND of k row sets' bits straight from their UNSORTED device rows
+        (lime_bitset_and_from_device): rows = [(n, d_contig, d_start, d_end)]"""
+        k = len(rows)
+        ns = (i64 * k)(*[int(r[0]) for r in rows])
+        cs, ss, es = ((vp * k)(*[vp(r[j]) for r in rows]) for j in (1, 2, 3))
+        h = vp()
+        check(_lib().lime_bitset_and_from_device(self._h, space.handle, k, ns, cs, ss, es,
+                                                 C.byref(h)))
+        return Bitset(self, h, space)
+
+    def bitset_and_from_global(self, space, lo, hi, rows):
+        """the same over a shard's window [lo, hi) from GLOBAL rows:
+        rows = [(n, d_gs, d_ge)]"""
+        k = len(rows)
+        ns = (i64 * k)(*[int(r[0]) for r in rows])
+        ss, es = ((vp * k)(*[vp(r[j]) for r in rows]) for j in (1, 2))
+        h = vp()
+        check(_lib().lime_bitset_and_from_global(self._h, space.handle, int(lo), int(hi), k, ns,
+                                                 ss, es, C.byref(h)))
+        return Bitset(self, h, space)
+
     def route_rows(self, space, n, d_contig, d_start, d_end, splits, clip=False, cap=-1,
                    d_gs=None, d_ge=None, d_row=None, row_base=0):
         """Rows -> coordinate shards (lime_route_rows): returns the per-shard

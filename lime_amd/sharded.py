@@ -205,9 +205,10 @@ class ShardedBitset:
     routes its slice of unsorted rows to the shards they overlap, clipped at
     the shard bounds (lime_route_rows, clip = 1: exact for base-level
     algebra, no halo); one all_to_all moves them (RCCL over
-    xGMI, device buffers); each shard paints the rows it received into a
-    bitset over its window (lime_bitset_from_global) and ANDs the k bitsets
-    (lime_bitset_and_runs).  Runs are in global coordinates; the one
+    xGMI, device buffers); each shard bins the rows it received and paints
+    and ANDs all k sets tile by tile in one kernel over its window
+    (lime_bitset_and_from_global; NOT / AND-NOT paint per-set bitsets,
+    lime_bitset_from_global).  Runs are in global coordinates; the one
     boundary fix-up (a run ending exactly at a shard bound continues in the
     next shard) is dist.bitset_carry, one all_gather of 4 numbers per shard.
     The runs stay sharded; run(gather=True) adds the emulated allgatherv.
@@ -238,11 +239,10 @@ class ShardedBitset:
             self.ctx.synchronize()
             torch.cuda.current_stream(self.dev).synchronize()
 
-    def bitset(self, n, d_contig, d_start, d_end):
-        """this shard's bitset of one set, from this rank's slice of its rows"""
+    def shard_rows(self, n, d_contig, d_start, d_end):
+        """this rank's slice of one set's rows -> the rows of this shard's
+        window from every rank (global coordinates, clipped): (m, gs, ge)"""
         ctx, sp = self.ctx, self.space
-        if self.world == 1:
-            return ctx.bitset_from_device(sp, n, d_contig, d_start, d_end)
         cap = n + 4096
         gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
         ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
@@ -258,8 +258,25 @@ class ShardedBitset:
         (rgs, rge), rc = ld.exchange([gs, ge], counts, self.group, self.comm)
         self._sync()
         self.moved += sum(rc) - rc[self.rank]
-        m = sum(rc)
+        return sum(rc), rgs, rge
+
+    def bitset(self, n, d_contig, d_start, d_end):
+        """this shard's bitset of one set, from this rank's slice of its rows"""
+        ctx, sp = self.ctx, self.space
+        if self.world == 1:
+            return ctx.bitset_from_device(sp, n, d_contig, d_start, d_end)
+        m, rgs, rge = self.shard_rows(n, d_contig, d_start, d_end)
         return ctx.bitset_from_global(sp, self.lo, self.hi, m, rgs.data_ptr(), rge.data_ptr())
+
+    def and_bitset(self, inputs):
+        """this shard's AND of k <= 16 sets in one fused paint
+        (lime_bitset_and_from_device / _from_global): no per-set bitsets"""
+        ctx, sp = self.ctx, self.space
+        if self.world == 1:
+            return ctx.bitset_and_from_device(sp, inputs)
+        got = [self.shard_rows(*x) for x in inputs]
+        return ctx.bitset_and_from_global(sp, self.lo, self.hi,
+                                          [(m, g.data_ptr(), e.data_ptr()) for m, g, e in got])
 
     def run(self, inputs, gather=False, op="and"):
         """inputs: [(n, d_contig, d_start, d_end)] per set (this rank's rows,
@@ -269,8 +286,11 @@ class ShardedBitset:
         coordinates), the carry (drop_first, new_last_end), the total run
         count of the unsharded result and, with gather=True, every run as an
         int64 [m, 2] tensor (global start, end) in order."""
-        bits = [self.bitset(*x) for x in inputs]
-        if op == "and":
+        fuse = op == "and" and len(inputs) <= 16
+        bits = [self.and_bitset(inputs)] if fuse else [self.bitset(*x) for x in inputs]
+        if fuse:
+            res = self.ctx.bitset_runs(0, bits[0])
+        elif op == "and":
             res = self.ctx.bitset_and(bits)
         elif op == "not":
             res = self.ctx.bitset_runs(1, bits[0])

@@ -278,15 +278,20 @@ def fold_and(n_contigs, merged):
 def test_c5_eight_way_and_density(ctx):
     sp = hg38(8)
     per = 125_000_000 // 8
-    merged, bits = [], []
+    merged, bits, devs = [], [], []
     for i in range(8):
         dev, X = device_rows(ctx, sp, per, 0x50 + i, 10, 40)
-        bits.append(dbits(ctx, sp, dev))  # the C5 path: unsorted rows -> binned paint
+        bits.append(dbits(ctx, sp, dev))  # unsorted rows -> binned paint, per set
         merged.append(oracle.merge_mt(len(sp.names), X))
-        del dev
+        devs.append(dev)
     got = ctx.bitset_and(bits).to_host()
     exp = fold_and(len(sp.names), merged)
     g = coalesce(got["contig"], got["start"], got["end"])
     assert_runs_equal(g, coalesce(exp["contig"], exp["start"], exp["end"]))
+    # the bench's path: the 8 sets binned and painted-and-ANDed in one kernel
+    fused = ctx.bitset_and_from_device(
+        sp, [(d[0].numel(), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr()) for d in devs])
+    f = ctx.bitset_runs(0, fused).to_host()
+    assert_runs_equal((f["contig"], f["start"], f["end"]), (got["contig"], got["start"], got["end"]))
     cov = int((g[2] - g[1]).sum())
     assert 0.01 < cov / sum(sp.lengths) < 0.05  # 8-way ~2.7% of the genome

@@ -527,3 +527,107 @@ def test_contig_table_lds_and_global(ctx, nc):
     exp = coalesce(ec["contig"], ec["start"], ec["end"])
     for x, y in zip(got, exp):
         assert x.tolist() == y.tolist()
+
+
+def _dev_rows(A):
+    import torch
+    dev = torch.device("cuda", 0)
+    t = [torch.from_numpy(np.ascontiguousarray(x).astype(np.int32)).to(dev) for x in A]
+    torch.cuda.synchronize()
+    return t
+
+
+@pytest.mark.parametrize("k,max_len", [(1, 300), (3, 700000), (5, 3000)])
+def test_bitset_and_fused(ctx, k, max_len):
+    # one fused paint of k row sets == the AND of their k bitsets (rows up to
+    # 0.7 Mb leave cross pieces and wholly covered tiles)
+    rng = np.random.default_rng(80 + k)
+    sets = [random_sets(rng, 20000, 1, n_contigs=3, contig_len=3_000_000, max_len=max_len,
+                        zero_frac=0.05, dup_frac=0.02)[0] for _ in range(k)]
+    sp = space_for(3, 3_000_000)
+    dev = [_dev_rows(A) for A in sets]
+    fused = ctx.bitset_and_from_device(
+        sp, [(len(A[0]), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr()) for A, t in
+             zip(sets, dev)])
+    bits = [ctx.bitset_from_device(sp, len(A[0]), *(x.data_ptr() for x in t))
+            for A, t in zip(sets, dev)]
+    exp = ctx.bitset_and(bits).to_host()
+    got = ctx.bitset_runs(0, fused).to_host()
+    assert len(exp["start"]) > 0
+    for key in ("contig", "start", "end"):
+        assert got[key].tolist() == exp[key].tolist()
+
+
+def test_bitset_and_fused_window(ctx):
+    # a shard's window from global rows == the per-set window bitsets' AND
+    import torch
+    rng = np.random.default_rng(91)
+    sp = space_for(3, 3_000_000)
+    lo, hi = 64 * 20000, 7_000_000
+    rows, bits = [], []
+    keep = []
+    for _ in range(4):
+        A, _ = random_sets(rng, 20000, 1, n_contigs=3, contig_len=3_000_000, max_len=5000)
+        off = sp.offsets[:3]
+        gs = (off[A[0]] + A[1]).astype(np.uint32).view(np.int32)
+        ge = (off[A[0]] + A[2]).astype(np.uint32).view(np.int32)
+        t = [torch.from_numpy(x).cuda() for x in (gs, ge)]
+        keep.append(t)
+        rows.append((len(gs), t[0].data_ptr(), t[1].data_ptr()))
+        bits.append(ctx.bitset_from_global(sp, lo, hi, len(gs), t[0].data_ptr(), t[1].data_ptr()))
+    torch.cuda.synchronize()
+    fused = ctx.bitset_and_from_global(sp, lo, hi, rows)
+    assert fused.window() == bits[0].window()
+    got = ctx.bitset_runs(0, fused).to_host()
+    exp = ctx.bitset_and(bits).to_host()
+    assert len(exp["start"]) > 0
+    for key in ("contig", "start", "end"):
+        assert got[key].tolist() == exp[key].tolist()
+
+
+def test_bitset_cross_capacity_two_pieces_per_row(ctx):
+    # rows longer than a bin piece (1023 bases) starting 10 bases before a
+    # 2^19-base paint tile end leave TWO cross pieces each (bin remainder +
+    # tile-crossing remainder): the cross list holds 2 n
+    T = 1 << 19
+    n = 60000
+    j = np.arange(n) % 5 + 1
+    A = (np.zeros(n, np.int32), (j * T - 10).astype(np.int64), (j * T - 10 + 2000).astype(np.int64))
+    sp = space_for(1, 4_000_000)
+    t = _dev_rows(A)
+    cov = int((oracle.merge(A)["end"] - oracle.merge(A)["start"]).sum())
+    b = ctx.bitset_from_device(sp, n, *(x.data_ptr() for x in t))
+    assert b.popcount() == cov == 5 * 2000
+    f = ctx.bitset_and_from_device(sp, [(n, *(x.data_ptr() for x in t))] * 2)
+    assert f.popcount() == cov
+    got = ctx.bitset_runs(0, f).to_host()
+    em = oracle.merge(A)
+    assert got["start"].tolist() == em["start"].tolist()
+    assert got["end"].tolist() == em["end"].tolist()
+
+
+def test_bitset_window_end_on_bin_bound(ctx):
+    # window width = 2 bins (2^23 bits): rows wholly past its end clamp to
+    # bit 2^23 and must land in the last tile the count pass gave them
+    # (a mismatch left a tile slot unwritten)
+    import torch
+    rng = np.random.default_rng(93)
+    sp = space_for(1, 12_000_000)
+    lo, hi = 0, 1 << 23
+    n = 40000
+    s = rng.integers(0, 12_000_000 - 500, n)
+    e = s + rng.integers(0, 500, n)
+    gs = torch.from_numpy(s.astype(np.uint32).view(np.int32)).cuda()
+    ge = torch.from_numpy(e.astype(np.uint32).view(np.int32)).cuda()
+    torch.cuda.synchronize()
+    m = oracle.merge((np.zeros(n, np.int32), s, e))
+    from tests.test_gpu_configs import coalesce  # book-ended runs joined (A.4)
+    cs, ce = np.clip(m["start"], lo, hi), np.clip(m["end"], lo, hi)
+    keep = ce > cs
+    _, xs, xe = coalesce(np.zeros(int(keep.sum())), cs[keep], ce[keep])
+    assert len(xs) > 1000
+    for b in (ctx.bitset_from_global(sp, lo, hi, n, gs.data_ptr(), ge.data_ptr()),
+              ctx.bitset_and_from_global(sp, lo, hi, [(n, gs.data_ptr(), ge.data_ptr())])):
+        got = ctx.bitset_runs(0, b).to_host()
+        assert got["start"].tolist() == xs.tolist()
+        assert got["end"].tolist() == xe.tolist()

@@ -136,6 +136,7 @@ struct BinArgs {
     uint64_t *cross;           // remainders (s << 32 | e) in window bits, capacity n
     unsigned int *ncross;
     unsigned int *err;         // bit0 contig, bit1 end < start, bit2 end > length
+    uint32_t *dummy;           // sink of the fixed-count store batches (see k_bin_write)
 };
 
 // global start of a row (0 for an invalid contig); every pass derives a
@@ -355,11 +356,18 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
                 sbin[j] = (uint16_t)tb[k];
             }
         __syncthreads();
-        // runs of a bin are consecutive: lane-consecutive stores
+        // runs of a bin are consecutive: lane-consecutive stores.  Every lane
+        // issues exactly SROWS stores (positions past the step's rows go to a
+        // sink): loads and stores share vmcnt, so with a static store count
+        // the next step's first use of its prefetched rows waits for the
+        // loads only, not for this step's stores
         const int cnt = (int)min((int64_t)WSTEP, r1 - base);
-        for (int j = threadIdx.x; j < cnt; j += WRB) {
+#pragma unroll
+        for (int k = 0; k < SROWS; ++k) {
+            const int j = threadIdx.x + k * WRB;
             const uint32_t t = sbin[j];
-            a.slab[cur[t] + (uint32_t)j - soff[t]] = stage[j];
+            uint32_t *dst = j < cnt ? a.slab + (cur[t] + (uint32_t)j - soff[t]) : a.dummy;
+            *dst = stage[j];
         }
         __syncthreads();
         for (int t = threadIdx.x; t < NBMAX; t += WRB) {
@@ -944,9 +952,10 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     const uint32_t nch = (uint32_t)std::max<int64_t>((n + R - 1) / R, 1);
     const int64_t mlen = (int64_t)nb * nch + 1;
     PoolBag bag{ctx, {}};
-    uint32_t *mat, *slab;
+    uint32_t *mat, *slab, *dummy;
     LIME_TRY(bag.get(&mat, (size_t)mlen));
     LIME_TRY(bag.get(&slab, (size_t)std::max<int64_t>(n, 1)));
+    LIME_TRY(bag.get(&dummy, 64));
     LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
     if (n == 0) {
         LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
@@ -975,6 +984,7 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     a.cross = cross;
     a.ncross = flags;
     a.err = flags + 1;
+    a.dummy = dummy;
     const bool lc = d_contig != nullptr && sp->n <= CMAX;
     if (lc)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);

@@ -397,66 +397,67 @@ __global__ __launch_bounds__(SPB) void k_bin_split(BinArgs a) {
     const int lane = dev::lane_id();
     const uint64_t bin0 = (uint64_t)b << BSH;
     const uint64_t lt = dev::lanemask_lt();
-    constexpr int PV = 8;   // slots per claim round (one wave of 8 x 8 counters)
-    constexpr int NG = 2;   // claim rounds per step: 16 loads in flight per lane
-    // rows of a wave per step: 64 lanes x PV x NG slots, lane-consecutive per slot
+    constexpr int PV = 8;  // slots per step (one wave of 8 x 8 claim counters)
+    // rows of a wave per step: 64 lanes x PV slots, lane-consecutive per slot.
+    // Software-pipelined with a static store count: the next step's loads
+    // (clamped addresses: always issued) go out before this step's PV stores
+    // (invalid slots to a sink), so its first use waits for the loads only
+    // and the stores stay in flight
     const int wv = threadIdx.x / 64, nwv = SPB / 64;
-    for (uint32_t rb0 = r0 + (uint32_t)wv * 64 * PV * NG; rb0 < r1;
-         rb0 += (uint32_t)nwv * 64 * PV * NG) {
-        uint32_t pa[NG][PV];
+    const uint32_t stride = (uint32_t)nwv * 64 * PV;
+    uint32_t pv[PV];
+    const uint32_t first = r0 + (uint32_t)wv * 64 * PV;
+    if (first < r1)
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+        for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(first + k * 64 + lane, r1 - 1)];
+    for (uint32_t rb = first; rb < r1; rb += stride) {
+        uint32_t q[PV], rk[PV], val[PV];
+        uint32_t myc = 0;  // lane 8 k + d: rows of slot k bound for tile d
 #pragma unroll
-            for (int k = 0; k < PV; ++k) {
-                const uint32_t r = rb0 + (g * PV + k) * 64 + lane;
-                pa[g][k] = r < r1 ? a.slab[r] : 0u;
-            }
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            const uint32_t rb = rb0 + g * PV * 64;
-            const uint32_t *pv = pa[g];
-            uint32_t q[PV], rk[PV], val[PV];
-            uint32_t myc = 0;  // lane 8 k + d: rows of slot k bound for tile d
-#pragma unroll
-            for (int k = 0; k < PV; ++k) {
-                const bool v = rb + k * 64 + lane < r1;
-                const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
-                q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
-                const uint32_t qend = (q[k] + 1) << PSH;
-                const uint32_t l2 = o + l > qend ? qend - o : l;  // clipped at the tile end
-                if (v && l2 < l)  // remainder [o + l2, o + l) into the next tile(s)
-                    a.cross[atomicAdd(a.ncross, 1u)] = ((bin0 + o + l2) << 32) | (bin0 + o + l);
-                val[k] = ((o - (q[k] << PSH)) << PLENB) | l2;
-                // rank by the 3 bits of the tile: 4 ballots, not 8
-                const uint64_t vm = __ballot(q[k] < PSUB);
-                const uint64_t b0 = __ballot(q[k] & 1), b1 = __ballot(q[k] & 2),
-                               b2 = __ballot(q[k] & 4);
-                const uint64_t mine = vm & (q[k] & 1 ? b0 : ~b0) & (q[k] & 2 ? b1 : ~b1) &
-                                      (q[k] & 4 ? b2 : ~b2);
-                rk[k] = (uint32_t)__popcll(mine & lt);
-                // lanes 8 k .. 8 k + 7 count slot k's rows for tile d = lane % 8
-                const uint32_t d = (uint32_t)lane & (PSUB - 1);
-                const uint64_t md = vm & (d & 1 ? b0 : ~b0) & (d & 2 ? b1 : ~b1) & (d & 4 ? b2 : ~b2);
-                if ((lane >> 3) == k) myc = (uint32_t)__popcll(md);
-            }
-            // exclusive prefix of myc over k for each d (lanes d, d + 8, ...)
-            uint32_t pre = myc;
-#pragma unroll
-            for (int sh = PSUB; sh < 64; sh <<= 1) {
-                const uint32_t o = __shfl_up(pre, sh, 64);
-                if (lane >= sh) pre += o;
-            }
-            pre -= myc;
-            uint32_t base = 0;
-            if (lane >= 64 - PSUB) base = atomicAdd(&cur[lane - (64 - PSUB)], pre + myc);
-            base = __shfl(base, 64 - PSUB + (lane & (PSUB - 1)), 64);
-            const uint32_t off = base + pre;  // first slot of (k = lane / 8, d = lane % 8)
-#pragma unroll
-            for (int k = 0; k < PV; ++k) {
-                const uint32_t o = __shfl(off, k * PSUB + (int)(q[k] & (PSUB - 1)), 64);
-                if (q[k] < PSUB) a.slab2[o + rk[k]] = val[k];
-            }
+        for (int k = 0; k < PV; ++k) {
+            const bool v = rb + k * 64 + lane < r1;
+            const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
+            q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
+            const uint32_t qend = (q[k] + 1) << PSH;
+            const uint32_t l2 = o + l > qend ? qend - o : l;  // clipped at the tile end
+            if (v && l2 < l)  // remainder [o + l2, o + l) into the next tile(s)
+                a.cross[atomicAdd(a.ncross, 1u)] = ((bin0 + o + l2) << 32) | (bin0 + o + l);
+            val[k] = ((o - (q[k] << PSH)) << PLENB) | l2;
+            // rank by the 3 bits of the tile: 4 ballots, not 8
+            const uint64_t vm = __ballot(q[k] < PSUB);
+            const uint64_t b0 = __ballot(q[k] & 1), b1 = __ballot(q[k] & 2),
+                           b2 = __ballot(q[k] & 4);
+            const uint64_t mine = vm & (q[k] & 1 ? b0 : ~b0) & (q[k] & 2 ? b1 : ~b1) &
+                                  (q[k] & 4 ? b2 : ~b2);
+            rk[k] = (uint32_t)__popcll(mine & lt);
+            // lanes 8 k .. 8 k + 7 count slot k's rows for tile d = lane % 8
+            const uint32_t d = (uint32_t)lane & (PSUB - 1);
+            const uint64_t md = vm & (d & 1 ? b0 : ~b0) & (d & 2 ? b1 : ~b1) & (d & 4 ? b2 : ~b2);
+            if ((lane >> 3) == k) myc = (uint32_t)__popcll(md);
         }
+        // exclusive prefix of myc over k for each d (lanes d, d + 8, ...)
+        uint32_t pre = myc;
+#pragma unroll
+        for (int sh = PSUB; sh < 64; sh <<= 1) {
+            const uint32_t o = __shfl_up(pre, sh, 64);
+            if (lane >= sh) pre += o;
+        }
+        pre -= myc;
+        uint32_t base = 0;
+        if (lane >= 64 - PSUB) base = atomicAdd(&cur[lane - (64 - PSUB)], pre + myc);
+        base = __shfl(base, 64 - PSUB + (lane & (PSUB - 1)), 64);
+        const uint32_t off = base + pre;  // first slot of (k = lane / 8, d = lane % 8)
+        uint32_t dst[PV];
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const uint32_t o = __shfl(off, k * PSUB + (int)(q[k] & (PSUB - 1)), 64);
+            dst[k] = o + rk[k];
+        }
+        if (rb + stride < r1)
+#pragma unroll
+            for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(rb + stride + k * 64 + lane, r1 - 1)];
+#pragma unroll
+        for (int k = 0; k < PV; ++k) *(q[k] < PSUB ? a.slab2 + dst[k] : a.dummy) = val[k];
     }
 }
 

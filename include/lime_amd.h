@@ -139,6 +139,10 @@ int64_t lime_set_lower_bound(const lime_set *set, uint32_t gkey);
  * can overlap a later shard: the left halo of pairwise ops); n if none;
  * on error -(LIME_ERR_*) */
 int64_t lime_set_first_reaching(const lime_set *set, uint32_t gkey);
+/* The same for k keys at once (host arrays; one launch, one read-back):
+ * the per-shard bounds of the sharded halos. */
+int lime_set_lower_bounds(const lime_set *set, int32_t k, const uint32_t *gkeys, int64_t *out);
+int lime_set_first_reachings(const lime_set *set, int32_t k, const uint32_t *gkeys, int64_t *out);
 /* device-to-device copy of sorted rows [first, first + count) */
 int lime_set_copy_rows_device(const lime_set *set, int64_t first, int64_t count, uint32_t *d_gstart,
                               uint32_t *d_gend, uint32_t *d_row);
@@ -196,6 +200,11 @@ int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64
  * fill and checksum them with lime_intersect_fill_* / lime_intersect_checksum. */
 int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int mode,
                        lime_pairs **plan, int64_t *n_pairs);
+/* Diagnostics of a closest plan: the Jacobi rounds its cache-head fixed point
+ * ran (capped at 32; LIME_CLOSEST_MAX_ROUNDS overrides) and whether the
+ * in-order per-contig recursion finished it (same fixed point: the head
+ * function is monotone). */
+int lime_closest_rounds(const lime_pairs *plan, int32_t *rounds, int32_t *sequential);
 
 /* ------------------------------------------------------------ merge et al. */
 int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs);

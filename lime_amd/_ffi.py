@@ -69,6 +69,8 @@ SIGNATURES = {
     "lime_set_size": (i64, [vp]),
     "lime_set_lower_bound": (i64, [vp, u32]),
     "lime_set_first_reaching": (i64, [vp, u32]),
+    "lime_set_lower_bounds": (C.c_int, [vp, C.c_int32, P(u32), P(i64)]),
+    "lime_set_first_reachings": (C.c_int, [vp, C.c_int32, P(u32), P(i64)]),
     "lime_set_copy_rows_device": (C.c_int, [vp, i64, i64, vp, vp, vp]),
     "lime_result_copy_range": (C.c_int, [vp, i64, i64, P(u32), P(u32)]),
     "lime_set_device_arrays": (C.c_int, [vp, pp, pp, pp]),
@@ -77,6 +79,7 @@ SIGNATURES = {
     "lime_intersect_count_owned": (C.c_int, [vp, vp, vp, i64, i64, i64, pp, P(i64)]),
     "lime_window_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),
     "lime_closest_count": (C.c_int, [vp, vp, vp, C.c_int, pp, P(i64)]),
+    "lime_closest_rounds": (C.c_int, [vp, P(C.c_int32), P(C.c_int32)]),
     "lime_intersect_fill_device": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_fill_host": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_checksum": (C.c_int, [vp, P(u64), P(u64)]),

@@ -114,6 +114,7 @@ int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out
 int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr);
 void closest_free(ClosestPlan *pl);
 int64_t closest_total(const ClosestPlan *pl);
+int closest_rounds(const ClosestPlan *pl, bool *sequential);
 int intersect_fill(PairsPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
 int intersect_checksum(PairsPlan *pl, uint64_t *sum, uint64_t *xr);
 void intersect_free(PairsPlan *pl);
@@ -585,6 +586,47 @@ int64_t lime_set_first_reaching(const lime_set *s, uint32_t gkey) {
     return h;
 }
 
+// k searches in one launch (thread i: key i) and one read-back: the
+// sharded halos look up one bound per shard
+__global__ void k_bounds(const uint32_t *arr, int64_t n, const uint32_t *keys, int k, int upper,
+                         int64_t *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) out[i] = upper ? dev::upper_bound(arr, 0, n, keys[i]) : dev::lower_bound(arr, 0, n, keys[i]);
+}
+
+static int set_bounds(const lime_set *s, int32_t k, const uint32_t *keys, int64_t *out,
+                      bool reaching) {
+    if (!s || k < 0 || (k > 0 && (!keys || !out))) return fail(LIME_ERR_ARG, "bad bounds arguments");
+    if (k == 0) return LIME_OK;
+    lime_ctx *ctx = s->ctx;
+    hipSetDevice(ctx->device);
+    if (s->n == 0) {
+        for (int i = 0; i < k; ++i) out[i] = 0;
+        return LIME_OK;
+    }
+    if (reaching) LIME_TRY(build_prefix_max(ctx, s));
+    uint32_t *d_keys = nullptr;
+    int64_t *d_out = nullptr;
+    LIME_TRY(alloc(ctx, &d_keys, (size_t)k));
+    PoolGuard<uint32_t> g0{ctx, d_keys};
+    LIME_TRY(alloc(ctx, &d_out, (size_t)k));
+    PoolGuard<int64_t> g1{ctx, d_out};
+    LIME_HIP(hipMemcpyAsync(d_keys, keys, 4 * (size_t)k, hipMemcpyHostToDevice, S(ctx)));
+    hipLaunchKernelGGL(k_bounds, dim3(blocks_for(k, 64)), dim3(64), 0, S(ctx),
+                       (const uint32_t *)(reaching ? s->pmax : s->gs), s->n,
+                       (const uint32_t *)d_keys, (int)k, reaching ? 1 : 0, d_out);
+    LIME_HIP(hipGetLastError());
+    return read_back(ctx, out, d_out, 8 * (size_t)k);
+}
+
+int lime_set_lower_bounds(const lime_set *s, int32_t k, const uint32_t *gkeys, int64_t *out) {
+    return set_bounds(s, k, gkeys, out, false);
+}
+
+int lime_set_first_reachings(const lime_set *s, int32_t k, const uint32_t *gkeys, int64_t *out) {
+    return set_bounds(s, k, gkeys, out, true);
+}
+
 int lime_set_copy_rows_device(const lime_set *s, int64_t first, int64_t count, uint32_t *d_gs,
                               uint32_t *d_ge, uint32_t *d_row) {
     if (!s || first < 0 || count < 0 || first + count > s->n)
@@ -702,6 +744,15 @@ int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int 
     p->closest = cl;
     *plan = p;
     if (n_pairs) *n_pairs = closest_total(cl);
+    return LIME_OK;
+}
+
+int lime_closest_rounds(const lime_pairs *plan, int32_t *rounds, int32_t *sequential) {
+    if (!plan || !plan->closest) return fail(LIME_ERR_ARG, "not a closest plan");
+    bool seq = false;
+    const int r = closest_rounds(plan->closest, &seq);
+    if (rounds) *rounds = r;
+    if (sequential) *sequential = seq ? 1 : 0;
     return LIME_OK;
 }
 

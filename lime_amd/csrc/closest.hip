@@ -58,12 +58,14 @@ struct ClosestPlan {
     uint32_t *deg = nullptr;   // directory of eg
     int64_t nb = 0;            // directory entries - 1
     int64_t total = 0;
-    int rounds = 0;            // cache-head rounds until the fixed point
+    int rounds = 0;            // cache-head rounds run (Jacobi, capped)
+    bool sequential = false;   // the in-order recursion finished the chain
 };
 
 namespace {
 
 constexpr int CB = 256;
+constexpr int MAX_ROUNDS = 32;  // Jacobi cache-head rounds before the in-order recursion
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int OCAP = 4096;  // contig offsets staged in LDS
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -354,6 +356,35 @@ __global__ __launch_bounds__(CB) void k_prune_round(Lefts L, Rights R, State s,
     if (nv != cur) atomicOr(changed, 1u);
 }
 
+// The same fixed point in order, one thread per contig: F_i is monotone in
+// its argument (the first hit at or after x), so the recursion p_i =
+// max(p_i, F_i(p_{i-1})) taken left to right reaches the rounds' least fixed
+// point.  Used past the round cap: an adversarial chain needs O(n) rounds of
+// the full grid, the recursion O(n log n) work.  A contig's first left starts
+// from r0 (every earlier contig's heads lie below it), so contigs are
+// independent.
+__global__ __launch_bounds__(CB) void k_seq_prune(Lefts L, Rights R, State s,
+                                                  const uint32_t *__restrict__ lb,
+                                                  const uint32_t *__restrict__ jp,
+                                                  const uint32_t *__restrict__ dd,
+                                                  uint32_t *__restrict__ p) {
+    const int c = blockIdx.x * CB + threadIdx.x;
+    if (c >= L.nc) return;
+    const int64_t r0 = L.rb[c], i0 = lb[c], i1 = lb[c + 1];
+    int64_t prev = r0;
+    for (int64_t i = i0; i < i1; ++i) {
+        int64_t v = p[i];
+        const uint32_t D = dd[i];
+        if (D != NONE) {
+            const int64_t f = near_from(R, L.gs[i], L.ge[i], D, s.A[i], jp[i], max(prev, r0),
+                                        false);
+            v = max(v, f);
+            p[i] = (uint32_t)v;
+        }
+        prev = v;
+    }
+}
+
 // SingleClosestSingleOverlap (Closest.scala:216-268): its advance also stops
 // inside the covering zone where the covered length drops, and its prune
 // drops covering rows shorter than a covering current closest.  Those stops
@@ -620,7 +651,10 @@ void closest_free(ClosestPlan *pl) {
 }
 
 int64_t closest_total(const ClosestPlan *pl) { return pl->total; }
-int closest_rounds(const ClosestPlan *pl) { return pl->rounds; }
+int closest_rounds(const ClosestPlan *pl, bool *sequential) {
+    if (sequential) *sequential = pl->sequential;
+    return pl->rounds;
+}
 
 namespace {
 
@@ -800,8 +834,15 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, Clo
         // cache head: prefix max of the fresh heads, then rounds to the fixed point
         CL_TRY(prefix_max_u32(ctx, P, pl->pp, nl));
     }
+    // Jacobi rounds (each a full-grid pass + one read-back) up to a cap --
+    // one round sufficed on every input measured -- then the in-order
+    // recursion finishes the chain (k_seq_prune)
+    const char *ev = getenv("LIME_CLOSEST_MAX_ROUNDS");  // (tests force the recursion)
+    const int env_cap = ev ? atoi(ev) : -1;
+    const int64_t cap = env_cap >= 0 ? env_cap : MAX_ROUNDS;
     uint32_t *cur = pl->pp, *nxt = p2;
-    for (int64_t r = 0; mode == 0 && r <= nl; ++r) {
+    bool done = mode != 0;
+    for (int64_t r = 0; !done && r < cap; ++r) {
         LIME_HIP(hipMemsetAsync(changed, 0, sizeof(unsigned int), S(ctx)));
         hipLaunchKernelGGL(k_prune_round, dim3(gl), dim3(CB), 0, S(ctx), L, R, s,
                            (const uint32_t *)pl->jp, (const uint32_t *)pl->dd,
@@ -811,11 +852,18 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, Clo
         LIME_TRY(read_back(ctx, &ch, changed, sizeof(ch)));
         std::swap(cur, nxt);
         ++pl->rounds;
-        if (!ch) break;
+        done = !ch;
     }
     if (cur != pl->pp)
         LIME_HIP(hipMemcpyAsync(pl->pp, cur, sizeof(uint32_t) * (size_t)nl,
                                 hipMemcpyDeviceToDevice, S(ctx)));
+    if (!done && nl > 0) {
+        pl->sequential = true;
+        hipLaunchKernelGGL(k_seq_prune, dim3(blocks_for(nc, CB)), dim3(CB), 0, S(ctx), L, R, s,
+                           (const uint32_t *)lbd, (const uint32_t *)pl->jp,
+                           (const uint32_t *)pl->dd, pl->pp);
+        LIME_HIP(hipGetLastError());
+    }
     // output counts and offsets
     uint64_t *cnt, *tot;
     CL_TRY(sc.get(&cnt, (size_t)nl));

@@ -132,6 +132,23 @@ class IntervalSet:
             check(int(-r))
         return int(r)
 
+    def lower_bounds(self, gkeys):
+        """lower_bound of every key in one launch and one read-back"""
+        return self._bounds(_lib().lime_set_lower_bounds, gkeys)
+
+    def first_reachings(self, gkeys):
+        """first_reaching of every key in one launch and one read-back"""
+        return self._bounds(_lib().lime_set_first_reachings, gkeys)
+
+    def _bounds(self, fn, gkeys):
+        k = len(gkeys)
+        if k == 0:
+            return []
+        keys = (C.c_uint32 * k)(*[int(x) for x in gkeys])
+        out = (i64 * k)()
+        check(fn(self._h, k, keys, out))
+        return list(out)
+
     def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
         check(_lib().lime_set_copy_rows_device(self._h, int(first), int(count), d_gs, d_ge,
                                                d_row))
@@ -234,6 +251,13 @@ class Pairs:
 
     def fill_device(self, first, count, d_out):
         check(_lib().lime_intersect_fill_device(self._h, first, count, d_out))
+
+    def closest_rounds(self):
+        """closest plans: (Jacobi rounds run, whether the in-order recursion
+        finished the cache-head fixed point)"""
+        r, q = C.c_int32(), C.c_int32()
+        check(_lib().lime_closest_rounds(self._h, C.byref(r), C.byref(q)))
+        return r.value, bool(q.value)
 
     def checksum(self):
         s, x = u64(), u64()

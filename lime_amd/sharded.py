@@ -92,9 +92,11 @@ class ShardStep:
         ends = ends.tolist()
         out = []
         for S in sets:
-            # rows of mine that shard r < me needs: gs < ends[r]
-            counts = [S.lower_bound(min(ends[r], 0xFFFFFFFF)) if r < me and ends[r] > 0 else 0
-                      for r in range(w)]
+            # rows of mine that shard r < me needs: gs < ends[r] (one batched
+            # search for every earlier shard)
+            ask = [r for r in range(w) if r < me and ends[r] > 0]
+            got = dict(zip(ask, S.lower_bounds([min(ends[r], 0xFFFFFFFF) for r in ask])))
+            counts = [got.get(r, 0) for r in range(w)]
             c = max(counts) if counts else 0
             pre = [self._i32(c) for _ in range(3)]
             if c:
@@ -123,11 +125,11 @@ class ShardStep:
         end passes split[r] (a superset of the rows overlapping r's range;
         extra rows overlap nothing there).  Device rows, in order."""
         w, me = self.world, self.rank
-        counts, first = [], []
-        for r in range(w):
-            f = S.first_reaching(min(self.splits[r], 0xFFFFFFFF)) if r > me else S.n
-            first.append(f)
-            counts.append(S.n - f)
+        later = list(range(me + 1, w))
+        got = dict(zip(later, S.first_reachings([min(self.splits[r], 0xFFFFFFFF)
+                                                 for r in later])))
+        first = [got.get(r, S.n) for r in range(w)]
+        counts = [S.n - f for f in first]
         f0 = min(first) if first else S.n
         c = S.n - f0
         suf = [self._i32(c) for _ in range(3)]

@@ -379,3 +379,44 @@ def test_gpu_single_overlap_random(ctx):
         sa = rng.integers(0, 4, n).astype(np.int8)
         sb = rng.integers(0, 4, n).astype(np.int8)
         assert _gpu_vs_oracle(ctx, _space(3, 40 * n), A, sa, B, sb, mode=1) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["0", "1"])
+def test_gpu_sequential_fixed_point(ctx, monkeypatch, cap):
+    # past the Jacobi round cap the in-order per-contig recursion finishes the
+    # cache-head chain (an adversarial chain needs O(n) rounds);
+    # forcing it from round 0 or 1 must give the oracle's answer
+    monkeypatch.setenv("LIME_CLOSEST_MAX_ROUNDS", cap)
+    seq = 0
+    for seed in range(60):
+        nc, A, sa, B, sb = _case(seed)
+        sp = _space(nc, 6000)
+        a = ctx.set_from_host_stranded(sp, *A, sa)
+        b = ctx.set_from_host_stranded(sp, *B, sb)
+        plan = ctx.closest(a, b, 0)
+        rounds, used = plan.closest_rounds()
+        assert rounds <= int(cap)
+        seq += used
+        _gpu_vs_oracle(ctx, sp, A, sa, B, sb)
+    rng = np.random.default_rng(5)
+    n = 100000
+    A, B = random_sets(rng, n, n, n_contigs=3, contig_len=40 * n, max_len=3000,
+                       zero_frac=0.05, dup_frac=0.05, book_frac=0.05)
+    s_a = rng.integers(0, 4, n).astype(np.int8)
+    s_b = rng.integers(0, 4, n).astype(np.int8)
+    assert _gpu_vs_oracle(ctx, _space(3, 40 * n), A, s_a, B, s_b) > 0
+    assert seq == 60 if cap == "0" else seq >= 0
+
+
+@pytest.mark.gpu
+def test_gpu_rounds_recorded(ctx):
+    rng = np.random.default_rng(6)
+    n = 50000
+    A, B = random_sets(rng, n, n, n_contigs=3, contig_len=40 * n, max_len=3000)
+    s_a = np.zeros(n, np.int8)
+    sp = _space(3, 40 * n)
+    plan = ctx.closest(ctx.set_from_host_stranded(sp, *A, s_a),
+                       ctx.set_from_host_stranded(sp, *B, s_a), 0)
+    rounds, used = plan.closest_rounds()
+    assert 1 <= rounds <= 32 and not used

@@ -40,6 +40,9 @@ class FakeSet:
     def lower_bound(self, key):
         return int(np.searchsorted(self.gs, key, "left"))
 
+    def lower_bounds(self, keys):
+        return [self.lower_bound(k) for k in keys]
+
     def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
         for src, dst in ((self.gs, d_gs), (self.ge, d_ge), (self.row, d_row)):
             a = np.ascontiguousarray(src[first:first + count], dtype=np.uint32)

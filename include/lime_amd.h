@@ -205,6 +205,14 @@ int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int 
  * in-order per-contig recursion finished it (same fixed point: the head
  * function is monotone). */
 int lime_closest_rounds(const lime_pairs *plan, int32_t *rounds, int32_t *sequential);
+/* closest over a genome cut into several spaces (spans >= 2^32: the host
+ * splits the contigs, in order, into spaces below 2^32).  The reference's
+ * sweep carries its liveness across contigs (a contig's lefts are reached
+ * only from the end of the previous contig's rights), so the spaces chain:
+ * alive_in = 1 for the first space, then the previous call's *alive_out. */
+int lime_closest_count_chained(lime_ctx *ctx, const lime_set *a, const lime_set *b, int mode,
+                               int32_t alive_in, int32_t *alive_out, lime_pairs **plan,
+                               int64_t *n_pairs);
 
 /* ------------------------------------------------------------ merge et al. */
 int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs);

@@ -80,6 +80,8 @@ SIGNATURES = {
     "lime_window_count": (C.c_int, [vp, vp, vp, i64, pp, P(i64)]),
     "lime_closest_count": (C.c_int, [vp, vp, vp, C.c_int, pp, P(i64)]),
     "lime_closest_rounds": (C.c_int, [vp, P(C.c_int32), P(C.c_int32)]),
+    "lime_closest_count_chained": (C.c_int, [vp, vp, vp, C.c_int, C.c_int32, P(C.c_int32), pp,
+                                             P(i64)]),
     "lime_intersect_fill_device": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_fill_host": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_checksum": (C.c_int, [vp, P(u64), P(u64)]),

@@ -108,8 +108,8 @@ int format_bed(lime_ctx *ctx, const std::vector<uint32_t> &off,
                const uint32_t *ge, const uint32_t *extra, char *out, int64_t cap,
                int64_t *total_len);
 struct ClosestPlan;
-int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode,
-                 ClosestPlan **out);
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, bool alive_in,
+                 bool *alive_out, ClosestPlan **out);
 int closest_fill(ClosestPlan *pl, int64_t first, int64_t count, lime_pair *d_out);
 int closest_checksum(ClosestPlan *pl, uint64_t *sum, uint64_t *xr);
 void closest_free(ClosestPlan *pl);
@@ -728,6 +728,12 @@ int lime_window_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64
 
 int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int mode,
                        lime_pairs **plan, int64_t *n_pairs) {
+    return lime_closest_count_chained(ctx, a, b, mode, 1, nullptr, plan, n_pairs);
+}
+
+int lime_closest_count_chained(lime_ctx *ctx, const lime_set *a, const lime_set *b, int mode,
+                               int32_t alive_in, int32_t *alive_out, lime_pairs **plan,
+                               int64_t *n_pairs) {
     if (!ctx || !a || !b || !plan) return fail(LIME_ERR_ARG, "bad closest arguments");
     if (!same_space(a, b)) return fail(LIME_ERR_ARG, "sets live in different coordinate spaces");
     if (mode != LIME_CLOSEST && mode != LIME_CLOSEST_SINGLE_OVERLAP)
@@ -739,7 +745,9 @@ int lime_closest_count(lime_ctx *ctx, const lime_set *a, const lime_set *b, int 
     LIME_TRY(same_ctx(ctx, b));
     hipSetDevice(ctx->device);
     ClosestPlan *cl = nullptr;
-    LIME_TRY(closest_plan(ctx, a, b, mode, &cl));
+    bool out_live = false;
+    LIME_TRY(closest_plan(ctx, a, b, mode, alive_in != 0, &out_live, &cl));
+    if (alive_out) *alive_out = out_live ? 1 : 0;
     lime_pairs *p = new lime_pairs{nullptr, ctx};
     p->closest = cl;
     *plan = p;

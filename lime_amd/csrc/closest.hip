@@ -60,6 +60,8 @@ struct ClosestPlan {
     int64_t total = 0;
     int rounds = 0;            // cache-head rounds run (Jacobi, capped)
     bool sequential = false;   // the in-order recursion finished the chain
+    bool alive_in = true;      // the sweep enters this space live (chained spaces)
+    bool alive_out = true;     // ... and leaves it live
 };
 
 namespace {
@@ -685,6 +687,8 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, Clo
     CL_TRY(alloc(ctx, &pl->off, (size_t)nl + 1));
     if (nl == 0) {
         LIME_HIP(hipMemsetAsync(pl->off, 0, sizeof(uint64_t), S(ctx)));
+        // no lefts: the sweep passes on only over a space without rights
+        pl->alive_out = pl->alive_in && nr == 0;
         return LIME_OK;
     }
     hipLaunchKernelGGL(k_bounds, dim3(blocks_for(nc + 1, CB)), dim3(CB), 0, S(ctx), B->gs, nr,
@@ -775,11 +779,11 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, Clo
         CL_TRY(read_back(ctx, lu.data(), lastU, sizeof(uint32_t) * nc));
         CL_TRY(read_back(ctx, st.data(), stuck, sizeof(unsigned long long) * nc));
         std::vector<uint8_t> lv(nc, 0);
-        bool alive = true, first = true;
+        bool alive = pl->alive_in, first = true;
         for (int32_t c = 0; c < nc; ++c) {
             if (lb[c + 1] <= lb[c]) continue;  // no lefts on c
-            if (first) {  // the sweep starts at right row 0
-                alive = rb[c] == 0;
+            if (first) {  // the sweep starts at right row 0 (of this space)
+                alive = alive && rb[c] == 0;
                 first = false;
             }
             lv[c] = alive ? 1 : 0;
@@ -788,12 +792,14 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, Clo
             const uint32_t jl =
                 (st[c] != ~0ull && last >= (st[c] >> 32)) ? (uint32_t)(st[c] & 0xffffffffu) : lu[c];
             // the next left contig is entered from the end of c's rights only,
-            // and only if no rights lie on the contigs in between
+            // and only if no rights lie on the contigs in between (the space's
+            // end included: alive_out chains a next space of contigs)
             alive = jl == rb[c + 1];
             int32_t cn = c + 1;
             while (cn < nc && lb[cn + 1] <= lb[cn]) ++cn;
-            if (alive && cn < nc) alive = rb[c + 1] == rb[cn];
+            if (alive) alive = rb[c + 1] == rb[cn];
         }
+        pl->alive_out = alive;
         LIME_HIP(hipMemcpyAsync(live, lv.data(), (size_t)nc, hipMemcpyHostToDevice, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));
     }
@@ -886,8 +892,8 @@ int plan_body(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, Clo
 
 }  // namespace
 
-int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode,
-                 ClosestPlan **out) {
+int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode, bool alive_in,
+                 bool *alive_out, ClosestPlan **out) {
     if (A->n >= (int64_t)NONE || B->n >= (int64_t)NONE)
         return fail(LIME_ERR_RANGE, "closest supports fewer than 2^32 - 1 rows per set");
     ClosestPlan *pl = new ClosestPlan();
@@ -895,11 +901,13 @@ int closest_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int mode,
     pl->A = A;
     pl->B = B;
     pl->nl = A->n;
+    pl->alive_in = alive_in;
     const int rc = plan_body(ctx, A, B, mode, pl);
     if (rc != LIME_OK) {
         closest_free(pl);
         return rc;
     }
+    if (alive_out) *alive_out = pl->alive_out;
     *out = pl;
     return LIME_OK;
 }

@@ -392,10 +392,15 @@ class Context:
         each left row, the cached right rows at the current closest's
         distance.  Both sets must be in RegionOrdering (set_from_host_stranded
         / set_from_device_stranded)."""
-        h, n = vp(), i64()
-        check(_lib().lime_closest_count(self._h, a._h, b._h, int(mode), C.byref(h),
-                                        C.byref(n)))
-        return Pairs(self, h, n.value, keep=(a, b))
+        return self.closest_chained(a, b, mode)[0]
+
+    def closest_chained(self, a, b, mode=0, alive_in=True):
+        """closest over one of several chained spaces (a genome whose span
+        needs more than one space): -> (Pairs, alive_out)"""
+        h, n, live = vp(), i64(), C.c_int32()
+        check(_lib().lime_closest_count_chained(self._h, a._h, b._h, int(mode), int(bool(alive_in)),
+                                                C.byref(live), C.byref(h), C.byref(n)))
+        return Pairs(self, h, n.value, keep=(a, b)), bool(live.value)
 
     def parse_bed(self, text):
         """Parse BED text (bytes) on the device -> DeviceBed (arrays in HBM)."""

@@ -80,14 +80,59 @@ def _rows(rdd):
     return regions, values
 
 
+# an engine space holds u32 global coordinates: its span sum(len + 1) must
+# not exceed 2^32 - 1 (lime_space_create).  Larger genomes are cut into
+# several spaces (tests lower the cap to exercise the cut).
+SPAN_CAP = 0xFFFFFFFF
+
+
+class _Genome:
+    """The contigs, in RegionOrdering (Java string order of the names), cut
+    into consecutive groups whose spans fit one engine space each.  Every
+    operator but closest is contig-local and runs group by group; closest
+    chains its sweep's liveness from group to group
+    (lime_closest_count_chained).  A genome below 2^32 is one group."""
+
+    def __init__(self, names, lengths):
+        # (engine.Space orders its contigs the same way)
+        order = sorted(range(len(names)), key=lambda i: _java_key(names[i]))
+        cap = SPAN_CAP
+        self.spaces, self.group = [], {}
+        cn, cl, span = [], [], 0
+        for i in order:
+            n, ln = names[i], int(lengths[i])
+            if ln + 1 > cap:
+                raise _ffi.LimeError(2, f"contig {n} is longer than a space can hold "
+                                        f"({cap - 1})")  # LIME_ERR_RANGE
+            if cn and span + ln + 1 > cap:
+                self.spaces.append(Space(cn, cl))
+                cn, cl, span = [], [], 0
+            self.group[n] = len(self.spaces)
+            cn.append(n)
+            cl.append(ln)
+            span += ln + 1
+        if cn or not self.spaces:
+            self.spaces.append(Space(cn, cl))
+
+    def split(self, regions, rows):
+        """rows (indices into regions) per group, in their given order"""
+        out = [[] for _ in self.spaces]
+        for i in rows:
+            try:
+                out[self.group[regions[i].referenceName]].append(i)
+            except KeyError as e:
+                raise NoSuchElementException(f"key not found: {e.args[0]}") from None
+        return out
+
+
 def _space_for(*region_lists, bounds=None):
     if bounds is not None:
-        return Space(list(bounds.keys()), [b.end for b in bounds.values()])
+        return _Genome(list(bounds.keys()), [b.end for b in bounds.values()])
     ext = {}
     for regs in region_lists:
         for r in regs:
             ext[r.referenceName] = max(ext.get(r.referenceName, 0), r.end)
-    return Space(list(ext.keys()), list(ext.values()))
+    return _Genome(list(ext.keys()), list(ext.values()))
 
 
 def _arrays(space, regions, rows):
@@ -135,24 +180,28 @@ class DistributedIntersection(_Op):
     def compute(self):
         lr, lv = _rows(self.left)
         rr, rv = _rows(self.right)
-        space = _space_for(lr, rr)
+        genome = _space_for(lr, rr)
         lg, rg = _strand_groups(lr), _strand_groups(rr)
         out = []
-        for strand, lrows in lg.items():
-            rrows = rg.get(strand)
-            if not rrows:
+        for strand, lrows_all in lg.items():
+            rrows_all = rg.get(strand)
+            if not rrows_all:
                 continue
-            A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
-            B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
-            plan = self.ctx.intersect(A, B, self.threshold)
-            pairs = plan.fill_host()
-            for p in pairs:
-                a = lrows[p["a_row"]]
-                b = rrows[p["b_row"]]
-                out.append((a, b, int(p["start"]), int(p["end"])))
-            plan.close()
-            A.close()
-            B.close()
+            for space, lrows, rrows in zip(genome.spaces, genome.split(lr, lrows_all),
+                                           genome.split(rr, rrows_all)):
+                if not lrows or not rrows:
+                    continue
+                A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
+                B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
+                plan = self.ctx.intersect(A, B, self.threshold)
+                pairs = plan.fill_host()
+                for p in pairs:
+                    a = lrows[p["a_row"]]
+                    b = rrows[p["b_row"]]
+                    out.append((a, b, int(p["start"]), int(p["end"])))
+                plan.close()
+                A.close()
+                B.close()
         # reference emission order (P = 1): left in sorted order, then cache
         # (= sorted right) order -- SetTheory.scala:181-186
         lrank, rrank = _sorted_rank(lr), _sorted_rank(rr)
@@ -173,21 +222,25 @@ class DistributedWindow(_Op):
     def compute(self):
         lr, lv = _rows(self.left)
         rr, rv = _rows(self.right)
-        space = _space_for(lr, rr)
+        genome = _space_for(lr, rr)
         lg, rg = _strand_groups(lr), _strand_groups(rr)
         out = []
-        for strand, lrows in lg.items():
-            rrows = rg.get(strand)
-            if not rrows:
+        for strand, lrows_all in lg.items():
+            rrows_all = rg.get(strand)
+            if not rrows_all:
                 continue
-            A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
-            B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
-            plan = self.ctx.window(A, B, self.threshold)
-            for p in plan.fill_host():
-                out.append((lrows[p["a_row"]], rrows[p["b_row"]]))
-            plan.close()
-            A.close()
-            B.close()
+            for space, lrows, rrows in zip(genome.spaces, genome.split(lr, lrows_all),
+                                           genome.split(rr, rrows_all)):
+                if not lrows or not rrows:
+                    continue
+                A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
+                B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
+                plan = self.ctx.window(A, B, self.threshold)
+                for p in plan.fill_host():
+                    out.append((lrows[p["a_row"]], rrows[p["b_row"]]))
+                plan.close()
+                A.close()
+                B.close()
         # P = 1 emission order: left in sorted order, then cache order
         lrank, rrank = _sorted_rank(lr), _sorted_rank(rr)
         out.sort(key=lambda t: (lrank[t[0]], rrank[t[1]]))
@@ -211,17 +264,23 @@ class SingleClosest(_Op):
     def compute(self):
         lr, lv = _rows(self.left)
         rr, rv = _rows(self.right)
-        space = _space_for(lr, rr)
-        codes = lambda regs: np.array([_STRAND_CODE[r.strand] for r in regs], np.int8)
-        A = self.ctx.set_from_host_stranded(space, *_arrays(space, lr, range(len(lr))),
-                                            codes(lr))
-        B = self.ctx.set_from_host_stranded(space, *_arrays(space, rr, range(len(rr))),
-                                            codes(rr))
-        plan = self.ctx.closest(A, B, self.MODE)
-        out = [(lr[p["a_row"]], (lv[p["a_row"]], rv[p["b_row"]])) for p in plan.fill_host()]
-        plan.close()
-        A.close()
-        B.close()
+        genome = _space_for(lr, rr)
+        codes = lambda regs, rows: np.array([_STRAND_CODE[regs[i].strand] for i in rows],
+                                            np.int8)
+        out, live = [], True
+        # one space after the other, the sweep's liveness carried across
+        for space, lrows, rrows in zip(genome.spaces, genome.split(lr, range(len(lr))),
+                                       genome.split(rr, range(len(rr)))):
+            A = self.ctx.set_from_host_stranded(space, *_arrays(space, lr, lrows),
+                                                codes(lr, lrows))
+            B = self.ctx.set_from_host_stranded(space, *_arrays(space, rr, rrows),
+                                                codes(rr, rrows))
+            plan, live = self.ctx.closest_chained(A, B, self.MODE, live)
+            out += [(lr[lrows[p["a_row"]]], (lv[lrows[p["a_row"]]], rv[rrows[p["b_row"]]]))
+                    for p in plan.fill_host()]
+            plan.close()
+            A.close()
+            B.close()
         return out
 
 
@@ -241,18 +300,22 @@ class DistributedSubtract(_Op):
     def compute(self):
         lr, lv = _rows(self.left)
         rr, rv = _rows(self.right)
-        space = _space_for(lr, rr)
+        genome = _space_for(lr, rr)
         lg, rg = _strand_groups(lr), _strand_groups(rr)
         out = []
-        for strand, lrows in lg.items():
-            rrows = rg.get(strand, [])
-            A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
-            B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
-            res = self.ctx.subtract(A, B, self.threshold, self.mode).to_host()
-            for k in range(len(res["start"])):
-                a = lrows[res["a_row"][k]]
-                b = rrows[res["b_row"][k]] if res["b_row"][k] >= 0 else None
-                out.append((a, k, b, int(res["start"][k]), int(res["end"][k])))
+        for strand, lrows_all in lg.items():
+            rrows_all = rg.get(strand, [])
+            for space, lrows, rrows in zip(genome.spaces, genome.split(lr, lrows_all),
+                                           genome.split(rr, rrows_all)):
+                if not lrows:
+                    continue
+                A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
+                B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
+                res = self.ctx.subtract(A, B, self.threshold, self.mode).to_host()
+                for k in range(len(res["start"])):
+                    a = lrows[res["a_row"][k]]
+                    b = rrows[res["b_row"][k]] if res["b_row"][k] >= 0 else None
+                    out.append((a, k, b, int(res["start"][k]), int(res["end"][k])))
         lrank = _sorted_rank(lr)
         out.sort(key=lambda t: (lrank[t[0]], t[1]))  # device order within a left row
         return [(ReferenceRegion(lr[a].referenceName, s, e, lr[a].strand),
@@ -270,27 +333,30 @@ class DistributedMerge(_Op):
         stranded set: RegionOrdering (start, end, strand) and a run break at
         every strand change, exactly the fold's overlaps test."""
         regs, vals = _rows(self.rdd)
-        space = _space_for(regs)
-        rows = list(range(len(regs)))
+        genome = _space_for(regs)
         rank = _sorted_rank(regs)
-        c, s, e = _arrays(space, regs, rows)
-        if len({r.strand for r in regs}) > 1:
-            st = np.array([_STRAND_CODE.get(r.strand, 0) for r in regs], dtype=np.int8)
-            A = self.ctx.set_from_host_stranded(space, c, s, e, st)
-        else:
-            A = self.ctx.set_from_host(space, c, s, e)
-        res = self.ctx.merge(A)
-        h = res.to_host()
-        rid = res.run_of_row(len(rows))
-        members = [[] for _ in range(len(h["start"]))]
-        for i in np.argsort(rank, kind="stable"):
-            members[rid[i]].append(i)
-        runs = [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
-                                 int(h["end"][k]), regs[members[k][0]].strand if members[k]
-                                 else "INDEPENDENT"), [vals[i] for i in members[k]])
-                for k in range(len(h["start"]))]
-        res.close()
-        A.close()
+        runs = []
+        for space, rows in zip(genome.spaces, genome.split(regs, range(len(regs)))):
+            if not rows:
+                continue
+            c, s, e = _arrays(space, regs, rows)
+            if len({regs[i].strand for i in rows}) > 1:
+                st = np.array([_STRAND_CODE.get(regs[i].strand, 0) for i in rows], dtype=np.int8)
+                A = self.ctx.set_from_host_stranded(space, c, s, e, st)
+            else:
+                A = self.ctx.set_from_host(space, c, s, e)
+            res = self.ctx.merge(A)
+            h = res.to_host()
+            rid = res.run_of_row(len(rows))
+            members = [[] for _ in range(len(h["start"]))]
+            for k in np.argsort(rank[rows], kind="stable"):
+                members[rid[k]].append(rows[k])
+            runs += [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
+                                      int(h["end"][k]), regs[members[k][0]].strand if members[k]
+                                      else "INDEPENDENT"), [vals[i] for i in members[k]])
+                     for k in range(len(h["start"]))]
+            res.close()
+            A.close()
         return runs
 
     def compute(self):
@@ -309,14 +375,15 @@ class DistributedComplement(_Op):
 
     def compute(self):
         regs, _ = _rows(self.rdd)
-        space = _space_for(bounds=self.bounds)
-        for r in regs:
-            if r.referenceName not in space.index:
-                raise NoSuchElementException(f"key not found: {r.referenceName}")
-        A = self.ctx.set_from_host(space, *_arrays(space, regs, range(len(regs))))
-        h = self.ctx.complement(space, A).to_host()
-        return [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
-                                 int(h["end"][k])), []) for k in range(len(h["start"]))]
+        genome = _space_for(bounds=self.bounds)
+        out = []
+        for space, rows in zip(genome.spaces, genome.split(regs, range(len(regs)))):
+            A = self.ctx.set_from_host(space, *_arrays(space, regs, rows))
+            h = self.ctx.complement(space, A).to_host()
+            out += [(ReferenceRegion(space.names[h["contig"][k]], int(h["start"][k]),
+                                     int(h["end"][k])), []) for k in range(len(h["start"]))]
+            A.close()
+        return out
 
 
 class _Cluster(_Op):
@@ -334,23 +401,28 @@ class _Cluster(_Op):
 
     def compute(self):
         regs, vals = _rows(self.rdd)
-        space = _space_for(regs)
+        genome = _space_for(regs)
         rank = _sorted_rank(regs)
-        c, s, e = _arrays(space, regs, list(range(len(regs))))
-        if self.STRANDED and len({r.strand for r in regs}) > 1:
-            st = np.array([_STRAND_CODE.get(r.strand, 0) for r in regs], dtype=np.int8)
-            A = self.ctx.set_from_host_stranded(space, c, s, e, st)
-        else:
-            A = self.ctx.set_from_host(space, c, s, e)
-        res = self.ctx.merge(A)
-        rid = res.run_of_row(len(regs))
-        members = [[] for _ in range(res.n)]
-        for i in np.argsort(rank, kind="stable"):
-            members[rid[i]].append(int(i))
-        res.close()
-        A.close()
-        # fold order = run order = order of each cluster's first member
-        return [(regs[m[0]], [vals[i] for i in m]) for m in members if m]
+        out = []
+        for space, rows in zip(genome.spaces, genome.split(regs, range(len(regs)))):
+            if not rows:
+                continue
+            c, s, e = _arrays(space, regs, rows)
+            if self.STRANDED and len({regs[i].strand for i in rows}) > 1:
+                st = np.array([_STRAND_CODE.get(regs[i].strand, 0) for i in rows], dtype=np.int8)
+                A = self.ctx.set_from_host_stranded(space, c, s, e, st)
+            else:
+                A = self.ctx.set_from_host(space, c, s, e)
+            res = self.ctx.merge(A)
+            rid = res.run_of_row(len(rows))
+            members = [[] for _ in range(res.n)]
+            for k in np.argsort(rank[rows], kind="stable"):
+                members[rid[k]].append(rows[k])
+            res.close()
+            A.close()
+            # fold order = run order = order of each cluster's first member
+            out += [(regs[m[0]], [vals[i] for i in m]) for m in members if m]
+        return out
 
 
 class UnstrandedCluster(_Cluster):

@@ -631,3 +631,52 @@ def test_bitset_window_end_on_bin_bound(ctx):
         got = ctx.bitset_runs(0, b).to_host()
         assert got["start"].tolist() == xs.tolist()
         assert got["end"].tolist() == xe.tolist()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_set_theory_genome_cut_into_spaces(ctx, monkeypatch, seed):
+    # a genome whose span exceeds one engine space (u32 coordinates: >= 2^32)
+    # is cut into consecutive spaces; lowering the cap cuts a small genome
+    # the same way.  Every operator must return exactly its one-space result
+    # (closest chains its sweep liveness across the cut)
+    import lime_amd.set_theory as st
+    rng = np.random.default_rng(300 + seed)
+    names = [f"chr{i}" for i in (1, 2, 3, 10, 11, 20, 7)]
+    lens = {n: int(rng.integers(5000, 20000)) for n in names}
+    only_left, only_right = names[1], names[4]
+
+    def rdd(n, side):
+        out = []
+        for i in range(n):
+            c = names[int(rng.integers(0, len(names)))]
+            if (side == "L" and c == only_right) or (side == "R" and c == only_left):
+                continue
+            s = int(rng.integers(0, lens[c] - 400))
+            e = s + int(rng.integers(0, 400))
+            strand = "INDEPENDENT" if rng.random() < 0.8 else "FORWARD"
+            out.append((st.ReferenceRegion(c, s, e, strand), f"{side}{i}"))
+        return out
+    L, R = rdd(600, "L"), rdd(500, "R")
+    Lu = [(st.ReferenceRegion(r.referenceName, r.start, r.end), v) for r, v in L]
+    Ru = [(st.ReferenceRegion(r.referenceName, r.start, r.end), v) for r, v in R]
+    bounds = {n: st.ReferenceRegion(n, 0, lens[n]) for n in names}
+    ops = [lambda: st.DistributedIntersection(L, R, ctx=ctx).compute(),
+           lambda: st.DistributedWindow(L, R, threshold=300, ctx=ctx).compute(),
+           lambda: st.DistributedSubtract(L, R, ctx=ctx).compute(),
+           lambda: st.DistributedMerge(L, ctx=ctx).compute(),
+           lambda: st.UnstrandedCluster(L, ctx=ctx).compute(),
+           lambda: st.StrandedCluster(L, ctx=ctx).compute(),
+           lambda: st.SingleClosest(Lu, Ru, ctx=ctx).compute(),
+           lambda: st.SingleClosestSingleOverlap(Lu, Ru, ctx=ctx).compute(),
+           lambda: st.DistributedComplement(L, referenceNameBounds=bounds, ctx=ctx).compute()]
+    one = [op() for op in ops]
+    assert len(st._space_for([r for r, _ in L], [r for r, _ in R]).spaces) == 1
+    monkeypatch.setattr(st, "SPAN_CAP", 26000)
+    assert len(st._space_for([r for r, _ in L], [r for r, _ in R]).spaces) >= 3
+    cut = [op() for op in ops]
+    for k, (x, y) in enumerate(zip(one, cut)):
+        assert x == y, k
+    assert all(len(x) for x in one)
+    with pytest.raises(LimeError):
+        monkeypatch.setattr(st, "SPAN_CAP", 1000)  # every contig is longer
+        ops[0]()

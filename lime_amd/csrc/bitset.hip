@@ -685,8 +685,44 @@ __device__ __forceinline__ void events_of(uint64_t x, uint64_t prev, uint64_t &s
     en = ~x & sh;
 }
 
+// NOT within contigs: clear the pad bits and every bit past the window
+__device__ __forceinline__ uint64_t not_mask(const OpArgs &a, int64_t w, uint64_t x,
+                                             const uint32_t *s_pad, int npad) {
+    const int64_t b0 = (a.word0 + w) * 64;
+    if (b0 + 64 > a.span) {
+        const int64_t keep = a.span - b0;
+        x &= keep <= 0 ? 0ull : (keep >= 64 ? ~0ull : ((1ull << keep) - 1));
+    }
+    for (int p = 0; p < npad; ++p) {
+        const int64_t d = (int64_t)s_pad[p] - b0;
+        if (d >= 0 && d < 64) x &= ~(1ull << d);
+    }
+    return x;
+}
+
+// word pairs (w, w + 1), w = w0 + 2 (t + j BB): 16-B loads, all issued
+// before any is used (0 past the window)
+constexpr int SJ = BT / (2 * BB);
+__device__ __forceinline__ void load_pairs(const uint64_t *__restrict__ src, int64_t w0,
+                                           int64_t nw, uint64_t (&x0)[SJ], uint64_t (&x1)[SJ]) {
+#pragma unroll
+    for (int j = 0; j < SJ; ++j) {
+        const int64_t w = w0 + 2 * (threadIdx.x + (int64_t)j * BB);
+        if (w + 1 < nw) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(src + w);
+            x0[j] = v.x;
+            x1[j] = v.y;
+        } else {
+            x0[j] = w < nw ? src[w] : 0ull;
+            x1[j] = 0ull;
+        }
+    }
+}
+
 // Stage op(words) of tile [w0, w0 + BT) plus the word before it into LDS
 // (img[0] = word w0 - 1).  NOT clears pad bits and bits beyond the span.
+// Every operand's 16 words per thread are loaded as 8 independent 16-B
+// loads, combined in registers, then stored to LDS once.
 __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned long long *img,
                                            uint32_t *s_pad, int *s_npad) {
     if (a.op == 1 && threadIdx.x == 0) {
@@ -696,26 +732,40 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
         for (; c < a.nc && (int64_t)a.pad[c] < hi && np < MAXPAD; ++c) s_pad[np++] = a.pad[c];
         *s_npad = np;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i <= BT; i += BB) {
-        const int64_t w = w0 - 1 + i;
-        uint64_t x = 0;
-        if (w >= 0 && w < a.n_words) {
-            x = op_raw(a, w);
-            if (a.op == 1) {
-                const int64_t b0 = (a.word0 + w) * 64;
-                if (b0 + 64 > a.span) {
-                    const int64_t keep = a.span - b0;
-                    x &= keep <= 0 ? 0ull : (keep >= 64 ? ~0ull : ((1ull << keep) - 1));
-                }
-                for (int p = 0; p < *s_npad; ++p) {
-                    const int64_t d = (int64_t)s_pad[p] - b0;
-                    if (d >= 0 && d < 64) x &= ~(1ull << d);
-                }
-            }
+    const int64_t nw = a.n_words;
+    uint64_t x0[SJ], x1[SJ];
+    load_pairs(a.w[0], w0, nw, x0, x1);
+    const int nops = a.op == 4 ? a.k : (a.op >= 2 ? 2 : 1);
+    for (int i = 1; i < nops; ++i) {
+        uint64_t y0[SJ], y1[SJ];
+        load_pairs(a.w[i], w0, nw, y0, y1);
+#pragma unroll
+        for (int j = 0; j < SJ; ++j) {
+            x0[j] &= a.op == 3 ? ~y0[j] : y0[j];
+            x1[j] &= a.op == 3 ? ~y1[j] : y1[j];
         }
-        img[i] = x;
     }
+    // the word before the tile (its events' left neighbour)
+    uint64_t xb = 0;
+    if (threadIdx.x == 0 && w0 > 0 && w0 - 1 < nw) xb = op_raw(a, w0 - 1);
+    __syncthreads();  // s_pad
+    if (a.op == 1) {
+        const int npad = *s_npad;
+#pragma unroll
+        for (int j = 0; j < SJ; ++j) {
+            const int64_t w = w0 + 2 * (threadIdx.x + (int64_t)j * BB);
+            x0[j] = w < nw ? not_mask(a, w, ~x0[j], s_pad, npad) : 0ull;
+            x1[j] = w + 1 < nw ? not_mask(a, w + 1, ~x1[j], s_pad, npad) : 0ull;
+        }
+        if (threadIdx.x == 0 && w0 > 0 && w0 - 1 < nw) xb = not_mask(a, w0 - 1, xb, s_pad, npad);
+    }
+#pragma unroll
+    for (int j = 0; j < SJ; ++j) {
+        const int q = 2 * (threadIdx.x + j * BB);
+        img[q + 1] = x0[j];
+        img[q + 2] = x1[j];
+    }
+    if (threadIdx.x == 0) img[0] = xb;
     __syncthreads();
 }
 
@@ -795,6 +845,7 @@ __global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w,
 // the per-tile status words (flag in bits 62-63, value below), and events
 // past the capacity only counted (the caller then falls back to two passes).
 constexpr uint64_t EV_AGG = 1ull << 62, EV_INC = 2ull << 62, EV_VAL = (1ull << 62) - 1;
+constexpr int EVCAP = 4096;  // events of a tile staged in LDS (3 blocks per CU)
 
 __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict__ status,
                                                  unsigned int *__restrict__ ticket,
@@ -807,6 +858,7 @@ __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict_
     __shared__ uint32_t scratch[BB / 64 + 1];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_excl;
+    __shared__ uint32_t s_ev[EVCAP];
     if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t tile = s_tile;
@@ -862,7 +914,12 @@ __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict_
     __syncthreads();
     const uint64_t excl = s_excl;
     if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = excl + tot;
+    // a tile's events (<= EVCAP) are staged in LDS and stored lane-consecutively
+    // (event i of the tile by lane i: runs' starts and ends as whole lines);
+    // denser tiles store each lane's own events directly
+    const bool staged = tot <= (uint32_t)EVCAP;
     uint64_t ev = excl + mine;
+    uint32_t le = mine;
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
         uint64_t st, en;
@@ -872,14 +929,27 @@ __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict_
         while (all) {
             const int b = __builtin_ctzll(all);
             all &= all - 1;
-            if ((int64_t)ev < cap_events) {
-                const uint32_t p = base + (uint32_t)b;
+            const uint32_t p = base + (uint32_t)b;
+            if (staged) {
+                s_ev[le++] = p;
+            } else if ((int64_t)ev < cap_events) {
                 if (ev & 1u)
                     rge[ev >> 1] = p;
                 else
                     rgs[ev >> 1] = p;
             }
             ++ev;
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += BB) {
+        const uint64_t e = excl + i;
+        if ((int64_t)e < cap_events) {
+            if (e & 1u)
+                rge[e >> 1] = s_ev[i];
+            else
+                rgs[e >> 1] = s_ev[i];
         }
     }
 }

@@ -41,6 +41,9 @@ struct SubArgs {
     const uint32_t *ags, *age, *arow;
     const uint32_t *bgs, *bge, *brow, *bpmax;
     const uint32_t *olo, *ocnt;
+    // RUNS (threshold <= 0): B's merge runs -- run id of every sorted row and
+    // the first sorted row of every run (nruns + 1 entries)
+    const uint32_t *brun, *rfirst;
     int64_t na;
     int64_t t;
     int mode;
@@ -88,13 +91,27 @@ __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__
     if (dev::lane_id() == 0) wstart[b] = (uint32_t)r;
 }
 
-template <bool WRITE>
+// RUNS (threshold <= 0): the inside hits are not walked one by one.  A new
+// block starts at an inside hit exactly when its start reaches the prefix
+// max end of every earlier B row -- B's merge run boundaries (earlier blocks
+// end at or before the current one's start; non-hit rows before a.s end at or
+// before a.s).  So each block is a run of B cut at hi1: seeded by the run's
+// first row (head re-picked among its same-start rows as below), ended by
+// the prefix max at its last row before hi1.  O(runs overlapping a) per left
+// row instead of O(hits): at C2's depth (~160 hits per row) one or two runs.
+template <bool WRITE, bool RUNS>
 __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     __shared__ uint32_t st_gs[WRITE ? SCAP : 1], st_ge[WRITE ? SCAP : 1];
     __shared__ uint32_t st_ar[WRITE ? SCAP : 1], st_br[WRITE ? SCAP : 1];
-    __shared__ uint32_t w_gs[BWIN], w_ge[BWIN], w_row[BWIN], w_pm[BWIN];
+    __shared__ uint32_t w_pm[BWIN];
+    // (RUNS reads starts, ends and row ids at block heads only: global memory)
+    __shared__ uint32_t w_gs[RUNS ? 1 : BWIN], w_ge[RUNS ? 1 : BWIN], w_row[RUNS ? 1 : BWIN];
+    __shared__ uint32_t w_run[RUNS ? BWIN : 1];
     __shared__ uint32_t s_whi[SUB_B / 64];
     const int64_t i = (int64_t)blockIdx.x * SUB_B + threadIdx.x;
+    // RUNS write pass: a block without records has nothing to do (at C2's
+    // depth nearly every block)
+    if (RUNS && WRITE && sa.off[blockIdx.x + 1] == sa.off[blockIdx.x]) return;
     // the block's hit window [wlo, whi) of B (spanning and inside hits):
     // consecutive left rows share most of it, so it is loaded once,
     // coalesced, into LDS
@@ -111,20 +128,26 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     const bool win = whi - wlo <= BWIN;
     if (win)
         for (int64_t k = threadIdx.x; k < whi - wlo; k += SUB_B) {
-            w_gs[k] = sa.bgs[wlo + k];
-            w_ge[k] = sa.bge[wlo + k];
-            w_row[k] = sa.brow[wlo + k];
             w_pm[k] = sa.bpmax[wlo + k];
+            if (RUNS) {
+                w_run[k] = sa.brun[wlo + k];
+            } else {
+                w_gs[k] = sa.bgs[wlo + k];
+                w_ge[k] = sa.bge[wlo + k];
+                w_row[k] = sa.brow[wlo + k];
+            }
         }
     __syncthreads();
     // B's arrays at row j, from the window when staged
-    auto Bgs = [&](int64_t j) { return win ? w_gs[j - wlo] : sa.bgs[j]; };
-    auto Bge = [&](int64_t j) { return win ? w_ge[j - wlo] : sa.bge[j]; };
-    auto Brow = [&](int64_t j) { return win ? w_row[j - wlo] : sa.brow[j]; };
+    auto Bgs = [&](int64_t j) { return win && !RUNS ? w_gs[j - wlo] : sa.bgs[j]; };
+    auto Bge = [&](int64_t j) { return win && !RUNS ? w_ge[j - wlo] : sa.bge[j]; };
+    auto Brow = [&](int64_t j) { return win && !RUNS ? w_row[j - wlo] : sa.brow[j]; };
+    auto Bpm = [&](int64_t j) { return win && j >= wlo ? w_pm[j - wlo] : sa.bpmax[j]; };
+    auto Brun = [&](int64_t j) { return RUNS ? (win && j >= wlo ? w_run[j - wlo] : sa.brun[j]) : 0u; };
     // the block's output window (write pass): staged in LDS when it fits
     int64_t bbase = 0, bend = 0;
     bool staged = false;
-    if (WRITE) {
+    if (WRITE && !RUNS) {
         const int64_t first = (int64_t)blockIdx.x * SUB_B;
         const int64_t last = min(first + SUB_B, sa.na);
         bbase = (int64_t)sa.off[first];
@@ -135,11 +158,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     if (i < sa.na) as = sa.ags[i], ae = sa.age[i], ar = sa.arow[i];
     const int64_t t = sa.t;
     int64_t pos = 0, end = 0;
-    if (WRITE && i < sa.na) {
+    if (WRITE && !RUNS && i < sa.na) {
         pos = (int64_t)sa.off[i];
         end = (int64_t)sa.off[i + 1];
     }
-    uint64_t n_out = 0;
     auto emit = [&](uint32_t s, uint32_t e, uint32_t br, int64_t at) {
         if (WRITE) {
             if (staged) {
@@ -156,6 +178,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             }
         }
     };
+    // the fold of one left row; do_emit = false only counts its records
+    auto fold = [&](bool do_emit) -> uint64_t {
+    const bool wr = WRITE && do_emit;
+    uint64_t n_out = 0;
     bool any = false;
     if (i < sa.na && !(t >= 1 && (int64_t)(ae - as) < t)) {
         const int64_t lo1 = sa.olo[i];
@@ -201,8 +227,66 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                 }
             }
         }
+        // close the current block (bs, be, bh): its records
+        auto close_block = [&]() {
+            if (sa.mode == LIME_SUBTRACT_LIME) {
+                uint32_t r = (bs > as) + (ae > be);
+                if (wr) {
+                    int64_t at = end - (int64_t)cum - r;
+                    if (bs > as) emit(as, bs, bh, at++);
+                    if (ae > be) emit(be, ae, bh, at++);
+                }
+                cum += r;
+            } else {
+                if (bs > setpos) {
+                    if (wr) emit(setpos, bs, bh, pos + (int64_t)cum);
+                    ++cum;
+                }
+                if (be > setpos) setpos = be;
+            }
+        };
+        if (RUNS) {
+            int64_t j = lo1;
+            // the spanning block goes on through the inside rows of its run
+            if (any && j < hi1 && Brun(j) == Brun(lo1 - 1)) {
+                const int64_t nx = min((int64_t)sa.rfirst[Brun(j) + 1], hi1);
+                be = max(be, Bpm(nx - 1));
+                j = nx;
+            }
+            while (j < hi1) {
+                const uint32_t r = Brun(j);
+                const int64_t nx = min((int64_t)sa.rfirst[r + 1], hi1);
+                const uint32_t gs = Bgs(j), ge = Bge(j), row = Brow(j);
+                if (!any) {  // foldLeft(List(head)): the head is folded against itself
+                    any = true;
+                    if (ge == gs) {  // a zero-width head closes a duplicate of itself
+                        bs = be = gs;
+                        bh = row;
+                        bhe = ge;
+                        close_block();
+                    }
+                } else {
+                    close_block();
+                }
+                bs = gs;
+                be = ge;
+                bh = row;
+                bhe = ge;
+                // the head among the run's same-start non-empty hits: min (end, row)
+                if (bhe > bs)
+                    for (int64_t k = j + 1; k < nx && Bgs(k) == bs; ++k) {
+                        const uint32_t e2 = Bge(k), r2 = Brow(k);
+                        if (e2 < bhe || (e2 == bhe && r2 < bh)) {
+                            bh = r2;
+                            bhe = e2;
+                        }
+                    }
+                be = max(be, Bpm(nx - 1));
+                j = nx;
+            }
+        }
         // four hits per step: their loads are independent of the fold state
-        for (int64_t j4 = lo1; j4 < hi1; j4 += 4) {
+        for (int64_t j4 = lo1; !RUNS && j4 < hi1; j4 += 4) {
             uint32_t vg[4], ve[4], vr[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -236,7 +320,7 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                 // close block (bs, be, bh)
                 if (sa.mode == LIME_SUBTRACT_LIME) {
                     uint32_t r = (bs > as) + (ae > be);
-                    if (WRITE) {
+                    if (wr) {
                         int64_t at = end - (int64_t)cum - r;
                         if (bs > as) emit(as, bs, bh, at++);
                         if (ae > be) emit(be, ae, bh, at++);
@@ -244,7 +328,7 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                     cum += r;
                 } else {
                     if (bs > setpos) {
-                        if (WRITE) emit(setpos, bs, bh, pos + (int64_t)cum);
+                        if (wr) emit(setpos, bs, bh, pos + (int64_t)cum);
                         ++cum;
                     }
                     if (be > setpos) setpos = be;
@@ -259,7 +343,7 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         if (any) {  // close the last block
             if (sa.mode == LIME_SUBTRACT_LIME) {
                 uint32_t r = (bs > as) + (ae > be);
-                if (WRITE) {
+                if (wr) {
                     int64_t at = end - (int64_t)cum - r;
                     if (bs > as) emit(as, bs, bh, at++);
                     if (ae > be) emit(be, ae, bh, at++);
@@ -267,12 +351,12 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                 cum += r;
             } else {
                 if (bs > setpos) {
-                    if (WRITE) emit(setpos, bs, bh, pos + (int64_t)cum);
+                    if (wr) emit(setpos, bs, bh, pos + (int64_t)cum);
                     ++cum;
                 }
                 if (be > setpos) setpos = be;
                 if (ae > setpos) {
-                    if (WRITE) emit(setpos, ae, bh, pos + (int64_t)cum);
+                    if (wr) emit(setpos, ae, bh, pos + (int64_t)cum);
                     ++cum;
                 }
             }
@@ -280,12 +364,40 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         }
     }
     if (i < sa.na && !any) {
-        if (WRITE) emit(as, ae, 0xffffffffu, pos);
+        if (wr) emit(as, ae, 0xffffffffu, pos);
         n_out = 1;
     }
-    if (!WRITE) {
-        if (i < sa.na) sa.count[i] = n_out;
-        return;
+    return n_out;
+    };
+    if (!RUNS) {
+        const uint64_t n_out = fold(WRITE);
+        if (!WRITE) {
+            if (i < sa.na) sa.count[i] = n_out;
+            return;
+        }
+    } else {
+        // RUNS: per-block totals (count pass); the write pass counts again
+        // (O(runs) per row) and places its rows by a block scan
+        __shared__ uint64_t s_part[SUB_B / 64];
+        const uint64_t n_out = fold(false);
+        const uint64_t inc = dev::wave_inclusive_sum(n_out);
+        if (dev::lane_id() == 63) s_part[threadIdx.x / 64] = inc;
+        __syncthreads();
+        uint64_t before = 0, total = 0;
+        for (int w = 0; w < SUB_B / 64; ++w) {
+            if (w < (int)(threadIdx.x / 64)) before += s_part[w];
+            total += s_part[w];
+        }
+        if (!WRITE) {
+            if (threadIdx.x == 0) sa.count[blockIdx.x] = total;
+            return;
+        }
+        bbase = (int64_t)sa.off[blockIdx.x];
+        bend = bbase + (int64_t)total;
+        staged = total <= (uint64_t)SCAP;
+        pos = bbase + (int64_t)(before + inc - n_out);
+        end = pos + (int64_t)n_out;
+        fold(true);
     }
     if (staged) {  // the block's records, lane-consecutive
         __syncthreads();
@@ -299,7 +411,17 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     }
 }
 
+// first sorted row of every run (rfirst[nruns] = n)
+__global__ __launch_bounds__(256) void k_run_first(const uint32_t *__restrict__ run, int64_t n,
+                                                   int64_t nruns, uint32_t *__restrict__ rfirst) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n && (j == 0 || run[j] != run[j - 1])) rfirst[run[j]] = (uint32_t)j;
+    if (j == 0) rfirst[nruns] = (uint32_t)n;
+}
+
 }  // namespace
+
+int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
 
 int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold, int mode,
                  lime_result *res) {
@@ -346,15 +468,40 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.count = cnt;
     sa.off = off;
     sa.ogs = sa.oge = sa.oar = sa.obr = nullptr;
-    if (B->n == 0) {
-        // every left row survives whole; the walk sees no candidates
-        sa.bpmax = B->pmax;
+    sa.brun = sa.rfirst = nullptr;
+    // threshold <= 0: blocks are B's merge runs (k_subtract<_, true>); the
+    // runs of a stranded set also break at strand changes, so those walk
+    const bool runs = threshold <= 0 && B->n > 0 && B->strand_in == nullptr;
+    lime_result mb;
+    mb.ctx = ctx;
+    uint32_t *rfirst = nullptr;
+    PoolGuard<uint32_t> g1{ctx, mb.run_of_sorted};
+    PoolGuard<uint32_t> g2{ctx, mb.gs};
+    PoolGuard<uint32_t> g3{ctx, mb.ge};
+    PoolGuard<uint32_t> g4{ctx, rfirst};
+    if (runs) {
+        LIME_TRY(merge_runs(ctx, B, &mb, true));
+        LIME_TRY(alloc(ctx, &rfirst, (size_t)mb.n + 1));
+        hipLaunchKernelGGL(k_run_first, dim3(blocks_for(B->n, 256)), dim3(256), 0, S(ctx),
+                           (const uint32_t *)mb.run_of_sorted, B->n, mb.n, rfirst);
+        LIME_HIP(hipGetLastError());
+        sa.brun = mb.run_of_sorted;
+        sa.rfirst = rfirst;
     }
-    hipLaunchKernelGGL(k_subtract<false>, dim3(blocks_for(na, SUB_B)), dim3(SUB_B), 0, S(ctx), sa);
+    auto launch = [&](bool write) {
+        const dim3 g(blocks_for(na, SUB_B)), b(SUB_B);
+        if (write && runs) hipLaunchKernelGGL((k_subtract<true, true>), g, b, 0, S(ctx), sa);
+        else if (write) hipLaunchKernelGGL((k_subtract<true, false>), g, b, 0, S(ctx), sa);
+        else if (runs) hipLaunchKernelGGL((k_subtract<false, true>), g, b, 0, S(ctx), sa);
+        else hipLaunchKernelGGL((k_subtract<false, false>), g, b, 0, S(ctx), sa);
+    };
+    launch(false);
     LIME_HIP(hipGetLastError());
-    LIME_TRY(scan_exclusive_u64(ctx, cnt, off, na, off + na));
+    // counts per left row (walk), per 256-row block (runs)
+    const int64_t nc = runs ? nblk : na;
+    LIME_TRY(scan_exclusive_u64(ctx, cnt, off, nc, off + nc));
     uint64_t total = 0;
-    LIME_TRY(read_back(ctx, &total, off + na, sizeof(total)));
+    LIME_TRY(read_back(ctx, &total, off + nc, sizeof(total)));
     LIME_TRY(alloc(ctx, &res->gs, (size_t)total));
     LIME_TRY(alloc(ctx, &res->ge, (size_t)total));
     LIME_TRY(alloc(ctx, &res->a_row, (size_t)total));
@@ -363,7 +510,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.oge = res->ge;
     sa.oar = res->a_row;
     sa.obr = res->b_row;
-    hipLaunchKernelGGL(k_subtract<true>, dim3(blocks_for(na, SUB_B)), dim3(SUB_B), 0, S(ctx), sa);
+    launch(true);
     LIME_HIP(hipGetLastError());
     release(ctx, olo);
     release(ctx, ocnt);

@@ -680,3 +680,32 @@ def test_set_theory_genome_cut_into_spaces(ctx, monkeypatch, seed):
     with pytest.raises(LimeError):
         monkeypatch.setattr(st, "SPAN_CAP", 1000)  # every contig is longer
         ops[0]()
+
+
+def _sub_equal(res, exp):
+    og, oe = np.argsort(res["a_row"], kind="stable"), np.argsort(exp["a_row"], kind="stable")
+    for key in ("contig", "start", "end", "a_row", "b_row"):
+        assert list(res[key][og]) == list(exp[key][oe]), key
+
+
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+@pytest.mark.parametrize("t", [0, -3])
+def test_subtract_runs_path(ctx, mode, t):
+    # threshold <= 0 takes the runs path (a block = one of B's merge runs cut
+    # at the left row's end): dense ties, zero-width rows (zero-width heads
+    # duplicate their block), duplicates and book-ended rows on short
+    # contigs, then deep coverage (C2-like: ~300 hits per left row)
+    for seed in range(40):
+        rng = np.random.default_rng(1000 + seed)
+        A, B = random_sets(rng, 300, 300, n_contigs=2, contig_len=400, max_len=30,
+                           zero_frac=0.2, dup_frac=0.2, book_frac=0.3)
+        sp = space_for(2, 400)
+        res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t,
+                           mode).to_host()
+        _sub_equal(res, oracle.subtract(A, B, t, mode))
+    rng = np.random.default_rng(77)
+    A, B = random_sets(rng, 20000, 20000, n_contigs=2, contig_len=100000, max_len=3000,
+                       zero_frac=0.02, dup_frac=0.02, book_frac=0.05)
+    sp = space_for(2, 100000)
+    res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t, mode).to_host()
+    _sub_equal(res, oracle.subtract(A, B, t, mode))

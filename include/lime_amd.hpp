@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <numeric>
@@ -115,8 +116,63 @@ struct Space {
     Space(const Space &) = delete;
 };
 
+// A space holds u32 global coordinates (span sum(len + 1) <= 2^32 - 1).  A
+// larger genome is cut, in Java String order, into consecutive spaces below
+// the cap; every operator but closest is contig-local and runs space by
+// space, closest chains its sweep liveness (lime_closest_count_chained).
+// LIME_SPAN_CAP lowers the cap (tests cut small genomes the same way).
+inline int64_t span_cap() {
+    const char *e = std::getenv("LIME_SPAN_CAP");
+    const int64_t v = e ? std::atoll(e) : 0;
+    return v > 0 && v < 0xFFFFFFFFll ? v : 0xFFFFFFFFll;
+}
+
+struct Genome {
+    std::vector<std::unique_ptr<Space>> spaces;
+    std::unordered_map<std::string, int> group;
+    Genome(const std::vector<std::string> &nm, const std::vector<int64_t> &len) {
+        std::vector<const char *> p;
+        for (auto &x : nm) p.push_back(x.c_str());
+        std::vector<int32_t> rank(nm.size());
+        if (!nm.empty()) check(lime_contig_rank((int32_t)nm.size(), p.data(), rank.data()));
+        std::vector<size_t> ord(nm.size());
+        std::iota(ord.begin(), ord.end(), 0);
+        std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return rank[a] < rank[b]; });
+        const int64_t cap = span_cap();
+        std::vector<std::string> cn;
+        std::vector<int64_t> cl;
+        int64_t span = 0;
+        for (size_t i : ord) {
+            if (len[i] + 1 > cap)
+                throw Error(LIME_ERR_RANGE, "contig " + nm[i] + " is longer than a space can hold");
+            if (!cn.empty() && span + len[i] + 1 > cap) {
+                spaces.push_back(std::make_unique<Space>(cn, cl));
+                cn.clear();
+                cl.clear();
+                span = 0;
+            }
+            group[nm[i]] = (int)spaces.size();
+            cn.push_back(nm[i]);
+            cl.push_back(len[i]);
+            span += len[i] + 1;
+        }
+        if (!cn.empty() || spaces.empty()) spaces.push_back(std::make_unique<Space>(cn, cl));
+    }
+    // rows (indices into rdd) per space, in their given order
+    template <class T>
+    std::vector<std::vector<size_t>> split(const RDD<T> &rdd, const std::vector<size_t> &rows) const {
+        std::vector<std::vector<size_t>> out(spaces.size());
+        for (size_t i : rows) {
+            auto it = group.find(rdd[i].first.referenceName);
+            if (it == group.end()) throw NoSuchElement("key not found: " + rdd[i].first.referenceName);
+            out[(size_t)it->second].push_back(i);
+        }
+        return out;
+    }
+};
+
 template <class T>
-std::unique_ptr<Space> space_of(std::initializer_list<const RDD<T> *> rdds) {
+std::unique_ptr<Genome> space_of(std::initializer_list<const RDD<T> *> rdds) {
     std::map<std::string, int64_t> ext;
     for (auto *r : rdds)
         for (auto &kv : *r) {
@@ -129,7 +185,13 @@ std::unique_ptr<Space> space_of(std::initializer_list<const RDD<T> *> rdds) {
         n.push_back(kv.first);
         l.push_back(kv.second);
     }
-    return std::make_unique<Space>(n, l);
+    return std::make_unique<Genome>(n, l);
+}
+
+inline std::vector<size_t> all_rows(size_t n) {
+    std::vector<size_t> r(n);
+    std::iota(r.begin(), r.end(), 0);
+    return r;
 }
 
 struct SetHandle {
@@ -219,10 +281,12 @@ std::vector<size_t> sorted_rank(const RDD<T> &rdd) {
 namespace detail {
 // the contigs of both sides, each as long as its furthest end
 template <class T, class U>
-std::unique_ptr<Space> join_space(const RDD<T> &left, const RDD<U> &right) {
-    auto sp = space_of<T>({&left});
+std::unique_ptr<Genome> join_space(const RDD<T> &left, const RDD<U> &right) {
     std::map<std::string, int64_t> ext;
-    for (size_t c = 0; c < sp->names.size(); ++c) ext[sp->names[c]] = sp->lengths[c];
+    for (auto &kv : left) {
+        auto &e = ext[kv.first.referenceName];
+        e = std::max(e, kv.first.end);
+    }
     for (auto &kv : right) {
         auto &e = ext[kv.first.referenceName];
         e = std::max(e, kv.first.end);
@@ -233,7 +297,7 @@ std::unique_ptr<Space> join_space(const RDD<T> &left, const RDD<U> &right) {
         n.push_back(kv.first);
         l.push_back(kv.second);
     }
-    return std::make_unique<Space>(n, l);
+    return std::make_unique<Genome>(n, l);
 }
 
 struct PairHit {
@@ -247,24 +311,28 @@ struct PairHit {
 template <typename T, typename U, typename PlanFn>
 std::vector<PairHit> pair_join(const RDD<T> &left, const RDD<U> &right, Engine &eng,
                                PlanFn make_plan) {
-    auto sp = join_space(left, right);
+    auto gn = join_space(left, right);
     auto lg = strand_groups(left);
     auto rg = strand_groups(right);
     std::vector<PairHit> hits;
     for (auto &g : lg) {
         auto it = rg.find(g.first);
         if (it == rg.end()) continue;
-        SetHandle A, B;
-        upload(eng.ctx(), *sp, left, g.second, A);
-        upload(eng.ctx(), *sp, right, it->second, B);
-        lime_pairs *plan = nullptr;
-        int64_t n = 0;
-        check(make_plan(eng.ctx(), A.h, B.h, &plan, &n));
-        std::vector<lime_pair> p((size_t)n);
-        int rc = lime_intersect_fill_host(plan, 0, n, p.data());
-        lime_pairs_destroy(plan);
-        check(rc);
-        for (auto &x : p) hits.push_back({g.second[x.a_row], it->second[x.b_row], x.start, x.end});
+        auto ls = gn->split(left, g.second), rs = gn->split(right, it->second);
+        for (size_t k = 0; k < gn->spaces.size(); ++k) {
+            if (ls[k].empty() || rs[k].empty()) continue;
+            SetHandle A, B;
+            upload(eng.ctx(), *gn->spaces[k], left, ls[k], A);
+            upload(eng.ctx(), *gn->spaces[k], right, rs[k], B);
+            lime_pairs *plan = nullptr;
+            int64_t n = 0;
+            check(make_plan(eng.ctx(), A.h, B.h, &plan, &n));
+            std::vector<lime_pair> p((size_t)n);
+            int rc = lime_intersect_fill_host(plan, 0, n, p.data());
+            lime_pairs_destroy(plan);
+            check(rc);
+            for (auto &x : p) hits.push_back({ls[k][x.a_row], rs[k][x.b_row], x.start, x.end});
+        }
     }
     auto lr = sorted_rank(left);
     auto rr = sorted_rank(right);
@@ -320,24 +388,29 @@ class ClosestOp {
           eng_(eng) {}
 
     std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> compute() {
-        auto sp = detail::join_space(left_, right_);
-        std::vector<size_t> la(left_.size()), ra(right_.size());
-        for (size_t i = 0; i < la.size(); ++i) la[i] = i;
-        for (size_t i = 0; i < ra.size(); ++i) ra[i] = i;
-        detail::SetHandle A, B;
-        detail::upload(eng_.ctx(), *sp, left_, la, A, true);
-        detail::upload(eng_.ctx(), *sp, right_, ra, B, true);
-        lime_pairs *plan = nullptr;
-        int64_t n = 0;
-        check(lime_closest_count(eng_.ctx(), A.h, B.h, MODE, &plan, &n));
-        std::vector<lime_pair> p((size_t)n);
-        int rc = lime_intersect_fill_host(plan, 0, n, p.data());
-        lime_pairs_destroy(plan);
-        check(rc);
+        auto gn = detail::join_space(left_, right_);
+        auto ls = gn->split(left_, detail::all_rows(left_.size()));
+        auto rs = gn->split(right_, detail::all_rows(right_.size()));
         std::vector<std::pair<ReferenceRegion, std::pair<T, U>>> out;
-        out.reserve(p.size());
-        for (auto &x : p)
-            out.push_back({left_[x.a_row].first, {left_[x.a_row].second, right_[x.b_row].second}});
+        int32_t live = 1;  // the sweep's liveness, carried from space to space
+        for (size_t k = 0; k < gn->spaces.size(); ++k) {
+            detail::SetHandle A, B;
+            detail::upload(eng_.ctx(), *gn->spaces[k], left_, ls[k], A, true);
+            detail::upload(eng_.ctx(), *gn->spaces[k], right_, rs[k], B, true);
+            lime_pairs *plan = nullptr;
+            int64_t n = 0;
+            int32_t next = 0;
+            check(lime_closest_count_chained(eng_.ctx(), A.h, B.h, MODE, live, &next, &plan, &n));
+            live = next;
+            std::vector<lime_pair> p((size_t)n);
+            int rc = lime_intersect_fill_host(plan, 0, n, p.data());
+            lime_pairs_destroy(plan);
+            check(rc);
+            for (auto &x : p) {
+                const size_t a = ls[k][x.a_row], b = rs[k][x.b_row];
+                out.push_back({left_[a].first, {left_[a].second, right_[b].second}});
+            }
+        }
         return out;
     }
 
@@ -395,16 +468,7 @@ class DistributedSubtract {
           threshold_(threshold), mode_(mode), eng_(eng) {}
 
     std::vector<std::pair<ReferenceRegion, std::pair<T, std::optional<U>>>> compute() {
-        std::map<std::string, int64_t> ext;
-        for (auto &kv : left_) ext[kv.first.referenceName] = std::max(ext[kv.first.referenceName], kv.first.end);
-        for (auto &kv : right_) ext[kv.first.referenceName] = std::max(ext[kv.first.referenceName], kv.first.end);
-        std::vector<std::string> n;
-        std::vector<int64_t> l;
-        for (auto &kv : ext) {
-            n.push_back(kv.first);
-            l.push_back(kv.second);
-        }
-        detail::Space sp(n, l);
+        auto gn = detail::join_space(left_, right_);
         auto lg = detail::strand_groups(left_);
         auto rg = detail::strand_groups(right_);
         struct Rem { size_t a; int64_t k; int64_t b; int64_t s, e; };
@@ -412,20 +476,24 @@ class DistributedSubtract {
         for (auto &g : lg) {
             static const std::vector<size_t> none;
             auto it = rg.find(g.first);
-            const auto &rrows = it == rg.end() ? none : it->second;
-            detail::SetHandle A, B;
-            detail::upload(eng_.ctx(), sp, left_, g.second, A);
-            detail::upload(eng_.ctx(), sp, right_, rrows, B);
-            lime_result *res = nullptr;
-            int64_t cnt = 0;
-            check(lime_subtract(eng_.ctx(), A.h, B.h, threshold_, mode_, &res, &cnt));
-            std::vector<int32_t> c((size_t)cnt);
-            std::vector<int64_t> s((size_t)cnt), e((size_t)cnt), ar((size_t)cnt), br((size_t)cnt);
-            int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), ar.data(), br.data());
-            lime_result_destroy(res);
-            check(rc);
-            for (int64_t k = 0; k < cnt; ++k)
-                rem.push_back({g.second[ar[k]], k, br[k] < 0 ? -1 : (int64_t)rrows[br[k]], s[k], e[k]});
+            auto ls = gn->split(left_, g.second);
+            auto rs = gn->split(right_, it == rg.end() ? none : it->second);
+            for (size_t q = 0; q < gn->spaces.size(); ++q) {
+                if (ls[q].empty()) continue;
+                detail::SetHandle A, B;
+                detail::upload(eng_.ctx(), *gn->spaces[q], left_, ls[q], A);
+                detail::upload(eng_.ctx(), *gn->spaces[q], right_, rs[q], B);
+                lime_result *res = nullptr;
+                int64_t cnt = 0;
+                check(lime_subtract(eng_.ctx(), A.h, B.h, threshold_, mode_, &res, &cnt));
+                std::vector<int32_t> c((size_t)cnt);
+                std::vector<int64_t> s((size_t)cnt), e((size_t)cnt), ar((size_t)cnt), br((size_t)cnt);
+                int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), ar.data(), br.data());
+                lime_result_destroy(res);
+                check(rc);
+                for (int64_t k = 0; k < cnt; ++k)
+                    rem.push_back({ls[q][ar[k]], k, br[k] < 0 ? -1 : (int64_t)rs[q][br[k]], s[k], e[k]});
+            }
         }
         auto lr = detail::sorted_rank(left_);
         std::stable_sort(rem.begin(), rem.end(), [&](const Rem &x, const Rem &y) {
@@ -460,32 +528,39 @@ class DistributedMerge {
     // the SetTheory.scala:208-225 fold; mixed strands run as ONE stranded set
     // (RegionOrdering order, a run break at every strand change)
     std::vector<std::pair<ReferenceRegion, std::vector<T>>> compute() {
-        auto sp = detail::space_of<T>({&rdd_});
+        auto gn = detail::space_of<T>({&rdd_});
         auto rank = detail::sorted_rank(rdd_);
-        std::vector<size_t> all(rdd_.size());
-        std::iota(all.begin(), all.end(), 0);
-        detail::SetHandle A;
-        detail::upload(eng_.ctx(), *sp, rdd_, all, A, detail::mixed_strands(rdd_));
-        lime_result *res = nullptr;
-        int64_t cnt = 0;
-        check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
-        std::vector<int32_t> c((size_t)cnt);
-        std::vector<int64_t> s((size_t)cnt), e((size_t)cnt), rid(all.size());
-        int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), nullptr, nullptr);
-        if (rc == LIME_OK) rc = lime_result_run_of_row(res, rid.data());
-        lime_result_destroy(res);
-        check(rc);
-        std::vector<std::vector<size_t>> members((size_t)cnt);
-        std::vector<size_t> order(all);
-        std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return rank[x] < rank[y]; });
-        for (size_t m : order) members[(size_t)rid[m]].push_back(m);
+        const bool mixed = detail::mixed_strands(rdd_);
+        auto parts = gn->split(rdd_, detail::all_rows(rdd_.size()));
         std::vector<std::pair<ReferenceRegion, std::vector<T>>> out;
-        for (int64_t k = 0; k < cnt; ++k) {
-            const Strand st = members[k].empty() ? Strand::Independent
-                                                 : rdd_[members[k][0]].first.strand;
-            std::vector<T> v;
-            for (size_t m : members[k]) v.push_back(rdd_[m].second);
-            out.push_back({ReferenceRegion(sp->names[c[k]], s[k], e[k], st), std::move(v)});
+        for (size_t q = 0; q < gn->spaces.size(); ++q) {
+            const auto &rows = parts[q];
+            if (rows.empty()) continue;
+            const auto &sp = *gn->spaces[q];
+            detail::SetHandle A;
+            detail::upload(eng_.ctx(), sp, rdd_, rows, A, mixed);
+            lime_result *res = nullptr;
+            int64_t cnt = 0;
+            check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
+            std::vector<int32_t> c((size_t)cnt);
+            std::vector<int64_t> s((size_t)cnt), e((size_t)cnt), rid(rows.size());
+            int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), nullptr, nullptr);
+            if (rc == LIME_OK) rc = lime_result_run_of_row(res, rid.data());
+            lime_result_destroy(res);
+            check(rc);
+            std::vector<std::vector<size_t>> members((size_t)cnt);
+            std::vector<size_t> order(rows.size());
+            std::iota(order.begin(), order.end(), 0);
+            std::sort(order.begin(), order.end(),
+                      [&](size_t x, size_t y) { return rank[rows[x]] < rank[rows[y]]; });
+            for (size_t m : order) members[(size_t)rid[m]].push_back(rows[m]);
+            for (int64_t k = 0; k < cnt; ++k) {
+                const Strand st = members[k].empty() ? Strand::Independent
+                                                     : rdd_[members[k][0]].first.strand;
+                std::vector<T> v;
+                for (size_t m : members[k]) v.push_back(rdd_[m].second);
+                out.push_back({ReferenceRegion(sp.names[c[k]], s[k], e[k], st), std::move(v)});
+            }
         }
         return out;
     }
@@ -510,26 +585,30 @@ class ClusterOp {
         : rdd_(std::move(rdd)), pm_(std::move(partitionMap)), threshold_(threshold), eng_(eng) {}
 
     std::vector<std::pair<ReferenceRegion, std::vector<T>>> compute() {
-        auto sp = detail::space_of<T>({&rdd_});
+        auto gn = detail::space_of<T>({&rdd_});
         auto rank = detail::sorted_rank(rdd_);
-        std::vector<size_t> all(rdd_.size());
-        std::iota(all.begin(), all.end(), 0);
+        const bool mixed = STRANDED && detail::mixed_strands(rdd_);
+        auto parts = gn->split(rdd_, detail::all_rows(rdd_.size()));
         std::vector<std::vector<size_t>> clusters;  // member rows in fold order
-        if (!all.empty()) {
+        for (size_t q = 0; q < gn->spaces.size(); ++q) {
+            const auto &rows = parts[q];
+            if (rows.empty()) continue;
             detail::SetHandle A;
-            detail::upload(eng_.ctx(), *sp, rdd_, all, A, STRANDED && detail::mixed_strands(rdd_));
+            detail::upload(eng_.ctx(), *gn->spaces[q], rdd_, rows, A, mixed);
             lime_result *res = nullptr;
             int64_t cnt = 0;
             check(lime_merge(eng_.ctx(), A.h, &res, &cnt));
-            std::vector<int64_t> rid(all.size());
+            std::vector<int64_t> rid(rows.size());
             int rc = lime_result_run_of_row(res, rid.data());
             lime_result_destroy(res);
             check(rc);
-            std::vector<size_t> order(all);
+            std::vector<size_t> order(rows.size());
+            std::iota(order.begin(), order.end(), 0);
             std::sort(order.begin(), order.end(),
-                      [&](size_t x, size_t y) { return rank[x] < rank[y]; });
-            clusters.resize((size_t)cnt);
-            for (size_t m : order) clusters[(size_t)rid[m]].push_back(m);
+                      [&](size_t x, size_t y) { return rank[rows[x]] < rank[rows[y]]; });
+            const size_t base = clusters.size();
+            clusters.resize(base + (size_t)cnt);
+            for (size_t m : order) clusters[base + (size_t)rid[m]].push_back(rows[m]);
         }
         std::sort(clusters.begin(), clusters.end(),
                   [&](const std::vector<size_t> &x, const std::vector<size_t> &y) {
@@ -575,22 +654,24 @@ class DistributedComplement {
             n.push_back(kv.first);
             l.push_back(kv.second.end);
         }
-        detail::Space sp(n, l);
-        std::vector<size_t> rows(rdd_.size());
-        std::iota(rows.begin(), rows.end(), 0);
-        detail::SetHandle A;
-        detail::upload(eng_.ctx(), sp, rdd_, rows, A);  // throws NoSuchElement
-        lime_result *res = nullptr;
-        int64_t cnt = 0;
-        check(lime_complement(eng_.ctx(), sp.h, A.h, &res, &cnt));
-        std::vector<int32_t> c((size_t)cnt);
-        std::vector<int64_t> s((size_t)cnt), e((size_t)cnt);
-        int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), nullptr, nullptr);
-        lime_result_destroy(res);
-        check(rc);
+        detail::Genome gn(n, l);
+        auto parts = gn.split(rdd_, detail::all_rows(rdd_.size()));  // throws NoSuchElement
         std::vector<std::pair<ReferenceRegion, std::vector<T>>> out;
-        for (int64_t k = 0; k < cnt; ++k)
-            out.push_back({ReferenceRegion(sp.names[c[k]], s[k], e[k]), {}});
+        for (size_t q = 0; q < gn.spaces.size(); ++q) {
+            const auto &sp = *gn.spaces[q];
+            detail::SetHandle A;
+            detail::upload(eng_.ctx(), sp, rdd_, parts[q], A);
+            lime_result *res = nullptr;
+            int64_t cnt = 0;
+            check(lime_complement(eng_.ctx(), sp.h, A.h, &res, &cnt));
+            std::vector<int32_t> c((size_t)cnt);
+            std::vector<int64_t> s((size_t)cnt), e((size_t)cnt);
+            int rc = lime_result_fill_host(res, c.data(), s.data(), e.data(), nullptr, nullptr);
+            lime_result_destroy(res);
+            check(rc);
+            for (int64_t k = 0; k < cnt; ++k)
+                out.push_back({ReferenceRegion(sp.names[c[k]], s[k], e[k]), {}});
+        }
         return out;
     }
 

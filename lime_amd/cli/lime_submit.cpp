@@ -184,28 +184,35 @@ int run(const std::vector<std::string> &args) {
             nm.push_back(kv.first);
             ln.push_back(kv.second);
         }
-        detail::Space sp(nm, ln);
-        std::vector<size_t> rows(rdd.size());
-        for (size_t i = 0; i < rows.size(); ++i) rows[i] = i;
-        detail::SetHandle A;
-        detail::upload(Engine::thread_default().ctx(), sp, rdd, rows, A);
-        std::vector<int32_t> c(rdd.size());
-        std::vector<int64_t> s(rdd.size()), e(rdd.size()), r(rdd.size());
-        check(lime_set_fill_host(A.h, c.data(), s.data(), e.data(), r.data()));
-        // the device order ties equal starts by (zero-width first, input row);
-        // RegionOrdering ties by end: re-order each (tiny) equal-start group
-        for (size_t i = 0; i < rdd.size();) {
-            size_t j = i + 1;
-            while (j < rdd.size() && c[j] == c[i] && s[j] == s[i]) ++j;
-            if (j - i > 1)
-                std::stable_sort(r.begin() + i, r.begin() + j, [&](int64_t x, int64_t y) {
-                    return rdd[x].first.end < rdd[y].first.end;
-                });
-            i = j;
+        // (a genome past 2^32 bases: one space after the other, in order)
+        detail::Genome gn(nm, ln);
+        auto parts = gn.split(rdd, detail::all_rows(rdd.size()));
+        std::vector<size_t> order;
+        for (size_t q = 0; q < gn.spaces.size(); ++q) {
+            const auto &rows = parts[q];
+            if (rows.empty()) continue;
+            detail::SetHandle A;
+            detail::upload(Engine::thread_default().ctx(), *gn.spaces[q], rdd, rows, A);
+            const size_t m = rows.size();
+            std::vector<int32_t> c(m);
+            std::vector<int64_t> s(m), e(m), r(m);
+            check(lime_set_fill_host(A.h, c.data(), s.data(), e.data(), r.data()));
+            // the device order ties equal starts by (zero-width first, input
+            // row); RegionOrdering ties by end: re-order each (tiny) group
+            for (size_t i = 0; i < m;) {
+                size_t j = i + 1;
+                while (j < m && c[j] == c[i] && s[j] == s[i]) ++j;
+                if (j - i > 1)
+                    std::stable_sort(r.begin() + i, r.begin() + j, [&](int64_t x, int64_t y) {
+                        return rdd[rows[x]].first.end < rdd[rows[y]].first.end;
+                    });
+                i = j;
+            }
+            for (size_t i = 0; i < m; ++i) order.push_back(rows[r[i]]);
         }
-        for (size_t i = 0; i < rdd.size(); ++i) {
-            print_region(rdd[r[i]].first);
-            printf("\t%s\n", rdd[r[i]].second.c_str());
+        for (size_t i : order) {
+            print_region(rdd[i].first);
+            printf("\t%s\n", rdd[i].second.c_str());
         }
     } else {
         usage();

@@ -99,3 +99,27 @@ def test_cli_closest():
              (ln.rstrip("\n").split("\t")[:4] for ln in open(g("intersect_with_overlap_01.bed")))}
     got = [[[c, int(s), int(e)], right[r]] for c, s, e, _, r in out]
     assert got == [list(map(list, p)) for p in expected()["closest"]]
+
+
+@pytest.mark.gpu
+def test_cli_genome_cut_into_spaces(tmp_path):
+    # a genome past 2^32 bases is cut into consecutive spaces (u32 engine
+    # coordinates); LIME_SPAN_CAP cuts hg19 (C1's inputs) into ~6 the same
+    # way: every command prints exactly its one-space output
+    from tests.test_gpu_configs import c1_inputs
+    _, _, (pa, pb), (gn, gl) = c1_inputs(tmp_path)
+    gfile = tmp_path / "genome.txt"
+    gfile.write_text("".join(f"{n}\t{ln}\n" for n, ln in zip(gn, gl)))
+    cmds = [("intersect", pa, pb), ("subtract", pa, pb), ("merge", pa),
+            ("complement", pa, str(gfile)), ("sort", pa), ("window", pa, pb),
+            ("cluster", pa), ("closest", pa, pb)]
+    env = dict(os.environ)
+    env.pop("LIME_SPAN_CAP", None)
+    one = [subprocess.run([CLI, *c], capture_output=True, text=True, timeout=300, env=env)
+           for c in cmds]
+    env["LIME_SPAN_CAP"] = "600000000"
+    cut = [subprocess.run([CLI, *c], capture_output=True, text=True, timeout=300, env=env)
+           for c in cmds]
+    for c, x, y in zip(cmds, one, cut):
+        assert x.returncode == 0 and y.returncode == 0, (c[0], x.stderr, y.stderr)
+        assert x.stdout and x.stdout == y.stdout, c[0]

@@ -491,6 +491,7 @@ __global__ __launch_bounds__(CB) void k_kill(Lefts L, const uint8_t *__restrict_
 // offsets (SCAN_FILL, only those inside [first, first + count)) or hashed
 // (SCAN_SUM).
 enum { SCAN_COUNT = 0, SCAN_FILL = 1, SCAN_SUM = 2 };
+constexpr int SWIN = 2048;  // rights staged per block for the covering scan (24 KiB)
 
 struct EndIndex {
     const uint32_t *eg, *ek;  // ends ascending, right index ascending among equal ends
@@ -510,12 +511,47 @@ __global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, EndIndex E,
                                              lime_pair *__restrict__ out,
                                              unsigned long long *__restrict__ ck) {
     __shared__ uint32_t s_off[OCAP];
+    // the block's covering-candidate window of rights [min p, max min(j, A)):
+    // consecutive lefts share most of their candidates (each right is tested
+    // by ~every left it covers, ~160 at C2's depth), so the count pass loads
+    // the window once into LDS instead of re-reading it from L2 per left
+    // (count pass only: the fill is store-bound and keeps its occupancy)
+    constexpr bool USEWIN = MODE == SCAN_COUNT;
+    __shared__ uint32_t w_gs[USEWIN ? SWIN : 1], w_ge[USEWIN ? SWIN : 1];
+    __shared__ uint32_t s_lo[CB / 64], s_hi[CB / 64];
     if (L.nc + 1 <= OCAP)
         for (int i = threadIdx.x; i <= L.nc; i += CB) s_off[i] = L.off[i];
-    __syncthreads();
     const uint32_t *o = L.nc + 1 <= OCAP ? s_off : L.off;
     const int lane = dev::lane_id();
     const int64_t i = ((int64_t)blockIdx.x * (CB / 64) + threadIdx.x / 64) * 64 + lane;
+    if (USEWIN) {
+        uint32_t lo = 0xffffffffu, hi = 0;
+        if (i < L.n && dd[i] == 0u) {
+            lo = pp[i];
+            hi = min(jp[i], E.aa[i]);
+        }
+        lo = dev::wave_reduce_min(lo);
+        hi = dev::wave_reduce_max(hi);
+        if (lane == 0) {
+            s_lo[threadIdx.x / 64] = lo;
+            s_hi[threadIdx.x / 64] = hi;
+        }
+    }
+    __syncthreads();
+    uint32_t wlo = 0xffffffffu, whi = 0;
+    if (USEWIN)
+#pragma unroll
+        for (int w = 0; w < CB / 64; ++w) {
+            wlo = min(wlo, s_lo[w]);
+            whi = max(whi, s_hi[w]);
+        }
+    const bool win = USEWIN && whi > wlo && whi - wlo <= (uint32_t)SWIN;
+    if (win)
+        for (uint32_t k = threadIdx.x; k < whi - wlo; k += CB) {
+            w_gs[k] = R.gs[wlo + k];
+            w_ge[k] = R.ge[wlo + k];
+        }
+    __syncthreads();
     uint32_t ls = 0, le = 0, D = NONE, p = 0, j = 0, s0 = 0, e0 = 0, ar = 0;
     uint64_t pos0 = 0;
     bool valid = i < L.n && dd[i] != NONE;
@@ -592,9 +628,14 @@ __global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, EndIndex E,
         uint32_t cs = 0, ce = 0, cr = 0;
         auto fetch = [&](int64_t kk, uint32_t &fs, uint32_t &fe, uint32_t &fr) {
             if (kk < (int64_t)bj) {
-                fs = R.gs[kk];
-                fe = R.ge[kk];
-                if (MODE != SCAN_COUNT) fr = R.row[kk];
+                if (win) {  // (every covering candidate of the block lies in the window)
+                    fs = w_gs[kk - wlo];
+                    fe = w_ge[kk - wlo];
+                } else {
+                    fs = R.gs[kk];
+                    fe = R.ge[kk];
+                    if (MODE != SCAN_COUNT) fr = R.row[kk];
+                }
             }
         };
         fetch(k0 + lane, cs, ce, cr);

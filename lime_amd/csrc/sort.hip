@@ -619,6 +619,141 @@ int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, co
     return LIME_OK;
 }
 
+// ---------------------------------------------------------- hybrid sort
+// (opt-in, LIME_SORT_HYBRID=1: measured slower, see sort_set_impl)
+// Plain sets over a span past 2^16: two LSD passes on bits 16..31 group the
+// rows into 65536-base buckets (input order kept inside each, the passes
+// being stable), then ONE pass sorts every bucket in LDS by
+// (low 16 bits of gs, non-zero width) -- 96 B per row instead of the 132 B of
+// four digit passes (+1 zero-width pass).  The LDS element is
+// (key17 << 15 | position in the bucket): unique, so ties keep input order.
+// Buckets of more than LCAP rows (pile-ups) take the digit passes instead.
+// Two block shapes: buckets of <= 4096 rows (256 threads, ~40 KiB LDS, 4
+// blocks per CU: C2's ~2,000-row buckets) and of <= 16384 rows (512 threads,
+// ~147 KiB: C3's pile-ups); each launch skips the other class's buckets.  A
+// bucket's items are spread evenly over the waves (contiguous, in order: the
+// ranks are stable), only as many 64-row steps as it needs.
+constexpr int LCAP = 16384;          // largest bucket sorted in LDS
+constexpr int LCAP_S = 4096;         // the small shape's capacity
+
+__global__ __launch_bounds__(256) void k_bucket_starts(const uint32_t *__restrict__ k, int64_t n,
+                                                       uint32_t nb, uint32_t *__restrict__ start) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b > nb) return;
+    start[b] = b == nb ? (uint32_t)n : (uint32_t)dev::lower_bound(k, 0, n, (uint64_t)b << 16);
+}
+
+// one stable LDS pass of D-bit digits of the elements at bit `shift`; wave w
+// holds items [w c, (w + 1) c), c = nit * 64
+template <int D, int NT, int ITEMS>
+__device__ __forceinline__ void local_pass(const uint32_t *src, uint32_t *dst,
+                                           uint32_t (*cnt)[512], uint32_t *scratch, int shift,
+                                           int nit) {
+    constexpr uint32_t ND = 1u << D;
+    constexpr int NW = NT / 64;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int c = nit * 64;
+    for (int i = threadIdx.x; i < NW * (int)ND; i += NT) cnt[i / ND][i % ND] = 0;
+    uint32_t v[ITEMS], pd[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it)
+        if (it < nit) v[it] = src[w * c + it * 64 + lane];
+    __syncthreads();
+    // stable ranks: items in (it, lane) order per wave, per-wave counters
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        if (it >= nit) break;
+        const uint32_t d = (v[it] >> shift) & (ND - 1);
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
+        const uint32_t old = cnt[w][d];
+        pd[it] = old + rank;
+        if (rank == 0) cnt[w][d] = old + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < (int)ND; d += NT) {
+        uint32_t tot = 0;
+        for (int ww = 0; ww < NW; ++ww) tot += cnt[ww][d];
+        cnt[NW][d] = tot;  // (row NW: digit totals)
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the ND totals by one wave
+        uint32_t carry = 0;
+        for (int d0 = 0; d0 < (int)ND; d0 += 64) {
+            const uint32_t t = cnt[NW][d0 + threadIdx.x];
+            const uint32_t inc = dev::wave_inclusive_sum(t);
+            cnt[NW][d0 + threadIdx.x] = carry + inc - t;
+            carry += __shfl(inc, 63, 64);
+        }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < (int)ND; d += NT) {
+        uint32_t run = cnt[NW][d];
+        for (int ww = 0; ww < NW; ++ww) {
+            const uint32_t cc = cnt[ww][d];
+            cnt[ww][d] = run;
+            run += cc;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it)
+        if (it < nit) dst[cnt[w][(v[it] >> shift) & (ND - 1)] + pd[it]] = v[it];
+    __syncthreads();
+    (void)scratch;
+}
+
+template <int NT, int CAP>
+__global__ __launch_bounds__(NT) void k_local_sort(const uint32_t *__restrict__ k0,
+                                                   const uint32_t *__restrict__ e0,
+                                                   const uint32_t *__restrict__ r0,
+                                                   const uint32_t *__restrict__ start,
+                                                   uint32_t lo_m, uint32_t *__restrict__ k1,
+                                                   uint32_t *__restrict__ e1,
+                                                   uint32_t *__restrict__ r1,
+                                                   unsigned int *__restrict__ nover,
+                                                   uint32_t *__restrict__ over) {
+    constexpr int NW = NT / 64;
+    constexpr int ITEMS = CAP / NT;
+    __shared__ uint32_t buf[2][CAP];
+    __shared__ uint32_t cnt[NW + 1][512];
+    const uint32_t b = blockIdx.x;
+    const uint32_t s0 = start[b], m = start[b + 1] - s0;
+    if (m <= lo_m) return;  // empty, or the small shape's
+    if (m > (uint32_t)CAP) {  // the large shape's, or a pile-up for the digit passes
+        if (CAP == LCAP && threadIdx.x == 0) over[atomicAdd(nover, 1u)] = b;
+        return;
+    }
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int nit = (int)((m + NW * 64 - 1) / (NW * 64));  // 64-row steps per wave
+    const int c = nit * 64;
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        if (it >= nit) break;
+        const uint32_t j = w * c + it * 64 + lane;
+        uint32_t x = 0xffffffffu;  // padding sorts last
+        if (j < m) {
+            const uint32_t g = k0[s0 + j], e = e0[s0 + j];
+            x = ((((g & 0xffffu) << 1) | (e > g ? 1u : 0u)) << 15) | j;
+        }
+        buf[0][j] = x;
+    }
+    __syncthreads();
+    local_pass<9, NT, ITEMS>(buf[0], buf[1], cnt, nullptr, 15, nit);  // key17 bits 0..8
+    local_pass<8, NT, ITEMS>(buf[1], buf[0], cnt, nullptr, 24, nit);  // key17 bits 9..16
+    for (uint32_t q = threadIdx.x; q < m; q += NT) {
+        const uint32_t j = buf[0][q] & 0x7fffu;
+        k1[s0 + q] = k0[s0 + j];
+        e1[s0 + q] = e0[s0 + j];
+        r1[s0 + q] = r0[s0 + j];
+    }
+}
+
 }  // namespace
 
 int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
@@ -633,6 +768,63 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
                     const uint32_t *d_row, const uint32_t *d_len) {
     return sort_set_impl(ctx, set, true, reinterpret_cast<const int32_t *>(d_gs), d_ge, d_row,
                          d_len);
+}
+
+// The hybrid sort's last pass: every 65536-base bucket of (k0, e0, r0)
+// sorted in LDS (k_local_sort) into (k1, e1, r1), pile-up buckets by the
+// digit passes on their own rows; the result is swapped into (k0, e0, r0).
+static int local_sort(lime_ctx *ctx, const lime_set *set, int64_t n, const SetStats &h,
+                      uint32_t *&k0, uint32_t *&e0, uint32_t *&r0, uint32_t *&k1, uint32_t *&e1,
+                      uint32_t *&r1, uint32_t *mat) {
+    const uint32_t nb = (h.max_gs >> 16) + 1;
+    uint32_t *start, *over;
+    unsigned int *nover;
+    LIME_TRY(alloc(ctx, &start, (size_t)nb + 1));
+    PoolGuard<uint32_t> g0{ctx, start};
+    LIME_TRY(alloc(ctx, &over, (size_t)nb));
+    PoolGuard<uint32_t> g1{ctx, over};
+    LIME_TRY(alloc(ctx, &nover, 1));
+    PoolGuard<unsigned int> g2{ctx, nover};
+    LIME_HIP(hipMemsetAsync(nover, 0, 4, S(ctx)));
+    hipLaunchKernelGGL(k_bucket_starts, dim3(blocks_for((int64_t)nb + 1, 256)), dim3(256), 0,
+                       S(ctx), (const uint32_t *)k0, n, nb, start);
+    hipLaunchKernelGGL((k_local_sort<256, LCAP_S>), dim3(nb), dim3(256), 0, S(ctx),
+                       (const uint32_t *)k0, (const uint32_t *)e0, (const uint32_t *)r0,
+                       (const uint32_t *)start, 0u, k1, e1, r1, nover, over);
+    hipLaunchKernelGGL((k_local_sort<512, LCAP>), dim3(nb), dim3(512), 0, S(ctx),
+                       (const uint32_t *)k0, (const uint32_t *)e0, (const uint32_t *)r0,
+                       (const uint32_t *)start, (uint32_t)LCAP_S, k1, e1, r1, nover, over);
+    LIME_HIP(hipGetLastError());
+    unsigned int no = 0;
+    LIME_TRY(read_back(ctx, &no, nover, 4));
+    if (no > 0) {
+        // pile-up buckets: (zero-width bit,) low two digits on their own rows
+        std::vector<uint32_t> hb(no), hs((size_t)nb + 1);
+        LIME_TRY(read_back(ctx, hb.data(), over, 4 * (size_t)no));
+        LIME_TRY(read_back(ctx, hs.data(), start, 4 * ((size_t)nb + 1)));
+        std::vector<std::pair<int, int>> passes;
+        if (set->has_zero_width && set->max_width > 0) passes.push_back({M_NZ, 0});
+        passes.push_back({M_GS, 0});
+        passes.push_back({M_GS, 8});
+        for (uint32_t b : hb) {
+            const int64_t s0 = hs[b], m = (int64_t)hs[b + 1] - hs[b];
+            const uint32_t nt = (uint32_t)((m + RTILE - 1) / RTILE);
+            uint32_t *a[3] = {k0 + s0, e0 + s0, r0 + s0}, *o[3] = {k1 + s0, e1 + s0, r1 + s0};
+            for (auto &p : passes) {
+                LIME_TRY(radix_pass(ctx, p.first, p.second, false, m, a[0], a[1], a[2], nullptr,
+                                    o[0], o[1], o[2], mat, nt, ROWS_LOAD));
+                std::swap(a, o);
+            }
+            if (a[0] != k1 + s0)  // (an even number of passes ends on the input side)
+                for (int q = 0; q < 3; ++q)
+                    LIME_HIP(hipMemcpyAsync(q == 0 ? k1 + s0 : q == 1 ? e1 + s0 : r1 + s0, a[q],
+                                            4 * (size_t)m, hipMemcpyDeviceToDevice, S(ctx)));
+        }
+    }
+    std::swap(k0, k1);
+    std::swap(e0, e1);
+    std::swap(r0, r1);
+    return LIME_OK;
 }
 
 int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
@@ -651,6 +843,17 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &st, 1));
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
+    // hybrid sort (k_local_sort): plain sets with row ids over a span past
+    // 2^16, large enough to fill the GPU.  Opt-in (LIME_SORT_HYBRID=1): parity
+    // green on the whole GPU suite, but measured SLOWER on MI355X (C2 sort
+    // 5.7 -> 6.1 ms, C3 13.4 -> 19.7 ms: the per-bucket LDS ranking, one
+    // 147 KiB block per CU for C3's ~10,600-row buckets, costs more than the
+    // two digit passes it replaces)
+    static const bool hyb_env = getenv("LIME_SORT_HYBRID") && atoi(getenv("LIME_SORT_HYBRID")) == 1;
+    const int64_t span = set->off.empty() ? 0 : (int64_t)set->off.back();
+    const bool hyb_cand = hyb_env && keep_rows && set->strand_in == nullptr &&
+                          set->min_shift == 0 && n >= (1 << 20) && span > (1 << 16);
+    const int hshift = hyb_cand ? 16 : set->min_shift;  // the digit k_prep histograms
     // plain caller rows: validate + histogram only, and let the first radix
     // pass read the caller's rows (saves writing gs / ge and reading them back)
     // Opt-in (LIME_SORT_RAW=1): measured SLOWER on MI355X (C2 sort 5.8 ->
@@ -675,17 +878,16 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         if (global)
             hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start,
                                d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0,
-                               e0, r0, part, mat, ntiles, set->min_shift);
+                               e0, r0, part, mat, ntiles, hshift);
         else if (set->n_contigs <= PCMAX)
             hipLaunchKernelGGL((k_prep<false, true, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
                                d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
                                set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
-                               set->min_shift);  // rows = positions: made by the first pass
+                               hshift);  // rows = positions: made by the first pass
         else
             hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
                                d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
-                               set->min_shift);
+                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, hshift);
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());
@@ -715,8 +917,13 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
         if (keep_rows) LIME_TRY(alloc(ctx, &r1, (size_t)n));
         const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
+        // hybrid: digit passes on bits 16.. only, then k_local_sort (its key
+        // carries the zero-width bit: no NZ pass)
+        const bool hybrid = hyb_cand && bits > 16;
         std::vector<std::pair<int, int>> passes;  // (mode, shift), least significant first
-        if (stranded) {
+        if (hybrid) {
+            for (int sh = 16; sh < bits; sh += 8) passes.push_back({M_GS, sh});
+        } else if (stranded) {
             // RegionOrdering (start, end, strand): strand, then ge, then gs.
             // The strand pass runs first, while row i is still input row i.
             const int wbits = h.max_width ? 32 - __builtin_clz(h.max_width) : 0;
@@ -726,12 +933,13 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             // (all rows zero-width: the bit is constant, no pass)
             passes.push_back({M_NZ, 0});
         }
-        for (int sh = 0; sh < bits; sh += 8)
-            if (sh >= set->min_shift) passes.push_back({M_GS, sh});
+        if (!hybrid)
+            for (int sh = 0; sh < bits; sh += 8)
+                if (sh >= set->min_shift) passes.push_back({M_GS, sh});
         // caller rows: the first pass writes row = position (k_prep did not)
         int rows = !keep_rows ? ROWS_NONE : global ? ROWS_LOAD : ROWS_IDENT;
-        // k_prep already histogrammed the gs digit at min_shift
-        bool have = passes.front().first == M_GS && passes.front().second == set->min_shift;
+        // k_prep already histogrammed the gs digit at hshift
+        bool have = passes.front().first == M_GS && passes.front().second == hshift;
         bool first = true;
         for (auto &p : passes) {
             if (first && raw) {
@@ -751,6 +959,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             std::swap(e0, e1);
             std::swap(r0, r1);
         }
+        if (hybrid) LIME_TRY(local_sort(ctx, set, n, h, k0, e0, r0, k1, e1, r1, mat));
         release(ctx, k1);
         release(ctx, e1);
         release(ctx, r1);

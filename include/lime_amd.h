@@ -270,12 +270,13 @@ int lime_bitset_from_set(lime_ctx *ctx, const lime_set *a, lime_bitset **out);
 int lime_bitset_from_global(lime_ctx *ctx, const lime_space *space, int64_t lo, int64_t hi,
                             int64_t n, const uint32_t *d_gstart, const uint32_t *d_gend,
                             lime_bitset **out);
-/* The AND of k <= 16 row sets' bits straight from their unsorted device rows
+/* The AND of k row sets' bits straight from their unsorted device rows
  * (C5's k-way intersection, SURVEY.md 8(d) and Appendix A.4: the fold of the
  * reference's pairwise intersect, cli/Intersection.scala:41-54, over merged
  * operands): every set is binned as above, then one
  * kernel paints each tile of every set in LDS and ANDs them in registers --
- * one bitset stored, no per-set bitsets.  n, d_contig, d_start, d_end: k
+ * one bitset stored, no per-set bitsets (past 16 sets, each group of 16
+ * ANDs into the words of the earlier ones).  n, d_contig, d_start, d_end: k
  * entries each (host arrays of device pointers).  Same bits as
  * lime_bitset_and_runs over the k sets' bitsets. */
 int lime_bitset_and_from_device(lime_ctx *ctx, const lime_space *space, int32_t k,
@@ -291,7 +292,8 @@ int lime_bitset_window(const lime_bitset *bs, int64_t *lo, int64_t *n_words);
 /* op: 0 = a, 1 = not a (within contigs), 2 = a and b, 3 = a and not b */
 int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bitset *b,
                      lime_result **out, int64_t *n_runs);
-/* k-way AND of k bitsets, runs extracted */
+/* k-way AND of k bitsets, runs extracted (any k: past 16 the words are ANDed
+ * group by group into a temporary bitset first) */
 int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, lime_result **out,
                          int64_t *n_runs);
 int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a);

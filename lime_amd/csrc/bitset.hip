@@ -573,6 +573,7 @@ struct AndArgs {
     const uint32_t *xoff[MAXK];   // nt + 1 bucket starts
     const uint32_t *full[MAXK];   // nt + 1 exclusive scan of the difference array
     int k;
+    int init;  // the AND continues the words already stored (sets past the first 16)
     uint64_t *words;
     int64_t n_words;
 };
@@ -587,8 +588,12 @@ __global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
     const int t = blockIdx.x;
     constexpr uint32_t B = APV * PAINTB;
     uint64_t acc[AWPT];
+    const int64_t wt = (int64_t)t * TWORDS;
 #pragma unroll
-    for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
+    for (int j = 0; j < AWPT; ++j) {
+        const int64_t w = wt + threadIdx.x + j * PAINTB;
+        acc[j] = a.init ? (w < a.n_words ? a.words[w] : 0ull) : ~0ull;
+    }
     // a tile wholly inside one of the set's cross pieces: AND unchanged
     auto skip = [&](int i) { return a.full[i] && a.full[i][t + 1] != 0u; };
     auto load = [&](int i, uint32_t rb, uint32_t(&p)[APV]) {
@@ -651,6 +656,21 @@ __global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
     for (int j = 0; j < AWPT; ++j) {
         const int64_t w = w0 + threadIdx.x + j * PAINTB;
         if (w < a.n_words) a.words[w] = acc[j];
+    }
+}
+
+// words = (init ? words : all ones) & AND of up to MAXK bitsets (chains a
+// k-way AND past 16 operands)
+struct WordsAnd {
+    const uint64_t *w[MAXK];
+    int k;
+};
+__global__ __launch_bounds__(BB) void k_and_words(WordsAnd a, int init, uint64_t *__restrict__ out,
+                                                  int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < n; i += (int64_t)gridDim.x * BB) {
+        uint64_t x = init ? out[i] : ~0ull;
+        for (int q = 0; q < a.k; ++q) x &= a.w[q][i];
+        out[i] = x;
     }
 }
 
@@ -1122,7 +1142,7 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
                     const int32_t *const *d_contig, const uint32_t *const *d_start,
                     const uint32_t *const *d_end, const uint32_t *d_off, const uint32_t *d_len,
                     int64_t lo, int64_t hi, lime_bitset *bs) {
-    if (k < 1 || k > MAXK) return fail(LIME_ERR_ARG, "1 to 16 row sets per AND");
+    if (k < 1) return fail(LIME_ERR_ARG, "at least one row set per AND");
     window_of(bs, sp, lo, hi);
     int64_t nmax = 0, bound = 0;
     for (int i = 0; i < k; ++i) {
@@ -1132,66 +1152,96 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     bs->runs_bound = bound;  // each AND run starts at a run start of some set
     LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
     const int nt = n_bins(hi - lo) * PSUB;
-    PoolBag bag{ctx, {}};
+    PoolBag keep{ctx, {}};
     uint64_t *cross;
     unsigned int *flags;
-    LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * nmax, 1)));
-    LIME_TRY(bag.get(&flags, 2 * (size_t)k));
+    LIME_TRY(keep.get(&cross, (size_t)std::max<int64_t>(2 * nmax, 1)));
+    LIME_TRY(keep.get(&flags, 2 * (size_t)k));
     LIME_HIP(hipMemsetAsync(flags, 0, 8 * (size_t)k, S(ctx)));
-    AndArgs aa;
-    for (int i = 0; i < MAXK; ++i) {
-        aa.slab2[i] = aa.tstart[i] = aa.xoff[i] = aa.full[i] = nullptr;
-        aa.xl[i] = nullptr;
-    }
-    aa.k = k;
-    aa.words = bs->words;
-    aa.n_words = bs->n_words;
-    for (int i = 0; i < k; ++i) {
-        uint32_t *slab2, *ttot;
-        LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
-        LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
-        LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo, hi,
-                          slab2, ttot, cross, flags + 2 * i));
-        aa.slab2[i] = slab2;
-        aa.tstart[i] = ttot;
-        // the cross buffer is reused by the next set: bucket its pieces now
-        unsigned int h[2] = {0, 0};
-        LIME_TRY(read_back(ctx, h, flags + 2 * i, sizeof(h)));
-        LIME_TRY(rows_error(h[1]));
-        if (h[0] == 0) continue;
-        uint32_t *xcnt, *diff, *xcur;
-        uint2 *xl;
-        LIME_TRY(bag.get(&xcnt, (size_t)nt + 1));
-        LIME_TRY(bag.get(&diff, (size_t)nt + 1));
-        LIME_TRY(bag.get(&xcur, (size_t)nt + 1));
-        LIME_TRY(bag.get(&xl, 2 * (size_t)h[0]));
-        LIME_HIP(hipMemsetAsync(xcnt, 0, 4 * ((size_t)nt + 1), S(ctx)));
-        LIME_HIP(hipMemsetAsync(diff, 0, 4 * ((size_t)nt + 1), S(ctx)));
-        const unsigned g = std::min<unsigned>(blocks_for(h[0], BB), 2048u);
-        hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
-                           (const unsigned int *)(flags + 2 * i), xcnt, diff);
-        LIME_TRY(scan_exclusive_u32(ctx, xcnt, xcnt, (int64_t)nt + 1, nullptr));
-        LIME_TRY(scan_exclusive_u32(ctx, diff, diff, (int64_t)nt + 1, nullptr));
-        LIME_HIP(hipMemcpyAsync(xcur, xcnt, 4 * ((size_t)nt + 1), hipMemcpyDeviceToDevice, S(ctx)));
-        hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
-                           (const unsigned int *)(flags + 2 * i), xcur, xl);
+    // groups of MAXK sets, each painted and ANDed in one k_paint_and; a group
+    // after the first ANDs into the words the earlier ones stored
+    for (int g0 = 0; g0 < k; g0 += MAXK) {
+        const int kg = std::min(MAXK, k - g0);
+        PoolBag bag{ctx, {}};  // (released in stream order after the paint)
+        AndArgs aa;
+        for (int i = 0; i < MAXK; ++i) {
+            aa.slab2[i] = aa.tstart[i] = aa.xoff[i] = aa.full[i] = nullptr;
+            aa.xl[i] = nullptr;
+        }
+        aa.k = kg;
+        aa.init = g0 > 0;
+        aa.words = bs->words;
+        aa.n_words = bs->n_words;
+        for (int q = 0; q < kg; ++q) {
+            const int i = g0 + q;
+            uint32_t *slab2, *ttot;
+            LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
+            LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
+            LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo,
+                              hi, slab2, ttot, cross, flags + 2 * i));
+            aa.slab2[q] = slab2;
+            aa.tstart[q] = ttot;
+            // the cross buffer is reused by the next set: bucket its pieces now
+            unsigned int h[2] = {0, 0};
+            LIME_TRY(read_back(ctx, h, flags + 2 * i, sizeof(h)));
+            LIME_TRY(rows_error(h[1]));
+            if (h[0] == 0) continue;
+            uint32_t *xcnt, *diff, *xcur;
+            uint2 *xl;
+            LIME_TRY(bag.get(&xcnt, (size_t)nt + 1));
+            LIME_TRY(bag.get(&diff, (size_t)nt + 1));
+            LIME_TRY(bag.get(&xcur, (size_t)nt + 1));
+            LIME_TRY(bag.get(&xl, 2 * (size_t)h[0]));
+            LIME_HIP(hipMemsetAsync(xcnt, 0, 4 * ((size_t)nt + 1), S(ctx)));
+            LIME_HIP(hipMemsetAsync(diff, 0, 4 * ((size_t)nt + 1), S(ctx)));
+            const unsigned g = std::min<unsigned>(blocks_for(h[0], BB), 2048u);
+            hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+                               (const unsigned int *)(flags + 2 * i), xcnt, diff);
+            LIME_TRY(scan_exclusive_u32(ctx, xcnt, xcnt, (int64_t)nt + 1, nullptr));
+            LIME_TRY(scan_exclusive_u32(ctx, diff, diff, (int64_t)nt + 1, nullptr));
+            LIME_HIP(hipMemcpyAsync(xcur, xcnt, 4 * ((size_t)nt + 1), hipMemcpyDeviceToDevice,
+                                    S(ctx)));
+            hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+                               (const unsigned int *)(flags + 2 * i), xcur, xl);
+            LIME_HIP(hipGetLastError());
+            aa.xl[q] = xl;
+            aa.xoff[q] = xcnt;
+            aa.full[q] = diff;
+        }
+        hipLaunchKernelGGL(k_paint_and, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), aa);
         LIME_HIP(hipGetLastError());
-        aa.xl[i] = xl;
-        aa.xoff[i] = xcnt;
-        aa.full[i] = diff;
     }
-    hipLaunchKernelGGL(k_paint_and, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), aa);
-    LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
 
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res) {
     const lime_bitset *a = sets[0];
-    if (k > MAXK) return fail(LIME_ERR_ARG, "at most 16 bitsets per op");
+    // an AND of more than MAXK bitsets: their words ANDed group by group into
+    // a temporary bitset, whose runs are then extracted (op 0)
+    uint64_t *tmp = nullptr;
+    PoolGuard<uint64_t> gt{ctx, tmp};
+    if (op == 4 && k > MAXK) {
+        LIME_TRY(alloc(ctx, &tmp, (size_t)std::max<int64_t>(a->n_words, 1)));
+        for (int g0 = 0; g0 < k; g0 += MAXK) {
+            WordsAnd wa;
+            wa.k = std::min(MAXK, k - g0);
+            for (int q = 0; q < MAXK; ++q) wa.w[q] = q < wa.k ? sets[g0 + q]->words : nullptr;
+            const unsigned g = std::min<unsigned>(blocks_for(a->n_words, BB), 8192u);
+            if (a->n_words > 0)
+                hipLaunchKernelGGL(k_and_words, dim3(g), dim3(BB), 0, S(ctx), wa, g0 > 0 ? 1 : 0,
+                                   tmp, a->n_words);
+        }
+        LIME_HIP(hipGetLastError());
+    }
     OpArgs oa;
-    for (int i = 0; i < MAXK; ++i) oa.w[i] = i < k ? sets[i]->words : nullptr;
-    oa.k = k;
+    for (int i = 0; i < MAXK; ++i) oa.w[i] = i < k && i < MAXK ? sets[i]->words : nullptr;
+    oa.k = std::min(k, MAXK);
     oa.op = op;
+    if (tmp) {
+        oa.w[0] = tmp;
+        oa.k = 1;
+        oa.op = 0;
+    }
     oa.n_words = a->n_words;
     oa.word0 = a->word0;
     oa.span = a->hi_bit;  // NOT clears every bit past the window

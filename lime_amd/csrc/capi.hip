@@ -1062,7 +1062,7 @@ static int bitset_and_entry(lime_ctx *ctx, const lime_space *sp, int64_t lo, int
                             int32_t k, const int64_t *n, const int32_t *const *d_contig,
                             const uint32_t *const *d_start, const uint32_t *const *d_end,
                             bool global, lime_bitset **out) {
-    if (!ctx || !sp || !out || !n || k < 1 || k > 16 || !d_start || !d_end ||
+    if (!ctx || !sp || !out || !n || k < 1 || !d_start || !d_end ||
         (!global && !d_contig))
         return fail(LIME_ERR_ARG, "bad bitset and arguments");
     for (int i = 0; i < k; ++i) {

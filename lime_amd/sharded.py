@@ -271,7 +271,7 @@ class ShardedBitset:
         return ctx.bitset_from_global(sp, self.lo, self.hi, m, rgs.data_ptr(), rge.data_ptr())
 
     def and_bitset(self, inputs):
-        """this shard's AND of k <= 16 sets in one fused paint
+        """this shard's AND of k sets in one fused paint per 16
         (lime_bitset_and_from_device / _from_global): no per-set bitsets"""
         ctx, sp = self.ctx, self.space
         if self.world == 1:
@@ -288,15 +288,14 @@ class ShardedBitset:
         coordinates), the carry (drop_first, new_last_end), the total run
         count of the unsharded result and, with gather=True, every run as an
         int64 [m, 2] tensor (global start, end) in order."""
-        fuse = op == "and" and len(inputs) <= 16
-        bits = [self.and_bitset(inputs)] if fuse else [self.bitset(*x) for x in inputs]
-        if fuse:
+        if op == "and":
+            bits = [self.and_bitset(inputs)]
             res = self.ctx.bitset_runs(0, bits[0])
-        elif op == "and":
-            res = self.ctx.bitset_and(bits)
         elif op == "not":
+            bits = [self.bitset(*inputs[0])]
             res = self.ctx.bitset_runs(1, bits[0])
         elif op == "andnot":
+            bits = [self.bitset(*x) for x in inputs[:2]]
             res = self.ctx.bitset_runs(3, bits[0], bits[1])
         else:
             raise ValueError(f"unknown op {op}")

@@ -709,3 +709,44 @@ def test_subtract_runs_path(ctx, mode, t):
     sp = space_for(2, 100000)
     res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t, mode).to_host()
     _sub_equal(res, oracle.subtract(A, B, t, mode))
+
+
+def test_bitset_and_past_sixteen_sets(ctx):
+    # the fused AND paints 16 sets per kernel and chains the groups
+    # (lime_bitset_and_from_device); lime_bitset_and_runs chains its words
+    # past 16 bitsets.  16 and 17 sets: fused == chained words == sharded run
+    # == the oracle's fold of intersect over the merged operands (A.4)
+    from lime_amd.sharded import ShardedBitset
+    from tests.test_gpu_configs import coalesce
+    rng = np.random.default_rng(95)
+    sp = space_for(2, 200000)
+    # ~1500 rows of <= 2 kb per set: each covers ~97% of the bases, so the
+    # AND of 17 keeps about two thirds in many runs
+    sets = [random_sets(rng, 1500, 1, n_contigs=2, contig_len=200000, max_len=2000)[0]
+            for _ in range(17)]
+    dev = [_dev_rows(A) for A in sets]
+    rows = [(len(A[0]), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr())
+            for A, t in zip(sets, dev)]
+    bits = [ctx.bitset_from_device(sp, *r) for r in rows]
+    cur = oracle.merge(sets[0])
+    for k in range(2, 18):
+        m = oracle.merge(sets[k - 1])
+        ix = oracle.intersect((cur["contig"], cur["start"], cur["end"]),
+                              (m["contig"], m["start"], m["end"]))
+        order = np.lexsort((ix["start"], ix["contig"]))
+        cur = {key: np.asarray(ix[key])[order] for key in ("contig", "start", "end")}
+        if k < 16:
+            continue
+        fused = ctx.bitset_and_from_device(sp, rows[:k])
+        got = ctx.bitset_runs(0, fused).to_host()
+        words = ctx.bitset_and(bits[:k]).to_host()
+        assert len(got["start"]) > 100
+        for key in ("contig", "start", "end"):
+            assert got[key].tolist() == words[key].tolist()
+        x = coalesce(cur["contig"], cur["start"], cur["end"])
+        for a_, b_ in zip((got["contig"], got["start"], got["end"]), x):
+            assert np.asarray(a_).tolist() == np.asarray(b_).tolist()
+        out = ShardedBitset(ctx, sp).run(rows[:k], gather=True)
+        gs = sp.offsets[np.asarray(got["contig"])] + np.asarray(got["start"], np.int64)
+        assert out["runs"].numpy()[:, 0].tolist() == gs.tolist()
+        out["result"].close()

@@ -105,8 +105,17 @@ __global__ __launch_bounds__(BB) void k_paint_cross(const uint64_t *__restrict__
 // direct per-row stores 0.90 vs 1.38 ms per 1.25e8 rows.
 // HBM per row: 8 B (count) + 12 B + 4 B (write) + 4 B + 4 B (split) + 4 B
 // (paint), + G/8 bits.
-constexpr int BSH = 22;                  // bin = 2^22 bases
-constexpr int PSH = 19;                  // paint tile = 2^19 bases = 8192 words (64 KiB)
+#ifndef LIME_BSH
+#define LIME_BSH 22
+#endif
+#ifndef LIME_PSH
+#define LIME_PSH 19
+#endif
+#ifndef LIME_PAINTB
+#define LIME_PAINTB 512
+#endif
+constexpr int BSH = LIME_BSH;            // bin = 2^22 bases
+constexpr int PSH = LIME_PSH;            // paint tile = 2^19 bases = 8192 words (64 KiB)
 constexpr int PSUB = 1 << (BSH - PSH);   // paint tiles per bin
 constexpr int TWORDS = 1 << (PSH - 6);
 constexpr int LENB = 32 - BSH;           // packed length bits (bin slab)
@@ -116,7 +125,7 @@ constexpr int NBMAX = 1 << (32 - BSH);   // bins (span < 2^32)
 constexpr int NTMAX = NBMAX * PSUB;      // paint tiles
 constexpr int BINB = 1024;               // count / split block
 constexpr int WRB = 512;                 // write block (<= 256 VGPRs: no spills)
-constexpr int PAINTB = 512;
+constexpr int PAINTB = LIME_PAINTB;
 
 struct BinArgs {
     const int32_t *contig;     // null: start / end are global coordinates
@@ -338,14 +347,19 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
         for (int k = 0; k < SROWS; ++k)
             if (vnow & (1u << k)) rk[k] = atomicAdd(&hist[tb[k]], 1u);
         __syncthreads();
-        {
-            // bins 2t, 2t + 1 per thread (NBMAX = 2 * WRB)
+        if (NBMAX == 2 * WRB) {
+            // bins 2t, 2t + 1 per thread
             const int t = 2 * threadIdx.x;
             const uint32_t h0 = hist[t], h1 = hist[t + 1];
             uint32_t tot;
             const uint32_t o = dev::block_exclusive_sum<WRB>(h0 + h1, scratch, &tot);
             soff[t] = o;
             soff[t + 1] = o + h0;
+        } else {
+            // bin t per thread
+            const int t = threadIdx.x;
+            uint32_t tot;
+            soff[t] = dev::block_exclusive_sum<WRB>(hist[t], scratch, &tot);
         }
         __syncthreads();
 #pragma unroll
@@ -386,7 +400,7 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
 // claims for d, and ONE LDS atomic instruction (lanes 56..63) reserves all
 // of them -- no chain of returning atomics per row.
 static_assert(PSUB == 8, "claims: 8 slots x 8 destinations = one wave");
-static_assert(NBMAX == 2 * WRB, "write-pass bin scan: two bins per thread");
+static_assert(NBMAX == 2 * WRB || NBMAX == WRB, "write-pass bin scan: one or two bins per thread");
 constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
 __global__ __launch_bounds__(SPB) void k_bin_split(BinArgs a) {
     __shared__ uint32_t cur[PSUB];
@@ -1153,11 +1167,27 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
     const int nt = n_bins(hi - lo) * PSUB;
     PoolBag keep{ctx, {}};
-    uint64_t *cross;
+    // two cross buffers: set q's rows are binned while set q - 1's cross
+    // pieces are read back and bucketed, so the host waits on an event of set
+    // q - 1 only and the stream never drains between sets
+    uint64_t *cross[2];
     unsigned int *flags;
-    LIME_TRY(keep.get(&cross, (size_t)std::max<int64_t>(2 * nmax, 1)));
+    LIME_TRY(keep.get(&cross[0], (size_t)std::max<int64_t>(2 * nmax, 1)));
+    LIME_TRY(keep.get(&cross[1], (size_t)std::max<int64_t>(2 * nmax, 1)));
     LIME_TRY(keep.get(&flags, 2 * (size_t)k));
     LIME_HIP(hipMemsetAsync(flags, 0, 8 * (size_t)k, S(ctx)));
+    // set q's (ncross, err) land in the upper half of the pinned scratch
+    // (read_back uses the lower half)
+    unsigned int *hflags = reinterpret_cast<unsigned int *>(static_cast<char *>(ctx->pinned) + 2048);
+    struct Events {
+        hipEvent_t e[2] = {nullptr, nullptr};
+        ~Events() {
+            for (hipEvent_t x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } ev;
+    for (int j = 0; j < 2; ++j)
+        LIME_HIP(hipEventCreateWithFlags(&ev.e[j], hipEventDisableTiming));
     // groups of MAXK sets, each painted and ANDed in one k_paint_and; a group
     // after the first ANDs into the words the earlier ones stored
     for (int g0 = 0; g0 < k; g0 += MAXK) {
@@ -1172,42 +1202,54 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
         aa.init = g0 > 0;
         aa.words = bs->words;
         aa.n_words = bs->n_words;
-        for (int q = 0; q < kg; ++q) {
+        // bucket set q's cross pieces by tile (its flags were copied to the
+        // host behind its binning; wait for that copy only)
+        auto bucket = [&](int q) -> int {
             const int i = g0 + q;
-            uint32_t *slab2, *ttot;
-            LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
-            LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
-            LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo,
-                              hi, slab2, ttot, cross, flags + 2 * i));
-            aa.slab2[q] = slab2;
-            aa.tstart[q] = ttot;
-            // the cross buffer is reused by the next set: bucket its pieces now
-            unsigned int h[2] = {0, 0};
-            LIME_TRY(read_back(ctx, h, flags + 2 * i, sizeof(h)));
-            LIME_TRY(rows_error(h[1]));
-            if (h[0] == 0) continue;
+            LIME_HIP(hipEventSynchronize(ev.e[q % 2]));
+            const unsigned int nx = hflags[2 * q], err = hflags[2 * q + 1];
+            LIME_TRY(rows_error(err));
+            if (nx == 0) return LIME_OK;
             uint32_t *xcnt, *diff, *xcur;
             uint2 *xl;
             LIME_TRY(bag.get(&xcnt, (size_t)nt + 1));
             LIME_TRY(bag.get(&diff, (size_t)nt + 1));
             LIME_TRY(bag.get(&xcur, (size_t)nt + 1));
-            LIME_TRY(bag.get(&xl, 2 * (size_t)h[0]));
+            LIME_TRY(bag.get(&xl, 2 * (size_t)nx));
             LIME_HIP(hipMemsetAsync(xcnt, 0, 4 * ((size_t)nt + 1), S(ctx)));
             LIME_HIP(hipMemsetAsync(diff, 0, 4 * ((size_t)nt + 1), S(ctx)));
-            const unsigned g = std::min<unsigned>(blocks_for(h[0], BB), 2048u);
-            hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+            const unsigned g = std::min<unsigned>(blocks_for(nx, BB), 2048u);
+            const uint64_t *cx = cross[q % 2];
+            hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), cx,
                                (const unsigned int *)(flags + 2 * i), xcnt, diff);
             LIME_TRY(scan_exclusive_u32(ctx, xcnt, xcnt, (int64_t)nt + 1, nullptr));
             LIME_TRY(scan_exclusive_u32(ctx, diff, diff, (int64_t)nt + 1, nullptr));
             LIME_HIP(hipMemcpyAsync(xcur, xcnt, 4 * ((size_t)nt + 1), hipMemcpyDeviceToDevice,
                                     S(ctx)));
-            hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), (const uint64_t *)cross,
+            hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), cx,
                                (const unsigned int *)(flags + 2 * i), xcur, xl);
             LIME_HIP(hipGetLastError());
             aa.xl[q] = xl;
             aa.xoff[q] = xcnt;
             aa.full[q] = diff;
+            return LIME_OK;
+        };
+        for (int q = 0; q < kg; ++q) {
+            const int i = g0 + q;
+            uint32_t *slab2, *ttot;
+            LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
+            LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
+            // (cross[q % 2] was last used by set q - 2, bucketed before this)
+            LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo,
+                              hi, slab2, ttot, cross[q % 2], flags + 2 * i));
+            LIME_HIP(hipMemcpyAsync(hflags + 2 * q, flags + 2 * i, 8, hipMemcpyDeviceToHost,
+                                    S(ctx)));
+            LIME_HIP(hipEventRecord(ev.e[q % 2], S(ctx)));
+            aa.slab2[q] = slab2;
+            aa.tstart[q] = ttot;
+            if (q > 0) LIME_TRY(bucket(q - 1));
         }
+        LIME_TRY(bucket(kg - 1));
         hipLaunchKernelGGL(k_paint_and, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), aa);
         LIME_HIP(hipGetLastError());
     }

@@ -86,7 +86,9 @@ void Pool::release_all() {
 }
 
 int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes) {
-    if (bytes > 4096) {  // larger than the pinned scratch: pageable copy
+    // the lower half of the pinned scratch (the upper half holds the k-way
+    // AND's per-set flags, bitset.hip); larger: pageable copy
+    if (bytes > 2048) {
         LIME_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, S(c)));
         LIME_HIP(hipStreamSynchronize(S(c)));
         return LIME_OK;

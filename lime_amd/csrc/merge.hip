@@ -139,7 +139,13 @@ struct MergeScanArgs {
 // LDS: global traffic is lane-consecutive 16-B accesses (whole lines per
 // wave instruction); the LDS image pads 4 words after every 16 rows so the
 // blocked b128 reads (stride 80 B per lane) are conflict-free.
-constexpr int SB = 512;              // scan workgroup
+#ifndef LIME_MERGE_SB
+#define LIME_MERGE_SB 512
+#endif
+#ifndef LIME_MERGE_WPE
+#define LIME_MERGE_WPE 1
+#endif
+constexpr int SB = LIME_MERGE_SB;    // scan workgroup
 constexpr int STILE = SB * MITEMS;   // 8192 rows per scan tile
 constexpr int MPADW = STILE + STILE / 4;
 __device__ __forceinline__ int pad_word(int u4) { return 4 * u4 + 4 * (u4 >> 2); }
@@ -220,7 +226,8 @@ __device__ SegMax block_exclusive_segmax(SegMax x, SegMax *scratch, SegMax *tota
 // the max-end carry restarts there, so a tile holding a strand change
 // publishes its inclusive carry without looking back.
 template <bool STR>
-__global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
+__global__ __launch_bounds__(SB) __attribute__((amdgpu_waves_per_eu(LIME_MERGE_WPE, 8)))
+void k_merge_scan(MergeScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[MPADW];
     __shared__ uint32_t scratch[SB / 64 + 1];
     __shared__ SegMax sscratch[SB / 64 + 1];
@@ -289,12 +296,11 @@ __global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
         if (threadIdx.x == 0) s_carry = ex;
     }
     __syncthreads();
-    uint32_t M = pre.b ? pre.v : max(pre.v, (uint32_t)s_carry);
-    uint32_t Mk[MITEMS];
+    const uint32_t M0 = pre.b ? pre.v : max(pre.v, (uint32_t)s_carry);
+    uint32_t M = M0;
     uint32_t flags = 0;
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) {
-        Mk[k] = M;  // the run so far; its end if row k starts a new run
         const bool b = (brk >> k) & 1u;
         if (r0 + k < n && (b || M <= s[k])) flags |= 1u << k;
         M = b ? e[k] : max(M, e[k]);
@@ -316,20 +322,23 @@ __global__ __launch_bounds__(SB) void k_merge_scan(MergeScanArgs a) {
     __syncthreads();
     uint32_t r = (uint32_t)s_carry + rpre;  // runs started before this thread's rows
     uint32_t rid[MITEMS];
+    M = M0;  // the run so far: its end where row k starts a new run
 #pragma unroll
     for (int k = 0; k < MITEMS; ++k) {
         const int64_t i = r0 + k;
+        const bool b = (brk >> k) & 1u;
         if (i < n) {
             if (flags & (1u << k)) {
                 a.run_gs[r] = s[k];
-                if (r > 0) a.run_ge[r - 1] = Mk[k];
+                if (r > 0) a.run_ge[r - 1] = M;
                 ++r;
             }
             if (i == n - 1) {
-                a.run_ge[r - 1] = ((brk >> k) & 1u) ? e[k] : max(Mk[k], e[k]);
+                a.run_ge[r - 1] = b ? e[k] : max(M, e[k]);
                 *a.total = r;
             }
         }
+        M = b ? e[k] : max(M, e[k]);
         rid[k] = r - 1;
     }
     if (a.run_of_sorted) {

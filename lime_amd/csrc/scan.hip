@@ -86,10 +86,60 @@ __global__ __launch_bounds__(SB) void k_scan_blocks(const T *__restrict__ in, T 
     }
 }
 
+// small n: ONE launch of one 1024-thread block, looping over 16384-item
+// chunks (blocked per thread, staged through LDS): the three-launch path's
+// fixed cost (~15-20 us of back-to-back tiny kernels) dominates below ~64k
+constexpr int QB = 1024;
+constexpr int QITEMS = 16;
+constexpr int QTILE = QB * QITEMS;
+constexpr int64_t SMALL_SCAN = 4 * QTILE;
+template <typename T>
+__global__ __launch_bounds__(QB) void k_scan_small(const T *in, T *out, int64_t n, T *total) {
+    __shared__ T tile[QTILE];
+    __shared__ T scratch[QB / 64 + 1];
+    T carry = 0;
+    for (int64_t base = 0; base < n; base += QTILE) {
+#pragma unroll
+        for (int k = 0; k < QITEMS; ++k) {
+            const int64_t i = base + k * QB + threadIdx.x;
+            tile[k * QB + threadIdx.x] = i < n ? in[i] : T(0);
+        }
+        __syncthreads();
+        T v[QITEMS];
+        T s = 0;
+#pragma unroll
+        for (int k = 0; k < QITEMS; ++k) {
+            v[k] = tile[threadIdx.x * QITEMS + k];
+            s += v[k];
+        }
+        T tot;
+        T run = carry + dev::block_exclusive_sum<QB>(s, scratch, &tot);
+#pragma unroll
+        for (int k = 0; k < QITEMS; ++k) {
+            tile[threadIdx.x * QITEMS + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < QITEMS; ++k) {
+            const int64_t i = base + k * QB + threadIdx.x;
+            if (i < n) out[i] = tile[k * QB + threadIdx.x];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
 template <typename T>
 int scan_exclusive(lime_ctx *ctx, const T *in, T *out, int64_t n, T *total_dev) {
     if (n <= 0) {
         if (total_dev) LIME_HIP(hipMemsetAsync(total_dev, 0, sizeof(T), S(ctx)));
+        return LIME_OK;
+    }
+    if (n <= SMALL_SCAN) {
+        hipLaunchKernelGGL(k_scan_small<T>, dim3(1), dim3(QB), 0, S(ctx), in, out, n, total_dev);
+        LIME_HIP(hipGetLastError());
         return LIME_OK;
     }
     const int64_t nb = (n + STILE - 1) / STILE;

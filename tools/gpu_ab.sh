@@ -25,5 +25,5 @@ for i in 1 2; do for lib in "$@"; do for W in $works; do
     *) timeout -k 10 300 python tools/bench_extra.py --workload $W > $out 2>&1 ;;
   esac || { tail -20 $out; exit 1; }
   echo "$lib $W $i: $(grep '^{' $out | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['ms_per_step'],3), d.get('breakdown_ms'))")"
-  [ "${lib#new:}" != "$lib" ] && unset "${ev%%=*}"
+  if [ "${lib#new:}" != "$lib" ]; then unset "${ev%%=*}"; fi
 done; done; done

@@ -736,12 +736,15 @@ __device__ __forceinline__ uint64_t not_mask(const OpArgs &a, int64_t w, uint64_
 
 // word pairs (w, w + 1), w = w0 + 2 (t + j BB): 16-B loads, all issued
 // before any is used (0 past the window)
-constexpr int SJ = BT / (2 * BB);
+// (NT threads staging a tile of TW words; defaults: the BB x BW tiles)
+template <int NT = BB, int TW = BT>
 __device__ __forceinline__ void load_pairs(const uint64_t *__restrict__ src, int64_t w0,
-                                           int64_t nw, uint64_t (&x0)[SJ], uint64_t (&x1)[SJ]) {
+                                           int64_t nw, uint64_t (&x0)[TW / (2 * NT)],
+                                           uint64_t (&x1)[TW / (2 * NT)]) {
+    constexpr int SJ = TW / (2 * NT);
 #pragma unroll
     for (int j = 0; j < SJ; ++j) {
-        const int64_t w = w0 + 2 * (threadIdx.x + (int64_t)j * BB);
+        const int64_t w = w0 + 2 * (threadIdx.x + (int64_t)j * NT);
         if (w + 1 < nw) {
             const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(src + w);
             x0[j] = v.x;
@@ -757,10 +760,12 @@ __device__ __forceinline__ void load_pairs(const uint64_t *__restrict__ src, int
 // (img[0] = word w0 - 1).  NOT clears pad bits and bits beyond the span.
 // Every operand's 16 words per thread are loaded as 8 independent 16-B
 // loads, combined in registers, then stored to LDS once.
+template <int NT = BB, int TW = BT>
 __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned long long *img,
                                            uint32_t *s_pad, int *s_npad) {
+    constexpr int SJ = TW / (2 * NT);
     if (a.op == 1 && threadIdx.x == 0) {
-        const int64_t lo = (a.word0 + (w0 > 0 ? w0 - 1 : 0)) * 64, hi = (a.word0 + w0 + BT) * 64;
+        const int64_t lo = (a.word0 + (w0 > 0 ? w0 - 1 : 0)) * 64, hi = (a.word0 + w0 + TW) * 64;
         int64_t c = dev::lower_bound(a.pad, 0, (int64_t)a.nc, (uint32_t)min(lo, (int64_t)0xffffffff));
         int np = 0;
         for (; c < a.nc && (int64_t)a.pad[c] < hi && np < MAXPAD; ++c) s_pad[np++] = a.pad[c];
@@ -768,11 +773,11 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
     }
     const int64_t nw = a.n_words;
     uint64_t x0[SJ], x1[SJ];
-    load_pairs(a.w[0], w0, nw, x0, x1);
+    load_pairs<NT, TW>(a.w[0], w0, nw, x0, x1);
     const int nops = a.op == 4 ? a.k : (a.op >= 2 ? 2 : 1);
     for (int i = 1; i < nops; ++i) {
         uint64_t y0[SJ], y1[SJ];
-        load_pairs(a.w[i], w0, nw, y0, y1);
+        load_pairs<NT, TW>(a.w[i], w0, nw, y0, y1);
 #pragma unroll
         for (int j = 0; j < SJ; ++j) {
             x0[j] &= a.op == 3 ? ~y0[j] : y0[j];
@@ -787,7 +792,7 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
         const int npad = *s_npad;
 #pragma unroll
         for (int j = 0; j < SJ; ++j) {
-            const int64_t w = w0 + 2 * (threadIdx.x + (int64_t)j * BB);
+            const int64_t w = w0 + 2 * (threadIdx.x + (int64_t)j * NT);
             x0[j] = w < nw ? not_mask(a, w, ~x0[j], s_pad, npad) : 0ull;
             x1[j] = w + 1 < nw ? not_mask(a, w + 1, ~x1[j], s_pad, npad) : 0ull;
         }
@@ -795,7 +800,7 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
     }
 #pragma unroll
     for (int j = 0; j < SJ; ++j) {
-        const int q = 2 * (threadIdx.x + j * BB);
+        const int q = 2 * (threadIdx.x + j * NT);
         img[q + 1] = x0[j];
         img[q + 2] = x1[j];
     }
@@ -879,35 +884,47 @@ __global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w,
 // the per-tile status words (flag in bits 62-63, value below), and events
 // past the capacity only counted (the caller then falls back to two passes).
 constexpr uint64_t EV_AGG = 1ull << 62, EV_INC = 2ull << 62, EV_VAL = (1ull << 62) - 1;
-constexpr int EVCAP = 4096;  // events of a tile staged in LDS (3 blocks per CU)
+// Tile geometry of the one-pass extraction: EV_NT threads x EV_W words.
+// Fewer, larger tiles mean fewer serial look-backs (as for k_merge_scan)
+#ifndef LIME_EV_NT
+#define LIME_EV_NT 256
+#endif
+#ifndef LIME_EV_W
+#define LIME_EV_W 16
+#endif
+#ifndef LIME_EVCAP
+#define LIME_EVCAP 4096
+#endif
+constexpr int EV_NT = LIME_EV_NT, EV_W = LIME_EV_W, EV_TW = EV_NT * EV_W;
+constexpr int EVCAP = LIME_EVCAP;  // events of a tile staged in LDS
 
-__global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict__ status,
+__global__ __launch_bounds__(EV_NT) void k_ev_fused(OpArgs a, uint64_t *__restrict__ status,
                                                  unsigned int *__restrict__ ticket,
                                                  int64_t cap_events, uint32_t *__restrict__ rgs,
                                                  uint32_t *__restrict__ rge,
                                                  unsigned long long *__restrict__ total) {
-    __shared__ unsigned long long img[BT + 1];
+    __shared__ unsigned long long img[EV_TW + 1];
     __shared__ uint32_t s_pad[MAXPAD];
     __shared__ int s_npad;
-    __shared__ uint32_t scratch[BB / 64 + 1];
+    __shared__ uint32_t scratch[EV_NT / 64 + 1];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_excl;
     __shared__ uint32_t s_ev[EVCAP];
     if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t tile = s_tile;
-    const int64_t w0 = (int64_t)tile * BT;
-    stage_tile(a, w0, img, s_pad, &s_npad);
-    const int q0 = threadIdx.x * BW;
+    const int64_t w0 = (int64_t)tile * EV_TW;
+    stage_tile<EV_NT, EV_TW>(a, w0, img, s_pad, &s_npad);
+    const int q0 = threadIdx.x * EV_W;
     uint32_t c = 0;
 #pragma unroll
-    for (int k = 0; k < BW; ++k) {
+    for (int k = 0; k < EV_W; ++k) {
         uint64_t st, en;
         events_of(img[q0 + k + 1], img[q0 + k], st, en);
         c += __popcll(st) + __popcll(en);
     }
     uint32_t tot;
-    const uint32_t mine = dev::block_exclusive_sum<BB>(c, scratch, &tot);
+    const uint32_t mine = dev::block_exclusive_sum<EV_NT>(c, scratch, &tot);
     if (threadIdx.x < 64) {  // one wave publishes and looks back
         const int lane = dev::lane_id();
         if (tile == 0) {
@@ -955,7 +972,7 @@ __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict_
     uint64_t ev = excl + mine;
     uint32_t le = mine;
 #pragma unroll
-    for (int k = 0; k < BW; ++k) {
+    for (int k = 0; k < EV_W; ++k) {
         uint64_t st, en;
         events_of(img[q0 + k + 1], img[q0 + k], st, en);
         uint64_t all = st | en;
@@ -977,7 +994,7 @@ __global__ __launch_bounds__(BB) void k_ev_fused(OpArgs a, uint64_t *__restrict_
     }
     if (!staged) return;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += BB) {
+    for (uint32_t i = threadIdx.x; i < tot; i += EV_NT) {
         const uint64_t e = excl + i;
         if ((int64_t)e < cap_events) {
             if (e & 1u)
@@ -1318,17 +1335,18 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     }
     const int64_t bound = op == 1 ? a->runs_bound + a->n_contigs + 1 : sum + 1;
     if (known && nt > 0 && bound < (int64_t)0x7fffffff) {
+        const int64_t ntf = a->n_words / EV_TW + 1;  // the fused pass's (larger) tiles
         uint64_t *status;
         unsigned int *ticket;
         unsigned long long *tot64;
-        LIME_TRY(alloc(ctx, &status, (size_t)nt));
+        LIME_TRY(alloc(ctx, &status, (size_t)ntf));
         LIME_TRY(alloc(ctx, &ticket, 1));
         LIME_TRY(alloc(ctx, &tot64, 1));
         LIME_TRY(alloc(ctx, &res->gs, (size_t)bound));
         LIME_TRY(alloc(ctx, &res->ge, (size_t)bound));
-        LIME_HIP(hipMemsetAsync(status, 0, sizeof(uint64_t) * (size_t)nt, S(ctx)));
+        LIME_HIP(hipMemsetAsync(status, 0, sizeof(uint64_t) * (size_t)ntf, S(ctx)));
         LIME_HIP(hipMemsetAsync(ticket, 0, sizeof(unsigned int), S(ctx)));
-        hipLaunchKernelGGL(k_ev_fused, dim3((unsigned)nt), dim3(BB), 0, S(ctx), oa, status,
+        hipLaunchKernelGGL(k_ev_fused, dim3((unsigned)ntf), dim3(EV_NT), 0, S(ctx), oa, status,
                            ticket, 2 * bound, res->gs, res->ge, tot64);
         LIME_HIP(hipGetLastError());
         unsigned long long nev = 0;

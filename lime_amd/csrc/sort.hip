@@ -424,8 +424,17 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
                                                 uint32_t ntiles, uint32_t *__restrict__ key_out,
                                                 uint32_t *__restrict__ ge_out,
                                                 uint32_t *__restrict__ row_out,
-                                                const uint32_t *__restrict__ off = nullptr) {
+                                                const uint32_t *__restrict__ off = nullptr,
+                                                int32_t nc = 0) {
     __shared__ uint32_t cnt[RWAVES][RBINS];
+    // RAW: the contig table staged in LDS (<= PCMAX contigs), so the per-row
+    // off[contig] gather is an LDS read, not a dependent cache round trip
+    __shared__ uint32_t s_off[RAW ? PCMAX : 1];
+    if (RAW && nc <= PCMAX) {
+        for (int i = threadIdx.x; i < nc; i += RB) s_off[i] = off[i];
+        __syncthreads();
+    }
+    const uint32_t *offp = RAW && nc <= PCMAX ? s_off : off;
     __shared__ uint32_t dstart[RBINS];
     __shared__ uint32_t gbase[RBINS];
     __shared__ uint32_t scratch[RWAVES + 1];
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         const bool valid = o < lim;
         if (RAW) {  // validated by k_prep: every contig id is in range
             const uint32_t c = valid ? kin[o] : 0u;
-            const uint32_t base = valid ? off[c] : 0u;
+            const uint32_t base = valid ? offp[c] : 0u;
             vk[k] = valid ? base + ein[o] : 0u;
             ve[k] = valid ? base + rin[o] : 0u;
         } else {
@@ -563,14 +572,14 @@ template <int M>
 void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                  const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
                  uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows, int &rc,
-                 const uint32_t *raw_off = nullptr) {
+                 const uint32_t *raw_off = nullptr, int32_t raw_nc = 0) {
     if (raw_off) {  // first gs pass straight from the caller's rows (k_prep's histogram)
         if ((rc = scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr)) != LIME_OK)
             return;
         if (M == M_GS && rows == ROWS_IDENT)
             hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, true>), dim3(ntiles), dim3(RB), 0,
                                S(ctx), k0, e0, r0, n, shift, st, (const uint32_t *)mat, ntiles, k1,
-                               e1, r1, raw_off);
+                               e1, r1, raw_off, raw_nc);
         return;
     }
     if (!have_hist)
@@ -592,11 +601,11 @@ void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint
 int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
                uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows,
-               const uint32_t *raw_off = nullptr) {
+               const uint32_t *raw_off = nullptr, int32_t raw_nc = 0) {
     int rc = LIME_OK;
     if (raw_off) {
         launch_pass<M_GS>(ctx, shift, true, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc,
-                          raw_off);
+                          raw_off, raw_nc);
         if (rc != LIME_OK) return rc;
         LIME_HIP(hipGetLastError());
         return LIME_OK;
@@ -864,9 +873,14 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
                         set->min_shift == 0;
     bool raw = false;
     if (n > 0 && raw_ok) {
-        hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
-                           d_start, d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n,
-                           k0, e0, nullptr, part, mat, ntiles, 0);
+        if (set->n_contigs <= PCMAX)
+            hipLaunchKernelGGL((k_prep<false, false, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                               d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, 0);
+        else
+            hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
+                               d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, 0);
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());
@@ -947,7 +961,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
                 LIME_TRY(radix_pass(ctx, p.first, p.second, true, n,
                                     reinterpret_cast<const uint32_t *>(d_contig), d_start, d_end,
                                     set->strand_in, k1, e1, r1, mat, ntiles, rows,
-                                    (const uint32_t *)set->d_off));
+                                    (const uint32_t *)set->d_off, set->n_contigs));
             } else {
                 LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in,
                                     k1, e1, r1, mat, ntiles, rows));

@@ -255,6 +255,8 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
     stage_contigs<LC>(a, coff, nullptr, BINB);
     __syncthreads();
     const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
+    // the matrix's extra last entry (it receives the total from the scan)
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.mat[(int64_t)a.nb * a.nchunks] = 0u;
     const int64_t r0 = (int64_t)ch * a.chunk_rows;
     const int64_t r1 = min(a.n, r0 + a.chunk_rows);
     for (int64_t base = r0; base < r1; base += STEP) {
@@ -562,9 +564,12 @@ __global__ __launch_bounds__(BB) void k_xcount(const uint64_t *__restrict__ cros
     }
 }
 
+// piece slots: the tile's scanned start xoff[t] + a claim on xfill[t]
+// (zeroed with the counters: no copy of the scanned starts to a cursor)
 __global__ __launch_bounds__(BB) void k_xwrite(const uint64_t *__restrict__ cross,
                                                const unsigned int *__restrict__ ncross,
-                                               uint32_t *__restrict__ xcur,
+                                               const uint32_t *__restrict__ xoff,
+                                               uint32_t *__restrict__ xfill,
                                                uint2 *__restrict__ xl) {
     const int64_t nx = *ncross;
     for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < nx; i += (int64_t)gridDim.x * BB) {
@@ -572,10 +577,11 @@ __global__ __launch_bounds__(BB) void k_xwrite(const uint64_t *__restrict__ cros
         const uint32_t t0 = (uint32_t)(s >> PSH), t1 = (uint32_t)((e - 1) >> PSH);
         const uint64_t b0 = (uint64_t)t0 << PSH;
         const uint64_t h = t1 > t0 ? b0 + (1ull << PSH) : e;  // head [s, h) in tile t0
-        xl[atomicAdd(&xcur[t0], 1u)] = make_uint2((uint32_t)(s - b0), (uint32_t)(h - b0));
+        xl[xoff[t0] + atomicAdd(&xfill[t0], 1u)] =
+            make_uint2((uint32_t)(s - b0), (uint32_t)(h - b0));
         if (t1 > t0) {
             const uint64_t b1 = (uint64_t)t1 << PSH;
-            xl[atomicAdd(&xcur[t1], 1u)] = make_uint2(0u, (uint32_t)(e - b1));
+            xl[xoff[t1] + atomicAdd(&xfill[t1], 1u)] = make_uint2(0u, (uint32_t)(e - b1));
         }
     }
 }
@@ -736,6 +742,13 @@ __device__ __forceinline__ uint64_t not_mask(const OpArgs &a, int64_t w, uint64_
 
 // word pairs (w, w + 1), w = w0 + 2 (t + j BB): 16-B loads, all issued
 // before any is used (0 past the window)
+// Tile images in LDS hold word q of [w0 - 1, w0 + TW) at ipad(q): one pad
+// word after every 16, so the blocked readers (thread t: words 16 t ..
+// 16 t + 16, a 128-B lane stride) spread over the banks instead of all
+// hitting one (SQ_LDS_BANK_CONFLICT was 69% of the extraction's LDS cycles)
+__device__ __forceinline__ int ipad(int q) { return q + (q >> 4); }
+constexpr int img_words(int tw) { return tw + 1 + (tw + 1) / 16 + 1; }
+
 // (NT threads staging a tile of TW words; defaults: the BB x BW tiles)
 template <int NT = BB, int TW = BT>
 __device__ __forceinline__ void load_pairs(const uint64_t *__restrict__ src, int64_t w0,
@@ -801,15 +814,15 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
 #pragma unroll
     for (int j = 0; j < SJ; ++j) {
         const int q = 2 * (threadIdx.x + j * NT);
-        img[q + 1] = x0[j];
-        img[q + 2] = x1[j];
+        img[ipad(q + 1)] = x0[j];
+        img[ipad(q + 2)] = x1[j];
     }
     if (threadIdx.x == 0) img[0] = xb;
     __syncthreads();
 }
 
 __global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict__ tcnt) {
-    __shared__ unsigned long long img[BT + 1];
+    __shared__ unsigned long long img[img_words(BT)];
     __shared__ uint32_t s_pad[MAXPAD];
     __shared__ int s_npad;
     __shared__ uint32_t ws[BB / 64];
@@ -818,7 +831,7 @@ __global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict_
     uint32_t c = 0;
     for (int i = threadIdx.x; i < BT; i += BB) {
         uint64_t st, en;
-        events_of(img[i + 1], img[i], st, en);
+        events_of(img[ipad(i + 1)], img[ipad(i)], st, en);
         c += __popcll(st) + __popcll(en);
     }
     c = dev::wave_reduce_sum(c);
@@ -834,7 +847,7 @@ __global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict_
 __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__restrict__ toff,
                                                  uint32_t *__restrict__ rgs,
                                                  uint32_t *__restrict__ rge) {
-    __shared__ unsigned long long img[BT + 1];
+    __shared__ unsigned long long img[img_words(BT)];
     __shared__ uint32_t s_pad[MAXPAD];
     __shared__ int s_npad;
     __shared__ uint32_t scratch[BB / 64 + 1];
@@ -846,7 +859,7 @@ __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__res
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
         uint64_t st, en;
-        events_of(img[q0 + k + 1], img[q0 + k], st, en);
+        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
         c += __popcll(st) + __popcll(en);
     }
     uint32_t tot;
@@ -854,7 +867,7 @@ __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__res
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
         uint64_t st, en;
-        events_of(img[q0 + k + 1], img[q0 + k], st, en);
+        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
         uint64_t all = st | en;
         const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
         while (all) {
@@ -903,7 +916,7 @@ __global__ __launch_bounds__(EV_NT) void k_ev_fused(OpArgs a, uint64_t *__restri
                                                  int64_t cap_events, uint32_t *__restrict__ rgs,
                                                  uint32_t *__restrict__ rge,
                                                  unsigned long long *__restrict__ total) {
-    __shared__ unsigned long long img[EV_TW + 1];
+    __shared__ unsigned long long img[img_words(EV_TW)];
     __shared__ uint32_t s_pad[MAXPAD];
     __shared__ int s_npad;
     __shared__ uint32_t scratch[EV_NT / 64 + 1];
@@ -920,7 +933,7 @@ __global__ __launch_bounds__(EV_NT) void k_ev_fused(OpArgs a, uint64_t *__restri
 #pragma unroll
     for (int k = 0; k < EV_W; ++k) {
         uint64_t st, en;
-        events_of(img[q0 + k + 1], img[q0 + k], st, en);
+        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
         c += __popcll(st) + __popcll(en);
     }
     uint32_t tot;
@@ -974,7 +987,7 @@ __global__ __launch_bounds__(EV_NT) void k_ev_fused(OpArgs a, uint64_t *__restri
 #pragma unroll
     for (int k = 0; k < EV_W; ++k) {
         uint64_t st, en;
-        events_of(img[q0 + k + 1], img[q0 + k], st, en);
+        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
         uint64_t all = st | en;
         const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
         while (all) {
@@ -1064,7 +1077,7 @@ int n_bins(int64_t width) {
 int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
              const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
              const uint32_t *d_len, int64_t lo, int64_t hi, uint32_t *slab2, uint32_t *ttot,
-             uint64_t *cross, unsigned int *flags) {
+             uint64_t *cross, unsigned int *flags, bool ttot_zeroed = false) {
     const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
     // chunk: ~2 chunks per CU, 1..16 steps of 16 rows per lane
@@ -1078,13 +1091,11 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     LIME_TRY(bag.get(&mat, (size_t)mlen));
     LIME_TRY(bag.get(&slab, (size_t)std::max<int64_t>(n, 1)));
     LIME_TRY(bag.get(&dummy, 64));
-    LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
+    if (!ttot_zeroed) LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
     if (n == 0) {
         LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
         return LIME_OK;
     }
-    // the total's slot (k_bin_count writes the nb * nch counts before it)
-    LIME_HIP(hipMemsetAsync(mat + mlen - 1, 0, 4, S(ctx)));
     BinArgs a;
     a.contig = d_contig;
     a.start = d_start;
@@ -1219,6 +1230,11 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
         aa.init = g0 > 0;
         aa.words = bs->words;
         aa.n_words = bs->n_words;
+        // the group's tile totals: one block, zeroed once
+        uint32_t *ttot_all;
+        const size_t tstride = (size_t)nt + 1;
+        LIME_TRY(bag.get(&ttot_all, tstride * (size_t)kg));
+        LIME_HIP(hipMemsetAsync(ttot_all, 0, 4 * tstride * (size_t)kg, S(ctx)));
         // bucket set q's cross pieces by tile (its flags were copied to the
         // host behind its binning; wait for that copy only)
         auto bucket = [&](int q) -> int {
@@ -1227,24 +1243,22 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
             const unsigned int nx = hflags[2 * q], err = hflags[2 * q + 1];
             LIME_TRY(rows_error(err));
             if (nx == 0) return LIME_OK;
-            uint32_t *xcnt, *diff, *xcur;
+            // [counts | difference array | fill claims], zeroed at once
+            uint32_t *xb;
             uint2 *xl;
-            LIME_TRY(bag.get(&xcnt, (size_t)nt + 1));
-            LIME_TRY(bag.get(&diff, (size_t)nt + 1));
-            LIME_TRY(bag.get(&xcur, (size_t)nt + 1));
+            LIME_TRY(bag.get(&xb, 3 * tstride));
             LIME_TRY(bag.get(&xl, 2 * (size_t)nx));
-            LIME_HIP(hipMemsetAsync(xcnt, 0, 4 * ((size_t)nt + 1), S(ctx)));
-            LIME_HIP(hipMemsetAsync(diff, 0, 4 * ((size_t)nt + 1), S(ctx)));
+            uint32_t *xcnt = xb, *diff = xb + tstride, *xfill = xb + 2 * tstride;
+            LIME_HIP(hipMemsetAsync(xb, 0, 4 * 3 * tstride, S(ctx)));
             const unsigned g = std::min<unsigned>(blocks_for(nx, BB), 2048u);
             const uint64_t *cx = cross[q % 2];
             hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), cx,
                                (const unsigned int *)(flags + 2 * i), xcnt, diff);
-            LIME_TRY(scan_exclusive_u32(ctx, xcnt, xcnt, (int64_t)nt + 1, nullptr));
-            LIME_TRY(scan_exclusive_u32(ctx, diff, diff, (int64_t)nt + 1, nullptr));
-            LIME_HIP(hipMemcpyAsync(xcur, xcnt, 4 * ((size_t)nt + 1), hipMemcpyDeviceToDevice,
-                                    S(ctx)));
+            LIME_TRY(scan_exclusive_u32_pair(ctx, xcnt, xcnt, (int64_t)tstride, diff, diff,
+                                             (int64_t)tstride));
             hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), cx,
-                               (const unsigned int *)(flags + 2 * i), xcur, xl);
+                               (const unsigned int *)(flags + 2 * i), (const uint32_t *)xcnt,
+                               xfill, xl);
             LIME_HIP(hipGetLastError());
             aa.xl[q] = xl;
             aa.xoff[q] = xcnt;
@@ -1253,12 +1267,11 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
         };
         for (int q = 0; q < kg; ++q) {
             const int i = g0 + q;
-            uint32_t *slab2, *ttot;
+            uint32_t *slab2, *ttot = ttot_all + tstride * (size_t)q;
             LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
-            LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
             // (cross[q % 2] was last used by set q - 2, bucketed before this)
             LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo,
-                              hi, slab2, ttot, cross[q % 2], flags + 2 * i));
+                              hi, slab2, ttot, cross[q % 2], flags + 2 * i, true));
             LIME_HIP(hipMemcpyAsync(hflags + 2 * q, flags + 2 * i, 8, hipMemcpyDeviceToHost,
                                     S(ctx)));
             LIME_HIP(hipEventRecord(ev.e[q % 2], S(ctx)));

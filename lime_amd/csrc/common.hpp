@@ -174,6 +174,8 @@ int sort_set(lime_ctx *ctx, lime_set *set, const int32_t *d_contig, const uint32
              const uint32_t *d_end, const uint32_t *d_len);
 int scan_exclusive_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n,
                        uint32_t *total_dev);
+int scan_exclusive_u32_pair(lime_ctx *ctx, const uint32_t *in0, uint32_t *out0, int64_t n0,
+                            const uint32_t *in1, uint32_t *out1, int64_t n1);
 int scan_exclusive_u64(lime_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n,
                        uint64_t *total_dev);
 int build_prefix_max(lime_ctx *ctx, const lime_set *set);

@@ -94,7 +94,22 @@ constexpr int QITEMS = 16;
 constexpr int QTILE = QB * QITEMS;
 constexpr int64_t SMALL_SCAN = 4 * QTILE;
 template <typename T>
+__device__ __forceinline__ void scan_small_block(const T *in, T *out, int64_t n, T *total);
+template <typename T>
 __global__ __launch_bounds__(QB) void k_scan_small(const T *in, T *out, int64_t n, T *total) {
+    scan_small_block(in, out, n, total);
+}
+// two independent small scans in one launch (block b scans array b)
+template <typename T>
+__global__ __launch_bounds__(QB) void k_scan_small2(const T *in0, T *out0, int64_t n0,
+                                                    const T *in1, T *out1, int64_t n1) {
+    if (blockIdx.x == 0)
+        scan_small_block(in0, out0, n0, (T *)nullptr);
+    else
+        scan_small_block(in1, out1, n1, (T *)nullptr);
+}
+template <typename T>
+__device__ __forceinline__ void scan_small_block(const T *in, T *out, int64_t n, T *total) {
     __shared__ T tile[QTILE];
     __shared__ T scratch[QB / 64 + 1];
     T carry = 0;
@@ -159,6 +174,18 @@ int scan_exclusive(lime_ctx *ctx, const T *in, T *out, int64_t n, T *total_dev) 
 int scan_exclusive_u32(lime_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n,
                        uint32_t *total_dev) {
     return scan_exclusive<uint32_t>(ctx, in, out, n, total_dev);
+}
+// two exclusive u32 scans, in one launch when both are small
+int scan_exclusive_u32_pair(lime_ctx *ctx, const uint32_t *in0, uint32_t *out0, int64_t n0,
+                            const uint32_t *in1, uint32_t *out1, int64_t n1) {
+    if (n0 > 0 && n1 > 0 && n0 <= SMALL_SCAN && n1 <= SMALL_SCAN) {
+        hipLaunchKernelGGL(k_scan_small2<uint32_t>, dim3(2), dim3(QB), 0, S(ctx), in0, out0, n0,
+                           in1, out1, n1);
+        LIME_HIP(hipGetLastError());
+        return LIME_OK;
+    }
+    LIME_TRY(scan_exclusive<uint32_t>(ctx, in0, out0, n0, nullptr));
+    return scan_exclusive<uint32_t>(ctx, in1, out1, n1, nullptr);
 }
 int scan_exclusive_u64(lime_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n,
                        uint64_t *total_dev) {

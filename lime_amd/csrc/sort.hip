@@ -103,13 +103,15 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t ntiles) {
     return x * q + (x < r ? x : r) + i;
 }
 
+// (tile = the block's tile: consecutive tiles on one XCD, so the digit-major
+// column stores of neighbouring tiles complete each other's lines in its L2)
 __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *counts,
-                                           uint32_t ntiles) {
+                                           uint32_t ntiles, uint32_t tile) {
     for (int d = threadIdx.x; d < RBINS; d += RB) {
         uint32_t t = 0;
 #pragma unroll
         for (int ww = 0; ww < RWAVES; ++ww) t += hist[ww][d];
-        counts[(int64_t)d * ntiles + blockIdx.x] = t;
+        counts[(int64_t)d * ntiles + tile] = t;
     }
 }
 
@@ -148,7 +150,8 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     }
     const uint32_t *off = LC ? s_off : goff, *len = LC ? s_len : glen;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
-    const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
+    const uint32_t tile = xcd_swizzle(blockIdx.x, ntiles);
+    const int64_t base = (int64_t)tile * RTILE + w * WITEMS;
     uint32_t err = 0, mx = 0, mnw = 0xffffffffu, mxw = 0, zero = 0, uns = 0;
     uint32_t vk[RITEMS], ve[RITEMS];
     bool valid[RITEMS];
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     uns = dev::wave_reduce_or(uns);
     if (lane == 0) ws[w] = SetStats{err, mx, mnw, mxw, zero, uns, {0, 0}};
     __syncthreads();
-    flush_hist(hist, counts, ntiles);
+    flush_hist(hist, counts, ntiles, tile);
     if (threadIdx.x == 0) {
         SetStats s = ws[0];
         for (int i = 1; i < RWAVES; ++i) {
@@ -361,7 +364,8 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     __shared__ uint32_t hist[RWAVES][RBINS];
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
-    const int64_t base = (int64_t)blockIdx.x * RTILE + w * WITEMS;
+    const uint32_t tile = xcd_swizzle(blockIdx.x, ntiles);
+    const int64_t base = (int64_t)tile * RTILE + w * WITEMS;
     constexpr bool NEED_E = M == M_NZ || M == M_GE;
     uint32_t vk[RITEMS], ve[RITEMS], vr[RITEMS];
     bool valid[RITEMS];
@@ -409,7 +413,7 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     for (int k = 0; k < RITEMS; ++k)
         if (valid[k]) atomicAdd(&hist[w][digit_of<M>(vk[k], ve[k], vr[k], shift, st)], 1u);
     __syncthreads();
-    flush_hist(hist, counts, ntiles);
+    flush_hist(hist, counts, ntiles, tile);
 }
 
 // RAW (first pass over caller rows only): key_in / ge_in / row_in are the

@@ -701,7 +701,7 @@ struct OpArgs {
     int64_t n_words;
     int64_t word0;        // global index of word 0 (a shard's window)
     int64_t span;
-    const uint32_t *pad;  // pad bit position of every contig (sorted), nc entries
+    const uint32_t *off;  // contig offsets (nc + 1): contig c's pad bit is off[c + 1] - 1
     int32_t nc;
 };
 
@@ -779,9 +779,11 @@ __device__ __forceinline__ void stage_tile(const OpArgs &a, int64_t w0, unsigned
     constexpr int SJ = TW / (2 * NT);
     if (a.op == 1 && threadIdx.x == 0) {
         const int64_t lo = (a.word0 + (w0 > 0 ? w0 - 1 : 0)) * 64, hi = (a.word0 + w0 + TW) * 64;
-        int64_t c = dev::lower_bound(a.pad, 0, (int64_t)a.nc, (uint32_t)min(lo, (int64_t)0xffffffff));
+        // first contig whose pad bit off[c + 1] - 1 is >= lo
+        int64_t c = dev::lower_bound(a.off + 1, 0, (int64_t)a.nc, (uint64_t)lo + 1);
         int np = 0;
-        for (; c < a.nc && (int64_t)a.pad[c] < hi && np < MAXPAD; ++c) s_pad[np++] = a.pad[c];
+        for (; c < a.nc && (int64_t)a.off[c + 1] - 1 < hi && np < MAXPAD; ++c)
+            s_pad[np++] = a.off[c + 1] - 1;
         *s_npad = np;
     }
     const int64_t nw = a.n_words;
@@ -1318,21 +1320,15 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     oa.word0 = a->word0;
     oa.span = a->hi_bit;  // NOT clears every bit past the window
     oa.nc = a->n_contigs;
-    // pad positions: off[c+1] - 1
-    std::vector<uint32_t> pad(a->n_contigs);
-    for (int c = 0; c < a->n_contigs; ++c) pad[c] = a->off[c + 1] - 1;
-    uint32_t *d_pad;
-    LIME_TRY(alloc(ctx, &d_pad, pad.size() + 1));
-    if (!pad.empty()) {
-        LIME_HIP(hipMemcpyAsync(d_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice, S(ctx)));
-        LIME_HIP(hipStreamSynchronize(S(ctx)));
-    }
-    oa.pad = d_pad;
+    // pad positions off[c + 1] - 1, from the context's cached offsets (no
+    // upload, no stream drain per call)
+    const uint32_t *d_off = nullptr;
+    LIME_TRY(space_device(ctx, a->off, &d_off, nullptr));
+    oa.off = d_off;
     // tiles cover one word past the last: a run reaching the window's end
     // closes there (a shard window may end on any word)
     const int64_t nt = a->n_words == 0 ? 0 : a->n_words / BT + 1;
     if (nt == 0) {  // an empty window (e.g. a zero-width shard): no runs
-        release(ctx, d_pad);
         LIME_TRY(alloc(ctx, &res->gs, 1));
         LIME_TRY(alloc(ctx, &res->ge, 1));
         res->n = 0;
@@ -1347,7 +1343,10 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
         sum += sets[i]->runs_bound;
     }
     const int64_t bound = op == 1 ? a->runs_bound + a->n_contigs + 1 : sum + 1;
-    if (known && nt > 0 && bound < (int64_t)0x7fffffff) {
+    // LIME_EV_TWOPASS=1: the count + scan + write passes even when the bound
+    // is known (measurement)
+    static const bool twopass = getenv("LIME_EV_TWOPASS") && atoi(getenv("LIME_EV_TWOPASS")) == 1;
+    if (known && nt > 0 && bound < (int64_t)0x7fffffff && !twopass) {
         const int64_t ntf = a->n_words / EV_TW + 1;  // the fused pass's (larger) tiles
         uint64_t *status;
         unsigned int *ticket;
@@ -1368,8 +1367,7 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
         release(ctx, ticket);
         release(ctx, tot64);
         if ((int64_t)nev <= 2 * bound) {
-            release(ctx, d_pad);
-            if (nev & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
+                if (nev & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
             const int64_t nr = (int64_t)nev / 2;
             if (nr < bound / 2) {  // keep the result's memory to its size
                 uint32_t *gs, *ge;
@@ -1412,7 +1410,6 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     release(ctx, tcnt);
     release(ctx, toff);
     release(ctx, total);
-    release(ctx, d_pad);
     res->n = nr;
     return LIME_OK;
 }

@@ -219,18 +219,32 @@ static int d2h(lime_ctx *ctx, std::vector<T> &v, const T *d, int64_t n) {
     return LIME_OK;
 }
 
-static int upload_space(lime_ctx *ctx, const lime_space *sp, uint32_t **d_off, uint32_t **d_len) {
-    LIME_TRY(alloc(ctx, d_off, (size_t)sp->n + 1));
-    std::vector<uint32_t> len32(sp->n + 1, 0);
-    for (int c = 0; c < sp->n; ++c) len32[c] = (uint32_t)sp->len[c];
-    LIME_HIP(hipMemcpyAsync(*d_off, sp->off.data(), 4 * ((size_t)sp->n + 1), hipMemcpyHostToDevice,
-                            S(ctx)));
-    if (d_len) {
-        LIME_TRY(alloc(ctx, d_len, (size_t)sp->n + 1));
-        LIME_HIP(hipMemcpyAsync(*d_len, len32.data(), 4 * ((size_t)sp->n + 1),
-                                hipMemcpyHostToDevice, S(ctx)));
+int space_device(lime_ctx *ctx, const std::vector<uint32_t> &off, const uint32_t **d_off,
+                 const uint32_t **d_len) {
+    auto it = ctx->spaces.find(off);
+    if (it == ctx->spaces.end()) {
+        const size_t n1 = off.size();
+        uint32_t *o = nullptr, *l = nullptr;
+        LIME_TRY(alloc(ctx, &o, n1));
+        LIME_TRY(alloc(ctx, &l, n1));
+        std::vector<uint32_t> len32(n1, 0);
+        for (size_t c = 0; c + 1 < n1; ++c) len32[c] = off[c + 1] - off[c] - 1;
+        LIME_HIP(hipMemcpyAsync(o, off.data(), 4 * n1, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipMemcpyAsync(l, len32.data(), 4 * n1, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipStreamSynchronize(S(ctx)));  // (once per space and context)
+        it = ctx->spaces.emplace(off, std::make_pair(o, l)).first;
     }
-    LIME_HIP(hipStreamSynchronize(S(ctx)));
+    *d_off = it->second.first;
+    if (d_len) *d_len = it->second.second;
+    return LIME_OK;
+}
+
+// the space's cached device arrays (borrowed: owned by the context)
+static int upload_space(lime_ctx *ctx, const lime_space *sp, uint32_t **d_off, uint32_t **d_len) {
+    const uint32_t *o = nullptr, *l = nullptr;
+    LIME_TRY(space_device(ctx, sp->off, &o, d_len ? &l : nullptr));
+    *d_off = const_cast<uint32_t *>(o);
+    if (d_len) *d_len = const_cast<uint32_t *>(l);
     return LIME_OK;
 }
 
@@ -256,11 +270,9 @@ static int create_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
     s->strand_uniform = strand_uniform;
     s->min_shift = min_shift;
     uint32_t *d_len = nullptr;
-    int rc = upload_space(ctx, sp, &s->d_off, &d_len);
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len);  // (borrowed)
     if (rc == LIME_OK) rc = sort_set(ctx, s, d_contig, d_start, d_end, d_len);
-    release(ctx, d_len);
     if (rc != LIME_OK) {
-        release(ctx, s->d_off);
         release(ctx, s->strand_in);
         delete s;
         return rc;
@@ -509,7 +521,7 @@ int lime_set_destroy(lime_set *s) {
     release(ctx, s->gs);
     release(ctx, s->ge);
     release(ctx, s->row);
-    release(ctx, s->d_off);
+    // (s->d_off is the context's cached space array: not released)
     release(ctx, s->pmax);
     release(ctx, s->strand_in);
     delete s;
@@ -535,11 +547,9 @@ int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const
     hipSetDevice(ctx->device);
     lime_set *s = new_set(ctx, sp, n);
     uint32_t *d_len = nullptr;
-    int rc = upload_space(ctx, sp, &s->d_off, &d_len);
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len);  // (borrowed)
     if (rc == LIME_OK) rc = sort_set_global(ctx, s, d_gs, d_ge, d_row, d_len);
-    release(ctx, d_len);
     if (rc != LIME_OK) {
-        release(ctx, s->d_off);
         delete s;
         return rc;
     }
@@ -861,8 +871,7 @@ int lime_complement(lime_ctx *ctx, const lime_space *genome, const lime_set *a, 
     int rc = complement_run(ctx, &runs, d_off, d_len, genome->n, r);
     release(ctx, runs.gs);
     release(ctx, runs.ge);
-    release(ctx, d_off);
-    release(ctx, d_len);
+
     if (rc != LIME_OK) {
         delete r;
         return rc;
@@ -1016,9 +1025,7 @@ int lime_bitset_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
     hipSetDevice(ctx->device);
     // rows binned by tile in one counting scatter, painted tile by tile
     uint32_t *d_off = nullptr, *d_len = nullptr;
-    LIME_TRY(upload_space(ctx, sp, &d_off, &d_len));
-    PoolGuard<uint32_t> g0{ctx, d_off};
-    PoolGuard<uint32_t> g1{ctx, d_len};
+    LIME_TRY(upload_space(ctx, sp, &d_off, &d_len));  // (borrowed)
     lime_bitset *bs = new lime_bitset();
     bs->ctx = ctx;
     bs->n_contigs = sp->n;
@@ -1074,9 +1081,7 @@ static int bitset_and_entry(lime_ctx *ctx, const lime_space *sp, int64_t lo, int
     }
     hipSetDevice(ctx->device);
     uint32_t *d_off = nullptr, *d_len = nullptr;
-    if (!global) LIME_TRY(upload_space(ctx, sp, &d_off, &d_len));
-    PoolGuard<uint32_t> g0{ctx, d_off};
-    PoolGuard<uint32_t> g1{ctx, d_len};
+    if (!global) LIME_TRY(upload_space(ctx, sp, &d_off, &d_len));  // (borrowed)
     std::vector<const int32_t *> contig(k, nullptr);
     if (!global)
         for (int i = 0; i < k; ++i) contig[i] = d_contig[i];

@@ -68,6 +68,10 @@ struct lime_ctx {
     std::mutex mu;
     // small pinned scratch for scalar read-backs
     void *pinned = nullptr;
+    // device copies of every space's (off, len) used with this context, keyed
+    // by the offsets (which determine the lengths): uploaded once, so an
+    // operator never drains the stream to upload them (space_device)
+    std::map<std::vector<uint32_t>, std::pair<uint32_t *, uint32_t *>> spaces;
     hipEvent_t ev = nullptr;
 };
 
@@ -162,6 +166,11 @@ struct PoolGuard {
 
 // read a device scalar back to the host (synchronises the context stream)
 int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes);
+
+// the context's device copy of a space's contig offsets (n + 1 entries) and
+// lengths (n + 1, the last 0), owned by the context: never released by callers
+int space_device(lime_ctx *c, const std::vector<uint32_t> &off, const uint32_t **d_off,
+                 const uint32_t **d_len);
 
 // grid helper
 inline unsigned blocks_for(int64_t n, int64_t per_block) {

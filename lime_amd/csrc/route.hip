@@ -168,28 +168,20 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
         if (splits[r + 1] < splits[r]) return fail(LIME_ERR_ARG, "splits must be non-decreasing");
     const uint32_t nblk = (uint32_t)std::max<int64_t>((n + RBLK - 1) / RBLK, 1);
     const int64_t mlen = (int64_t)nsh * nblk + 1;
-    uint32_t *mat = nullptr, *d_split = nullptr, *d_off = nullptr, *d_len = nullptr;
+    uint32_t *mat = nullptr, *d_split = nullptr;
+    const uint32_t *d_off = nullptr, *d_len = nullptr;  // the context's cached space arrays
     unsigned int *err = nullptr;
     int64_t *tot = nullptr;
     LIME_TRY(alloc(ctx, &mat, (size_t)mlen));
     PoolGuard<uint32_t> g0{ctx, mat};
     LIME_TRY(alloc(ctx, &d_split, (size_t)nsh + 1));
     PoolGuard<uint32_t> g1{ctx, d_split};
-    LIME_TRY(alloc(ctx, &d_off, (size_t)sp->n + 1));
-    PoolGuard<uint32_t> g2{ctx, d_off};
-    LIME_TRY(alloc(ctx, &d_len, (size_t)sp->n + 1));
-    PoolGuard<uint32_t> g3{ctx, d_len};
+    LIME_TRY(space_device(ctx, sp->off, &d_off, &d_len));
     LIME_TRY(alloc(ctx, &err, 1));
     PoolGuard<unsigned int> g4{ctx, err};
     LIME_TRY(alloc(ctx, &tot, (size_t)nsh + 1));
     PoolGuard<int64_t> g5{ctx, tot};
-    std::vector<uint32_t> len32(sp->n + 1, 0);
-    for (int c = 0; c < sp->n; ++c) len32[c] = (uint32_t)sp->len[c];
     LIME_HIP(hipMemcpyAsync(d_split, splits, 4 * ((size_t)nsh + 1), hipMemcpyHostToDevice, S(ctx)));
-    LIME_HIP(hipMemcpyAsync(d_off, sp->off.data(), 4 * ((size_t)sp->n + 1), hipMemcpyHostToDevice,
-                            S(ctx)));
-    LIME_HIP(hipMemcpyAsync(d_len, len32.data(), 4 * ((size_t)sp->n + 1), hipMemcpyHostToDevice,
-                            S(ctx)));
     LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
     LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
     RouteArgs a;

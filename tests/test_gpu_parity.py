@@ -750,3 +750,35 @@ def test_bitset_and_past_sixteen_sets(ctx):
         gs = sp.offsets[np.asarray(got["contig"])] + np.asarray(got["start"], np.int64)
         assert out["runs"].numpy()[:, 0].tolist() == gs.tolist()
         out["result"].close()
+
+
+def test_spaces_cached_per_context(ctx):
+    # the context keeps one device copy of each space's offsets (keyed by the
+    # offsets): sets and bitsets of different spaces, built and queried in
+    # interleaved order, and a space destroyed and rebuilt, all stay exact
+    rng = np.random.default_rng(97)
+    lens_a = [50000, 50000, 50000, 777]
+    lens_b = [60000, 40000, 50000]
+    A, _ = random_sets(rng, 3000, 1, n_contigs=3, contig_len=40000, max_len=400)
+    B, _ = random_sets(rng, 3000, 1, n_contigs=3, contig_len=40000, max_len=400)
+    for rep in range(2):
+        spa, spb = Space(NAMES[:4], lens_a), Space(NAMES[:3], lens_b)
+        sa, sb = ctx.set_from_host(spa, *A), ctx.set_from_host(spb, *B)
+        ca = ctx.complement(spa, sa).to_host()
+        cb = ctx.complement(spb, sb).to_host()
+        ea, eb = oracle.complement(A, lens_a), oracle.complement(B, lens_b)
+        for k in ("contig", "start", "end"):
+            assert list(ca[k]) == list(ea[k]), (rep, k)
+            assert list(cb[k]) == list(eb[k]), (rep, k)
+        # the bit-per-base NOT over each space: the same gaps, book-ended
+        # zero-width gaps aside (Appendix A.4)
+        da, db = _dev_rows(A), _dev_rows(B)
+        na = ctx.bitset_runs(1, ctx.bitset_from_device(spa, len(A[0]),
+                                                       *(x.data_ptr() for x in da))).to_host()
+        nb = ctx.bitset_runs(1, ctx.bitset_from_device(spb, len(B[0]),
+                                                       *(x.data_ptr() for x in db))).to_host()
+        assert sum(e - s for s, e in zip(na["start"], na["end"])) == \
+            sum(e - s for s, e in zip(ea["start"], ea["end"]))
+        assert sum(e - s for s, e in zip(nb["start"], nb["end"])) == \
+            sum(e - s for s, e in zip(eb["start"], eb["end"]))
+        del sa, sb, spa, spb

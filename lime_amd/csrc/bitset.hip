@@ -280,8 +280,12 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
         if (hist[t]) atomicAdd(&a.ttot[t], hist[t]);
 }
 
+#ifndef LIME_WRITE_BLOCKS
+#define LIME_WRITE_BLOCKS 1
+#endif
 template <bool LC>
-__global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
+__global__ __launch_bounds__(WRB)
+__attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bin_write(BinArgs a) {
     __shared__ uint32_t stage[WSTEP];
     __shared__ uint16_t sbin[WSTEP];
     __shared__ uint32_t hist[NBMAX], soff[NBMAX], cur[NBMAX];
@@ -303,6 +307,8 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
     uint32_t valid = 0;
     if (r0 < r1) load_step<true, WRB>(a, r0, r1, c, s, e, valid);
     for (int64_t base = r0; base < r1; base += WSTEP) {
+        // tb[k]: the row's bin, then (bin << 13 | its rank among the step's
+        // rows of the bin) once ranked: one register per row for both
         uint32_t tb[SROWS], pk[SROWS];
 #pragma unroll
         for (int k = 0; k < SROWS; ++k) {
@@ -344,10 +350,10 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
         if (base + WSTEP < r1) load_step<true, WRB>(a, base + WSTEP, r1, c, s, e, valid);
         // rank per bin (16 independent LDS atomics), then bin offsets in the
         // step (one scan over <= 1024 bins), then stage in bin order
-        uint32_t rk[SROWS];
+        static_assert(WSTEP <= (1 << 13) && NBMAX <= (1 << 19), "bin / rank packing");
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
-            if (vnow & (1u << k)) rk[k] = atomicAdd(&hist[tb[k]], 1u);
+            if (vnow & (1u << k)) tb[k] = (tb[k] << 13) | atomicAdd(&hist[tb[k]], 1u);
         __syncthreads();
         if (NBMAX == 2 * WRB) {
             // bins 2t, 2t + 1 per thread
@@ -367,9 +373,10 @@ __global__ __launch_bounds__(WRB) void k_bin_write(BinArgs a) {
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
             if (vnow & (1u << k)) {
-                const uint32_t j = soff[tb[k]] + rk[k];
+                const uint32_t t = tb[k] >> 13;
+                const uint32_t j = soff[t] + (tb[k] & 0x1fffu);
                 stage[j] = pk[k];
-                sbin[j] = (uint16_t)tb[k];
+                sbin[j] = (uint16_t)t;
             }
         __syncthreads();
         // runs of a bin are consecutive: lane-consecutive stores.  Every lane
@@ -468,6 +475,50 @@ __global__ __launch_bounds__(SPB) void k_bin_split(BinArgs a) {
         for (int k = 0; k < PV; ++k) {
             const uint32_t o = __shfl(off, k * PSUB + (int)(q[k] & (PSUB - 1)), 64);
             dst[k] = o + rk[k];
+        }
+        if (rb + stride < r1)
+#pragma unroll
+            for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(rb + stride + k * 64 + lane, r1 - 1)];
+#pragma unroll
+        for (int k = 0; k < PV; ++k) *(q[k] < PSUB ? a.slab2 + dst[k] : a.dummy) = val[k];
+    }
+}
+
+// The split with one returning LDS atomic per row on its tile's cursor
+// (the default; LIME_SPLIT_ATOMIC=0 selects k_bin_split): no stable ranking is needed -- a tile's rows are
+// ORed into its image in any order -- and the lanes of one wave that claim
+// the same cursor get consecutive slots (the LDS serves a wave instruction's
+// lanes in order), so the stores stay runs.  Replaces the 4 ballots, the
+// claim prefix and the 9 shuffles per slot of k_bin_split.
+__global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
+    __shared__ uint32_t cur[PSUB];
+    const int b = blockIdx.x;
+    if (threadIdx.x < PSUB) cur[threadIdx.x] = a.ttot[b * PSUB + threadIdx.x];
+    const uint32_t r0 = a.mat[(int64_t)b * a.nchunks], r1 = a.mat[(int64_t)(b + 1) * a.nchunks];
+    __syncthreads();
+    const int lane = dev::lane_id();
+    const uint64_t bin0 = (uint64_t)b << BSH;
+    constexpr int PV = 8;
+    const int wv = threadIdx.x / 64, nwv = SPB / 64;
+    const uint32_t stride = (uint32_t)nwv * 64 * PV;
+    uint32_t pv[PV];
+    const uint32_t first = r0 + (uint32_t)wv * 64 * PV;
+    if (first < r1)
+#pragma unroll
+        for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(first + k * 64 + lane, r1 - 1)];
+    for (uint32_t rb = first; rb < r1; rb += stride) {
+        uint32_t q[PV], val[PV], dst[PV];
+#pragma unroll
+        for (int k = 0; k < PV; ++k) {
+            const bool v = rb + k * 64 + lane < r1;
+            const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
+            q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
+            const uint32_t qend = (q[k] + 1) << PSH;
+            const uint32_t l2 = o + l > qend ? qend - o : l;  // clipped at the tile end
+            if (v && l2 < l)  // remainder [o + l2, o + l) into the next tile(s)
+                a.cross[atomicAdd(a.ncross, 1u)] = ((bin0 + o + l2) << 32) | (bin0 + o + l);
+            val[k] = ((o - (q[k] << PSH)) << PLENB) | l2;
+            dst[k] = v ? atomicAdd(&cur[q[k]], 1u) : 0u;
         }
         if (rb + stride < r1)
 #pragma unroll
@@ -1132,7 +1183,14 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
         hipLaunchKernelGGL(k_bin_write<true>, dim3(nch), dim3(WRB), 0, S(ctx), a);
     else
         hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
-    hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
+    // the atomic-claim split by default (C5 12.05 -> 11.73 ms); LIME_SPLIT_ATOMIC=0
+    // selects the ballot-ranked one
+    static const bool split_atomic =
+        !getenv("LIME_SPLIT_ATOMIC") || atoi(getenv("LIME_SPLIT_ATOMIC")) != 0;
+    if (split_atomic)
+        hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
+    else
+        hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }

@@ -782,3 +782,21 @@ def test_spaces_cached_per_context(ctx):
         assert sum(e - s for s, e in zip(nb["start"], nb["end"])) == \
             sum(e - s for s, e in zip(eb["start"], eb["end"]))
         del sa, sb, spa, spb
+
+
+def test_bitset_runs_dense_tile_falls_back(ctx):
+    # a tile with more events than the extraction's per-tile stage (4096):
+    # 3000 one-base runs two bases apart in the first 262144-base tile, plus
+    # a sparse tail; the runs come back exact either way
+    rng = np.random.default_rng(5)
+    dense = np.arange(3000, dtype=np.int64) * 2
+    tail = np.sort(rng.choice(np.arange(300000, 990000, 7), 500, replace=False)).astype(np.int64)
+    starts = np.concatenate([dense, tail])
+    ends = starts + 1
+    contig = np.zeros(len(starts), np.int32)
+    sp = Space(NAMES[:1], [1_000_000])
+    dev = _dev_rows((contig, starts, ends))
+    bs = ctx.bitset_from_device(sp, len(starts), *(x.data_ptr() for x in dev))
+    got = ctx.bitset_runs(0, bs).to_host()
+    assert got["start"].tolist() == starts.tolist()
+    assert got["end"].tolist() == ends.tolist()

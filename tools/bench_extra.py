@@ -139,7 +139,8 @@ def main():
             b = W + 2 * W + 8 * (nc + nd)  # NOT reads 1 operand, ANDN 2, once each
             return {"bitset_build_ms (bin + paint)": t1.elapsed_time(t2),
                     "extract_ms": ms, "complement_runs": nc, "difference_runs": nd}, \
-                {"kernel": "bitset extraction (k_ev_fused: one pass, look-back offsets)",
+                {"kernel": "bitset extraction (k_ev_local: per-tile event slots, no look-back; "
+                           "k_ev_gather)",
                  "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "subtract":

@@ -1201,8 +1201,17 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
              uint64_t *cross, unsigned int *flags, bool ttot_zeroed = false) {
     const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
-    // chunk: ~2 chunks per CU, 1..16 steps of 16 rows per lane
-    int64_t R = (n + 511) / 512;
+    // chunk: 1..16 count steps; as many chunks as whole rounds of the write
+    // pass's resident workgroups (one per CU) need, so its last round is not
+    // a small tail (1e7 rows: 204 chunks in one round, not 306 in two)
+    static const int64_t cus = [] {
+        int dev = 0, c = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return (int64_t)(c > 0 ? c : 256);
+    }();
+    const int64_t rounds = std::max<int64_t>((n + cus * 16 * STEP - 1) / (cus * 16 * STEP), 1);
+    int64_t R = (n + cus * rounds - 1) / (cus * rounds);
     R = std::min<int64_t>(std::max<int64_t>(R, STEP), 16 * (int64_t)STEP);
     R = (R + STEP - 1) / STEP * STEP;
     const uint32_t nch = (uint32_t)std::max<int64_t>((n + R - 1) / R, 1);

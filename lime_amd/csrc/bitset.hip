@@ -124,7 +124,10 @@ constexpr int PLENB = 32 - PSH;          // packed length bits (tile slab)
 constexpr int NBMAX = 1 << (32 - BSH);   // bins (span < 2^32)
 constexpr int NTMAX = NBMAX * PSUB;      // paint tiles
 constexpr int BINB = 1024;               // count / split block
-constexpr int WRB = 512;                 // write block (<= 256 VGPRs: no spills)
+#ifndef LIME_WRB
+#define LIME_WRB 512
+#endif
+constexpr int WRB = LIME_WRB;            // write block (<= 256 VGPRs: no spills)
 constexpr int PAINTB = LIME_PAINTB;
 
 struct BinArgs {
@@ -355,19 +358,20 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
         for (int k = 0; k < SROWS; ++k)
             if (vnow & (1u << k)) tb[k] = (tb[k] << 13) | atomicAdd(&hist[tb[k]], 1u);
         __syncthreads();
-        if (NBMAX == 2 * WRB) {
-            // bins 2t, 2t + 1 per thread
-            const int t = 2 * threadIdx.x;
-            const uint32_t h0 = hist[t], h1 = hist[t + 1];
+        {
+            // bins BPT t .. BPT t + BPT - 1 per thread
+            constexpr int BPT = NBMAX / WRB;
+            const int t = BPT * threadIdx.x;
+            uint32_t h[BPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) sum += (h[q] = hist[t + q]);
             uint32_t tot;
-            const uint32_t o = dev::block_exclusive_sum<WRB>(h0 + h1, scratch, &tot);
-            soff[t] = o;
-            soff[t + 1] = o + h0;
-        } else {
-            // bin t per thread
-            const int t = threadIdx.x;
-            uint32_t tot;
-            soff[t] = dev::block_exclusive_sum<WRB>(hist[t], scratch, &tot);
+            uint32_t o = dev::block_exclusive_sum<WRB>(sum, scratch, &tot);
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                soff[t + q] = o;
+                o += h[q];
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -409,7 +413,7 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 // claims for d, and ONE LDS atomic instruction (lanes 56..63) reserves all
 // of them -- no chain of returning atomics per row.
 static_assert(PSUB == 8, "claims: 8 slots x 8 destinations = one wave");
-static_assert(NBMAX == 2 * WRB || NBMAX == WRB, "write-pass bin scan: one or two bins per thread");
+static_assert(NBMAX % WRB == 0, "write-pass bin scan: whole bins per thread");
 constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
 __global__ __launch_bounds__(SPB) void k_bin_split(BinArgs a) {
     __shared__ uint32_t cur[PSUB];
@@ -1202,13 +1206,14 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
     // chunk: 1..16 count steps; as many chunks as whole rounds of the write
-    // pass's resident workgroups (one per CU) need, so its last round is not
+    // pass's resident workgroups (`cus`: per CU x CUs) need, so its last round is not
     // a small tail (1e7 rows: 204 chunks in one round, not 306 in two)
     static const int64_t cus = [] {
-        int dev = 0, c = 256;
+        int dev = 0, c = 256, occ = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        return (int64_t)(c > 0 ? c : 256);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bin_write<true>, WRB, 0);
+        return (int64_t)(c > 0 ? c : 256) * (occ > 0 ? occ : 1);
     }();
     const int64_t rounds = std::max<int64_t>((n + cus * 16 * STEP - 1) / (cus * 16 * STEP), 1);
     int64_t R = (n + cus * rounds - 1) / (cus * rounds);

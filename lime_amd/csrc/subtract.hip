@@ -411,6 +411,133 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     }
 }
 
+// RUNS count pass: the fold of k_subtract<false, true>, counting only, four
+// 256-row blocks per workgroup (one per wave: its block total is a wave sum).
+// The per-row work of that fold is a chain of dependent loads (window start,
+// spanning start, the run's end row): here every B row of the workgroup's
+// 1024-row window is staged in LDS with its run's end row already resolved
+// (rfirst[run + 1]), so after one staging round per 1024 rows each row
+// folds from LDS and its registers.  Rows outside the window (a B row wider
+// than the window holds) read global memory, as in k_subtract.
+constexpr int CNT_WAVES = 4;
+constexpr int CNT_ROWS = CNT_WAVES * SUB_B;  // left rows per workgroup
+constexpr int CNT_WIN = 1536;                // B rows staged (C2: ~1200 needed)
+
+__global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, int64_t nblk) {
+    __shared__ uint32_t w_pm[CNT_WIN], w_gs[CNT_WIN], w_rend[CNT_WIN];
+    __shared__ uint32_t s_whi[CNT_WAVES];
+    const int wv = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t base = (int64_t)blockIdx.x * CNT_ROWS + (int64_t)wv * SUB_B;
+    constexpr int RPL = SUB_B / 64;  // rows per lane
+    uint32_t as[RPL], ae[RPL], lo[RPL], hi[RPL];
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+        const int64_t i = base + k * 64 + lane;
+        as[k] = ae[k] = lo[k] = hi[k] = 0;
+        if (i < sa.na) {
+            as[k] = sa.ags[i];
+            ae[k] = sa.age[i];
+            lo[k] = sa.olo[i];
+            hi[k] = lo[k] + sa.ocnt[i];
+            h = max(h, hi[k]);
+        }
+    }
+    h = dev::wave_reduce_max(h);
+    if (lane == 0) s_whi[wv] = h;
+    // the first block's window start is the workgroup's (wstart is monotone)
+    const int64_t wlo = sa.wstart[(int64_t)blockIdx.x * CNT_WAVES];
+    __syncthreads();
+    int64_t whi = wlo;
+    for (int w = 0; w < CNT_WAVES; ++w) whi = max(whi, (int64_t)s_whi[w]);
+    const bool win = whi - wlo <= CNT_WIN;
+    if (win)
+        for (int64_t k = threadIdx.x; k < whi - wlo; k += CNT_WAVES * 64) {
+            w_pm[k] = sa.bpmax[wlo + k];
+            w_gs[k] = sa.bgs[wlo + k];
+            w_rend[k] = sa.rfirst[sa.brun[wlo + k] + 1];
+        }
+    __syncthreads();
+    auto in = [&](int64_t j) { return win && j >= wlo && j < whi; };
+    auto PM = [&](int64_t j) { return in(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
+    auto GS = [&](int64_t j) { return in(j) ? w_gs[j - wlo] : sa.bgs[j]; };
+    auto REND = [&](int64_t j) { return in(j) ? w_rend[j - wlo] : sa.rfirst[sa.brun[j] + 1]; };
+    const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
+    uint64_t tot = 0;
+#pragma unroll 1
+    for (int k = 0; k < RPL; ++k) {
+        if (base + k * 64 + lane >= sa.na) break;
+        const uint32_t a_s = as[k], a_e = ae[k];
+        const int64_t lo1 = lo[k], hi1 = hi[k];
+        const uint32_t thr = a_s;  // RUNS: threshold <= 0
+        bool any = false;
+        uint32_t bs = 0, be = 0, setpos = a_s;
+        uint64_t cum = 0;
+        auto close_block = [&]() {
+            if (lime_mode) {
+                cum += (uint64_t)(bs > a_s) + (uint64_t)(a_e > be);
+            } else {
+                if (bs > setpos) ++cum;
+                if (be > setpos) setpos = be;
+            }
+        };
+        // the spanning block: first j in [wlo, lo1) with pmax > thr
+        const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
+        if (lo1 > 0 && pm_last > thr) {
+            int64_t j0;
+            if (win) {
+                int64_t l = wlo, r = lo1 - 1;
+                while (l < r) {
+                    const int64_t mid = (l + r) >> 1;
+                    if (w_pm[mid - wlo] > thr)
+                        r = mid;
+                    else
+                        l = mid + 1;
+                }
+                j0 = l;
+            } else {
+                j0 = first_spanning(sa.bpmax, lo1, thr);
+            }
+            any = true;
+            bs = GS(j0);
+            be = pm_last;
+        }
+        int64_t j = lo1;
+        // the spanning block goes on through the inside rows of its run
+        if (any && j < hi1 && REND(j) == REND(lo1 - 1)) {
+            const int64_t nx = min((int64_t)REND(j), hi1);
+            be = max(be, PM(nx - 1));
+            j = nx;
+        }
+        while (j < hi1) {
+            const int64_t nx = min((int64_t)REND(j), hi1);
+            const uint32_t gs = GS(j);
+            if (!any) {
+                any = true;
+                if (sa.bge[j] == gs) {  // a zero-width head closes a duplicate of itself
+                    bs = be = gs;
+                    close_block();
+                }
+            } else {
+                close_block();
+            }
+            bs = gs;
+            be = PM(nx - 1);  // the inclusive prefix max: >= the head's end
+            j = nx;
+        }
+        uint64_t n_out = 1;  // no hit: (L, None)
+        if (any) {
+            close_block();
+            if (!lime_mode && a_e > setpos) ++cum;
+            n_out = cum;
+        }
+        tot += n_out;
+    }
+    tot = dev::wave_reduce_sum(tot);
+    const int64_t sb = (int64_t)blockIdx.x * CNT_WAVES + wv;
+    if (lane == 0 && sb < nblk) sa.count[sb] = tot;
+}
+
 // first sorted row of every run (rfirst[nruns] = n)
 __global__ __launch_bounds__(256) void k_run_first(const uint32_t *__restrict__ run, int64_t n,
                                                    int64_t nruns, uint32_t *__restrict__ rfirst) {
@@ -495,7 +622,17 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         else if (runs) hipLaunchKernelGGL((k_subtract<false, true>), g, b, 0, S(ctx), sa);
         else hipLaunchKernelGGL((k_subtract<false, false>), g, b, 0, S(ctx), sa);
     };
-    launch(false);
+    // RUNS counts by the staged-window kernel (LIME_SUB_COUNT_FOLD=1: the
+    // write pass's own fold, for A/B)
+    static const bool count_fold = [] {
+        const char *e = getenv("LIME_SUB_COUNT_FOLD");
+        return e && atoi(e) != 0;
+    }();
+    if (runs && !count_fold)
+        hipLaunchKernelGGL(k_sub_count_runs, dim3(blocks_for(na, CNT_ROWS)), dim3(CNT_WAVES * 64),
+                           0, S(ctx), sa, nblk);
+    else
+        launch(false);
     LIME_HIP(hipGetLastError());
     // counts per left row (walk), per 256-row block (runs)
     const int64_t nc = runs ? nblk : na;

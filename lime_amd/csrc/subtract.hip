@@ -44,9 +44,12 @@ struct SubArgs {
     // RUNS (threshold <= 0): B's merge runs -- run id of every sorted row and
     // the first sorted row of every run (nruns + 1 entries)
     const uint32_t *brun, *rfirst;
-    int64_t na;
+    int64_t na, nb;
     int64_t t;
     int mode;
+    // RUNS: lo1 / hi1 found in the staged window (no owner_ranges); zw = B
+    // holds zero-width rows
+    int inl, zw;
     uint64_t *count;        // pass 1
     const uint64_t *off;    // pass 2
     uint32_t *ogs, *oge, *oar, *obr;
@@ -78,6 +81,42 @@ constexpr int SCAP = 512;   // records staged per block in the write pass
 constexpr int BWIN = 1024;  // B rows of a block's hit window staged in LDS
 // (24 KiB of LDS in all: the walk is latency-bound, occupancy is its speed)
 
+// A left row's inside-hit range [lo1, hi1) at threshold <= 0: stream 0 of
+// owner_ranges (intersect.hip k_count, tp = 1): lo = lb(B.gs, a.s) past the
+// zero-width rows at a.s, hi = lb(B.gs, a.e) if a.e > a.s, else lo.  Searched
+// in the staged starts w_gs of B rows [wlo, wlo + nst) (wlo <= lb(B.gs, a.s):
+// the window start of a block is the bound of its first row minus B's max
+// width), then in global memory past them.
+__device__ __forceinline__ void sub_range(const SubArgs &sa, const uint32_t *w_gs, int64_t wlo,
+                                          int nst, uint32_t a_s, uint32_t a_e, int64_t &lo1,
+                                          int64_t &hi1) {
+    auto lb = [&](int64_t from, uint32_t key) -> int64_t {
+        if (from - wlo < nst) {
+            int l = (int)(from - wlo), r = nst;
+            while (l < r) {
+                const int m = (l + r) >> 1;
+                if (w_gs[m] < key)
+                    l = m + 1;
+                else
+                    r = m;
+            }
+            if (l < nst) return wlo + l;
+            from = wlo + nst;
+        }
+        return dev::lower_bound(sa.bgs, from, sa.nb, (int64_t)key);
+    };
+    int64_t lo = lb(wlo, a_s);
+    int64_t hi = a_e > a_s ? lb(lo, a_e) : lo;
+    if (sa.zw) {
+        while (lo < sa.nb && (lo - wlo < nst ? w_gs[lo - wlo] : sa.bgs[lo]) == a_s &&
+               sa.bge[lo] == a_s)
+            ++lo;
+        if (hi < lo) hi = lo;
+    }
+    lo1 = lo;
+    hi1 = hi;
+}
+
 // per block: first B row that can span any of the block's left rows: a
 // spanning b starts after a.s - max width(B) (one 65-ary wave search)
 __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__ ags, int64_t na,
@@ -105,7 +144,7 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     __shared__ uint32_t st_ar[WRITE ? SCAP : 1], st_br[WRITE ? SCAP : 1];
     __shared__ uint32_t w_pm[BWIN];
     // (RUNS reads starts, ends and row ids at block heads only: global memory)
-    __shared__ uint32_t w_gs[RUNS ? 1 : BWIN], w_ge[RUNS ? 1 : BWIN], w_row[RUNS ? 1 : BWIN];
+    __shared__ uint32_t w_gs[BWIN], w_ge[RUNS ? 1 : BWIN], w_row[RUNS ? 1 : BWIN];
     __shared__ uint32_t w_run[RUNS ? BWIN : 1];
     __shared__ uint32_t s_whi[SUB_B / 64];
     const int64_t i = (int64_t)blockIdx.x * SUB_B + threadIdx.x;
@@ -116,17 +155,28 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     // consecutive left rows share most of it, so it is loaded once,
     // coalesced, into LDS
     const int64_t wlo = sa.wstart[blockIdx.x];
-    {
+    // inline ranges (RUNS): BWIN rows from wlo staged with their starts,
+    // without waiting for the candidate ranges
+    const bool inl = RUNS && sa.inl;
+    const int nst = inl ? (int)min((int64_t)BWIN, sa.nb - wlo) : 0;
+    if (inl)
+        for (int k = threadIdx.x; k < nst; k += SUB_B) {
+            w_pm[k] = sa.bpmax[wlo + k];
+            w_gs[k] = sa.bgs[wlo + k];
+            w_run[k] = sa.brun[wlo + k];
+        }
+    if (!inl) {
         uint32_t h = 0;
         if (i < sa.na) h = sa.olo[i] + sa.ocnt[i];
         h = dev::wave_reduce_max(h);
         if (dev::lane_id() == 0) s_whi[threadIdx.x / 64] = h;
     }
     __syncthreads();
-    int64_t whi = wlo;
-    for (int w = 0; w < SUB_B / 64; ++w) whi = max(whi, (int64_t)s_whi[w]);
+    int64_t whi = inl ? wlo + nst : wlo;
+    if (!inl)
+        for (int w = 0; w < SUB_B / 64; ++w) whi = max(whi, (int64_t)s_whi[w]);
     const bool win = whi - wlo <= BWIN;
-    if (win)
+    if (win && !inl)
         for (int64_t k = threadIdx.x; k < whi - wlo; k += SUB_B) {
             w_pm[k] = sa.bpmax[wlo + k];
             if (RUNS) {
@@ -139,11 +189,15 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         }
     __syncthreads();
     // B's arrays at row j, from the window when staged
-    auto Bgs = [&](int64_t j) { return win && !RUNS ? w_gs[j - wlo] : sa.bgs[j]; };
+    // (inl: rows [wlo, whi) are staged whatever the rows' ranges)
+    auto inw = [&](int64_t j) { return win && j >= wlo && (!inl || j < whi); };
+    auto Bgs = [&](int64_t j) {
+        return (win && !RUNS) || (inl && inw(j)) ? w_gs[j - wlo] : sa.bgs[j];
+    };
     auto Bge = [&](int64_t j) { return win && !RUNS ? w_ge[j - wlo] : sa.bge[j]; };
     auto Brow = [&](int64_t j) { return win && !RUNS ? w_row[j - wlo] : sa.brow[j]; };
-    auto Bpm = [&](int64_t j) { return win && j >= wlo ? w_pm[j - wlo] : sa.bpmax[j]; };
-    auto Brun = [&](int64_t j) { return RUNS ? (win && j >= wlo ? w_run[j - wlo] : sa.brun[j]) : 0u; };
+    auto Bpm = [&](int64_t j) { return inw(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
+    auto Brun = [&](int64_t j) { return RUNS ? (inw(j) ? w_run[j - wlo] : sa.brun[j]) : 0u; };
     // the block's output window (write pass): staged in LDS when it fits
     int64_t bbase = 0, bend = 0;
     bool staged = false;
@@ -156,6 +210,8 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     }
     uint32_t as = 0, ae = 0, ar = 0;
     if (i < sa.na) as = sa.ags[i], ae = sa.age[i], ar = sa.arow[i];
+    int64_t rlo = 0, rhi = 0;  // inline: the row's inside-hit range
+    if (inl && i < sa.na) sub_range(sa, w_gs, wlo, nst, as, ae, rlo, rhi);
     const int64_t t = sa.t;
     int64_t pos = 0, end = 0;
     if (WRITE && !RUNS && i < sa.na) {
@@ -184,8 +240,8 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     uint64_t n_out = 0;
     bool any = false;
     if (i < sa.na && !(t >= 1 && (int64_t)(ae - as) < t)) {
-        const int64_t lo1 = sa.olo[i];
-        const int64_t hi1 = lo1 + sa.ocnt[i];
+        const int64_t lo1 = inl ? rlo : (int64_t)sa.olo[i];
+        const int64_t hi1 = inl ? rhi : lo1 + (int64_t)sa.ocnt[i];
         const uint32_t thr = t <= 0 ? as : (uint32_t)((int64_t)as + t - 1);
         // fold state.  The block's value is its head = first hit in the
         // reference's (start, end, row) order; the device order only ties
@@ -196,12 +252,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         uint32_t setpos = as;
         // the spanning block (all spanning hits overlap at a.s): the first
         // spanning row lies in [wlo, lo1) (rows before wlo end before a.s)
-        const uint32_t pm_last = lo1 > 0 ? (win && lo1 - 1 >= wlo ? w_pm[lo1 - 1 - wlo]
-                                                                   : sa.bpmax[lo1 - 1])
-                                         : 0u;
+        const uint32_t pm_last = lo1 > 0 ? Bpm(lo1 - 1) : 0u;
         if (lo1 > 0 && pm_last > thr) {
             int64_t j0;
-            if (win) {  // first j in [wlo, lo1) with pmax > thr, in LDS
+            if (win && (!inl || lo1 - 1 < whi)) {  // first j in [wlo, lo1) with pmax > thr, in LDS
                 int64_t lo = wlo, hi = lo1 - 1;
                 while (lo < hi) {
                     const int64_t mid = (lo + hi) >> 1;
@@ -414,61 +468,59 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
 // RUNS count pass: the fold of k_subtract<false, true>, counting only, four
 // 256-row blocks per workgroup (one per wave: its block total is a wave sum).
 // The per-row work of that fold is a chain of dependent loads (window start,
-// spanning start, the run's end row): here every B row of the workgroup's
-// 1024-row window is staged in LDS with its run's end row already resolved
-// (rfirst[run + 1]), so after one staging round per 1024 rows each row
-// folds from LDS and its registers.  Rows outside the window (a B row wider
-// than the window holds) read global memory, as in k_subtract.
+// candidate range, spanning start, run ids): here CNT_WIN B rows from the
+// workgroup's window start are staged in LDS at once, and every row finds its
+// inside-hit range in them (sub_range: no owner_ranges pass), so 1024 rows
+// cost two load round trips and one barrier, then fold from LDS and
+// registers.  A run that goes on through hi1 - 1 ends the row's walk without
+// its rfirst entry.  Rows outside the window (a B row wider than it holds)
+// read global memory, as in k_subtract.
 constexpr int CNT_WAVES = 4;
 constexpr int CNT_ROWS = CNT_WAVES * SUB_B;  // left rows per workgroup
 constexpr int CNT_WIN = 1536;                // B rows staged (C2: ~1200 needed)
 
 __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, int64_t nblk) {
-    __shared__ uint32_t w_pm[CNT_WIN], w_gs[CNT_WIN], w_rend[CNT_WIN];
-    __shared__ uint32_t s_whi[CNT_WAVES];
+    __shared__ uint32_t w_pm[CNT_WIN], w_gs[CNT_WIN], w_run[CNT_WIN];
     const int wv = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t base = (int64_t)blockIdx.x * CNT_ROWS + (int64_t)wv * SUB_B;
     constexpr int RPL = SUB_B / 64;  // rows per lane
-    uint32_t as[RPL], ae[RPL], lo[RPL], hi[RPL];
-    uint32_t h = 0;
+    uint32_t as[RPL], ae[RPL];
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
         const int64_t i = base + k * 64 + lane;
-        as[k] = ae[k] = lo[k] = hi[k] = 0;
+        as[k] = ae[k] = 0;
         if (i < sa.na) {
             as[k] = sa.ags[i];
             ae[k] = sa.age[i];
-            lo[k] = sa.olo[i];
-            hi[k] = lo[k] + sa.ocnt[i];
-            h = max(h, hi[k]);
         }
     }
-    h = dev::wave_reduce_max(h);
-    if (lane == 0) s_whi[wv] = h;
     // the first block's window start is the workgroup's (wstart is monotone)
     const int64_t wlo = sa.wstart[(int64_t)blockIdx.x * CNT_WAVES];
+    const int nst = (int)min((int64_t)CNT_WIN, sa.nb - wlo);
+    for (int k = threadIdx.x; k < nst; k += CNT_WAVES * 64) {
+        w_pm[k] = sa.bpmax[wlo + k];
+        w_gs[k] = sa.bgs[wlo + k];
+        w_run[k] = sa.brun[wlo + k];
+    }
     __syncthreads();
-    int64_t whi = wlo;
-    for (int w = 0; w < CNT_WAVES; ++w) whi = max(whi, (int64_t)s_whi[w]);
-    const bool win = whi - wlo <= CNT_WIN;
-    if (win)
-        for (int64_t k = threadIdx.x; k < whi - wlo; k += CNT_WAVES * 64) {
-            w_pm[k] = sa.bpmax[wlo + k];
-            w_gs[k] = sa.bgs[wlo + k];
-            w_rend[k] = sa.rfirst[sa.brun[wlo + k] + 1];
-        }
-    __syncthreads();
-    auto in = [&](int64_t j) { return win && j >= wlo && j < whi; };
+    const int64_t whi = wlo + nst;
+    auto in = [&](int64_t j) { return j >= wlo && j < whi; };
     auto PM = [&](int64_t j) { return in(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
     auto GS = [&](int64_t j) { return in(j) ? w_gs[j - wlo] : sa.bgs[j]; };
-    auto REND = [&](int64_t j) { return in(j) ? w_rend[j - wlo] : sa.rfirst[sa.brun[j] + 1]; };
+    auto RUN = [&](int64_t j) { return in(j) ? w_run[j - wlo] : sa.brun[j]; };
+    // end of j's run, cut at hi1 (the run of hi1 - 1 needs no lookup)
+    auto NX = [&](int64_t j, int64_t hi1) {
+        const uint32_t r = RUN(j);
+        return RUN(hi1 - 1) == r ? hi1 : min((int64_t)sa.rfirst[r + 1], hi1);
+    };
     const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
     uint64_t tot = 0;
 #pragma unroll 1
     for (int k = 0; k < RPL; ++k) {
         if (base + k * 64 + lane >= sa.na) break;
         const uint32_t a_s = as[k], a_e = ae[k];
-        const int64_t lo1 = lo[k], hi1 = hi[k];
+        int64_t lo1, hi1;
+        sub_range(sa, w_gs, wlo, nst, a_s, a_e, lo1, hi1);
         const uint32_t thr = a_s;  // RUNS: threshold <= 0
         bool any = false;
         uint32_t bs = 0, be = 0, setpos = a_s;
@@ -485,7 +537,7 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
         const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
         if (lo1 > 0 && pm_last > thr) {
             int64_t j0;
-            if (win) {
+            if (lo1 - 1 < whi) {  // in the staged window
                 int64_t l = wlo, r = lo1 - 1;
                 while (l < r) {
                     const int64_t mid = (l + r) >> 1;
@@ -504,13 +556,13 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
         }
         int64_t j = lo1;
         // the spanning block goes on through the inside rows of its run
-        if (any && j < hi1 && REND(j) == REND(lo1 - 1)) {
-            const int64_t nx = min((int64_t)REND(j), hi1);
+        if (any && j < hi1 && RUN(j) == RUN(lo1 - 1)) {
+            const int64_t nx = NX(j, hi1);
             be = max(be, PM(nx - 1));
             j = nx;
         }
         while (j < hi1) {
-            const int64_t nx = min((int64_t)REND(j), hi1);
+            const int64_t nx = NX(j, hi1);
             const uint32_t gs = GS(j);
             if (!any) {
                 any = true;
@@ -562,13 +614,27 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         return LIME_OK;
     }
     LIME_TRY(build_prefix_max(ctx, B));
-    uint32_t *olo, *ocnt;
+    // threshold <= 0: blocks are B's merge runs (k_subtract<_, true>); the
+    // runs of a stranded set also break at strand changes, so those walk
+    const bool runs = threshold <= 0 && B->n > 0 && B->strand_in == nullptr;
+    // runs: the count (k_sub_count_runs) and write passes find each row's
+    // inside-hit range in their staged windows, no owner_ranges pass
+    // (LIME_SUB_COUNT_FOLD=1: owner_ranges + the write pass's own fold as
+    // the count pass, for A/B)
+    static const bool count_fold = [] {
+        const char *e = getenv("LIME_SUB_COUNT_FOLD");
+        return e && atoi(e) != 0;
+    }();
+    const bool inl = runs && !count_fold;
+    uint32_t *olo = nullptr, *ocnt = nullptr;
     uint64_t *cnt, *off;
-    LIME_TRY(alloc(ctx, &olo, (size_t)na));
-    LIME_TRY(alloc(ctx, &ocnt, (size_t)na));
+    if (!inl) {
+        LIME_TRY(alloc(ctx, &olo, (size_t)na));
+        LIME_TRY(alloc(ctx, &ocnt, (size_t)na));
+    }
     LIME_TRY(alloc(ctx, &cnt, (size_t)na + 1));
     LIME_TRY(alloc(ctx, &off, (size_t)na + 1));
-    LIME_TRY(owner_ranges(ctx, A, B, 0, threshold, olo, ocnt));
+    if (!inl) LIME_TRY(owner_ranges(ctx, A, B, 0, threshold, olo, ocnt));
     const int64_t nblk = (na + SUB_B - 1) / SUB_B;
     uint32_t *wstart;
     LIME_TRY(alloc(ctx, &wstart, (size_t)nblk));
@@ -590,15 +656,15 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.olo = olo;
     sa.ocnt = ocnt;
     sa.na = na;
+    sa.nb = B->n;
     sa.t = threshold;
     sa.mode = mode;
     sa.count = cnt;
     sa.off = off;
     sa.ogs = sa.oge = sa.oar = sa.obr = nullptr;
     sa.brun = sa.rfirst = nullptr;
-    // threshold <= 0: blocks are B's merge runs (k_subtract<_, true>); the
-    // runs of a stranded set also break at strand changes, so those walk
-    const bool runs = threshold <= 0 && B->n > 0 && B->strand_in == nullptr;
+    sa.inl = inl ? 1 : 0;
+    sa.zw = B->has_zero_width ? 1 : 0;
     lime_result mb;
     mb.ctx = ctx;
     uint32_t *rfirst = nullptr;
@@ -622,13 +688,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         else if (runs) hipLaunchKernelGGL((k_subtract<false, true>), g, b, 0, S(ctx), sa);
         else hipLaunchKernelGGL((k_subtract<false, false>), g, b, 0, S(ctx), sa);
     };
-    // RUNS counts by the staged-window kernel (LIME_SUB_COUNT_FOLD=1: the
-    // write pass's own fold, for A/B)
-    static const bool count_fold = [] {
-        const char *e = getenv("LIME_SUB_COUNT_FOLD");
-        return e && atoi(e) != 0;
-    }();
-    if (runs && !count_fold)
+    if (inl)
         hipLaunchKernelGGL(k_sub_count_runs, dim3(blocks_for(na, CNT_ROWS)), dim3(CNT_WAVES * 64),
                            0, S(ctx), sa, nblk);
     else

@@ -514,13 +514,35 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
         return RUN(hi1 - 1) == r ? hi1 : min((int64_t)sa.rfirst[r + 1], hi1);
     };
     const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
+    // the rows' bounds in the staged window, a lane's 3 * RPL searches in
+    // lockstep (branchless binary lifting: their LDS reads overlap): lower
+    // bounds of a.s and a.e among the starts, and the number of prefix maxima
+    // <= a.s (pmax is monotone: the first spanning row)
+    int bl[RPL], bh[RPL], bp[RPL];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = bp[k] = 0;
+    for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            if (bl[k] + step <= nst && w_gs[bl[k] + step - 1] < as[k]) bl[k] += step;
+            if (bh[k] + step <= nst && w_gs[bh[k] + step - 1] < ae[k]) bh[k] += step;
+            if (bp[k] + step <= nst && w_pm[bp[k] + step - 1] <= as[k]) bp[k] += step;
+        }
+    }
     uint64_t tot = 0;
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < RPL; ++k) {
         if (base + k * 64 + lane >= sa.na) break;
         const uint32_t a_s = as[k], a_e = ae[k];
-        int64_t lo1, hi1;
-        sub_range(sa, w_gs, wlo, nst, a_s, a_e, lo1, hi1);
+        // the inside-hit range, as sub_range: past the window by global search
+        int64_t lo1 = bl[k] < nst ? wlo + bl[k] : dev::lower_bound(sa.bgs, whi, sa.nb, (int64_t)a_s);
+        int64_t hi1 = lo1;
+        if (a_e > a_s)
+            hi1 = bh[k] < nst ? wlo + bh[k] : dev::lower_bound(sa.bgs, max(lo1, whi), sa.nb, (int64_t)a_e);
+        if (sa.zw) {
+            while (lo1 < sa.nb && GS(lo1) == a_s && sa.bge[lo1] == a_s) ++lo1;
+            if (hi1 < lo1) hi1 = lo1;
+        }
         const uint32_t thr = a_s;  // RUNS: threshold <= 0
         bool any = false;
         uint32_t bs = 0, be = 0, setpos = a_s;
@@ -536,20 +558,8 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
         // the spanning block: first j in [wlo, lo1) with pmax > thr
         const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
         if (lo1 > 0 && pm_last > thr) {
-            int64_t j0;
-            if (lo1 - 1 < whi) {  // in the staged window
-                int64_t l = wlo, r = lo1 - 1;
-                while (l < r) {
-                    const int64_t mid = (l + r) >> 1;
-                    if (w_pm[mid - wlo] > thr)
-                        r = mid;
-                    else
-                        l = mid + 1;
-                }
-                j0 = l;
-            } else {
-                j0 = first_spanning(sa.bpmax, lo1, thr);
-            }
+            // in the staged window when any staged pmax exceeds thr
+            const int64_t j0 = bp[k] < nst ? wlo + bp[k] : first_spanning(sa.bpmax, lo1, thr);
             any = true;
             bs = GS(j0);
             be = pm_last;

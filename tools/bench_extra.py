@@ -170,7 +170,8 @@ def main():
             # A rows (gs, ge, row) + B's gs / ge / row / prefix max + 16 B per remnant
             b = 12 * n + 16 * n + 16 * k
             return {"sort_ms": t0.elapsed_time(t1), "subtract_ms": ms, "remnants": k}, \
-                {"kernel": "subtract (owner ranges + k_subtract count / write)", "bound": "hbm",
+                {"kernel": "subtract (B's merge runs + k_sub_count_runs + k_subtract write)",
+                 "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "window":
         # DistributedWindow (distance 1000) on C2's inputs: every pair within
@@ -273,7 +274,7 @@ def main():
             b = k * W + 8 * nr  # every operand read once (single-pass extraction)
             return {"bitset_build_ms (bin + paint)": t1.elapsed_time(t2),
                     "and_extract_ms": ms, "runs": nr}, \
-                {"kernel": "8-way AND + extraction (k_ev_fused)", "bound": "hbm",
+                {"kernel": "8-way AND + extraction (k_ev_local + k_ev_gather)", "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
 
     torch.cuda.synchronize(dev)

@@ -37,7 +37,9 @@ namespace {
 constexpr int SUB_B = 256;
 
 struct SubArgs {
-    const uint32_t *wstart;  // per block: first B row a spanning hit can be (or null)
+    // per block (inline ranges: per 4 blocks): first B row a spanning hit can be
+    const uint32_t *wstart;
+    uint32_t maxw;  // max width of B
     const uint32_t *ags, *age, *arow;
     const uint32_t *bgs, *bge, *brow, *bpmax;
     const uint32_t *olo, *ocnt;
@@ -77,6 +79,10 @@ __device__ __forceinline__ int64_t first_spanning(const uint32_t *__restrict__ p
     return lo;
 }
 
+// the runs count pass (k_sub_count_runs): blocks per workgroup, rows, B window
+constexpr int CNT_WAVES = 4;
+constexpr int CNT_ROWS = CNT_WAVES * SUB_B;  // left rows per workgroup
+constexpr int CNT_WIN = 1536;                // B rows staged (C2: ~1200 needed)
 constexpr int SCAP = 512;   // records staged per block in the write pass
 constexpr int BWIN = 1024;  // B rows of a block's hit window staged in LDS
 // (24 KiB of LDS in all: the walk is latency-bound, occupancy is its speed)
@@ -121,11 +127,11 @@ __device__ __forceinline__ void sub_range(const SubArgs &sa, const uint32_t *w_g
 // spanning b starts after a.s - max width(B) (one 65-ary wave search)
 __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__ ags, int64_t na,
                                                     const uint32_t *__restrict__ bgs, int64_t nb,
-                                                    uint32_t maxw, int64_t nblk,
+                                                    uint32_t maxw, int64_t nblk, int stride,
                                                     uint32_t *__restrict__ wstart) {
     const int64_t b = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
     if (b >= nblk) return;
-    const int64_t key = (int64_t)ags[b * SUB_B] - maxw;
+    const int64_t key = (int64_t)ags[b * SUB_B * stride] - maxw;
     const int64_t r = dev::wave_lower_bound(bgs, nb, key < 0 ? 0 : key);
     if (dev::lane_id() == 0) wstart[b] = (uint32_t)r;
 }
@@ -154,10 +160,19 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     // the block's hit window [wlo, whi) of B (spanning and inside hits):
     // consecutive left rows share most of it, so it is loaded once,
     // coalesced, into LDS
-    const int64_t wlo = sa.wstart[blockIdx.x];
+    const bool inl = RUNS && sa.inl;
+    // inline ranges: wstart holds one start per 4 blocks (the count pass's
+    // workgroups); the block's own is searched from there (every wave alike)
+    int64_t wlo;
+    if (inl) {
+        const int64_t c = sa.wstart[blockIdx.x / CNT_WAVES];
+        const int64_t key = max((int64_t)sa.ags[(int64_t)blockIdx.x * SUB_B] - sa.maxw, (int64_t)0);
+        wlo = c + dev::wave_lower_bound(sa.bgs + c, sa.nb - c, key);
+    } else {
+        wlo = sa.wstart[blockIdx.x];
+    }
     // inline ranges (RUNS): BWIN rows from wlo staged with their starts,
     // without waiting for the candidate ranges
-    const bool inl = RUNS && sa.inl;
     const int nst = inl ? (int)min((int64_t)BWIN, sa.nb - wlo) : 0;
     if (inl)
         for (int k = threadIdx.x; k < nst; k += SUB_B) {
@@ -475,9 +490,6 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
 // registers.  A run that goes on through hi1 - 1 ends the row's walk without
 // its rfirst entry.  Rows outside the window (a B row wider than it holds)
 // read global memory, as in k_subtract.
-constexpr int CNT_WAVES = 4;
-constexpr int CNT_ROWS = CNT_WAVES * SUB_B;  // left rows per workgroup
-constexpr int CNT_WIN = 1536;                // B rows staged (C2: ~1200 needed)
 
 __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, int64_t nblk) {
     __shared__ uint32_t w_pm[CNT_WIN], w_gs[CNT_WIN], w_run[CNT_WIN];
@@ -494,8 +506,8 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
             ae[k] = sa.age[i];
         }
     }
-    // the first block's window start is the workgroup's (wstart is monotone)
-    const int64_t wlo = sa.wstart[(int64_t)blockIdx.x * CNT_WAVES];
+    // the workgroup's window start (its first block's)
+    const int64_t wlo = sa.wstart[blockIdx.x];
     const int nst = (int)min((int64_t)CNT_WIN, sa.nb - wlo);
     for (int k = threadIdx.x; k < nst; k += CNT_WAVES * 64) {
         w_pm[k] = sa.bpmax[wlo + k];
@@ -646,16 +658,21 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     LIME_TRY(alloc(ctx, &off, (size_t)na + 1));
     if (!inl) LIME_TRY(owner_ranges(ctx, A, B, 0, threshold, olo, ocnt));
     const int64_t nblk = (na + SUB_B - 1) / SUB_B;
+    // window starts: per block, or per count workgroup (CNT_WAVES blocks)
+    // with inline ranges
+    const int stride = inl ? CNT_WAVES : 1;
+    const int64_t nws = (nblk + stride - 1) / stride;
     uint32_t *wstart;
-    LIME_TRY(alloc(ctx, &wstart, (size_t)nblk));
+    LIME_TRY(alloc(ctx, &wstart, (size_t)nws));
     PoolGuard<uint32_t> gw{ctx, wstart};
     if (B->n > 0)
-        hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nblk, 4)), dim3(256), 0, S(ctx), A->gs,
-                           na, B->gs, B->n, B->max_width, nblk, wstart);
+        hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nws, 4)), dim3(256), 0, S(ctx), A->gs,
+                           na, B->gs, B->n, B->max_width, nws, stride, wstart);
     else
-        LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nblk, S(ctx)));
+        LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nws, S(ctx)));
     SubArgs sa;
     sa.wstart = wstart;
+    sa.maxw = B->max_width;
     sa.ags = A->gs;
     sa.age = A->ge;
     sa.arow = A->row;

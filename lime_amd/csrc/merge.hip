@@ -130,6 +130,7 @@ struct MergeScanArgs {
     uint32_t *ticket;
     uint32_t *run_gs, *run_ge;  // capacity n
     uint32_t *run_of_sorted;    // may be null
+    uint32_t *pmax;             // may be null: inclusive prefix max of ge (plain sets)
     uint64_t *total;            // runs
     const int8_t *strand;       // stranded sets: strand per input row
     const uint32_t *row;        // sorted row ids (strand lookups)
@@ -353,6 +354,26 @@ void k_merge_scan(MergeScanArgs a) {
                 if (r0 + k < n) a.run_of_sorted[r0 + k] = rid[k];
         }
     }
+    // the inclusive prefix max of ge per row (subtract's spanning search),
+    // recomputed from the tile's carry: saves the set a k_tile_max +
+    // k_prefix_max pass over ge
+    if (!STR && a.pmax) {
+        uint32_t pm[MITEMS];
+        M = M0;
+#pragma unroll
+        for (int k = 0; k < MITEMS; ++k) {
+            M = max(M, e[k]);
+            pm[k] = M;
+        }
+        if (full) {
+            __syncthreads();  // the LDS image is reused
+            blocked_to_tile(pm, lds, a.pmax + t0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < MITEMS; ++k)
+                if (r0 + k < n) a.pmax[r0 + k] = pm[k];
+        }
+    }
 }
 
 // inclusive prefix max of ge (subtract's spanning-hit search)
@@ -422,7 +443,8 @@ int build_prefix_max(lime_ctx *ctx, const lime_set *set) {
 }
 
 // merge runs of a sorted set; result owns run_gs / run_ge / run_of_sorted
-int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids) {
+static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
+                           bool want_run_ids, uint32_t *pmax) {
     const int64_t n = set->n;
     res->n = 0;
     if (n == 0) {
@@ -450,6 +472,7 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
     a.run_gs = run_gs;
     a.run_ge = run_ge;
     a.run_of_sorted = res->run_of_sorted;
+    a.pmax = pmax;
     a.strand = set->strand_in;
     a.row = set->row;
     if (set->strand_in)
@@ -475,6 +498,32 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
         release(ctx, run_ge);
     }
     res->n = (int64_t)nr;
+    return LIME_OK;
+}
+
+int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids) {
+    return merge_runs_impl(ctx, set, res, want_run_ids, nullptr);
+}
+
+// merge runs with run ids of a plain set, building the set's prefix max in
+// the same pass when it is not built yet (under the set's context lock, as
+// build_prefix_max)
+int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res) {
+    if (set->ctx != ctx) return fail(LIME_ERR_ARG, "set belongs to another context");
+    if (set->strand_in || set->n == 0) {
+        LIME_TRY(build_prefix_max(ctx, set));
+        return merge_runs_impl(ctx, set, res, true, nullptr);
+    }
+    std::lock_guard<std::mutex> lock(set->ctx->mu);
+    if (set->pmax) return merge_runs_impl(ctx, set, res, true, nullptr);
+    uint32_t *pm;
+    LIME_TRY(alloc(set->ctx, &pm, (size_t)set->n));
+    const int rc = merge_runs_impl(ctx, set, res, true, pm);
+    if (rc != LIME_OK) {
+        release(set->ctx, pm);
+        return rc;
+    }
+    set->pmax = pm;
     return LIME_OK;
 }
 

@@ -623,6 +623,7 @@ __global__ __launch_bounds__(256) void k_run_first(const uint32_t *__restrict__ 
 }  // namespace
 
 int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
+int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res);
 
 int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold, int mode,
                  lime_result *res) {
@@ -635,10 +636,11 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         LIME_TRY(alloc(ctx, &res->b_row, 1));
         return LIME_OK;
     }
-    LIME_TRY(build_prefix_max(ctx, B));
     // threshold <= 0: blocks are B's merge runs (k_subtract<_, true>); the
     // runs of a stranded set also break at strand changes, so those walk
     const bool runs = threshold <= 0 && B->n > 0 && B->strand_in == nullptr;
+    // B's prefix max: with the runs, out of the same merge scan (below)
+    if (!runs) LIME_TRY(build_prefix_max(ctx, B));
     // runs: the count (k_sub_count_runs) and write passes find each row's
     // inside-hit range in their staged windows, no owner_ranges pass
     // (LIME_SUB_COUNT_FOLD=1: owner_ranges + the write pass's own fold as
@@ -700,7 +702,8 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     PoolGuard<uint32_t> g3{ctx, mb.ge};
     PoolGuard<uint32_t> g4{ctx, rfirst};
     if (runs) {
-        LIME_TRY(merge_runs(ctx, B, &mb, true));
+        LIME_TRY(merge_runs_with_pmax(ctx, B, &mb));
+        sa.bpmax = B->pmax;  // built by the merge scan when it was not yet
         LIME_TRY(alloc(ctx, &rfirst, (size_t)mb.n + 1));
         hipLaunchKernelGGL(k_run_first, dim3(blocks_for(B->n, 256)), dim3(256), 0, S(ctx),
                            (const uint32_t *)mb.run_of_sorted, B->n, mb.n, rfirst);

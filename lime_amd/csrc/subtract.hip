@@ -213,6 +213,22 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     auto Brow = [&](int64_t j) { return win && !RUNS ? w_row[j - wlo] : sa.brow[j]; };
     auto Bpm = [&](int64_t j) { return inw(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
     auto Brun = [&](int64_t j) { return RUNS ? (inw(j) ? w_run[j - wlo] : sa.brun[j]) : 0u; };
+    // end of j's run cut at hi1 (j < hi1): rfirst, or with inline ranges a
+    // search over the run ids (monotone), no rfirst table
+    auto run_end = [&](int64_t j, int64_t hi1) -> int64_t {
+        const uint32_t r = Brun(j);
+        if (!inl) return min((int64_t)sa.rfirst[r + 1], hi1);
+        if (Brun(hi1 - 1) == r) return hi1;
+        int64_t l = j + 1, h = hi1 - 1;
+        while (l < h) {
+            const int64_t m = (l + h) >> 1;
+            if (Brun(m) > r)
+                h = m;
+            else
+                l = m + 1;
+        }
+        return l;
+    };
     // the block's output window (write pass): staged in LDS when it fits
     int64_t bbase = 0, bend = 0;
     bool staged = false;
@@ -318,13 +334,13 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             int64_t j = lo1;
             // the spanning block goes on through the inside rows of its run
             if (any && j < hi1 && Brun(j) == Brun(lo1 - 1)) {
-                const int64_t nx = min((int64_t)sa.rfirst[Brun(j) + 1], hi1);
+                const int64_t nx = run_end(j, hi1);
                 be = max(be, Bpm(nx - 1));
                 j = nx;
             }
             while (j < hi1) {
                 const uint32_t r = Brun(j);
-                const int64_t nx = min((int64_t)sa.rfirst[r + 1], hi1);
+                const int64_t nx = run_end(j, hi1);
                 const uint32_t gs = Bgs(j), ge = Bge(j), row = Brow(j);
                 if (!any) {  // foldLeft(List(head)): the head is folded against itself
                     any = true;
@@ -487,9 +503,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
 // workgroup's window start are staged in LDS at once, and every row finds its
 // inside-hit range in them (sub_range: no owner_ranges pass), so 1024 rows
 // cost two load round trips and one barrier, then fold from LDS and
-// registers.  A run that goes on through hi1 - 1 ends the row's walk without
-// its rfirst entry.  Rows outside the window (a B row wider than it holds)
-// read global memory, as in k_subtract.
+// registers.  A run's end inside the row's range is found by a search over
+// the (monotone) run ids, so no first-row-of-run table is built.  Rows
+// outside the window (a B row wider than it holds) read global memory, as in
+// k_subtract.
 
 __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, int64_t nblk) {
     __shared__ uint32_t w_pm[CNT_WIN], w_gs[CNT_WIN], w_run[CNT_WIN];
@@ -520,10 +537,20 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     auto PM = [&](int64_t j) { return in(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
     auto GS = [&](int64_t j) { return in(j) ? w_gs[j - wlo] : sa.bgs[j]; };
     auto RUN = [&](int64_t j) { return in(j) ? w_run[j - wlo] : sa.brun[j]; };
-    // end of j's run, cut at hi1 (the run of hi1 - 1 needs no lookup)
-    auto NX = [&](int64_t j, int64_t hi1) {
+    // end of j's run, cut at hi1 (j < hi1): the first row of a later run,
+    // by a search over the run ids (monotone)
+    auto NX = [&](int64_t j, int64_t hi1) -> int64_t {
         const uint32_t r = RUN(j);
-        return RUN(hi1 - 1) == r ? hi1 : min((int64_t)sa.rfirst[r + 1], hi1);
+        if (RUN(hi1 - 1) == r) return hi1;
+        int64_t l = j + 1, h = hi1 - 1;
+        while (l < h) {
+            const int64_t m = (l + h) >> 1;
+            if (RUN(m) > r)
+                h = m;
+            else
+                l = m + 1;
+        }
+        return l;
     };
     const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
     // the rows' bounds in the staged window, a lane's 3 * RPL searches in
@@ -704,10 +731,12 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     if (runs) {
         LIME_TRY(merge_runs_with_pmax(ctx, B, &mb));
         sa.bpmax = B->pmax;  // built by the merge scan when it was not yet
-        LIME_TRY(alloc(ctx, &rfirst, (size_t)mb.n + 1));
-        hipLaunchKernelGGL(k_run_first, dim3(blocks_for(B->n, 256)), dim3(256), 0, S(ctx),
-                           (const uint32_t *)mb.run_of_sorted, B->n, mb.n, rfirst);
-        LIME_HIP(hipGetLastError());
+        if (!inl) {  // inline ranges search the run ids instead
+            LIME_TRY(alloc(ctx, &rfirst, (size_t)mb.n + 1));
+            hipLaunchKernelGGL(k_run_first, dim3(blocks_for(B->n, 256)), dim3(256), 0, S(ctx),
+                               (const uint32_t *)mb.run_of_sorted, B->n, mb.n, rfirst);
+            LIME_HIP(hipGetLastError());
+        }
         sa.brun = mb.run_of_sorted;
         sa.rfirst = rfirst;
     }

@@ -80,9 +80,15 @@ __device__ __forceinline__ int64_t first_spanning(const uint32_t *__restrict__ p
 }
 
 // the runs count pass (k_sub_count_runs): blocks per workgroup, rows, B window
-constexpr int CNT_WAVES = 4;
+#ifndef LIME_SUB_CNT_WAVES
+#define LIME_SUB_CNT_WAVES 4
+#endif
+#ifndef LIME_SUB_CNT_WIN
+#define LIME_SUB_CNT_WIN 1536
+#endif
+constexpr int CNT_WAVES = LIME_SUB_CNT_WAVES;
 constexpr int CNT_ROWS = CNT_WAVES * SUB_B;  // left rows per workgroup
-constexpr int CNT_WIN = 1536;                // B rows staged (C2: ~1200 needed)
+constexpr int CNT_WIN = LIME_SUB_CNT_WIN;    // B rows staged (C2: ~1200 needed at 4 waves)
 constexpr int SCAP = 512;   // records staged per block in the write pass
 constexpr int BWIN = 1024;  // B rows of a block's hit window staged in LDS
 // (24 KiB of LDS in all: the walk is latency-bound, occupancy is its speed)

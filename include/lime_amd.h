@@ -43,7 +43,9 @@
 extern "C" {
 #endif
 
-#define LIME_ABI_VERSION 1
+/* 2: lime_set_lower_bound / _first_reaching return -(LIME_ERR_*) on error
+ *    (was -1); lime_pairs_checksum_device and the sharded-path helpers added */
+#define LIME_ABI_VERSION 2
 
 /* status codes */
 #define LIME_OK 0
@@ -174,6 +176,11 @@ int lime_intersect_fill_host(lime_pairs *plan, int64_t first, int64_t count, lim
 /* Order-independent checksum (sum and xor of lime_pair_hash over every pair)
  * computed on device without materialising the pairs. */
 int lime_intersect_checksum(lime_pairs *plan, uint64_t *sum, uint64_t *xr);
+/* The same checksum over `count` records already STORED in a device buffer
+ * (e.g. a chunk lime_intersect_fill_device wrote): verifies the bytes a fill
+ * wrote, not only the fill's arithmetic. */
+int lime_pairs_checksum_device(lime_ctx *ctx, const lime_pair *d_pairs, int64_t count,
+                               uint64_t *sum, uint64_t *xr);
 int lime_pairs_destroy(lime_pairs *plan);
 
 /* ------------------------------------------------------------------- window */

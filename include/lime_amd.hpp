@@ -76,7 +76,14 @@ using PartitionMap = std::vector<std::optional<std::pair<ReferenceRegion, Refere
 // One device context shared by the operators of a thread.
 class Engine {
    public:
-    explicit Engine(int device = 0) { check(lime_ctx_create(device, &ctx_)); }
+    explicit Engine(int device = 0) {
+        // the header and the loaded library must agree on the C-ABI contract
+        if (lime_abi_version() != LIME_ABI_VERSION)
+            throw std::runtime_error("liblime_amd C-ABI version " +
+                                     std::to_string(lime_abi_version()) + ", header " +
+                                     std::to_string(LIME_ABI_VERSION));
+        check(lime_ctx_create(device, &ctx_));
+    }
     ~Engine() { lime_ctx_destroy(ctx_); }
     Engine(const Engine &) = delete;
     Engine &operator=(const Engine &) = delete;

@@ -23,6 +23,9 @@ ERRORS = {
     6: "LIME_ERR_IO",
     7: "LIME_ERR_OVERFLOW",
 }
+# the C-ABI contract this binding is written against (include/lime_amd.h
+# LIME_ABI_VERSION): checked at load, so a stale library fails loudly
+ABI_VERSION = 2
 SUBTRACT_LIME = 0
 SUBTRACT_SET = 1
 
@@ -85,6 +88,7 @@ SIGNATURES = {
     "lime_intersect_fill_device": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_fill_host": (C.c_int, [vp, i64, i64, vp]),
     "lime_intersect_checksum": (C.c_int, [vp, P(u64), P(u64)]),
+    "lime_pairs_checksum_device": (C.c_int, [vp, vp, i64, P(u64), P(u64)]),
     "lime_pairs_destroy": (C.c_int, [vp]),
     "lime_merge": (C.c_int, [vp, vp, pp, P(i64)]),
     "lime_subtract": (C.c_int, [vp, vp, vp, i64, C.c_int, pp, P(i64)]),
@@ -164,6 +168,9 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)  # AttributeError if the symbol is missing
         fn.restype = res
         fn.argtypes = args
+    if lib.lime_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path}: C-ABI version {lib.lime_abi_version()}, this binding "
+                          f"needs {ABI_VERSION}: rebuild the engine")
     _lib = lib
     return lib
 

@@ -92,10 +92,11 @@ __global__ __launch_bounds__(BB) void k_paint_cross(const uint64_t *__restrict__
 //                runs, one u32 each (offset in bin << LENB | length); longer
 //                rows and rows crossing the bin end leave their remainder to
 //                the cross list (k_paint_cross)
-//   k_bin_split  one block per bin: its rows to its PSUB paint tiles (wave-
-//                aggregated LDS cursors: 8 destinations, coalesced runs),
-//                re-packed relative to the tile, tile-crossing remainders to
-//                the cross list
+//   k_bin_split_atomic  one block per bin: its rows to its PSUB paint tiles
+//                (one returning LDS atomic per row on the tile's cursor: a
+//                wave's claims on one cursor come back consecutive, so the
+//                stores stay runs), re-packed relative to the tile,
+//                tile-crossing remainders to the cross list
 //   k_paint_bins one block per paint tile: its rows OR-ed into a 64 KiB LDS
 //                image, stored once (every word written exactly once)
 // Why two levels: a one-level scatter to 5,900 paint tiles (hg38) keeps
@@ -415,85 +416,6 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 static_assert(PSUB == 8, "claims: 8 slots x 8 destinations = one wave");
 static_assert(NBMAX % WRB == 0, "write-pass bin scan: whole bins per thread");
 constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
-__global__ __launch_bounds__(SPB) void k_bin_split(BinArgs a) {
-    __shared__ uint32_t cur[PSUB];
-    const int b = blockIdx.x;
-    if (threadIdx.x < PSUB) cur[threadIdx.x] = a.ttot[b * PSUB + threadIdx.x];
-    const uint32_t r0 = a.mat[(int64_t)b * a.nchunks], r1 = a.mat[(int64_t)(b + 1) * a.nchunks];
-    __syncthreads();
-    const int lane = dev::lane_id();
-    const uint64_t bin0 = (uint64_t)b << BSH;
-    const uint64_t lt = dev::lanemask_lt();
-    constexpr int PV = 8;  // slots per step (one wave of 8 x 8 claim counters)
-    // rows of a wave per step: 64 lanes x PV slots, lane-consecutive per slot.
-    // Software-pipelined with a static store count: the next step's loads
-    // (clamped addresses: always issued) go out before this step's PV stores
-    // (invalid slots to a sink), so its first use waits for the loads only
-    // and the stores stay in flight
-    const int wv = threadIdx.x / 64, nwv = SPB / 64;
-    const uint32_t stride = (uint32_t)nwv * 64 * PV;
-    uint32_t pv[PV];
-    const uint32_t first = r0 + (uint32_t)wv * 64 * PV;
-    if (first < r1)
-#pragma unroll
-        for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(first + k * 64 + lane, r1 - 1)];
-    for (uint32_t rb = first; rb < r1; rb += stride) {
-        uint32_t q[PV], rk[PV], val[PV];
-        uint32_t myc = 0;  // lane 8 k + d: rows of slot k bound for tile d
-#pragma unroll
-        for (int k = 0; k < PV; ++k) {
-            const bool v = rb + k * 64 + lane < r1;
-            const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
-            q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
-            const uint32_t qend = (q[k] + 1) << PSH;
-            const uint32_t l2 = o + l > qend ? qend - o : l;  // clipped at the tile end
-            if (v && l2 < l)  // remainder [o + l2, o + l) into the next tile(s)
-                a.cross[atomicAdd(a.ncross, 1u)] = ((bin0 + o + l2) << 32) | (bin0 + o + l);
-            val[k] = ((o - (q[k] << PSH)) << PLENB) | l2;
-            // rank by the 3 bits of the tile: 4 ballots, not 8
-            const uint64_t vm = __ballot(q[k] < PSUB);
-            const uint64_t b0 = __ballot(q[k] & 1), b1 = __ballot(q[k] & 2),
-                           b2 = __ballot(q[k] & 4);
-            const uint64_t mine = vm & (q[k] & 1 ? b0 : ~b0) & (q[k] & 2 ? b1 : ~b1) &
-                                  (q[k] & 4 ? b2 : ~b2);
-            rk[k] = (uint32_t)__popcll(mine & lt);
-            // lanes 8 k .. 8 k + 7 count slot k's rows for tile d = lane % 8
-            const uint32_t d = (uint32_t)lane & (PSUB - 1);
-            const uint64_t md = vm & (d & 1 ? b0 : ~b0) & (d & 2 ? b1 : ~b1) & (d & 4 ? b2 : ~b2);
-            if ((lane >> 3) == k) myc = (uint32_t)__popcll(md);
-        }
-        // exclusive prefix of myc over k for each d (lanes d, d + 8, ...)
-        uint32_t pre = myc;
-#pragma unroll
-        for (int sh = PSUB; sh < 64; sh <<= 1) {
-            const uint32_t o = __shfl_up(pre, sh, 64);
-            if (lane >= sh) pre += o;
-        }
-        pre -= myc;
-        uint32_t base = 0;
-        if (lane >= 64 - PSUB) base = atomicAdd(&cur[lane - (64 - PSUB)], pre + myc);
-        base = __shfl(base, 64 - PSUB + (lane & (PSUB - 1)), 64);
-        const uint32_t off = base + pre;  // first slot of (k = lane / 8, d = lane % 8)
-        uint32_t dst[PV];
-#pragma unroll
-        for (int k = 0; k < PV; ++k) {
-            const uint32_t o = __shfl(off, k * PSUB + (int)(q[k] & (PSUB - 1)), 64);
-            dst[k] = o + rk[k];
-        }
-        if (rb + stride < r1)
-#pragma unroll
-            for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(rb + stride + k * 64 + lane, r1 - 1)];
-#pragma unroll
-        for (int k = 0; k < PV; ++k) *(q[k] < PSUB ? a.slab2 + dst[k] : a.dummy) = val[k];
-    }
-}
-
-// The split with one returning LDS atomic per row on its tile's cursor
-// (the default; LIME_SPLIT_ATOMIC=0 selects k_bin_split): no stable ranking is needed -- a tile's rows are
-// ORed into its image in any order -- and the lanes of one wave that claim
-// the same cursor get consecutive slots (the LDS serves a wave instruction's
-// lanes in order), so the stores stay runs.  Replaces the 4 ballots, the
-// claim prefix and the 9 shuffles per slot of k_bin_split.
 __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
     __shared__ uint32_t cur[PSUB];
     const int b = blockIdx.x;
@@ -949,11 +871,6 @@ __global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w,
     if (dev::lane_id() == 0) atomicAdd(out, (unsigned long long)c);
 }
 
-// Single pass (count + write) when the run count has a known bound: tiles
-// in ticket order, the event offset of a tile by decoupled look-back over
-// the per-tile status words (flag in bits 62-63, value below), and events
-// past the capacity only counted (the caller then falls back to two passes).
-constexpr uint64_t EV_AGG = 1ull << 62, EV_INC = 2ull << 62, EV_VAL = (1ull << 62) - 1;
 // Tile geometry of the one-pass extraction: EV_NT threads x EV_W words.
 // Fewer, larger tiles mean fewer serial look-backs (as for k_merge_scan)
 #ifndef LIME_EV_NT
@@ -967,113 +884,6 @@ constexpr uint64_t EV_AGG = 1ull << 62, EV_INC = 2ull << 62, EV_VAL = (1ull << 6
 #endif
 constexpr int EV_NT = LIME_EV_NT, EV_W = LIME_EV_W, EV_TW = EV_NT * EV_W;
 constexpr int EVCAP = LIME_EVCAP;  // events of a tile staged in LDS
-
-__global__ __launch_bounds__(EV_NT) void k_ev_fused(OpArgs a, uint64_t *__restrict__ status,
-                                                 unsigned int *__restrict__ ticket,
-                                                 int64_t cap_events, uint32_t *__restrict__ rgs,
-                                                 uint32_t *__restrict__ rge,
-                                                 unsigned long long *__restrict__ total) {
-    __shared__ unsigned long long img[img_words(EV_TW)];
-    __shared__ uint32_t s_pad[MAXPAD];
-    __shared__ int s_npad;
-    __shared__ uint32_t scratch[EV_NT / 64 + 1];
-    __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_excl;
-    __shared__ uint32_t s_ev[EVCAP];
-    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const int64_t w0 = (int64_t)tile * EV_TW;
-    stage_tile<EV_NT, EV_TW>(a, w0, img, s_pad, &s_npad);
-    const int q0 = threadIdx.x * EV_W;
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < EV_W; ++k) {
-        uint64_t st, en;
-        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
-        c += __popcll(st) + __popcll(en);
-    }
-    uint32_t tot;
-    const uint32_t mine = dev::block_exclusive_sum<EV_NT>(c, scratch, &tot);
-    if (threadIdx.x < 64) {  // one wave publishes and looks back
-        const int lane = dev::lane_id();
-        if (tile == 0) {
-            if (lane == 0) {
-                __hip_atomic_store(status, EV_INC | tot, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                s_excl = 0;
-            }
-        } else {
-            if (lane == 0)
-                __hip_atomic_store(status + tile, EV_AGG | tot, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t acc = 0;
-            for (int64_t base = (int64_t)tile - 1; base >= 0; base -= 64) {
-                const int64_t t = base - lane;
-                uint64_t v = EV_INC;  // before tile 0: the inclusive identity
-                if (t >= 0) {
-                    v = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    while ((v >> 62) == 0) {
-                        __builtin_amdgcn_s_sleep(1);
-                        v = __hip_atomic_load(status + t, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-                const uint64_t inc = __ballot((v >> 62) == 2);
-                uint64_t val = v & EV_VAL;
-                if (inc && lane > __builtin_ctzll(inc)) val = 0;
-                acc += dev::wave_reduce_sum(val);
-                if (inc) break;
-            }
-            if (lane == 0) {
-                __hip_atomic_store(status + tile, EV_INC | (acc + tot), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                s_excl = acc;
-            }
-        }
-    }
-    __syncthreads();
-    const uint64_t excl = s_excl;
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) *total = excl + tot;
-    // a tile's events (<= EVCAP) are staged in LDS and stored lane-consecutively
-    // (event i of the tile by lane i: runs' starts and ends as whole lines);
-    // denser tiles store each lane's own events directly
-    const bool staged = tot <= (uint32_t)EVCAP;
-    uint64_t ev = excl + mine;
-    uint32_t le = mine;
-#pragma unroll
-    for (int k = 0; k < EV_W; ++k) {
-        uint64_t st, en;
-        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
-        uint64_t all = st | en;
-        const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
-        while (all) {
-            const int b = __builtin_ctzll(all);
-            all &= all - 1;
-            const uint32_t p = base + (uint32_t)b;
-            if (staged) {
-                s_ev[le++] = p;
-            } else if ((int64_t)ev < cap_events) {
-                if (ev & 1u)
-                    rge[ev >> 1] = p;
-                else
-                    rgs[ev >> 1] = p;
-            }
-            ++ev;
-        }
-    }
-    if (!staged) return;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += EV_NT) {
-        const uint64_t e = excl + i;
-        if ((int64_t)e < cap_events) {
-            if (e & 1u)
-                rge[e >> 1] = s_ev[i];
-            else
-                rgs[e >> 1] = s_ev[i];
-        }
-    }
-}
 
 }  // namespace
 
@@ -1265,14 +1075,8 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
         hipLaunchKernelGGL(k_bin_write<true>, dim3(nch), dim3(WRB), 0, S(ctx), a);
     else
         hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
-    // the atomic-claim split by default (C5 12.05 -> 11.73 ms); LIME_SPLIT_ATOMIC=0
-    // selects the ballot-ranked one
-    static const bool split_atomic =
-        !getenv("LIME_SPLIT_ATOMIC") || atoi(getenv("LIME_SPLIT_ATOMIC")) != 0;
-    if (split_atomic)
-        hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
-    else
-        hipLaunchKernelGGL(k_bin_split, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
+    // the atomic-claim split (C5 12.05 -> 11.73 ms against a ballot-ranked one)
+    hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
@@ -1474,23 +1278,9 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
         res->n = 0;
         return LIME_OK;
     }
-    // bound on the result's runs: each run starts at a run start of one
-    // operand (AND / ANDN also at a run end of B); NOT adds one gap per contig
-    bool known = true;
-    int64_t sum = 0;
-    for (int i = 0; i < k; ++i) {
-        known = known && sets[i]->runs_bound >= 0;
-        sum += sets[i]->runs_bound;
-    }
-    const int64_t bound = op == 1 ? a->runs_bound + a->n_contigs + 1 : sum + 1;
-    // LIME_EV_TWOPASS=1: the count + scan + write passes even when the bound
-    // is known (measurement)
-    static const bool twopass = getenv("LIME_EV_TWOPASS") && atoi(getenv("LIME_EV_TWOPASS")) == 1;
-    // per-tile event slots + scan + gather (no look-back) by default: C4's two
-    // extractions 0.61 -> 0.43 ms; LIME_EV_LOCAL=0 selects the one-pass
-    // look-back kernel (k_ev_fused)
-    static const bool local = !getenv("LIME_EV_LOCAL") || atoi(getenv("LIME_EV_LOCAL")) != 0;
-    if (local && !twopass && nt > 0) {
+    // per-tile event slots + scan + gather (no look-back): C4's two
+    // extractions 0.61 -> 0.43 ms against a one-pass decoupled look-back
+    {
         const int64_t ntl = a->n_words / EV_TW + 1;
         uint32_t *tev, *tcnt, *toff;
         unsigned int *hdr;  // [0] overflow flag, [1] total events
@@ -1523,50 +1313,6 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
             return LIME_OK;
         }
         // a tile past EVCAP events: the two-pass path below
-    } else if (known && nt > 0 && bound < (int64_t)0x7fffffff && !twopass) {
-        const int64_t ntf = a->n_words / EV_TW + 1;  // the fused pass's (larger) tiles
-        uint64_t *status;
-        unsigned int *ticket;
-        unsigned long long *tot64;
-        LIME_TRY(alloc(ctx, &status, (size_t)ntf));
-        LIME_TRY(alloc(ctx, &ticket, 1));
-        LIME_TRY(alloc(ctx, &tot64, 1));
-        LIME_TRY(alloc(ctx, &res->gs, (size_t)bound));
-        LIME_TRY(alloc(ctx, &res->ge, (size_t)bound));
-        LIME_HIP(hipMemsetAsync(status, 0, sizeof(uint64_t) * (size_t)ntf, S(ctx)));
-        LIME_HIP(hipMemsetAsync(ticket, 0, sizeof(unsigned int), S(ctx)));
-        hipLaunchKernelGGL(k_ev_fused, dim3((unsigned)ntf), dim3(EV_NT), 0, S(ctx), oa, status,
-                           ticket, 2 * bound, res->gs, res->ge, tot64);
-        LIME_HIP(hipGetLastError());
-        unsigned long long nev = 0;
-        LIME_TRY(read_back(ctx, &nev, tot64, sizeof(nev)));
-        release(ctx, status);
-        release(ctx, ticket);
-        release(ctx, tot64);
-        if ((int64_t)nev <= 2 * bound) {
-                if (nev & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
-            const int64_t nr = (int64_t)nev / 2;
-            if (nr < bound / 2) {  // keep the result's memory to its size
-                uint32_t *gs, *ge;
-                LIME_TRY(alloc(ctx, &gs, (size_t)nr));
-                LIME_TRY(alloc(ctx, &ge, (size_t)nr));
-                if (nr > 0) {
-                    LIME_HIP(hipMemcpyAsync(gs, res->gs, 4 * (size_t)nr, hipMemcpyDeviceToDevice,
-                                            S(ctx)));
-                    LIME_HIP(hipMemcpyAsync(ge, res->ge, 4 * (size_t)nr, hipMemcpyDeviceToDevice,
-                                            S(ctx)));
-                }
-                release(ctx, res->gs);
-                release(ctx, res->ge);
-                res->gs = gs;
-                res->ge = ge;
-            }
-            res->n = nr;
-            return LIME_OK;
-        }
-        // the bound did not hold (it always should): count first, then write
-        release(ctx, res->gs);
-        release(ctx, res->ge);
     }
     uint32_t *tcnt, *toff, *total;
     LIME_TRY(alloc(ctx, &tcnt, (size_t)nt));

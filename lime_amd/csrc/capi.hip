@@ -194,6 +194,28 @@ __global__ __launch_bounds__(256) void k_result_checksum(
     }
 }
 
+// Order-independent checksum of pair records STORED in device memory (sum /
+// xor of pair_hash over every record): the check that the bytes a fill wrote
+// hash to what lime_intersect_checksum computes in registers.
+__global__ __launch_bounds__(256) void k_pairs_hash(const uint4 *__restrict__ rec, int64_t n,
+                                                    unsigned long long *__restrict__ out) {
+    uint64_t hs = 0, hx = 0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const uint4 r = rec[i];
+        const uint64_t h = dev::pair_hash(r.x, r.y, r.z, r.w);
+        hs += h;
+        hx ^= h;
+    }
+    hs = dev::wave_reduce_sum(hs);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) hx ^= __shfl_xor(hx, d, 64);
+    if (dev::lane_id() == 0) {
+        atomicAdd(&out[0], (unsigned long long)hs);
+        atomicXor(&out[1], (unsigned long long)hx);
+    }
+}
+
 // every set / bitset an operator reads must belong to the operator's context:
 // its arrays live in that context's pool and device (a foreign set
 // could otherwise be read on another device, or have lazily built state
@@ -219,30 +241,43 @@ static int d2h(lime_ctx *ctx, std::vector<T> &v, const T *d, int64_t n) {
     return LIME_OK;
 }
 
+SpaceDev::~SpaceDev() {
+    release(ctx, off);
+    release(ctx, len);
+}
+
 int space_device(lime_ctx *ctx, const std::vector<uint32_t> &off, const uint32_t **d_off,
-                 const uint32_t **d_len) {
+                 const uint32_t **d_len, std::shared_ptr<SpaceDev> *keep) {
     auto it = ctx->spaces.find(off);
     if (it == ctx->spaces.end()) {
         const size_t n1 = off.size();
-        uint32_t *o = nullptr, *l = nullptr;
-        LIME_TRY(alloc(ctx, &o, n1));
-        LIME_TRY(alloc(ctx, &l, n1));
+        auto sd = std::make_shared<SpaceDev>();
+        sd->ctx = ctx;  // (a failed upload releases what it got)
+        LIME_TRY(alloc(ctx, &sd->off, n1));
+        LIME_TRY(alloc(ctx, &sd->len, n1));
         std::vector<uint32_t> len32(n1, 0);
         for (size_t c = 0; c + 1 < n1; ++c) len32[c] = off[c + 1] - off[c] - 1;
-        LIME_HIP(hipMemcpyAsync(o, off.data(), 4 * n1, hipMemcpyHostToDevice, S(ctx)));
-        LIME_HIP(hipMemcpyAsync(l, len32.data(), 4 * n1, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipMemcpyAsync(sd->off, off.data(), 4 * n1, hipMemcpyHostToDevice, S(ctx)));
+        LIME_HIP(hipMemcpyAsync(sd->len, len32.data(), 4 * n1, hipMemcpyHostToDevice, S(ctx)));
         LIME_HIP(hipStreamSynchronize(S(ctx)));  // (once per space and context)
-        it = ctx->spaces.emplace(off, std::make_pair(o, l)).first;
+        it = ctx->spaces.emplace(off, sd).first;
+        // bound the cache: drop entries no set holds (stream-ordered pool:
+        // work already queued on them finishes before the blocks are reused)
+        if (ctx->spaces.size() > lime_ctx::SPACE_CACHE)
+            for (auto e = ctx->spaces.begin(); e != ctx->spaces.end();)
+                e = (e != it && e->second.use_count() == 1) ? ctx->spaces.erase(e) : std::next(e);
     }
-    *d_off = it->second.first;
-    if (d_len) *d_len = it->second.second;
+    *d_off = it->second->off;
+    if (d_len) *d_len = it->second->len;
+    if (keep) *keep = it->second;
     return LIME_OK;
 }
 
 // the space's cached device arrays (borrowed: owned by the context)
-static int upload_space(lime_ctx *ctx, const lime_space *sp, uint32_t **d_off, uint32_t **d_len) {
+static int upload_space(lime_ctx *ctx, const lime_space *sp, uint32_t **d_off, uint32_t **d_len,
+                        std::shared_ptr<SpaceDev> *keep = nullptr) {
     const uint32_t *o = nullptr, *l = nullptr;
-    LIME_TRY(space_device(ctx, sp->off, &o, d_len ? &l : nullptr));
+    LIME_TRY(space_device(ctx, sp->off, &o, d_len ? &l : nullptr, keep));
     *d_off = const_cast<uint32_t *>(o);
     if (d_len) *d_len = const_cast<uint32_t *>(l);
     return LIME_OK;
@@ -270,7 +305,7 @@ static int create_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
     s->strand_uniform = strand_uniform;
     s->min_shift = min_shift;
     uint32_t *d_len = nullptr;
-    int rc = upload_space(ctx, sp, &s->d_off, &d_len);  // (borrowed)
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len, &s->space_keep);
     if (rc == LIME_OK) rc = sort_set(ctx, s, d_contig, d_start, d_end, d_len);
     if (rc != LIME_OK) {
         release(ctx, s->strand_in);
@@ -359,6 +394,7 @@ int lime_ctx_destroy(lime_ctx *ctx) {
     if (!ctx) return LIME_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
+    ctx->spaces.clear();
     ctx->pool.release_all();
     if (ctx->pinned) hipHostFree(ctx->pinned);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -521,7 +557,7 @@ int lime_set_destroy(lime_set *s) {
     release(ctx, s->gs);
     release(ctx, s->ge);
     release(ctx, s->row);
-    // (s->d_off is the context's cached space array: not released)
+    // (s->d_off is the context's cached space array: held by s->space_keep)
     release(ctx, s->pmax);
     release(ctx, s->strand_in);
     delete s;
@@ -547,7 +583,7 @@ int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const
     hipSetDevice(ctx->device);
     lime_set *s = new_set(ctx, sp, n);
     uint32_t *d_len = nullptr;
-    int rc = upload_space(ctx, sp, &s->d_off, &d_len);  // (borrowed)
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len, &s->space_keep);
     if (rc == LIME_OK) rc = sort_set_global(ctx, s, d_gs, d_ge, d_row, d_len);
     if (rc != LIME_OK) {
         delete s;
@@ -805,6 +841,27 @@ int lime_intersect_checksum(lime_pairs *plan, uint64_t *sum, uint64_t *xr) {
     hipSetDevice(plan->ctx->device);
     if (plan->closest) return closest_checksum(plan->closest, sum, xr);
     return intersect_checksum(plan->plan, sum, xr);
+}
+
+int lime_pairs_checksum_device(lime_ctx *ctx, const lime_pair *d_pairs, int64_t count,
+                               uint64_t *sum, uint64_t *xr) {
+    if (!ctx || count < 0 || (count > 0 && !d_pairs) || !sum || !xr)
+        return fail(LIME_ERR_ARG, "bad checksum arguments");
+    hipSetDevice(ctx->device);
+    unsigned long long *d_out = nullptr;
+    LIME_TRY(alloc(ctx, &d_out, 2));
+    PoolGuard<unsigned long long> g{ctx, d_out};
+    LIME_HIP(hipMemsetAsync(d_out, 0, 16, S(ctx)));
+    if (count > 0)
+        hipLaunchKernelGGL(k_pairs_hash, dim3(std::min<unsigned>(blocks_for(count, 256), 8192u)),
+                           dim3(256), 0, S(ctx), reinterpret_cast<const uint4 *>(d_pairs), count,
+                           d_out);
+    LIME_HIP(hipGetLastError());
+    uint64_t h[2];
+    LIME_TRY(read_back(ctx, h, d_out, 16));
+    *sum = h[0];
+    *xr = h[1];
+    return LIME_OK;
 }
 
 int lime_pairs_destroy(lime_pairs *plan) {

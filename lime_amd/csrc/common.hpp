@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -58,6 +59,14 @@ struct Pool {
     void release_all();
 };
 
+// A space's contig offsets and lengths on the device, cached per context
+// (space_device) and shared by the sets created in it
+struct SpaceDev {
+    lime_ctx *ctx = nullptr;
+    uint32_t *off = nullptr, *len = nullptr;
+    ~SpaceDev();
+};
+
 }  // namespace lime
 
 struct lime_ctx {
@@ -68,10 +77,13 @@ struct lime_ctx {
     std::mutex mu;
     // small pinned scratch for scalar read-backs
     void *pinned = nullptr;
-    // device copies of every space's (off, len) used with this context, keyed
+    // device copies of the spaces' (off, len) used with this context, keyed
     // by the offsets (which determine the lengths): uploaded once, so an
-    // operator never drains the stream to upload them (space_device)
-    std::map<std::vector<uint32_t>, std::pair<uint32_t *, uint32_t *>> spaces;
+    // operator never drains the stream to upload them (space_device).
+    // Bounded: past SPACE_CACHE entries, the ones no live set holds are
+    // dropped (ad-hoc spaces no longer accumulate)
+    std::map<std::vector<uint32_t>, std::shared_ptr<lime::SpaceDev>> spaces;
+    static constexpr size_t SPACE_CACHE = 8;
     hipEvent_t ev = nullptr;
 };
 
@@ -89,8 +101,10 @@ struct lime_set {
     uint32_t *gs = nullptr;   // global start
     uint32_t *ge = nullptr;   // global end
     uint32_t *row = nullptr;  // input row
-    // device copy of the space offsets (n_contigs + 1)
+    // device copy of the space offsets (n_contigs + 1), borrowed from the
+    // context's cache entry `space_keep` (held while the set lives)
     uint32_t *d_off = nullptr;
+    std::shared_ptr<lime::SpaceDev> space_keep;
     int32_t n_contigs = 0;
     std::vector<uint32_t> off;  // host copy
     std::vector<int64_t> len;
@@ -168,9 +182,10 @@ struct PoolGuard {
 int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes);
 
 // the context's device copy of a space's contig offsets (n + 1 entries) and
-// lengths (n + 1, the last 0), owned by the context: never released by callers
+// lengths (n + 1, the last 0), owned by the context's cache: never released
+// by callers; valid for the call, or as long as `keep` is held
 int space_device(lime_ctx *c, const std::vector<uint32_t> &off, const uint32_t **d_off,
-                 const uint32_t **d_len);
+                 const uint32_t **d_len, std::shared_ptr<SpaceDev> *keep = nullptr);
 
 // grid helper
 inline unsigned blocks_for(int64_t n, int64_t per_block) {

@@ -718,36 +718,21 @@ FillArgs fill_args(PairsPlan *pl) {
     return fa;
 }
 
-// Output records per fill workgroup.  Default (0): one wave of resident
-// workgroups covers the window, each prefetching its next tile behind its
-// stores (1-3% faster than 131072-record workgroups,
-// profiles/r05_fill_sweep.txt); LIME_FILL_SPAN overrides it for tuning.
+// Output records per fill workgroup: one wave of resident workgroups covers
+// the window, each prefetching its next tile behind its stores (1-3% faster
+// than 131072-record workgroups, profiles/r05_fill_sweep.txt).  The device's
+// slot count is queried once per process.
 int64_t fill_span(int64_t count) {
-    static const int64_t env = [] {
-        const char *e = getenv("LIME_FILL_SPAN");
-        return e ? (int64_t)atoll(e) : (int64_t)-1;
-    }();
-    int64_t per = env < 0 ? 0 : env;
-    if (per == 0) {
+    static const int64_t slots = [] {
         int dev = 0, cus = 256, occ = 2;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fill<false, false>, FB, 0);
-        const int64_t slots = (int64_t)cus * (occ > 0 ? occ : 1);
-        per = (count + slots - 1) / slots;
-    }
+        return (int64_t)cus * (occ > 0 ? occ : 1);
+    }();
+    int64_t per = (count + slots - 1) / slots;
     per = (per + 63) & ~(int64_t)63;
     return per < 4096 ? 4096 : per;
-}
-
-// Wave granule of the fill (records); LIME_FILL_GRAN overrides GR for tuning.
-int64_t fill_gran() {
-    static const int64_t g = [] {
-        const char *e = getenv("LIME_FILL_GRAN");
-        const int64_t v = e ? (int64_t)atoll(e) : GR;
-        return v < 64 ? (int64_t)64 : v;
-    }();
-    return g;
 }
 
 int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_t *cksum) {
@@ -773,14 +758,14 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
         const dim3 g((unsigned)grid);
         const bool win = pl->reach >= 0;
         if (cksum && win)
-            hipLaunchKernelGGL((k_fill<true, true>), g, dim3(FB), 0, S(ctx), fa, per, fill_gran());
+            hipLaunchKernelGGL((k_fill<true, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
         else if (cksum)
-            hipLaunchKernelGGL((k_fill<true, false>), g, dim3(FB), 0, S(ctx), fa, per, fill_gran());
+            hipLaunchKernelGGL((k_fill<true, false>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
         else if (win)
-            hipLaunchKernelGGL((k_fill<false, true>), g, dim3(FB), 0, S(ctx), fa, per, fill_gran());
+            hipLaunchKernelGGL((k_fill<false, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
         else
             hipLaunchKernelGGL((k_fill<false, false>), g, dim3(FB), 0, S(ctx), fa, per,
-                               fill_gran());
+                               (int64_t)GR);
     }
     LIME_HIP(hipGetLastError());
     return LIME_OK;
@@ -957,6 +942,7 @@ int window_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t d,
     W->n = A->n;
     W->row = A->row;  // borrowed: W's row i is A's row i
     W->d_off = A->d_off;
+    W->space_keep = A->space_keep;
     W->n_contigs = A->n_contigs;
     W->off = A->off;
     W->len = A->len;

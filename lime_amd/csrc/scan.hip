@@ -90,9 +90,14 @@ __global__ __launch_bounds__(SB) void k_scan_blocks(const T *__restrict__ in, T 
 // chunks (blocked per thread, staged through LDS): the three-launch path's
 // fixed cost (~15-20 us of back-to-back tiny kernels) dominates below ~64k
 constexpr int QB = 1024;
-constexpr int QITEMS = 16;
-constexpr int QTILE = QB * QITEMS;
-constexpr int64_t SMALL_SCAN = 4 * QTILE;
+// items per thread: a 64 KiB LDS tile for either width (16 u32 / 8 u64), so
+// the kernel fits a 64 KiB-LDS target as well as gfx950's 160 KiB
+template <typename T>
+constexpr int qitems() { return 64 / (int)sizeof(T); }
+template <typename T>
+constexpr int qtile() { return QB * qitems<T>(); }
+static_assert(qtile<uint64_t>() * sizeof(uint64_t) == 65536, "64 KiB small-scan tile");
+constexpr int64_t SMALL_SCAN = 4 * QB * 16;
 template <typename T>
 __device__ __forceinline__ void scan_small_block(const T *in, T *out, int64_t n, T *total);
 template <typename T>
@@ -110,6 +115,7 @@ __global__ __launch_bounds__(QB) void k_scan_small2(const T *in0, T *out0, int64
 }
 template <typename T>
 __device__ __forceinline__ void scan_small_block(const T *in, T *out, int64_t n, T *total) {
+    constexpr int QITEMS = qitems<T>(), QTILE = qtile<T>();
     __shared__ T tile[QTILE];
     __shared__ T scratch[QB / 64 + 1];
     T carry = 0;

@@ -43,17 +43,16 @@ struct SubArgs {
     const uint32_t *ags, *age, *arow;
     const uint32_t *bgs, *bge, *brow, *bpmax;
     const uint32_t *olo, *ocnt;
-    // RUNS (threshold <= 0): B's merge runs -- run id of every sorted row and
-    // the first sorted row of every run (nruns + 1 entries)
-    const uint32_t *brun, *rfirst;
+    // RUNS (threshold <= 0): B's merge runs -- run id of every sorted row
+    const uint32_t *brun;
     int64_t na, nb;
     int64_t t;
     int mode;
-    // RUNS: lo1 / hi1 found in the staged window (no owner_ranges); zw = B
-    // holds zero-width rows
-    int inl, zw;
+    // zw = B holds zero-width rows
+    int zw;
     uint64_t *count;        // pass 1
     const uint64_t *off;    // pass 2
+    unsigned int *err;      // pass 2 (RUNS): a block's recount differs from pass 1
     uint32_t *ogs, *oge, *oar, *obr;
 };
 
@@ -166,7 +165,9 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     // the block's hit window [wlo, whi) of B (spanning and inside hits):
     // consecutive left rows share most of it, so it is loaded once,
     // coalesced, into LDS
-    const bool inl = RUNS && sa.inl;
+    // RUNS: each row's inside-hit range is found in the staged window (no
+    // owner_ranges pass)
+    constexpr bool inl = RUNS;
     // inline ranges: wstart holds one start per 4 blocks (the count pass's
     // workgroups); the block's own is searched from there (every wave alike)
     int64_t wlo;
@@ -219,11 +220,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     auto Brow = [&](int64_t j) { return win && !RUNS ? w_row[j - wlo] : sa.brow[j]; };
     auto Bpm = [&](int64_t j) { return inw(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
     auto Brun = [&](int64_t j) { return RUNS ? (inw(j) ? w_run[j - wlo] : sa.brun[j]) : 0u; };
-    // end of j's run cut at hi1 (j < hi1): rfirst, or with inline ranges a
-    // search over the run ids (monotone), no rfirst table
+    // end of j's run cut at hi1 (j < hi1): a search over the run ids
+    // (monotone)
     auto run_end = [&](int64_t j, int64_t hi1) -> int64_t {
         const uint32_t r = Brun(j);
-        if (!inl) return min((int64_t)sa.rfirst[r + 1], hi1);
         if (Brun(hi1 - 1) == r) return hi1;
         int64_t l = j + 1, h = hi1 - 1;
         while (l < h) {
@@ -484,6 +484,12 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             return;
         }
         bbase = (int64_t)sa.off[blockIdx.x];
+        // the recount must equal the count pass's block total (k_sub_count_runs
+        // folds the same runs): a mismatch would write outside the block
+        if ((int64_t)total != (int64_t)sa.off[blockIdx.x + 1] - bbase) {
+            if (threadIdx.x == 0) atomicOr(sa.err, 1u);
+            return;
+        }
         bend = bbase + (int64_t)total;
         staged = total <= (uint64_t)SCAP;
         pos = bbase + (int64_t)(before + inc - n_out);
@@ -645,14 +651,6 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     if (lane == 0 && sb < nblk) sa.count[sb] = tot;
 }
 
-// first sorted row of every run (rfirst[nruns] = n)
-__global__ __launch_bounds__(256) void k_run_first(const uint32_t *__restrict__ run, int64_t n,
-                                                   int64_t nruns, uint32_t *__restrict__ rfirst) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j < n && (j == 0 || run[j] != run[j - 1])) rfirst[run[j]] = (uint32_t)j;
-    if (j == 0) rfirst[nruns] = (uint32_t)n;
-}
-
 }  // namespace
 
 int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
@@ -676,13 +674,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     if (!runs) LIME_TRY(build_prefix_max(ctx, B));
     // runs: the count (k_sub_count_runs) and write passes find each row's
     // inside-hit range in their staged windows, no owner_ranges pass
-    // (LIME_SUB_COUNT_FOLD=1: owner_ranges + the write pass's own fold as
-    // the count pass, for A/B)
-    static const bool count_fold = [] {
-        const char *e = getenv("LIME_SUB_COUNT_FOLD");
-        return e && atoi(e) != 0;
-    }();
-    const bool inl = runs && !count_fold;
+    const bool inl = runs;
     uint32_t *olo = nullptr, *ocnt = nullptr;
     uint64_t *cnt, *off;
     if (!inl) {
@@ -691,6 +683,10 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     }
     LIME_TRY(alloc(ctx, &cnt, (size_t)na + 1));
     LIME_TRY(alloc(ctx, &off, (size_t)na + 1));
+    unsigned int *err;
+    LIME_TRY(alloc(ctx, &err, 1));
+    PoolGuard<unsigned int> ge{ctx, err};
+    LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
     if (!inl) LIME_TRY(owner_ranges(ctx, A, B, 0, threshold, olo, ocnt));
     const int64_t nblk = (na + SUB_B - 1) / SUB_B;
     // window starts: per block, or per count workgroup (CNT_WAVES blocks)
@@ -723,28 +719,19 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.mode = mode;
     sa.count = cnt;
     sa.off = off;
+    sa.err = err;
     sa.ogs = sa.oge = sa.oar = sa.obr = nullptr;
-    sa.brun = sa.rfirst = nullptr;
-    sa.inl = inl ? 1 : 0;
+    sa.brun = nullptr;
     sa.zw = B->has_zero_width ? 1 : 0;
     lime_result mb;
     mb.ctx = ctx;
-    uint32_t *rfirst = nullptr;
     PoolGuard<uint32_t> g1{ctx, mb.run_of_sorted};
     PoolGuard<uint32_t> g2{ctx, mb.gs};
     PoolGuard<uint32_t> g3{ctx, mb.ge};
-    PoolGuard<uint32_t> g4{ctx, rfirst};
     if (runs) {
         LIME_TRY(merge_runs_with_pmax(ctx, B, &mb));
         sa.bpmax = B->pmax;  // built by the merge scan when it was not yet
-        if (!inl) {  // inline ranges search the run ids instead
-            LIME_TRY(alloc(ctx, &rfirst, (size_t)mb.n + 1));
-            hipLaunchKernelGGL(k_run_first, dim3(blocks_for(B->n, 256)), dim3(256), 0, S(ctx),
-                               (const uint32_t *)mb.run_of_sorted, B->n, mb.n, rfirst);
-            LIME_HIP(hipGetLastError());
-        }
         sa.brun = mb.run_of_sorted;
-        sa.rfirst = rfirst;
     }
     auto launch = [&](bool write) {
         const dim3 g(blocks_for(na, SUB_B)), b(SUB_B);
@@ -753,7 +740,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         else if (runs) hipLaunchKernelGGL((k_subtract<false, true>), g, b, 0, S(ctx), sa);
         else hipLaunchKernelGGL((k_subtract<false, false>), g, b, 0, S(ctx), sa);
     };
-    if (inl)
+    if (runs)
         hipLaunchKernelGGL(k_sub_count_runs, dim3(blocks_for(na, CNT_ROWS)), dim3(CNT_WAVES * 64),
                            0, S(ctx), sa, nblk);
     else
@@ -774,6 +761,11 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.obr = res->b_row;
     launch(true);
     LIME_HIP(hipGetLastError());
+    if (runs) {
+        unsigned int e = 0;
+        LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
+        if (e) return fail(LIME_ERR_DEVICE, "subtract: write pass recount differs from the count pass");
+    }
     release(ctx, olo);
     release(ctx, ocnt);
     release(ctx, cnt);

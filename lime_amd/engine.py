@@ -493,6 +493,14 @@ class Context:
         check(_lib().lime_bitset_and_runs(self._h, len(sets), arr, C.byref(h), C.byref(n)))
         return Result(self, h, sets[0].space)
 
+    def pairs_checksum_device(self, d_pairs, count):
+        """(sum, xor) of pair_hash over `count` 16-B records already stored in
+        a device buffer (e.g. a chunk fill_device wrote)"""
+        s, x = u64(), u64()
+        check(_lib().lime_pairs_checksum_device(self._h, vp(d_pairs), int(count), C.byref(s),
+                                                C.byref(x)))
+        return s.value, x.value
+
     # ----------------------------------------------------------- synth
     def synth_uniform(self, space, n, seed, len_lo, len_hi, d_contig, d_start, d_end):
         check(_lib().lime_synth_uniform(self._h, space.handle, int(n), int(seed), int(len_lo),

@@ -311,7 +311,10 @@ class DistributedSubtract(_Op):
                     continue
                 A = self.ctx.set_from_host(space, *_arrays(space, lr, lrows))
                 B = self.ctx.set_from_host(space, *_arrays(space, rr, rrows))
-                res = self.ctx.subtract(A, B, self.threshold, self.mode).to_host()
+                r = self.ctx.subtract(A, B, self.threshold, self.mode)
+                res = r.to_host()
+                for h in (r, A, B):  # back to the pool now, not at GC
+                    h.close()
                 for k in range(len(res["start"])):
                     a = lrows[res["a_row"][k]]
                     b = rrows[res["b_row"][k]] if res["b_row"][k] >= 0 else None

@@ -116,13 +116,16 @@ typedef struct {
     int32_t *contig;
     int64_t *start, *end, *lrow, *rrow;
     /* hash: also fold lo_pair_hash(start, end, lrow, rrow) into (hsum, hxor),
-     * the order-independent checksum of SURVEY.md 8(d); grow: the arrays are
-     * owned and doubled on demand (the contig-sharded drivers below) */
+     * the order-independent checksum of SURVEY.md 8(d) (hash == 2: the result
+     * form, mix64(lo_pair_hash(...) + contig), absent rows as 0xffffffff, as
+     * the engine's lime_result_checksum); grow: the arrays are owned and
+     * doubled on demand (the contig-sharded drivers below) */
     int hash, grow;
     uint64_t hsum, hxor;
 } lo_out;
 
 uint64_t lo_pair_hash(uint32_t start, uint32_t end, uint32_t a, uint32_t b);
+static uint64_t lo_mix64(uint64_t z);
 
 static void lo_out_grow(lo_out *o) {
     int64_t cap = o->cap ? 2 * o->cap : 1024;
@@ -137,6 +140,7 @@ static void lo_out_grow(lo_out *o) {
 static void lo_emit(lo_out *o, int32_t c, int64_t s, int64_t e, int64_t lr, int64_t rr) {
     if (o->hash) {
         uint64_t h = lo_pair_hash((uint32_t)s, (uint32_t)e, (uint32_t)lr, (uint32_t)rr);
+        if (o->hash == 2) h = lo_mix64(h + (uint64_t)(uint32_t)c);
         o->hsum += h;
         o->hxor ^= h;
     }
@@ -393,14 +397,10 @@ typedef struct {
     int64_t start, end, rrow;
 } lo_block;
 
-int64_t lo_subtract(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
-                    const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
-                    const int64_t *re, const int8_t *rstr, int64_t threshold, int mode,
-                    int64_t cap, int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow,
-                    int64_t *orrow) {
-    lo_region *L = lo_load(nl, lc, ls, le, lstr);
-    lo_region *R = lo_load(nr, rc, rs, re, rstr);
-    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+/* Subtract.scala:91-116 processHits over the SetTheory.scala:131-187 sweep,
+ * on one sorted partition */
+static void lo_subtract_sorted(const lo_region *L, int64_t nl, const lo_region *R, int64_t nr,
+                               int64_t threshold, int mode, lo_out *o) {
     lo_cache cache = {0};
     int64_t rpos = 0;
     lo_block *blocks = NULL;
@@ -451,30 +451,41 @@ int64_t lo_subtract(int64_t nl, const int32_t *lc, const int64_t *ls, const int6
             nb++;
         }
         if (nb == 0) { /* :100-101 (L, (v, None)) */
-            lo_emit(&out, cur->contig, cur->start, cur->end, cur->row, -1);
+            lo_emit(o, cur->contig, cur->start, cur->end, cur->row, -1);
             continue;
         }
         if (mode == LO_SUB_LIME) {
             /* :109-114 over the reversed block list; subtract() :53-75 */
             for (int64_t b = nb - 1; b >= 0; --b) {
                 if (blocks[b].start > cur->start)
-                    lo_emit(&out, cur->contig, cur->start, blocks[b].start, cur->row, blocks[b].rrow);
+                    lo_emit(o, cur->contig, cur->start, blocks[b].start, cur->row, blocks[b].rrow);
                 if (cur->end > blocks[b].end)
-                    lo_emit(&out, cur->contig, blocks[b].end, cur->end, cur->row, blocks[b].rrow);
+                    lo_emit(o, cur->contig, blocks[b].end, cur->end, cur->row, blocks[b].rrow);
             }
         } else {
             /* a \ (B_0 u ... u B_{nb-1}); blocks are disjoint, sorted */
             int64_t pos = cur->start;
             for (int64_t b = 0; b < nb; ++b) {
                 if (blocks[b].start > pos)
-                    lo_emit(&out, cur->contig, pos, blocks[b].start, cur->row, blocks[b].rrow);
+                    lo_emit(o, cur->contig, pos, blocks[b].start, cur->row, blocks[b].rrow);
                 if (blocks[b].end > pos) pos = blocks[b].end;
             }
-            if (cur->end > pos) lo_emit(&out, cur->contig, pos, cur->end, cur->row, blocks[nb - 1].rrow);
+            if (cur->end > pos) lo_emit(o, cur->contig, pos, cur->end, cur->row, blocks[nb - 1].rrow);
         }
     }
     free(blocks);
     free(cache.v);
+}
+
+int64_t lo_subtract(int64_t nl, const int32_t *lc, const int64_t *ls, const int64_t *le,
+                    const int8_t *lstr, int64_t nr, const int32_t *rc, const int64_t *rs,
+                    const int64_t *re, const int8_t *rstr, int64_t threshold, int mode,
+                    int64_t cap, int32_t *oc, int64_t *os, int64_t *oe, int64_t *olrow,
+                    int64_t *orrow) {
+    lo_region *L = lo_load(nl, lc, ls, le, lstr);
+    lo_region *R = lo_load(nr, rc, rs, re, rstr);
+    lo_out out = {0, cap, oc, os, oe, olrow, orrow};
+    lo_subtract_sorted(L, nl, R, nr, threshold, mode, &out);
     free(L);
     free(R);
     return out.count;
@@ -538,6 +549,32 @@ int64_t lo_merge(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e
  * Q4) are dropped.  Strand is ignored (the gap regions carry none).
  * Returns -1 if a data contig is outside [0, n_genome) (the reference throws
  * NoSuchElementException from referenceNameBounds(name), :106,118). */
+/* the gaps of one contig g (its rows A[0..n), sorted) */
+static void lo_complement_contig(const lo_region *A, int64_t n, int32_t g, int64_t glen,
+                                 lo_out *o) {
+    int64_t pos = 0;
+    int have = 0;
+    lo_region head;
+    for (int64_t i = 0; i < n; ++i) {
+        const lo_region *a = &A[i];
+        if (have && lo_overlaps(&head, a)) {
+            if (a->end > head.end) head.end = a->end;
+            continue;
+        }
+        if (have) { /* close the previous run: gap before the new one */
+            if (head.start > pos) lo_emit(o, g, pos, head.start, -1, -1);
+            if (head.end > pos) pos = head.end;
+        }
+        head = *a;
+        have = 1;
+    }
+    if (have) {
+        if (head.start > pos) lo_emit(o, g, pos, head.start, -1, -1);
+        if (head.end > pos) pos = head.end;
+    }
+    if (glen > pos) lo_emit(o, g, pos, glen, -1, -1);
+}
+
 int64_t lo_complement(int64_t n, const int32_t *c, const int64_t *s, const int64_t *e,
                       int32_t n_genome, const int64_t *genome_len, int64_t cap, int32_t *oc,
                       int64_t *os, int64_t *oe) {
@@ -547,27 +584,9 @@ int64_t lo_complement(int64_t n, const int32_t *c, const int64_t *s, const int64
     lo_out out = {0, cap, oc, os, oe, NULL, NULL};
     int64_t i = 0;
     for (int32_t g = 0; g < n_genome; ++g) {
-        int64_t pos = 0;
-        int have = 0;
-        lo_region head;
-        while (i < n && A[i].contig == g) {
-            const lo_region *a = &A[i++];
-            if (have && lo_overlaps(&head, a)) {
-                if (a->end > head.end) head.end = a->end;
-                continue;
-            }
-            if (have) { /* close the previous run: gap before the new one */
-                if (head.start > pos) lo_emit(&out, g, pos, head.start, -1, -1);
-                if (head.end > pos) pos = head.end;
-            }
-            head = *a;
-            have = 1;
-        }
-        if (have) {
-            if (head.start > pos) lo_emit(&out, g, pos, head.start, -1, -1);
-            if (head.end > pos) pos = head.end;
-        }
-        if (genome_len[g] > pos) lo_emit(&out, g, pos, genome_len[g], -1, -1);
+        const int64_t i0 = i;
+        while (i < n && A[i].contig == g) ++i;
+        lo_complement_contig(A + i0, i - i0, g, genome_len[g], &out);
     }
     free(A);
     return out.count;
@@ -649,10 +668,12 @@ static lo_region *lo_load_group(const lo_groups *g, int32_t k, int64_t *n_out) {
 }
 
 typedef struct {
-    int op; /* 0 intersect, 1 merge */
+    int op; /* 0 intersect, 1 merge, 2 subtract, 3 complement */
     int32_t nc;
     lo_groups L, R;
     int64_t threshold;
+    int mode;                  /* subtract */
+    const int64_t *genome_len; /* complement */
     int keep;            /* buffer the records (else count + checksum only) */
     int32_t *order;      /* contigs, largest first */
     int next;            /* work-queue head (atomic) */
@@ -669,12 +690,18 @@ static void *lo_mt_worker(void *arg) {
         lo_out *o = &m->res[k];
         int64_t nl = 0, nr = 0;
         lo_region *L = lo_load_group(&m->L, k, &nl);
-        if (m->op == 0) {
+        if (m->op == 0 || m->op == 2) {
             lo_region *R = lo_load_group(&m->R, k, &nr);
-            o->hash = 1;
+            o->hash = m->op == 0 ? 1 : 2;
             o->grow = m->keep;
-            lo_intersect_sorted(L, nl, R, nr, m->threshold, o);
+            if (m->op == 0)
+                lo_intersect_sorted(L, nl, R, nr, m->threshold, o);
+            else
+                lo_subtract_sorted(L, nl, R, nr, m->threshold, m->mode, o);
             free(R);
+        } else if (m->op == 3) {
+            o->hash = 2;
+            lo_complement_contig(L, nl, k, m->genome_len[k], o);
         } else {
             /* at most one run per row: the buffers are sized by the rows */
             o->cap = nl;
@@ -693,12 +720,12 @@ static void lo_mt_run(lo_mt *m, int nthreads) {
     for (int32_t k = 0; k < m->nc; ++k) m->order[k] = k;
     for (int32_t a = 1; a < m->nc; ++a) { /* insertion sort: nc is small */
         const int32_t k = m->order[a];
-        const int64_t w = (m->L.off[k + 1] - m->L.off[k]) + (m->op == 0 ? m->R.off[k + 1] - m->R.off[k] : 0);
+        const int64_t w = (m->L.off[k + 1] - m->L.off[k]) + (m->R.off ? m->R.off[k + 1] - m->R.off[k] : 0);
         int32_t b = a - 1;
         while (b >= 0) {
             const int32_t j = m->order[b];
             const int64_t wj = (m->L.off[j + 1] - m->L.off[j]) +
-                               (m->op == 0 ? m->R.off[j + 1] - m->R.off[j] : 0);
+                               (m->R.off ? m->R.off[j + 1] - m->R.off[j] : 0);
             if (wj >= w) break;
             m->order[b + 1] = j;
             --b;
@@ -830,5 +857,74 @@ int64_t lo_merge_mt(int32_t n_contigs, int64_t n, const int32_t *c, const uint32
     if (!run_of_row) free(rid);
     if (gsum) *gsum = hs;
     if (gxr) *gxr = hx;
+    return total;
+}
+
+/* subtract (Subtract.scala:91-116 over the sweep) sharded by contig, both
+ * modes.  Returns the region count; (*sum, *xr) receive the result checksum
+ * of every region -- sum / xor of mix64(lo_pair_hash(start, end, a_row,
+ * b_row) + contig), an absent b_row (None) as 0xffffffff -- the form of the
+ * engine's lime_result_checksum. */
+int64_t lo_subtract_mt(int32_t n_contigs, int64_t nl, const int32_t *lc, const uint32_t *ls,
+                       const uint32_t *le, int64_t nr, const int32_t *rc, const uint32_t *rs,
+                       const uint32_t *re, int64_t threshold, int mode, int nthreads,
+                       uint64_t *sum, uint64_t *xr) {
+    for (int64_t i = 0; i < nl; ++i)
+        if (lc[i] < 0 || lc[i] >= n_contigs) return -1;
+    for (int64_t i = 0; i < nr; ++i)
+        if (rc[i] < 0 || rc[i] >= n_contigs) return -1;
+    lo_mt m;
+    memset(&m, 0, sizeof(m));
+    m.op = 2;
+    m.nc = n_contigs;
+    m.threshold = threshold;
+    m.mode = mode;
+    lo_group(&m.L, n_contigs, nl, lc, ls, le);
+    lo_group(&m.R, n_contigs, nr, rc, rs, re);
+    lo_mt_run(&m, nthreads);
+    int64_t total = 0;
+    uint64_t hs = 0, hx = 0;
+    for (int32_t k = 0; k < n_contigs; ++k) {
+        total += m.res[k].count;
+        hs += m.res[k].hsum;
+        hx ^= m.res[k].hxor;
+        lo_out_free(&m.res[k]);
+    }
+    free(m.res);
+    lo_ungroup(&m.L);
+    lo_ungroup(&m.R);
+    if (sum) *sum = hs;
+    if (xr) *xr = hx;
+    return total;
+}
+
+/* complement (Complement.scala:59-128 in the ComplementSuite-pinned form)
+ * sharded by contig: the genome has n_contigs contigs (String order), every
+ * row's contig among them.  Returns the gap count and the result checksum
+ * (as lo_subtract_mt, both rows absent). */
+int64_t lo_complement_mt(int32_t n_contigs, const int64_t *genome_len, int64_t n,
+                         const int32_t *c, const uint32_t *s, const uint32_t *e, int nthreads,
+                         uint64_t *sum, uint64_t *xr) {
+    for (int64_t i = 0; i < n; ++i)
+        if (c[i] < 0 || c[i] >= n_contigs) return -1;
+    lo_mt m;
+    memset(&m, 0, sizeof(m));
+    m.op = 3;
+    m.nc = n_contigs;
+    m.genome_len = genome_len;
+    lo_group(&m.L, n_contigs, n, c, s, e);
+    lo_mt_run(&m, nthreads);
+    int64_t total = 0;
+    uint64_t hs = 0, hx = 0;
+    for (int32_t k = 0; k < n_contigs; ++k) {
+        total += m.res[k].count;
+        hs += m.res[k].hsum;
+        hx ^= m.res[k].hxor;
+        lo_out_free(&m.res[k]);
+    }
+    free(m.res);
+    lo_ungroup(&m.L);
+    if (sum) *sum = hs;
+    if (xr) *xr = hx;
     return total;
 }

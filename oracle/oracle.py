@@ -61,6 +61,11 @@ def lib():
         L.lo_merge_mt.restype = i64
         L.lo_merge_mt.argtypes = [i32, i64, P(i32), u32p, u32p, C.c_int, i64, P(i32), P(i64),
                                   P(i64), P(i64), u64p, u64p]
+        L.lo_subtract_mt.restype = i64
+        L.lo_subtract_mt.argtypes = [i32, i64, P(i32), u32p, u32p, i64, P(i32), u32p, u32p, i64,
+                                     C.c_int, C.c_int, u64p, u64p]
+        L.lo_complement_mt.restype = i64
+        L.lo_complement_mt.argtypes = [i32, P(i64), i64, P(i32), u32p, u32p, C.c_int, u64p, u64p]
         L.lo_pair_hash.restype = C.c_uint64
         L.lo_pair_hash.argtypes = [C.c_uint32] * 4
         _lib = L
@@ -264,3 +269,59 @@ def grouping_checksum(run_of_row):
     with np.errstate(over="ignore"):
         tot = int(np.sum(h, dtype=np.uint64))
     return tot, (int(np.bitwise_xor.reduce(h)) if len(h) else 0)
+
+
+def subtract_mt(n_contigs, a, b, threshold=0, mode=SUB_LIME, nthreads=None):
+    """Contig-sharded subtract (lo_subtract_mt): {"n", "sum", "xor"}, the
+    checksum in lime_result_checksum's region form."""
+    L = lib()
+    na, ac, as_, ae = _in32(*a)
+    nb, bc, bs, be = _in32(*b)
+    u32p = P(C.c_uint32)
+    sm, xr = C.c_uint64(), C.c_uint64()
+    n = L.lo_subtract_mt(int(n_contigs), na, _p(ac, i32), as_.ctypes.data_as(u32p),
+                         ae.ctypes.data_as(u32p), nb, _p(bc, i32), bs.ctypes.data_as(u32p),
+                         be.ctypes.data_as(u32p), int(threshold), int(mode),
+                         int(nthreads or threads()), C.byref(sm), C.byref(xr))
+    if n < 0:
+        raise KeyError("contig id outside [0, n_contigs)")
+    return {"n": int(n), "sum": sm.value, "xor": xr.value}
+
+
+def complement_mt(genome_lengths, a, nthreads=None):
+    """Contig-sharded complement (lo_complement_mt): {"n", "sum", "xor"}, the
+    checksum in lime_result_checksum's region form."""
+    L = lib()
+    g = np.ascontiguousarray(genome_lengths, dtype=np.int64)
+    n, c, s, e = _in32(*a)
+    u32p = P(C.c_uint32)
+    sm, xr = C.c_uint64(), C.c_uint64()
+    k = L.lo_complement_mt(len(g), _p(g, i64), n, _p(c, i32), s.ctypes.data_as(u32p),
+                           e.ctypes.data_as(u32p), int(nthreads or threads()), C.byref(sm),
+                           C.byref(xr))
+    if k < 0:
+        raise KeyError("contig not in genome")
+    return {"n": int(k), "sum": sm.value, "xor": xr.value}
+
+
+def result_checksum(res):
+    """numpy restatement of lime_result_checksum's region part: sum / xor of
+    mix64(pair_hash(start, end, a_row, b_row) + contig), absent rows
+    (missing, or < 0) as 0xffffffff"""
+    from lime_amd.synth import mix64
+    n = len(res["start"])
+    ff = np.full(n, 0xFFFFFFFF, np.uint64)
+
+    def rows(k):
+        r = res.get(k)
+        if r is None:
+            return ff
+        r = np.asarray(r, np.int64)
+        return np.where(r < 0, ff, r.astype(np.uint64))
+    s = np.asarray(res["start"], np.uint64)
+    e = np.asarray(res["end"], np.uint64)
+    a, b = rows("a_row"), rows("b_row")
+    with np.errstate(over="ignore"):
+        h = mix64(mix64(((s << np.uint64(32)) | e) ^ mix64((a << np.uint64(32)) | b)) +
+                  np.asarray(res["contig"], np.uint64))
+        return int(np.sum(h, dtype=np.uint64)), (int(np.bitwise_xor.reduce(h)) if n else 0)

@@ -6,7 +6,8 @@ at scale"), HIP engine through the C-ABI against the CPU oracle.
       autosomes of genome.txt (chr1-22 in file order, len U[200,2000], seed 1)
   C2  2 x 1e8 rows, uniform over hg38, len U[50,5000]: the pair count and the
       order-independent checksum of all ~1.63e10 pairs == the oracle's
-      (contig-sharded, lo_intersect_mt); merge runs exact, grouping checksum
+      (contig-sharded, lo_intersect_mt), both as the fill computes it and
+      over the records it stores in HBM; merge runs exact, grouping checksum
   C3  pile-up merge: exact runs + run_of_row at 1/50 scale; at full size
       (5e8 rows) exact runs and the checksum of every row's run
   C4  the hg38 bitset path (unsorted rows -> binned paint), A, B = 1e7 rows,
@@ -192,6 +193,21 @@ def test_c2_full_size_checksum(ctx):
     assert plan.n == exp["n"]
     assert 1.5e10 < plan.n < 1.75e10  # E[pairs] ~ 1.63e10
     assert got == (exp["sum"], exp["xor"])
+    # the bytes the benchmarked fill STORES (k_fill<false, false>, 2^31-record
+    # chunks through one reusable 34 GB buffer, as bench.py), hashed from HBM
+    # by a separate kernel: every stored record, not only the fill's
+    # register-side checksum instantiation
+    import torch
+    chunk = 1 << 31
+    buf = torch.empty((chunk, 4), dtype=torch.int32, device="cuda")
+    hs, hx, f = 0, 0, 0
+    while f < plan.n:
+        k = min(chunk, plan.n - f)
+        plan.fill_device(f, k, buf.data_ptr())
+        s, x = ctx.pairs_checksum_device(buf.data_ptr(), k)
+        hs, hx, f = (hs + s) & 0xFFFFFFFFFFFFFFFF, hx ^ x, f + k
+    del buf
+    assert (hs, hx) == (exp["sum"], exp["xor"])
     plan.close()
     # merge(A), merge(B): runs exact, grouping checksum of every row
     for S, X in ((a, A), (b, B)):

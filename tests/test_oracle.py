@@ -339,6 +339,27 @@ def test_mt_drivers_equal_single_partition(seed):
     assert (mm["grp_sum"], mm["grp_xor"]) == oracle.grouping_checksum(em["run_of_row"])
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_mt_subtract_complement_equal_single_partition(seed):
+    # lo_subtract_mt (both modes) / lo_complement_mt: the P = 1 restatement's
+    # regions, by count and lime_result_checksum's region checksum
+    from tests.util import random_sets
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 4000, 3000, n_contigs=5, contig_len=30000, max_len=400,
+                       zero_frac=0.1, dup_frac=0.05, book_frac=0.1)
+    for t in (0, 1, 30, -3):
+        for mode in (oracle.SUB_LIME, oracle.SUB_SET):
+            e = oracle.subtract(A, B, t, mode)
+            m = oracle.subtract_mt(5, A, B, t, mode, nthreads=4)
+            assert m["n"] == len(e["start"])
+            assert (m["sum"], m["xor"]) == oracle.result_checksum(e)
+    genome = [30000, 31000, 32000, 33000, 34000, 40000]  # one contig without rows
+    e = oracle.complement(A, genome)
+    m = oracle.complement_mt(genome, A, nthreads=3)
+    assert m["n"] == len(e["start"])
+    assert (m["sum"], m["xor"]) == oracle.result_checksum(e)
+
+
 def test_mt_drivers_on_reference_fixtures(golden):
     # the IntersectionSuite / MergeSuite inputs through the sharded drivers
     from tests.util import expected, ranked, read_bed_py

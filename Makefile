@@ -22,7 +22,14 @@ LIB      = lime_amd/liblime_amd.so
 ORACLE   = oracle/build/liblime_oracle.so
 CLI      = bin/lime-submit
 
-all: $(LIB) $(ORACLE) $(CLI) bin/bw_probe bin/alloc_probe
+all: $(LIB) $(ORACLE) $(CLI)
+
+# measurement probes (tools/, not part of the product): make probes
+probes: bin/bw_probe bin/alloc_probe bin/rocprim_sort_probe
+
+bin/rocprim_sort_probe: tools/rocprim_sort_probe.hip
+	@mkdir -p bin
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Wno-unused-result -o $@ $<
 
 bin/alloc_probe: tools/alloc_probe.hip
 	@mkdir -p bin
@@ -54,7 +61,7 @@ $(CLI): lime_amd/cli/lime_submit.cpp include/lime_amd.hpp include/lime_amd.h $(L
 clean:
 	rm -rf build oracle/build $(LIB) bin
 
-.PHONY: all clean
+.PHONY: all clean probes
 
 # tuning variant: 3 fill workgroups per CU (tools/ experiments only)
 build/var3/liblime_amd.so: $(HIP_SRCS) $(SRC)/common.hpp include/lime_amd.h $(CPP_OBJS)

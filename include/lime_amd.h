@@ -132,6 +132,13 @@ int lime_set_create_device_stranded(lime_ctx *ctx, const lime_space *space, int6
 int lime_set_create_global(lime_ctx *ctx, const lime_space *space, int64_t n,
                            const uint32_t *d_gstart, const uint32_t *d_gend,
                            const uint32_t *d_row, lime_set **out);
+/* The same with strand codes (device, one per input row, as
+ * lime_set_create_device_stranded): sorted in the full RegionOrdering; a
+ * coordinate shard's stranded rows (merge breaks runs at strand changes). */
+int lime_set_create_global_stranded(lime_ctx *ctx, const lime_space *space, int64_t n,
+                                    const uint32_t *d_gstart, const uint32_t *d_gend,
+                                    const uint32_t *d_row, const int8_t *d_strand,
+                                    lime_set **out);
 int lime_set_destroy(lime_set *set);
 int64_t lime_set_size(const lime_set *set);
 /* first sorted row with gstart >= gkey; on error -(LIME_ERR_*) */
@@ -227,6 +234,18 @@ int lime_subtract(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t t
                   int mode, lime_result **out, int64_t *n_regions);
 int lime_complement(lime_ctx *ctx, const lime_space *genome_space, const lime_set *a,
                     lime_result **out, int64_t *n_regions);
+/* Gaps of sorted, disjoint runs already in HBM (global coordinates, e.g. a
+ * coordinate shard's merged runs after the cross-shard carry) over the genome,
+ * keeping only the gaps whose START lies in [lo, hi) -- a shard's share of
+ * the complement (Complement.scala:59-128 per partition, :67-73 / :112-122
+ * at partition bounds, :39-45 for contigs without data).  The shard passes
+ * its runs framed by the previous shards' last run end (a zero-width run at
+ * it) and the next shards' first run start, so the gaps at its bounds end
+ * where the unsharded result's do; lo = 0, hi = span gives lime_complement
+ * of the runs. */
+int lime_complement_runs(lime_ctx *ctx, const lime_space *genome, int64_t n,
+                         const uint32_t *d_gstart, const uint32_t *d_gend, int64_t lo, int64_t hi,
+                         lime_result **out, int64_t *n_regions);
 int64_t lime_result_size(const lime_result *res);
 /* Host copy of a result: regions in contig-local coordinates plus the
  * left/right input rows (-1 where the reference has None / no payload). */
@@ -234,6 +253,18 @@ int lime_result_fill_host(const lime_result *res, int32_t *contig, int64_t *star
                           int64_t *a_row, int64_t *b_row);
 /* merge only: run index of every input row (the Iterable[T] grouping). */
 int lime_result_run_of_row(const lime_result *res, int64_t *run_of_row);
+/* merge only: the run of every SORTED input row and that row's id, copied
+ * to caller DEVICE buffers (as many as the merged set has rows) -- the
+ * Iterable[T] grouping on the device, which a sharded merge maps to global
+ * run ids after the cross-shard carry */
+int lime_result_copy_run_ids_device(const lime_result *res, uint32_t *d_run, uint32_t *d_row);
+/* device-to-device copy of regions [first, first + count) (global) */
+int lime_result_copy_rows_device(const lime_result *res, int64_t first, int64_t count,
+                                 uint32_t *d_gstart, uint32_t *d_gend);
+/* merge of a stranded set: strand codes of runs [first, first + count) to a
+ * host array (0 for every run of an unstranded merge) -- the sharded merge
+ * carry continues a run across a shard bound only on the same strand */
+int lime_result_run_strands(const lime_result *res, int64_t first, int64_t count, int8_t *out);
 int lime_result_device_arrays(const lime_result *res, const uint32_t **gstart,
                               const uint32_t **gend);
 /* host copy of regions [first, first + count) in global coordinates */
@@ -318,11 +349,14 @@ int lime_bitset_destroy(lime_bitset *bs);
  * counts[r] receives the rows for shard r; when their total is <= cap the
  * rows are also written grouped by shard (shard order, input order within a
  * shard) as global (d_gs, d_ge) and row id row_base + input index (d_row may
- * be NULL).  Validation and error codes as lime_set_create_device. */
+ * be NULL); d_strand_in (per input row, may be NULL) travels with its rows
+ * to d_strand_out (stranded sets: the CLI's ReferenceRegion.stranded keys).
+ * Validation and error codes as lime_set_create_device. */
 int lime_route_rows(lime_ctx *ctx, const lime_space *space, int64_t n, const int32_t *d_contig,
                     const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base,
                     int32_t n_shards, const uint32_t *splits, int clip, int64_t cap,
-                    uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts);
+                    uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts,
+                    const int8_t *d_strand_in, int8_t *d_strand_out);
 
 /* ------------------------------------------------------ synthetic inputs */
 /* Counter-based generators (splitmix64 keyed by (seed, row)) identical to

@@ -68,6 +68,7 @@ SIGNATURES = {
     "lime_set_create_device": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
     "lime_set_create_device_stranded": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, pp]),
     "lime_set_create_global": (C.c_int, [vp, vp, i64, vp, vp, vp, pp]),
+    "lime_set_create_global_stranded": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, pp]),
     "lime_set_destroy": (C.c_int, [vp]),
     "lime_set_size": (i64, [vp]),
     "lime_set_lower_bound": (i64, [vp, u32]),
@@ -93,9 +94,13 @@ SIGNATURES = {
     "lime_merge": (C.c_int, [vp, vp, pp, P(i64)]),
     "lime_subtract": (C.c_int, [vp, vp, vp, i64, C.c_int, pp, P(i64)]),
     "lime_complement": (C.c_int, [vp, vp, vp, pp, P(i64)]),
+    "lime_complement_runs": (C.c_int, [vp, vp, i64, vp, vp, i64, i64, pp, P(i64)]),
     "lime_result_size": (i64, [vp]),
     "lime_result_fill_host": (C.c_int, [vp, P(i32), P(i64), P(i64), P(i64), P(i64)]),
     "lime_result_run_of_row": (C.c_int, [vp, P(i64)]),
+    "lime_result_copy_run_ids_device": (C.c_int, [vp, vp, vp]),
+    "lime_result_copy_rows_device": (C.c_int, [vp, i64, i64, vp, vp]),
+    "lime_result_run_strands": (C.c_int, [vp, i64, i64, P(C.c_int8)]),
     "lime_result_device_arrays": (C.c_int, [vp, pp, pp]),
     "lime_result_destroy": (C.c_int, [vp]),
     "lime_result_checksum": (C.c_int, [vp, P(u64), P(u64), P(u64), P(u64)]),
@@ -107,7 +112,7 @@ SIGNATURES = {
                                               pp]),
     "lime_bitset_window": (C.c_int, [vp, P(i64), P(i64)]),
     "lime_route_rows": (C.c_int, [vp, vp, i64, vp, vp, vp, u32, i32, P(u32), C.c_int, i64, vp,
-                                  vp, vp, P(i64)]),
+                                  vp, vp, P(i64), vp, vp]),
     "lime_bitset_runs": (C.c_int, [vp, C.c_int, vp, vp, pp, P(i64)]),
     "lime_bitset_and_runs": (C.c_int, [vp, C.c_int, P(vp), pp, P(i64)]),
     "lime_bitset_popcount": (i64, [vp, vp]),

@@ -125,7 +125,8 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
 int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold, int mode,
                  lime_result *res);
 int complement_run(lime_ctx *ctx, const lime_result *runs, const uint32_t *d_off,
-                   const uint32_t *d_len, int32_t nc, lime_result *res);
+                   const uint32_t *d_len, int32_t nc, lime_result *res, uint32_t wlo = 0,
+                   uint32_t whi = 0xffffffffu);
 int bitset_build(lime_ctx *ctx, const lime_set *a, lime_bitset *bs);
 int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                       const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
@@ -137,7 +138,8 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
 int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
                const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
-               uint32_t *d_row, int64_t *counts);
+               uint32_t *d_row, int64_t *counts, const int8_t *d_strand_in,
+               int8_t *d_strand_out);
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
 int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t first, int64_t n, uint64_t seed,
@@ -181,11 +183,8 @@ __global__ __launch_bounds__(256) void k_result_checksum(
     }
     rs = dev::wave_reduce_sum(rs);
     gsum = dev::wave_reduce_sum(gsum);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        rx ^= __shfl_xor(rx, d, 64);
-        gx ^= __shfl_xor(gx, d, 64);
-    }
+    rx = dev::wave_reduce_xor(rx);
+    gx = dev::wave_reduce_xor(gx);
     if (dev::lane_id() == 0) {
         atomicAdd(&out[0], (unsigned long long)rs);
         atomicXor(&out[1], (unsigned long long)rx);
@@ -208,8 +207,7 @@ __global__ __launch_bounds__(256) void k_pairs_hash(const uint4 *__restrict__ re
         hx ^= h;
     }
     hs = dev::wave_reduce_sum(hs);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) hx ^= __shfl_xor(hx, d, 64);
+    hx = dev::wave_reduce_xor(hx);
     if (dev::lane_id() == 0) {
         atomicAdd(&out[0], (unsigned long long)hs);
         atomicXor(&out[1], (unsigned long long)hx);
@@ -593,6 +591,75 @@ int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const
     return LIME_OK;
 }
 
+__global__ void k_positions(uint32_t *__restrict__ p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = (uint32_t)i;
+}
+// sorted positions -> the caller's row ids and strand codes of those rows
+__global__ void k_rows_of_positions(const uint32_t *__restrict__ pos,
+                                    const uint32_t *__restrict__ crow,
+                                    const int8_t *__restrict__ cstr, uint32_t *__restrict__ orow,
+                                    int8_t *__restrict__ ostr, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = pos[i];
+    orow[i] = crow[p];
+    ostr[i] = cstr ? cstr[p] : (int8_t)0;
+}
+
+int lime_set_create_global_stranded(lime_ctx *ctx, const lime_space *sp, int64_t n,
+                                    const uint32_t *d_gs, const uint32_t *d_ge,
+                                    const uint32_t *d_row, const int8_t *d_strand,
+                                    lime_set **out) {
+    if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_gs || !d_ge || !d_row)))
+        return fail(LIME_ERR_ARG, "bad set arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    // sorted with positions as the row ids (so the strand pass and the
+    // merge's strand lookups index the caller's codes), then the caller's row
+    // ids and the codes gathered per sorted row
+    uint32_t *pos;
+    int8_t *st;
+    LIME_TRY(alloc(ctx, &pos, (size_t)std::max<int64_t>(n, 1)));
+    PoolGuard<uint32_t> g0{ctx, pos};
+    LIME_TRY(alloc(ctx, &st, (size_t)std::max<int64_t>(n, 1)));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_positions, dim3(blocks_for(n, 256)), dim3(256), 0, S(ctx), pos, n);
+        if (d_strand)
+            LIME_HIP(hipMemcpyAsync(st, d_strand, (size_t)n, hipMemcpyDeviceToDevice, S(ctx)));
+        else
+            LIME_HIP(hipMemsetAsync(st, 0, (size_t)n, S(ctx)));
+    }
+    lime_set *s = new_set(ctx, sp, n);
+    s->strand_in = st;
+    s->strand_uniform = !d_strand;
+    uint32_t *d_len = nullptr;
+    int rc = upload_space(ctx, sp, &s->d_off, &d_len, &s->space_keep);
+    if (rc == LIME_OK) rc = sort_set_global(ctx, s, d_gs, d_ge, pos, d_len);
+    uint32_t *row = nullptr;
+    int8_t *sst = nullptr;
+    if (rc == LIME_OK) rc = alloc(ctx, &row, (size_t)std::max<int64_t>(n, 1));
+    if (rc == LIME_OK) rc = alloc(ctx, &sst, (size_t)std::max<int64_t>(n, 1));
+    if (rc == LIME_OK && n > 0) {
+        hipLaunchKernelGGL(k_rows_of_positions, dim3(blocks_for(n, 256)), dim3(256), 0, S(ctx),
+                           (const uint32_t *)s->row, d_row, (const int8_t *)st, row, sst, n);
+        if (hipGetLastError() != hipSuccess) rc = fail(LIME_ERR_DEVICE, "row gather failed");
+    }
+    if (rc != LIME_OK) {
+        release(ctx, row);
+        release(ctx, sst);
+        lime_set_destroy(s);
+        return rc;
+    }
+    release(ctx, s->row);
+    release(ctx, s->strand_in);
+    s->row = row;
+    s->strand_in = sst;
+    s->strand_sorted = true;
+    *out = s;
+    return LIME_OK;
+}
+
 int64_t lime_set_lower_bound(const lime_set *s, uint32_t gkey) {
     if (!s) return -(int64_t)fail(LIME_ERR_ARG, "set is null");
     lime_ctx *ctx = s->ctx;
@@ -938,6 +1005,79 @@ int lime_complement(lime_ctx *ctx, const lime_space *genome, const lime_set *a, 
     return LIME_OK;
 }
 
+int lime_complement_runs(lime_ctx *ctx, const lime_space *genome, int64_t n, const uint32_t *d_gs,
+                         const uint32_t *d_ge, int64_t lo, int64_t hi, lime_result **out,
+                         int64_t *n_regions) {
+    if (!ctx || !genome || !out || n < 0 || (n > 0 && (!d_gs || !d_ge)) || lo < 0 || hi < lo)
+        return fail(LIME_ERR_ARG, "bad complement arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 runs");
+    hipSetDevice(ctx->device);
+    uint32_t *d_len = nullptr, *d_off = nullptr;
+    LIME_TRY(upload_space(ctx, genome, &d_off, &d_len));
+    lime_result runs;  // (borrowed arrays)
+    runs.ctx = ctx;
+    runs.n = n;
+    runs.gs = const_cast<uint32_t *>(d_gs);
+    runs.ge = const_cast<uint32_t *>(d_ge);
+    lime_result *r = new lime_result();
+    r->ctx = ctx;
+    r->off = genome->off;
+    r->n_contigs = genome->n;
+    const uint32_t whi = hi >= 0xffffffffLL ? 0xffffffffu : (uint32_t)hi;
+    int rc = complement_run(ctx, &runs, d_off, d_len, genome->n, r, (uint32_t)std::min<int64_t>(lo, whi), whi);
+    runs.gs = runs.ge = nullptr;
+    if (rc != LIME_OK) {
+        lime_result_destroy(r);
+        return rc;
+    }
+    *out = r;
+    if (n_regions) *n_regions = r->n;
+    return LIME_OK;
+}
+
+// merge results: the run of every sorted input row and that row's id,
+// copied to caller device buffers (n = the merged set's rows)
+int lime_result_copy_run_ids_device(const lime_result *r, uint32_t *d_run, uint32_t *d_row) {
+    if (!r) return fail(LIME_ERR_ARG, "result is null");
+    if (!r->run_of_sorted || !r->src) return fail(LIME_ERR_ARG, "not a merge result");
+    lime_ctx *ctx = r->ctx;
+    hipSetDevice(ctx->device);
+    const size_t b = 4 * (size_t)r->src->n;
+    if (b && d_run)
+        LIME_HIP(hipMemcpyAsync(d_run, r->run_of_sorted, b, hipMemcpyDeviceToDevice, S(ctx)));
+    if (b && d_row) LIME_HIP(hipMemcpyAsync(d_row, r->src->row, b, hipMemcpyDeviceToDevice, S(ctx)));
+    return LIME_OK;
+}
+
+int lime_result_copy_rows_device(const lime_result *r, int64_t first, int64_t count,
+                                 uint32_t *d_gs, uint32_t *d_ge) {
+    if (!r || first < 0 || count < 0 || first + count > r->n)
+        return fail(LIME_ERR_ARG, "bad copy range");
+    lime_ctx *ctx = r->ctx;
+    hipSetDevice(ctx->device);
+    if (count && d_gs)
+        LIME_HIP(hipMemcpyAsync(d_gs, r->gs + first, 4 * (size_t)count, hipMemcpyDeviceToDevice,
+                                S(ctx)));
+    if (count && d_ge)
+        LIME_HIP(hipMemcpyAsync(d_ge, r->ge + first, 4 * (size_t)count, hipMemcpyDeviceToDevice,
+                                S(ctx)));
+    return LIME_OK;
+}
+
+// strand codes of runs [first, first + count) of a stranded merge (host)
+int lime_result_run_strands(const lime_result *r, int64_t first, int64_t count, int8_t *out) {
+    if (!r || !out || first < 0 || count < 0 || first + count > r->n)
+        return fail(LIME_ERR_ARG, "bad strand range");
+    if (!r->run_strand) {
+        memset(out, 0, (size_t)count);
+        return LIME_OK;
+    }
+    lime_ctx *ctx = r->ctx;
+    hipSetDevice(ctx->device);
+    if (count) LIME_TRY(read_back(ctx, out, r->run_strand + first, (size_t)count));
+    return LIME_OK;
+}
+
 int64_t lime_result_size(const lime_result *r) { return r ? r->n : -1; }
 
 int lime_result_fill_host(const lime_result *r, int32_t *contig, int64_t *start, int64_t *end,
@@ -1050,6 +1190,7 @@ int lime_result_destroy(lime_result *r) {
     release(ctx, r->a_row);
     release(ctx, r->b_row);
     release(ctx, r->run_of_sorted);
+    release(ctx, r->run_strand);
     delete r;
     return LIME_OK;
 }
@@ -1184,13 +1325,14 @@ int lime_bitset_window(const lime_bitset *bs, int64_t *lo, int64_t *n_words) {
 int lime_route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                     const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base,
                     int32_t n_shards, const uint32_t *splits, int clip, int64_t cap,
-                    uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts) {
+                    uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts,
+                    const int8_t *d_strand_in, int8_t *d_strand_out) {
     if (!ctx || !sp || !splits || !counts || n < 0 || (n > 0 && (!d_start || !d_end)))
         return fail(LIME_ERR_ARG, "bad route arguments");
     if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one call");
     hipSetDevice(ctx->device);
     return route_rows(ctx, sp, n, d_contig, d_start, d_end, row_base, n_shards, splits, clip, cap,
-                      d_gs, d_ge, d_row, counts);
+                      d_gs, d_ge, d_row, counts, d_strand_in, d_strand_out);
 }
 
 static lime_result *bitset_result(lime_ctx *ctx, const lime_bitset *b) {

@@ -667,8 +667,7 @@ __global__ __launch_bounds__(CB) void k_scan(Lefts L, Rights R, EndIndex E,
     if (MODE == SCAN_COUNT && i < L.n) cnt[i] = valid ? mine : 0;
     if (MODE == SCAN_SUM) {
         hs = dev::wave_reduce_sum(hs);
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) hx ^= __shfl_xor(hx, d, 64);
+        hx = dev::wave_reduce_xor(hx);
         if (lane == 0) {
             atomicAdd(&ck[0], (unsigned long long)hs);
             atomicXor(&ck[1], (unsigned long long)hx);

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <limits>
+
 #include <map>
 #include <memory>
 #include <mutex>
@@ -118,6 +120,9 @@ struct lime_set {
     // strand changes (the reference fold's overlaps test)
     int8_t *strand_in = nullptr;
     bool strand_uniform = false;  // every row has the same strand code
+    // strand_in indexed by SORTED position instead of row id (global
+    // stranded sets, whose row ids are the caller's)
+    bool strand_sorted = false;
     // binned sets (bitset painting from unsorted rows): only the gs digits
     // at shifts >= min_shift are sorted, i.e. rows grouped by gs >> min_shift
     int min_shift = 0;
@@ -131,6 +136,7 @@ struct lime_result {
     uint32_t *a_row = nullptr;  // may be null
     uint32_t *b_row = nullptr;  // may be null (0xffffffff = None)
     uint32_t *run_of_sorted = nullptr;  // merge only (per sorted input)
+    int8_t *run_strand = nullptr;       // merge of a stranded set: strand per run
     const lime_set *src = nullptr;      // merge only
     uint32_t *d_off = nullptr;          // contig offsets used to localise
     int32_t n_contigs = 0;
@@ -223,53 +229,84 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Wave scans and reductions on DPP (data-parallel primitives: a VALU
+// operand read from another lane of the row / wave, no LDS crossbar): row_shr
+// 1, 2, 4, 8 scan each 16-lane row, row_bcast:15 / :31 carry the row totals
+// into the rows above (rows 1, 3 then rows 2, 3).  Lanes whose source is
+// outside the row or whose row is masked off get `ident`.  A reduction is the
+// scan's lane 63, read into a scalar register (v_readlane).  (The
+// ds_bpermute-based __shfl_up / __shfl_xor version cost an LDS round trip per
+// step.)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t ident, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf, typename T>
+__device__ __forceinline__ T dpp_move(T ident, T v) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t a = (uint64_t)ident, b = (uint64_t)v;
+        const uint32_t lo = dpp32<CTRL, ROWS>((uint32_t)a, (uint32_t)b);
+        const uint32_t hi = dpp32<CTRL, ROWS>((uint32_t)(a >> 32), (uint32_t)(b >> 32));
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)dpp32<CTRL, ROWS>((uint32_t)ident, (uint32_t)v);
+    }
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_scan_dpp(T x, T ident, Op op) {
+    x = op(x, dpp_move<0x111>(ident, x));        // row_shr:1
+    x = op(x, dpp_move<0x112>(ident, x));        // row_shr:2
+    x = op(x, dpp_move<0x114>(ident, x));        // row_shr:4
+    x = op(x, dpp_move<0x118>(ident, x));        // row_shr:8
+    x = op(x, dpp_move<0x142, 0xa>(ident, x));   // row_bcast:15 -> rows 1, 3
+    x = op(x, dpp_move<0x143, 0xc>(ident, x));   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+// the value of lane 63, wave-uniform
+template <typename T>
+__device__ __forceinline__ T lane63(T v) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t b = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__builtin_amdgcn_readlane((int)v, 63);
+    }
+}
+// lane l gets lane l - 1's value (lane 0: ident): DPP wave_shr:1
+template <typename T>
+__device__ __forceinline__ T wave_shr1(T v, T ident) {
+    return dpp_move<0x138>(ident, v);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_sum(T v) {
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-        T o = __shfl_up(v, d, WAVE);
-        if (__lane_id() >= d) v += o;
-    }
-    return v;
+    return wave_scan_dpp(v, (T)0, [](T a, T b) { return a + b; });
 }
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_max(T v) {
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-        T o = __shfl_up(v, d, WAVE);
-        if (__lane_id() >= d) v = v > o ? v : o;
-    }
-    return v;
+    return wave_scan_dpp(v, std::numeric_limits<T>::lowest(), [](T a, T b) { return a > b ? a : b; });
 }
 template <typename T>
 __device__ __forceinline__ T wave_reduce_sum(T v) {
-#pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) v += __shfl_xor(v, d, WAVE);
-    return v;
+    return lane63(wave_inclusive_sum(v));
 }
 template <typename T>
 __device__ __forceinline__ T wave_reduce_max(T v) {
-#pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) {
-        T o = __shfl_xor(v, d, WAVE);
-        v = v > o ? v : o;
-    }
-    return v;
+    return lane63(wave_inclusive_max(v));
 }
 template <typename T>
 __device__ __forceinline__ T wave_reduce_or(T v) {
-#pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) v |= __shfl_xor(v, d, WAVE);
-    return v;
+    return lane63(wave_scan_dpp(v, (T)0, [](T a, T b) { return a | b; }));
+}
+template <typename T>
+__device__ __forceinline__ T wave_reduce_xor(T v) {
+    return lane63(wave_scan_dpp(v, (T)0, [](T a, T b) { return a ^ b; }));
 }
 template <typename T>
 __device__ __forceinline__ T wave_reduce_min(T v) {
-#pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) {
-        T o = __shfl_xor(v, d, WAVE);
-        v = v < o ? v : o;
-    }
-    return v;
+    return lane63(wave_scan_dpp(v, std::numeric_limits<T>::max(), [](T a, T b) { return a < b ? a : b; }));
 }
 
 // Block-wide exclusive sum. `scratch` holds >= BLOCK/64 + 1 T's.  Returns the
@@ -304,8 +341,7 @@ __device__ __forceinline__ T block_exclusive_max(T v, T ident, T *scratch, T *to
     constexpr int NW = BLOCK / WAVE;
     const int w = threadIdx.x / WAVE;
     T inc = wave_inclusive_max(v);
-    T exc = __shfl_up(inc, 1, WAVE);
-    if (__lane_id() == 0) exc = ident;
+    T exc = wave_shr1(inc, ident);
     if (__lane_id() == WAVE - 1) scratch[w] = inc;
     __syncthreads();
     if (threadIdx.x == 0) {

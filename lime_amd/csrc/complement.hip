@@ -30,7 +30,14 @@ struct GapArgs {
     const uint32_t *off;  // nc + 1
     const uint32_t *len;  // nc
     int32_t nc;
+    // only gaps whose start lies in [wlo, whi) (a coordinate shard's window;
+    // [0, 2^32) unsharded)
+    uint32_t wlo, whi;
 };
+
+__device__ __forceinline__ bool in_win(const GapArgs &a, uint32_t lo, uint32_t hi) {
+    return hi > lo && lo >= a.wlo && lo < a.whi;
+}
 
 // gap before run r (lo, hi) and tail after r if last in its contig
 __device__ __forceinline__ void run_gaps(const GapArgs &a, int64_t r, uint32_t &b_lo, uint32_t &b_hi,
@@ -54,7 +61,7 @@ __global__ __launch_bounds__(CB) void k_gap_count(GapArgs a, uint32_t *__restric
     if (r >= a.nr) return;
     uint32_t bl, bh, tl, th;
     run_gaps(a, r, bl, bh, tl, th);
-    cnt[r] = (bh > bl) + (th > tl);
+    cnt[r] = in_win(a, bl, bh) + in_win(a, tl, th);
 }
 
 // single block: per contig gap counts -> exclusive offsets coff[c], first run crb[c]
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(CB) void k_contig_off(GapArgs a, const uint32_t *__
             const int64_t rb = dev::lower_bound(a.rgs, 0, a.nr, a.off[c]);
             const int64_t re = dev::lower_bound(a.rgs, rb, a.nr, a.off[c + 1]);
             crb[c] = (uint32_t)rb;
-            n = rb == re ? (a.len[c] > 0 ? 1u : 0u) : pre[re] - pre[rb];
+            n = rb == re ? (in_win(a, a.off[c], a.off[c] + a.len[c]) ? 1u : 0u) : pre[re] - pre[rb];
         }
         uint32_t tot;
         uint32_t ex = dev::block_exclusive_sum<CB>(n, scratch, &tot);
@@ -92,12 +99,12 @@ __global__ __launch_bounds__(CB) void k_gap_write(GapArgs a, const uint32_t *__r
         run_gaps(a, r, bl, bh, tl, th);
         const int32_t c = seg_of(a.off, a.nc, a.rgs[r]);
         uint32_t at = coff[c] + pre[r] - pre[crb[c]];
-        if (bh > bl) {
+        if (in_win(a, bl, bh)) {
             ogs[at] = bl;
             oge[at] = bh;
             ++at;
         }
-        if (th > tl) {
+        if (in_win(a, tl, th)) {
             ogs[at] = tl;
             oge[at] = th;
         }
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(CB) void k_gap_write(GapArgs a, const uint32_t *__r
     if (c < a.nc) {
         const int64_t rb = crb[c];
         const bool empty = rb >= a.nr || a.rgs[rb] >= a.off[c + 1];
-        if (empty && a.len[c] > 0) {
+        if (empty && in_win(a, a.off[c], a.off[c] + a.len[c])) {
             ogs[coff[c]] = a.off[c];
             oge[coff[c]] = a.off[c] + a.len[c];
         }
@@ -116,10 +123,15 @@ __global__ __launch_bounds__(CB) void k_gap_write(GapArgs a, const uint32_t *__r
 
 }  // namespace
 
+// gaps of the sorted, disjoint runs (rgs, rge) over the genome, those
+// starting in [wlo, whi) only
 int complement_run(lime_ctx *ctx, const lime_result *runs, const uint32_t *d_off,
-                   const uint32_t *d_len, int32_t nc, lime_result *res) {
+                   const uint32_t *d_len, int32_t nc, lime_result *res, uint32_t wlo,
+                   uint32_t whi) {
     const int64_t nr = runs->n;
     GapArgs a;
+    a.wlo = wlo;
+    a.whi = whi;
     a.rgs = runs->gs;
     a.rge = runs->ge;
     a.nr = nr;

@@ -567,8 +567,7 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
     if (CKSUM) {
         hsum = dev::wave_reduce_sum(hsum);
         uint64_t x = hxor;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
+        x = dev::wave_reduce_xor(x);
         if (lane == 0) {
             s_red[0][w] = hsum;
             s_red[1][w] = x;
@@ -648,8 +647,7 @@ __global__ __launch_bounds__(IB) void k_fill_filtered(FillArgs fa, int64_t thres
     if (CKSUM) {
         hsum = dev::wave_reduce_sum(hsum);
         uint64_t x = hxor;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
+        x = dev::wave_reduce_xor(x);
         if (dev::lane_id() == 0) {
             s_red[0][threadIdx.x / 64] = hsum;
             s_red[1][threadIdx.x / 64] = x;

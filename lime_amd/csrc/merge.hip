@@ -133,7 +133,8 @@ struct MergeScanArgs {
     uint32_t *pmax;             // may be null: inclusive prefix max of ge (plain sets)
     uint64_t *total;            // runs
     const int8_t *strand;       // stranded sets: strand per input row
-    const uint32_t *row;        // sorted row ids (strand lookups)
+    const uint32_t *row;        // sorted row ids (strand lookups; null: by position)
+    int8_t *run_strand;         // stranded sets: the strand of every run (may be null)
 };
 
 // Full tile <-> blocked registers (thread t: rows 16t .. 16t+15) through
@@ -199,14 +200,13 @@ template <int BLOCK>
 __device__ SegMax block_exclusive_segmax(SegMax x, SegMax *scratch, SegMax *total) {
     constexpr int NW = BLOCK / 64;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
-    SegMax inc = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        SegMax o{(uint32_t)__shfl_up((int)inc.b, d, 64), (uint32_t)__shfl_up((int)inc.v, d, 64)};
-        if (lane >= d) inc = seg_combine(o, inc);
-    }
-    SegMax exc{(uint32_t)__shfl_up((int)inc.b, 1, 64), (uint32_t)__shfl_up((int)inc.v, 1, 64)};
-    if (lane == 0) exc = SegMax{0u, 0u};
+    // the pair packed as b << 32 | v: the DPP scan with seg_combine
+    auto pk = [](SegMax m) { return ((uint64_t)m.b << 32) | m.v; };
+    auto up = [](uint64_t u) { return SegMax{(uint32_t)(u >> 32), (uint32_t)u}; };
+    const uint64_t incp = dev::wave_scan_dpp(
+        pk(x), (uint64_t)0, [&](uint64_t a, uint64_t b) { return pk(seg_combine(up(b), up(a))); });
+    const SegMax inc = up(incp);
+    const SegMax exc = up(dev::wave_shr1(incp, (uint64_t)0));
     if (lane == 63) scratch[w] = inc;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -258,11 +258,11 @@ void k_merge_scan(MergeScanArgs a) {
     }
     uint32_t brk = 0;  // bit k: row r0 + k starts a strand segment
     if (STR) {
-        int prev = r0 > 0 && r0 - 1 < n ? a.strand[a.row[r0 - 1]] : -1;
+        int prev = r0 > 0 && r0 - 1 < n ? a.strand[a.row ? a.row[r0 - 1] : r0 - 1] : -1;
 #pragma unroll
         for (int k = 0; k < MITEMS; ++k) {
             if (r0 + k < n) {
-                const int c = a.strand[a.row[r0 + k]];
+                const int c = a.strand[a.row ? a.row[r0 + k] : r0 + k];
                 if (c != prev) brk |= 1u << k;
                 prev = c;
             }
@@ -334,6 +334,7 @@ void k_merge_scan(MergeScanArgs a) {
         if (i < n) {
             if (flags & (1u << k)) {
                 a.run_gs[r] = s[k];
+                if (STR && a.run_strand) a.run_strand[r] = a.strand[a.row ? a.row[i] : i];
                 if (r > 0) a.run_ge[r - 1] = M;
                 ++r;
             }
@@ -461,6 +462,8 @@ static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
     LIME_TRY(alloc(ctx, &run_gs, (size_t)n));
     LIME_TRY(alloc(ctx, &run_ge, (size_t)n));
     if (want_run_ids) LIME_TRY(alloc(ctx, &res->run_of_sorted, (size_t)n));
+    int8_t *run_st = nullptr;  // stranded sets: the strand of every run
+    if (set->strand_in) LIME_TRY(alloc(ctx, &run_st, (size_t)n));
     MergeScanArgs a;
     a.gs = set->gs;
     a.ge = set->ge;
@@ -474,7 +477,8 @@ static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
     a.run_of_sorted = res->run_of_sorted;
     a.pmax = pmax;
     a.strand = set->strand_in;
-    a.row = set->row;
+    a.row = set->strand_sorted ? nullptr : set->row;
+    a.run_strand = run_st;
     if (set->strand_in)
         hipLaunchKernelGGL(k_merge_scan<true>, dim3((unsigned)nt), dim3(SB), 0, S(ctx), a);
     else
@@ -487,6 +491,7 @@ static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
         // most rows start a run: keep the capacity-n arrays
         res->gs = run_gs;
         res->ge = run_ge;
+        res->run_strand = run_st;
     } else {
         LIME_TRY(alloc(ctx, &res->gs, (size_t)nr));
         LIME_TRY(alloc(ctx, &res->ge, (size_t)nr));
@@ -496,6 +501,12 @@ static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
                                 S(ctx)));
         release(ctx, run_gs);
         release(ctx, run_ge);
+        if (run_st) {
+            LIME_TRY(alloc(ctx, &res->run_strand, (size_t)std::max<uint64_t>(nr, 1)));
+            LIME_HIP(hipMemcpyAsync(res->run_strand, run_st, (size_t)nr, hipMemcpyDeviceToDevice,
+                                    S(ctx)));
+            release(ctx, run_st);
+        }
     }
     res->n = (int64_t)nr;
     return LIME_OK;

@@ -41,6 +41,8 @@ struct RouteArgs {
     uint32_t *mat;  // nsh * nblk + 1
     uint32_t nblk;
     uint32_t *gs, *ge, *row;
+    const int8_t *strand_in;  // may be null
+    int8_t *strand_out;
     unsigned int *err;  // bit0 contig, bit1 end < start, bit2 end > length / span
 };
 
@@ -142,8 +144,9 @@ __global__ __launch_bounds__(RT) void k_route_write(RouteArgs a) {
             const uint32_t lo = sp[d], hi = sp[d + 1];
             a.gs[pos] = a.clip ? max(g0[k], lo) : g0[k];
             a.ge[pos] = a.clip && g1[k] > g0[k] ? min(g1[k], hi) : g1[k];
-            if (a.row)
-                a.row[pos] = a.row_base + (uint32_t)((int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k);
+            const int64_t i = (int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k;
+            if (a.row) a.row[pos] = a.row_base + (uint32_t)i;
+            if (a.strand_out) a.strand_out[pos] = a.strand_in ? a.strand_in[i] : (int8_t)0;
             ++pos;
         }
     }
@@ -160,7 +163,8 @@ __global__ void k_route_totals(const uint32_t *__restrict__ mat, uint32_t nblk, 
 int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
                const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
-               uint32_t *d_row, int64_t *counts) {
+               uint32_t *d_row, int64_t *counts, const int8_t *d_strand_in,
+               int8_t *d_strand_out) {
     if (nsh < 1 || nsh > MAXSH) return fail(LIME_ERR_ARG, "1 to 64 shards");
     if (splits[0] != 0 || (int64_t)splits[nsh] != sp->span)
         return fail(LIME_ERR_ARG, "splits must start at 0 and end at the span");
@@ -202,6 +206,8 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
     a.gs = d_gs;
     a.ge = d_ge;
     a.row = d_row;
+    a.strand_in = d_strand_in;
+    a.strand_out = d_strand_out;
     a.err = err;
     if (n > 0) hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(RT), 0, S(ctx), a);
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));

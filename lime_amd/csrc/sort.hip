@@ -120,9 +120,10 @@ __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *co
 // GLOBAL: the input is already (gs, ge, row) in global coordinates (rows of
 // sets of this space, e.g. a shard's own rows + its halo); `contig` / `start`
 // / `end` then carry gs / ge / row and only order and span are validated.
-// WRITE = false (plain caller rows): only validate, gather statistics and
-// histogram -- the first radix pass then reads the caller's rows itself
-// (k_scatter RAW), so gs / ge are never written and read back in between.
+// WRITE = false: only validate, gather statistics and histogram -- the first
+// radix pass then reads the caller's rows itself (k_scatter RAW for plain
+// rows, the caller's (gs, ge, row) for global ones), so nothing is written
+// and read back in between (the bucketed sort).
 // LC: the contig table (<= PCMAX contigs) is staged in LDS, so the per-row
 // off / len gathers are LDS reads rather than dependent cache round trips
 constexpr int PCMAX = 1024;
@@ -168,9 +169,11 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                 g1 = start[i];
                 if (g1 < g0) err |= 2u;
                 if (g1 >= span) err |= 4u;
-                gs[i] = g0;
-                ge[i] = g1;
-                if (row) row[i] = end[i];
+                if (WRITE) {
+                    gs[i] = g0;
+                    ge[i] = g1;
+                    if (row) row[i] = end[i];
+                }
                 mx = g0 > mx ? g0 : mx;
                 const uint32_t wd = g1 - g0;
                 mnw = wd < mnw ? wd : mnw;
@@ -224,7 +227,8 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
             }
             // canonical-order check: the row before this lane's first row is
             // the previous lane's last one (lane 0 reads it from memory)
-            uint32_t p0 = __shfl_up(a0[3], 1), p1 = __shfl_up(a1[3], 1), pok = __shfl_up(ok[3], 1);
+            uint32_t p0 = dev::wave_shr1(a0[3], 0u), p1 = dev::wave_shr1(a1[3], 0u),
+                     pok = dev::wave_shr1(ok[3], 0u);
             const int64_t i0 = base + 4 * (int64_t)q;
             if (lane == 0) {
                 pok = 0;
@@ -434,10 +438,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     // RAW: the contig table staged in LDS (<= PCMAX contigs), so the per-row
     // off[contig] gather is an LDS read, not a dependent cache round trip
     __shared__ uint32_t s_off[RAW ? PCMAX : 1];
-    if (RAW && nc <= PCMAX) {
+    if (RAW && nc <= PCMAX)  // (its barrier follows the tile's loads)
         for (int i = threadIdx.x; i < nc; i += RB) s_off[i] = off[i];
-        __syncthreads();
-    }
     const uint32_t *offp = RAW && nc <= PCMAX ? s_off : off;
     __shared__ uint32_t dstart[RBINS];
     __shared__ uint32_t gbase[RBINS];
@@ -468,20 +470,33 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     for (int k = 0; k < RITEMS; ++k) {
         const int o = k * 64 + lane;
         const bool valid = o < lim;
-        if (RAW) {  // validated by k_prep: every contig id is in range
-            const uint32_t c = valid ? kin[o] : 0u;
-            const uint32_t base = valid ? offp[c] : 0u;
-            vk[k] = valid ? base + ein[o] : 0u;
-            ve[k] = valid ? base + rin[o] : 0u;
+        if (RAW) {  // the contig ids (in vr), starts and ends: all loads first
+            vr[k] = valid ? kin[o] : 0u;
+            vk[k] = valid ? ein[o] : 0u;
+            ve[k] = valid ? rin[o] : 0u;
         } else {
             vk[k] = valid ? kin[o] : 0u;
             ve[k] = valid ? ein[o] : 0u;
         }
         // (GS passes write identity rows straight from the position below,
         // keeping vr out of the registers of that path)
-        vr[k] = ROWS == ROWS_IDENT && M != M_GS ? (uint32_t)(base + o)
-                : ROWS == ROWS_LOAD && !RAW     ? (valid ? rin[o] : 0u)
-                                                : 0u;
+        if (!RAW)
+            vr[k] = ROWS == ROWS_IDENT && M != M_GS ? (uint32_t)(base + o)
+                    : ROWS == ROWS_LOAD             ? (valid ? rin[o] : 0u)
+                                                    : 0u;
+    }
+    if (RAW) {
+        // (gs, ge) = off[contig] + (start, end), the table in LDS; the
+        // lookups follow every load of the tile (one dependent round trip
+        // per item serialised the loads: 1.14 ms per 1e8 rows)
+        if (nc <= PCMAX) __syncthreads();  // s_off staged
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) {
+            const uint32_t o = offp[vr[k]];  // (vr = 0 for invalid rows: in range)
+            vk[k] += o;
+            ve[k] += o;
+            vr[k] = 0u;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -632,138 +647,311 @@ int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, co
     return LIME_OK;
 }
 
-// ---------------------------------------------------------- hybrid sort
-// (opt-in, LIME_SORT_HYBRID=1: measured slower, see sort_set_impl)
-// Plain sets over a span past 2^16: two LSD passes on bits 16..31 group the
-// rows into 65536-base buckets (input order kept inside each, the passes
-// being stable), then ONE pass sorts every bucket in LDS by
-// (low 16 bits of gs, non-zero width) -- 96 B per row instead of the 132 B of
-// four digit passes (+1 zero-width pass).  The LDS element is
-// (key17 << 15 | position in the bucket): unique, so ties keep input order.
-// Buckets of more than LCAP rows (pile-ups) take the digit passes instead.
-// Two block shapes: buckets of <= 4096 rows (256 threads, ~40 KiB LDS, 4
-// blocks per CU: C2's ~2,000-row buckets) and of <= 16384 rows (512 threads,
-// ~147 KiB: C3's pile-ups); each launch skips the other class's buckets.  A
-// bucket's items are spread evenly over the waves (contiguous, in order: the
-// ranks are stable), only as many 64-row steps as it needs.
-constexpr int LCAP = 16384;          // largest bucket sorted in LDS
-constexpr int LCAP_S = 4096;         // the small shape's capacity
+
+// ------------------------------------------------------------ bucketed sort
+// Plain sets past 2^16 rows (the default for C2 / C3-sized inputs): two 8-bit
+// LSD digit passes on bits [L, L + 16) of gs group the rows into buckets of
+// 2^L bases (input order kept inside each: the passes are stable), then ONE
+// pass sorts every bucket in LDS by (gs mod 2^L, non-zero width) -- the
+// zero-width rule rides in the local key, so no NZ pass.  The first digit
+// pass reads the caller's rows itself (k_scatter RAW: k_prep only validates
+// and histograms), so per row: 12 B (prep) + 24 B (pass 1) + 4 B (hist) +
+// 24 B (pass 2) + 24 B (local) = 88 B, against 12 + 8 + 20 + 3 x 28 = 124 B
+// (+28 with zero-width rows) of five digit passes.
+//
+// The local key packs (gs mod 2^L) << 1 | (width > 0) above the row's
+// position in its bucket, so a stable pair of LDS digit passes over the key
+// bits gives (gs, zero-width first, input order) -- the canonical order.
+// Buckets of <= LCAP_S rows: one 512-thread workgroup each, their ge / row
+// staged in LDS; larger ones are listed and taken by a persistent 1024-thread
+// kernel (<= LCAP_B rows in LDS, gathering ge / row from L2; past that a
+// chunked workgroup-wide radix over the bucket's rows in global memory).
+constexpr int LNT_B = 1024, LPOS_B = 14, LCAP_B = 1 << LPOS_B;  // 16 items / thread
+constexpr int LDMAX = 9;  // local digit bits (key L + 1 <= 18 bits in two passes)
+
+struct LocalArgs {
+    const uint32_t *k0, *e0, *r0;  // rows grouped by gs >> L
+    const uint32_t *start;         // nb + 1 bucket starts
+    int L;
+    uint32_t *k1, *e1, *r1;        // the sorted set
+    unsigned int *nover;           // [0] listed buckets, [1] the big kernel's ticket
+    uint32_t *over;                // listed bucket ids
+};
 
 __global__ __launch_bounds__(256) void k_bucket_starts(const uint32_t *__restrict__ k, int64_t n,
-                                                       uint32_t nb, uint32_t *__restrict__ start) {
+                                                       uint32_t nb, int L,
+                                                       uint32_t *__restrict__ start) {
     const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (b > nb) return;
-    start[b] = b == nb ? (uint32_t)n : (uint32_t)dev::lower_bound(k, 0, n, (uint64_t)b << 16);
+    start[b] = b == nb ? (uint32_t)n : (uint32_t)dev::lower_bound(k, 0, n, (uint64_t)b << L);
 }
 
-// one stable LDS pass of D-bit digits of the elements at bit `shift`; wave w
-// holds items [w c, (w + 1) c), c = nit * 64
-template <int D, int NT, int ITEMS>
-__device__ __forceinline__ void local_pass(const uint32_t *src, uint32_t *dst,
-                                           uint32_t (*cnt)[512], uint32_t *scratch, int shift,
-                                           int nit) {
-    constexpr uint32_t ND = 1u << D;
+// One stable LDS digit pass of D (<= LDMAX) bits at `shift` over the packed
+// items v (wave w holds items [w c, (w + 1) c) in (it, lane) order, c =
+// nit * 64): ranks by wave ballots with per-wave digit counters, offsets by a
+// digit-major scan, items written to dst.
+template <int NT, int ITEMS, typename CT>
+__device__ __forceinline__ void lds_digit_pass(const uint32_t (&v)[ITEMS], int nit, int shift,
+                                               int D, CT (*cnt)[1 << LDMAX], uint32_t *scratch,
+                                               uint32_t *dst) {
     constexpr int NW = NT / 64;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
-    const int c = nit * 64;
-    for (int i = threadIdx.x; i < NW * (int)ND; i += NT) cnt[i / ND][i % ND] = 0;
-    uint32_t v[ITEMS], pd[ITEMS];
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it)
-        if (it < nit) v[it] = src[w * c + it * 64 + lane];
+    const uint32_t ND = 1u << D, dm = ND - 1;
+    for (int i = threadIdx.x; i < NW * (1 << LDMAX); i += NT) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    // stable ranks: items in (it, lane) order per wave, per-wave counters
+    uint32_t pd[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-        if (it >= nit) break;
-        const uint32_t d = (v[it] >> shift) & (ND - 1);
-        uint64_t m = ~0ull;
-#pragma unroll
-        for (int b = 0; b < D; ++b) {
-            const uint64_t bb = __ballot((d >> b) & 1u);
-            m &= ((d >> b) & 1u) ? bb : ~bb;
+        if (it < nit) {
+            const uint32_t d = (v[it] >> shift) & dm;
+            uint64_t m = ~0ull;
+    #pragma unroll
+            for (int b = 0; b < LDMAX; ++b) {
+                const uint32_t bit = (d >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
+            const uint32_t old = cnt[w][d];
+            pd[it] = old + rank;
+            if (rank == 0) cnt[w][d] = (CT)(old + (uint32_t)__popcll(m));
         }
-        const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
-        const uint32_t old = cnt[w][d];
-        pd[it] = old + rank;
-        if (rank == 0) cnt[w][d] = old + (uint32_t)__popcll(m);
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < (int)ND; d += NT) {
+    {  // digit d's start, then each wave's start within it
+        const int d = threadIdx.x;
         uint32_t tot = 0;
-        for (int ww = 0; ww < NW; ++ww) tot += cnt[ww][d];
-        cnt[NW][d] = tot;  // (row NW: digit totals)
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the ND totals by one wave
-        uint32_t carry = 0;
-        for (int d0 = 0; d0 < (int)ND; d0 += 64) {
-            const uint32_t t = cnt[NW][d0 + threadIdx.x];
-            const uint32_t inc = dev::wave_inclusive_sum(t);
-            cnt[NW][d0 + threadIdx.x] = carry + inc - t;
-            carry += __shfl(inc, 63, 64);
+        if (d < (int)ND)
+            for (int ww = 0; ww < NW; ++ww) tot += cnt[ww][d];
+        uint32_t all;
+        const uint32_t ds = dev::block_exclusive_sum<NT>(tot, scratch, &all);
+        if (d < (int)ND) {
+            uint32_t run = ds;
+            for (int ww = 0; ww < NW; ++ww) {
+                const uint32_t c = cnt[ww][d];
+                cnt[ww][d] = (CT)run;
+                run += c;
+            }
         }
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < (int)ND; d += NT) {
-        uint32_t run = cnt[NW][d];
-        for (int ww = 0; ww < NW; ++ww) {
-            const uint32_t cc = cnt[ww][d];
-            cnt[ww][d] = run;
-            run += cc;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it)
-        if (it < nit) dst[cnt[w][(v[it] >> shift) & (ND - 1)] + pd[it]] = v[it];
-    __syncthreads();
-    (void)scratch;
-}
-
-template <int NT, int CAP>
-__global__ __launch_bounds__(NT) void k_local_sort(const uint32_t *__restrict__ k0,
-                                                   const uint32_t *__restrict__ e0,
-                                                   const uint32_t *__restrict__ r0,
-                                                   const uint32_t *__restrict__ start,
-                                                   uint32_t lo_m, uint32_t *__restrict__ k1,
-                                                   uint32_t *__restrict__ e1,
-                                                   uint32_t *__restrict__ r1,
-                                                   unsigned int *__restrict__ nover,
-                                                   uint32_t *__restrict__ over) {
-    constexpr int NW = NT / 64;
-    constexpr int ITEMS = CAP / NT;
-    __shared__ uint32_t buf[2][CAP];
-    __shared__ uint32_t cnt[NW + 1][512];
-    const uint32_t b = blockIdx.x;
-    const uint32_t s0 = start[b], m = start[b + 1] - s0;
-    if (m <= lo_m) return;  // empty, or the small shape's
-    if (m > (uint32_t)CAP) {  // the large shape's, or a pile-up for the digit passes
-        if (CAP == LCAP && threadIdx.x == 0) over[atomicAdd(nover, 1u)] = b;
-        return;
-    }
-    const int w = threadIdx.x / 64, lane = dev::lane_id();
-    const int nit = (int)((m + NW * 64 - 1) / (NW * 64));  // 64-row steps per wave
-    const int c = nit * 64;
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-        if (it >= nit) break;
-        const uint32_t j = w * c + it * 64 + lane;
-        uint32_t x = 0xffffffffu;  // padding sorts last
-        if (j < m) {
-            const uint32_t g = k0[s0 + j], e = e0[s0 + j];
-            x = ((((g & 0xffffu) << 1) | (e > g ? 1u : 0u)) << 15) | j;
+        if (it < nit) {
+            dst[(uint32_t)cnt[w][(v[it] >> shift) & dm] + pd[it]] = v[it];
         }
-        buf[0][j] = x;
     }
     __syncthreads();
-    local_pass<9, NT, ITEMS>(buf[0], buf[1], cnt, nullptr, 15, nit);  // key17 bits 0..8
-    local_pass<8, NT, ITEMS>(buf[1], buf[0], cnt, nullptr, 24, nit);  // key17 bits 9..16
+}
+
+// bucket b = rows [s0, s0 + m), m <= NT * ITEMS, sorted in LDS from its
+// rows in registers (g, e, r: item it * 64 + lane of wave w at position
+// w c + it 64 + lane, c = nit 64; past m: padding).  STAGE: ge and row are
+// staged in LDS (else gathered from global memory, where the bucket's lines
+// are L2-resident after the load).
+template <int NT, int ITEMS, int POSB, bool STAGE, typename CT>
+__device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b, uint32_t s0,
+                                                 uint32_t m, const uint32_t (&g)[ITEMS],
+                                                 const uint32_t (&e)[ITEMS],
+                                                 const uint32_t (&r)[ITEMS], uint32_t *A,
+                                                 uint32_t *B, CT (*cnt)[1 << LDMAX],
+                                                 uint32_t *scratch, uint32_t *s_e, uint32_t *s_r) {
+    constexpr int NW = NT / 64;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int nit = (int)((m + NW * 64 - 1) / (NW * 64));
+    const int c = nit * 64;
+    const uint32_t lmask = (1u << a.L) - 1u;
+    uint32_t v[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
+        // padding sorts last (after every row: it follows them)
+        v[it] = pos < m ? ((((g[it] & lmask) << 1) | (e[it] > g[it] ? 1u : 0u)) << POSB) | pos
+                        : 0xffffffffu;
+        if (STAGE && it < nit && pos < m) {
+            s_e[pos] = e[it];
+            s_r[pos] = r[it];
+        }
+    }
+    const int kb = a.L + 1, d1 = kb - kb / 2, d2 = kb / 2;
+    lds_digit_pass<NT, ITEMS, CT>(v, nit, POSB, d1, cnt, scratch, B);
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        if (it < nit) {
+            v[it] = B[w * c + it * 64 + lane];
+        }
+    }
+    lds_digit_pass<NT, ITEMS, CT>(v, nit, POSB + d1, d2, cnt, scratch, A);
+    const uint32_t base = b << a.L, pm = (1u << POSB) - 1u;
     for (uint32_t q = threadIdx.x; q < m; q += NT) {
-        const uint32_t j = buf[0][q] & 0x7fffu;
-        k1[s0 + q] = k0[s0 + j];
-        e1[s0 + q] = e0[s0 + j];
-        r1[s0 + q] = r0[s0 + j];
+        const uint32_t x = A[q], j = x & pm;
+        a.k1[s0 + q] = base | ((x >> (POSB + 1)) & lmask);
+        a.e1[s0 + q] = STAGE ? s_e[j] : a.e0[s0 + j];
+        a.r1[s0 + q] = STAGE ? s_r[j] : a.r0[s0 + j];
+    }
+}
+
+// a bucket's rows into registers, branch-free (positions past the bucket
+// clamped to its last row; a bucket too large for the shape, or empty, loads
+// row 0): every load issued before any is used
+template <int NT, int ITEMS, int CAP>
+struct BucketRegs {
+    uint32_t g[ITEMS], e[ITEMS], r[ITEMS];
+    uint32_t s0, m;
+    __device__ __forceinline__ void load(const LocalArgs &a, uint32_t b, uint32_t nb) {
+        constexpr int NW = NT / 64;
+        const int w = threadIdx.x / 64, lane = dev::lane_id();
+        s0 = 0;
+        m = 0;
+        if (b < nb) {
+            s0 = a.start[b];
+            m = a.start[b + 1] - s0;
+        }
+        const bool ok = m >= 1 && m <= (uint32_t)CAP;
+        const uint32_t base = ok ? s0 : 0u;
+        const int c = ok ? (int)((m + NW * 64 - 1) / (NW * 64)) * 64 : 0;
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
+            const uint32_t q = base + (ok ? min(pos, m - 1) : 0u);
+            g[it] = a.k0[q];
+            e[it] = a.e0[q];
+            r[it] = a.r0[q];
+        }
+    }
+};
+
+// Persistent (two workgroups per CU): each workgroup takes buckets b,
+// b + grid, ... and loads the next one's rows into registers before sorting
+// the current one, so the load latency hides behind the LDS passes (one
+// bucket per workgroup, loads then sort, left the memory pipe idle half the
+// time: 1.0 vs 0.X ms per 1e8 rows).  Buckets past LCAP_S rows are listed for
+// k_local_big.
+constexpr int LNT_S = 512, LPOS_S = 12, LCAP_S = 1 << LPOS_S;  // 8 items / thread
+using SmallRegs = BucketRegs<LNT_S, LCAP_S / LNT_S, LCAP_S>;
+__global__ __launch_bounds__(LNT_S) void k_local_small(LocalArgs a, uint32_t nb) {
+    __shared__ uint32_t A[LCAP_S], B[LCAP_S], s_e[LCAP_S], s_r[LCAP_S];
+    __shared__ uint16_t cnt[LNT_S / 64][1 << LDMAX];
+    __shared__ uint32_t scratch[LNT_S / 64 + 1];
+    SmallRegs cur, nxt;
+    cur.load(a, blockIdx.x, nb);
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        nxt.load(a, b + gridDim.x, nb);
+        if (cur.m > (uint32_t)LCAP_S) {  // for the big kernel
+            if (threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;
+        } else if (cur.m > 0) {
+            bucket_sort_regs<LNT_S, LCAP_S / LNT_S, LPOS_S, true, uint16_t>(
+                a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, cnt, scratch, s_e, s_r);
+        }
+        __syncthreads();  // (the next bucket overwrites the staging)
+        cur = nxt;
+    }
+}
+
+// A bucket past LCAP_B rows: LSD over its key (gs mod 2^L, non-zero width) in
+// 6-bit digits by the whole workgroup, NT rows per step in order (wave ballot
+// ranks, per-wave digit counts, running digit offsets): stable.  Passes
+// alternate (k0, e0, r0) -> (k1, e1, r1) -> ...; an even number of passes
+// ends with a copy into (k1, e1, r1).
+template <int NT>
+__device__ void bucket_sort_global(const LocalArgs &a, uint32_t s0, uint32_t m, uint32_t *lds) {
+    constexpr int NW = NT / 64, GD = 6, GB = 1 << GD;
+    uint32_t *hist = lds, *run = lds + GB, *wc = lds + 2 * GB;  // wc[NW][GB]
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const uint32_t lmask = (1u << a.L) - 1u;
+    const int kb = a.L + 1, np = (kb + GD - 1) / GD;
+    const uint32_t *src[3] = {a.k0 + s0, a.e0 + s0, a.r0 + s0};
+    uint32_t *dst[3] = {a.k1 + s0, a.e1 + s0, a.r1 + s0};
+    for (int p = 0; p < np; ++p) {
+        const int shift = p * GD;
+        auto digit = [&](uint32_t g, uint32_t e) {
+            return ((((g & lmask) << 1) | (e > g ? 1u : 0u)) >> shift) & (GB - 1);
+        };
+        for (int i = threadIdx.x; i < GB; i += NT) hist[i] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += NT) atomicAdd(&hist[digit(src[0][i], src[1][i])], 1u);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t r = 0;
+            for (int d = 0; d < GB; ++d) {
+                run[d] = r;
+                r += hist[d];
+            }
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < m; c0 += NT) {
+            const uint32_t i = c0 + threadIdx.x;
+            const bool ok = i < m;
+            uint32_t g = 0, e = 0, r = 0;
+            if (ok) g = src[0][i], e = src[1][i], r = src[2][i];
+            const uint32_t d = ok ? digit(g, e) : 0u;
+            uint64_t mm = __ballot(ok);
+#pragma unroll
+            for (int bt = 0; bt < GD; ++bt) {
+                const uint32_t bit = (d >> bt) & 1u;
+                const uint64_t bb = __ballot(bit);
+                mm &= bit ? bb : ~bb;
+            }
+            const uint32_t rank = (uint32_t)__popcll(mm & dev::lanemask_lt());
+            for (int q = threadIdx.x; q < NW * GB; q += NT) wc[q] = 0;
+            __syncthreads();
+            if (ok && rank == 0) wc[w * GB + d] = (uint32_t)__popcll(mm);
+            __syncthreads();
+            if (threadIdx.x < GB) {  // per digit: the waves' starts, then the run
+                uint32_t t = run[threadIdx.x];
+                for (int ww = 0; ww < NW; ++ww) {
+                    const uint32_t x = wc[ww * GB + threadIdx.x];
+                    wc[ww * GB + threadIdx.x] = t;
+                    t += x;
+                }
+                run[threadIdx.x] = t;
+            }
+            __syncthreads();
+            if (ok) {
+                const uint32_t o = wc[w * GB + d] + rank;
+                dst[0][o] = g;
+                dst[1][o] = e;
+                dst[2][o] = r;
+            }
+            __syncthreads();
+        }
+        for (int q = 0; q < 3; ++q) {
+            const uint32_t *t = src[q];
+            src[q] = dst[q];
+            dst[q] = const_cast<uint32_t *>(t);
+        }
+    }
+    if (np % 2 == 0)  // the result is in (k0, e0, r0): copy it over
+        for (uint32_t i = threadIdx.x; i < m; i += NT) {
+            a.k1[s0 + i] = a.k0[s0 + i];
+            a.e1[s0 + i] = a.e0[s0 + i];
+            a.r1[s0 + i] = a.r0[s0 + i];
+        }
+}
+
+// the listed buckets (> LCAP_S rows), taken in ticket order by one resident
+// workgroup per CU until the list is done
+__global__ __launch_bounds__(LNT_B) void k_local_big(LocalArgs a) {
+    __shared__ uint32_t A[LCAP_B], B[LCAP_B];
+    __shared__ uint16_t cnt[LNT_B / 64][1 << LDMAX];
+    __shared__ uint32_t scratch[LNT_B / 64 + 1];
+    __shared__ uint32_t s_i;
+    for (;;) {
+        if (threadIdx.x == 0) s_i = atomicAdd(&a.nover[1], 1u);
+        __syncthreads();
+        const uint32_t i = s_i;
+        __syncthreads();
+        if (i >= a.nover[0]) break;
+        const uint32_t b = a.over[i];
+        const uint32_t s0 = a.start[b], m = a.start[b + 1] - s0;
+        if (m <= (uint32_t)LCAP_B) {
+            BucketRegs<LNT_B, LCAP_B / LNT_B, LCAP_B> R;
+            R.load(a, b, b + 1);
+            bucket_sort_regs<LNT_B, LCAP_B / LNT_B, LPOS_B, false, uint16_t>(
+                a, b, s0, m, R.g, R.e, R.r, A, B, cnt, scratch, nullptr, nullptr);
+        } else
+            bucket_sort_global<LNT_B>(a, s0, m, A);
+        __syncthreads();
     }
 }
 
@@ -783,129 +971,68 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
                          d_len);
 }
 
-// The hybrid sort's last pass: every 65536-base bucket of (k0, e0, r0)
-// sorted in LDS (k_local_sort) into (k1, e1, r1), pile-up buckets by the
-// digit passes on their own rows; the result is swapped into (k0, e0, r0).
-static int local_sort(lime_ctx *ctx, const lime_set *set, int64_t n, const SetStats &h,
-                      uint32_t *&k0, uint32_t *&e0, uint32_t *&r0, uint32_t *&k1, uint32_t *&e1,
-                      uint32_t *&r1, uint32_t *mat) {
-    const uint32_t nb = (h.max_gs >> 16) + 1;
-    uint32_t *start, *over;
-    unsigned int *nover;
-    LIME_TRY(alloc(ctx, &start, (size_t)nb + 1));
-    PoolGuard<uint32_t> g0{ctx, start};
-    LIME_TRY(alloc(ctx, &over, (size_t)nb));
-    PoolGuard<uint32_t> g1{ctx, over};
-    LIME_TRY(alloc(ctx, &nover, 1));
-    PoolGuard<unsigned int> g2{ctx, nover};
-    LIME_HIP(hipMemsetAsync(nover, 0, 4, S(ctx)));
-    hipLaunchKernelGGL(k_bucket_starts, dim3(blocks_for((int64_t)nb + 1, 256)), dim3(256), 0,
-                       S(ctx), (const uint32_t *)k0, n, nb, start);
-    hipLaunchKernelGGL((k_local_sort<256, LCAP_S>), dim3(nb), dim3(256), 0, S(ctx),
-                       (const uint32_t *)k0, (const uint32_t *)e0, (const uint32_t *)r0,
-                       (const uint32_t *)start, 0u, k1, e1, r1, nover, over);
-    hipLaunchKernelGGL((k_local_sort<512, LCAP>), dim3(nb), dim3(512), 0, S(ctx),
-                       (const uint32_t *)k0, (const uint32_t *)e0, (const uint32_t *)r0,
-                       (const uint32_t *)start, (uint32_t)LCAP_S, k1, e1, r1, nover, over);
-    LIME_HIP(hipGetLastError());
-    unsigned int no = 0;
-    LIME_TRY(read_back(ctx, &no, nover, 4));
-    if (no > 0) {
-        // pile-up buckets: (zero-width bit,) low two digits on their own rows
-        std::vector<uint32_t> hb(no), hs((size_t)nb + 1);
-        LIME_TRY(read_back(ctx, hb.data(), over, 4 * (size_t)no));
-        LIME_TRY(read_back(ctx, hs.data(), start, 4 * ((size_t)nb + 1)));
-        std::vector<std::pair<int, int>> passes;
-        if (set->has_zero_width && set->max_width > 0) passes.push_back({M_NZ, 0});
-        passes.push_back({M_GS, 0});
-        passes.push_back({M_GS, 8});
-        for (uint32_t b : hb) {
-            const int64_t s0 = hs[b], m = (int64_t)hs[b + 1] - hs[b];
-            const uint32_t nt = (uint32_t)((m + RTILE - 1) / RTILE);
-            uint32_t *a[3] = {k0 + s0, e0 + s0, r0 + s0}, *o[3] = {k1 + s0, e1 + s0, r1 + s0};
-            for (auto &p : passes) {
-                LIME_TRY(radix_pass(ctx, p.first, p.second, false, m, a[0], a[1], a[2], nullptr,
-                                    o[0], o[1], o[2], mat, nt, ROWS_LOAD));
-                std::swap(a, o);
-            }
-            if (a[0] != k1 + s0)  // (an even number of passes ends on the input side)
-                for (int q = 0; q < 3; ++q)
-                    LIME_HIP(hipMemcpyAsync(q == 0 ? k1 + s0 : q == 1 ? e1 + s0 : r1 + s0, a[q],
-                                            4 * (size_t)m, hipMemcpyDeviceToDevice, S(ctx)));
-        }
-    }
-    std::swap(k0, k1);
-    std::swap(e0, e1);
-    std::swap(r0, r1);
-    return LIME_OK;
-}
+// the bucketed sort's choice: 2^L-base buckets under two 8-bit digit passes
+// (L = bits - 16), averaging LMIN to LAVG rows (else the digit passes)
+constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4;
 
 int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
                   const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_len) {
     const int64_t n = set->n;
     const uint32_t ntiles = (uint32_t)((n + RTILE - 1) / RTILE);
-    uint32_t *k0, *e0, *r0, *mat;
+    uint32_t *k0 = nullptr, *e0 = nullptr, *r0 = nullptr, *mat = nullptr;
     SetStats *part, *st;
-    LIME_TRY(alloc(ctx, &k0, (size_t)n));
-    LIME_TRY(alloc(ctx, &e0, (size_t)n));
     // binned sets (bitset painting) keep no row ids: 8 B per row per pass
     const bool keep_rows = set->min_shift == 0;
-    r0 = nullptr;
-    if (keep_rows) LIME_TRY(alloc(ctx, &r0, (size_t)n));
+    const bool stranded = set->strand_in != nullptr;
     LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * (ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &st, 1));
-    SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
-    // hybrid sort (k_local_sort): plain sets with row ids over a span past
-    // 2^16, large enough to fill the GPU.  Opt-in (LIME_SORT_HYBRID=1): parity
-    // green on the whole GPU suite, but measured SLOWER on MI355X (C2 sort
-    // 5.7 -> 6.1 ms, C3 13.4 -> 19.7 ms: the per-bucket LDS ranking, one
-    // 147 KiB block per CU for C3's ~10,600-row buckets, costs more than the
-    // two digit passes it replaces)
-    static const bool hyb_env = getenv("LIME_SORT_HYBRID") && atoi(getenv("LIME_SORT_HYBRID")) == 1;
+    // the bucketed sort is a candidate for plain sets whose span needs more
+    // than 16 key bits: its prep then only validates and histograms the
+    // first digit (bits [L, L + 8)), L = bits(span) - 16
+    // (and rows enough that the buckets average LMIN rows: a workgroup per
+    // bucket costs more than the digit passes below that)
     const int64_t span = set->off.empty() ? 0 : (int64_t)set->off.back();
-    const bool hyb_cand = hyb_env && keep_rows && set->strand_in == nullptr &&
-                          set->min_shift == 0 && n >= (1 << 20) && span > (1 << 16);
-    const int hshift = hyb_cand ? 16 : set->min_shift;  // the digit k_prep histograms
-    // plain caller rows: validate + histogram only, and let the first radix
-    // pass read the caller's rows (saves writing gs / ge and reading them back)
-    // Opt-in (LIME_SORT_RAW=1): measured SLOWER on MI355X (C2 sort 5.8 ->
-    // 7.1 ms, C3 13.4 -> 17.2 ms: the first pass's off[contig] gather costs
-    // more than the ~4 B/row it saves), kept for experiments only.
-    static const bool raw_env = getenv("LIME_SORT_RAW") && atoi(getenv("LIME_SORT_RAW")) == 1;
-    const bool raw_ok = raw_env && !global && keep_rows && set->strand_in == nullptr &&
-                        set->min_shift == 0;
-    bool raw = false;
-    if (n > 0 && raw_ok) {
-        if (set->n_contigs <= PCMAX)
-            hipLaunchKernelGGL((k_prep<false, false, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
-                               d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, 0);
-        else
-            hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
-                               d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, 0);
-        hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
-                           (int64_t)ntiles, st);
-        LIME_HIP(hipGetLastError());
-        LIME_TRY(read_back(ctx, &h, st, sizeof(h)));
-        // the fast path needs the first pass to be a gs pass over unsorted rows
-        raw = !h.err && n > 1 && h.unsorted && !(h.has_zero && h.max_width > 0);
-    }
-    if (n > 0 && !raw) {
-        if (global)
-            hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig, d_start,
-                               d_end, (const uint32_t *)set->d_off, d_len, set->n_contigs, n, k0,
-                               e0, r0, part, mat, ntiles, hshift);
-        else if (set->n_contigs <= PCMAX)
-            hipLaunchKernelGGL((k_prep<false, true, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
-                               d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
-                               hshift);  // rows = positions: made by the first pass
-        else
-            hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
-                               d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                               set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, hshift);
+    const int sbits = span > 1 ? 64 - __builtin_clzll((uint64_t)(span - 1)) : 1;
+    const bool bucket_cand = keep_rows && !stranded && sbits > 16 &&
+                             n >= LMIN * ((span >> (sbits - 16)) + 1);
+    const int hshift = bucket_cand ? sbits - 16 : set->min_shift;
+    SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
+    if (n > 0) {
+        if (bucket_cand) {  // validate + statistics + histogram only
+            if (global)
+                hipLaunchKernelGGL((k_prep<true, false>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles,
+                                   hshift);
+            else if (set->n_contigs <= PCMAX)
+                hipLaunchKernelGGL((k_prep<false, false, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles,
+                                   hshift);
+            else
+                hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles,
+                                   hshift);
+        } else {
+            LIME_TRY(alloc(ctx, &k0, (size_t)n));
+            LIME_TRY(alloc(ctx, &e0, (size_t)n));
+            if (keep_rows) LIME_TRY(alloc(ctx, &r0, (size_t)n));
+            if (global)
+                hipLaunchKernelGGL(k_prep<true>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
+                                   d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, k0, e0, r0, part, mat, ntiles, hshift);
+            else if (set->n_contigs <= PCMAX)
+                hipLaunchKernelGGL((k_prep<false, true, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles,
+                                   hshift);  // rows = positions: made by the first pass
+            else
+                hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
+                                   d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, hshift);
+        }
         hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, S(ctx), (const SetStats *)part,
                            (int64_t)ntiles, st);
         LIME_HIP(hipGetLastError());
@@ -925,23 +1052,108 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     set->min_width = n > 0 ? h.min_width : 0;
     set->max_width = h.max_width;
     set->has_zero_width = h.has_zero != 0;
+    const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
+    const bool need = n > 1 && (h.unsorted || stranded) &&
+                      !(set->min_shift > 0 && (h.max_gs >> set->min_shift) == 0);
 
-    const bool stranded = set->strand_in != nullptr;
-    // (a binned set whose keys all share one bin needs no pass)
-    if (n > 1 && (h.unsorted || stranded) &&
-        !(set->min_shift > 0 && (h.max_gs >> set->min_shift) == 0)) {
+    if (bucket_cand) {
+        // the bucketed sort when the rows are not in order yet and the
+        // buckets stay small on average; else materialise (gs, ge, row) the
+        // way the digit passes start from
+        const int L = sbits - 16;
+        const uint32_t nb = (h.max_gs >> L) + 1;
+        if (need && n / (int64_t)nb <= LAVG) {
+            uint32_t *a[3], *o[3];
+            for (int q = 0; q < 3; ++q) {
+                LIME_TRY(alloc(ctx, &a[q], (size_t)n));
+                LIME_TRY(alloc(ctx, &o[q], (size_t)n));
+            }
+            // pass 1 (bits [L, L + 8)) straight from the caller's rows,
+            // histogrammed by k_prep
+            LIME_TRY(scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr));
+            if (global)
+                hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                                   reinterpret_cast<const uint32_t *>(d_contig), d_start, d_end,
+                                   n, L, (const int8_t *)nullptr, (const uint32_t *)mat, ntiles,
+                                   a[0], a[1], a[2]);
+            else
+                hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, true>), dim3(ntiles), dim3(RB), 0,
+                                   S(ctx), reinterpret_cast<const uint32_t *>(d_contig), d_start,
+                                   d_end, n, L, (const int8_t *)nullptr, (const uint32_t *)mat,
+                                   ntiles, a[0], a[1], a[2], (const uint32_t *)set->d_off,
+                                   set->n_contigs);
+            LIME_HIP(hipGetLastError());
+            // pass 2 (bits [L + 8, L + 16))
+            LIME_TRY(radix_pass(ctx, M_GS, L + 8, false, n, a[0], a[1], a[2], nullptr, o[0], o[1],
+                                o[2], mat, ntiles, ROWS_LOAD));
+            release(ctx, mat);
+            // every bucket sorted locally: (o) -> (a)
+            uint32_t *start, *over;
+            unsigned int *nover;
+            LIME_TRY(alloc(ctx, &start, (size_t)nb + 1));
+            PoolGuard<uint32_t> g0{ctx, start};
+            LIME_TRY(alloc(ctx, &over, (size_t)nb));
+            PoolGuard<uint32_t> g1{ctx, over};
+            LIME_TRY(alloc(ctx, &nover, 2));
+            PoolGuard<unsigned int> g2{ctx, nover};
+            LIME_HIP(hipMemsetAsync(nover, 0, 8, S(ctx)));
+            hipLaunchKernelGGL(k_bucket_starts, dim3(blocks_for((int64_t)nb + 1, 256)), dim3(256),
+                               0, S(ctx), (const uint32_t *)o[0], n, nb, L, start);
+            LocalArgs la;
+            la.k0 = o[0], la.e0 = o[1], la.r0 = o[2];
+            la.start = start;
+            la.L = L;
+            la.k1 = a[0], la.e1 = a[1], la.r1 = a[2];
+            la.nover = nover;
+            la.over = over;
+            int dev = 0, cus = 256;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (cus <= 0) cus = 256;
+            hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)),
+                               dim3(LNT_S), 0, S(ctx), la, nb);
+            hipLaunchKernelGGL(k_local_big, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B), 0,
+                               S(ctx), la);
+            LIME_HIP(hipGetLastError());
+            for (int q = 0; q < 3; ++q) release(ctx, o[q]);
+            set->gs = a[0];
+            set->ge = a[1];
+            set->row = a[2];
+            return LIME_OK;
+        }
+        // (in order, or dense buckets) the digit-pass layout from the caller's rows
+        LIME_TRY(alloc(ctx, &k0, (size_t)n));
+        LIME_TRY(alloc(ctx, &e0, (size_t)n));
+        LIME_TRY(alloc(ctx, &r0, (size_t)n));
+        if (global) {
+            LIME_HIP(hipMemcpyAsync(k0, d_contig, 4 * (size_t)n, hipMemcpyDeviceToDevice, S(ctx)));
+            LIME_HIP(hipMemcpyAsync(e0, d_start, 4 * (size_t)n, hipMemcpyDeviceToDevice, S(ctx)));
+            LIME_HIP(hipMemcpyAsync(r0, d_end, 4 * (size_t)n, hipMemcpyDeviceToDevice, S(ctx)));
+        } else {
+            // gs / ge, and the digit-0 histogram the passes below start from
+            PoolGuard<SetStats> gp{ctx, part};
+            PoolGuard<SetStats> gq{ctx, st};
+            LIME_TRY(alloc(ctx, &part, (size_t)ntiles));
+            LIME_TRY(alloc(ctx, &st, 1));
+            if (set->n_contigs <= PCMAX)
+                hipLaunchKernelGGL((k_prep<false, true, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, 0);
+            else
+                hipLaunchKernelGGL(k_prep<false>, dim3(ntiles), dim3(RB), 0, S(ctx), d_contig,
+                                   d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                                   set->n_contigs, n, k0, e0, nullptr, part, mat, ntiles, 0);
+            LIME_HIP(hipGetLastError());
+        }
+    }
+
+    if (need) {
         uint32_t *k1, *e1, *r1 = nullptr;
         LIME_TRY(alloc(ctx, &k1, (size_t)n));
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
         if (keep_rows) LIME_TRY(alloc(ctx, &r1, (size_t)n));
-        const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
-        // hybrid: digit passes on bits 16.. only, then k_local_sort (its key
-        // carries the zero-width bit: no NZ pass)
-        const bool hybrid = hyb_cand && bits > 16;
         std::vector<std::pair<int, int>> passes;  // (mode, shift), least significant first
-        if (hybrid) {
-            for (int sh = 16; sh < bits; sh += 8) passes.push_back({M_GS, sh});
-        } else if (stranded) {
+        if (stranded) {
             // RegionOrdering (start, end, strand): strand, then ge, then gs.
             // The strand pass runs first, while row i is still input row i.
             const int wbits = h.max_width ? 32 - __builtin_clz(h.max_width) : 0;
@@ -951,33 +1163,24 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             // (all rows zero-width: the bit is constant, no pass)
             passes.push_back({M_NZ, 0});
         }
-        if (!hybrid)
-            for (int sh = 0; sh < bits; sh += 8)
-                if (sh >= set->min_shift) passes.push_back({M_GS, sh});
+        for (int sh = 0; sh < bits; sh += 8)
+            if (sh >= set->min_shift) passes.push_back({M_GS, sh});
         // caller rows: the first pass writes row = position (k_prep did not)
         int rows = !keep_rows ? ROWS_NONE : global ? ROWS_LOAD : ROWS_IDENT;
-        // k_prep already histogrammed the gs digit at hshift
-        bool have = passes.front().first == M_GS && passes.front().second == hshift;
-        bool first = true;
+        // k_prep already histogrammed the gs digit at its shift (the bucketed
+        // candidate's fallback re-ran it at 0)
+        const int prep_shift = bucket_cand ? 0 : hshift;
+        bool have = passes.front().first == M_GS && passes.front().second == prep_shift &&
+                    !(bucket_cand && global);
         for (auto &p : passes) {
-            if (first && raw) {
-                // the caller's (contig, start, end) in place of (gs, ge, row)
-                LIME_TRY(radix_pass(ctx, p.first, p.second, true, n,
-                                    reinterpret_cast<const uint32_t *>(d_contig), d_start, d_end,
-                                    set->strand_in, k1, e1, r1, mat, ntiles, rows,
-                                    (const uint32_t *)set->d_off, set->n_contigs));
-            } else {
-                LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in,
-                                    k1, e1, r1, mat, ntiles, rows));
-            }
-            first = false;
+            LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
+                                e1, r1, mat, ntiles, rows));
             have = false;
             if (rows == ROWS_IDENT) rows = ROWS_LOAD;
             std::swap(k0, k1);
             std::swap(e0, e1);
             std::swap(r0, r1);
         }
-        if (hybrid) LIME_TRY(local_sort(ctx, set, n, h, k0, e0, r0, k1, e1, r1, mat));
         release(ctx, k1);
         release(ctx, e1);
         release(ctx, r1);

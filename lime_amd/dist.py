@@ -74,16 +74,17 @@ def _alltoallv(send, counts, group):
     return recv, rcounts
 
 
-def route_rows(gs, ge, row, splits, group=None):
-    """Send every row to the shard owning its start; returns (gs, ge, row)."""
+def route_rows(gs, ge, row, splits, group=None, *extra):
+    """Send every row to the shard owning its start; returns (gs, ge, row,
+    *extra) -- extra per-row int64 columns (e.g. strand codes) travel along."""
     w, _ = _ws(group)
     bounds = torch.tensor(splits[1:-1], dtype=torch.int64, device=gs.device)
     owner = torch.bucketize(gs, bounds, right=True)
     order = torch.argsort(owner, stable=True)
     counts = torch.bincount(owner, minlength=w).tolist()
-    send = torch.stack([gs[order], ge[order], row[order]], dim=1)
+    send = torch.stack([x[order] for x in (gs, ge, row) + tuple(extra)], dim=1)
     recv, _ = _alltoallv(send, counts, group)
-    return recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous()
+    return tuple(recv[:, j].contiguous() for j in range(send.shape[1]))
 
 
 def right_halo(sets, group=None):
@@ -115,57 +116,68 @@ def right_halo(sets, group=None):
 
 
 class TensorRuns:
-    """Runs held as int64 tensors (global coordinates)."""
+    """Runs held as int64 tensors (global coordinates), optionally with a
+    strand code per run (stranded merges)."""
 
-    def __init__(self, run_gs, run_ge):
-        self.gs, self.ge = run_gs, run_ge
+    def __init__(self, run_gs, run_ge, run_strand=None):
+        self.gs, self.ge, self.st = run_gs, run_ge, run_strand
         self.n = run_gs.numel()
         self.last_end = int(run_ge[-1].item()) if self.n else -1
+        self.last_strand = int(run_strand[-1].item()) if self.n and run_strand is not None else 0
 
     def head(self, k):
         return self.gs[:k].tolist(), self.ge[:k].tolist()
 
+    def head_strands(self, k):
+        return self.st[:k].tolist() if self.st is not None else [0] * min(k, self.n)
 
-def merge_carry(run_gs, run_ge=None, group=None, k=256, device=None):
-    """Cross-shard fix-up of locally merged runs (sorted, disjoint per shard).
 
-    `run_gs` is either an int64 tensor of run starts (with `run_ge`) or any
-    object with `.n`, `.last_end` and `.head(k) -> (starts, ends)`.
-    Returns (drop, new_last_end): this shard must drop its first `drop` runs
-    (they continue a run that starts on an earlier shard) and, if
-    new_last_end is not None, set the end of its last remaining run to it.
-    One all_gather of (n_runs, last_end, first k runs) per call; k doubles
-    and the gather repeats only if a shard's k leading runs are all absorbed.
-    """
-    runs = TensorRuns(run_gs, run_ge) if run_ge is not None else run_gs
+def carry_table(runs, group=None, k=256, device=None, stranded=False):
+    """Every shard's view of the cross-shard merge carry (sorted, disjoint
+    runs per shard, shards in coordinate order).  `runs` has `.n`,
+    `.last_end`, `.head(k) -> (starts, ends)` and, when stranded,
+    `.last_strand` and `.head_strands(k)`.
+
+    The reference folds the sorted rows into runs with Merge.condition =
+    overlaps (SetTheory.scala:208-225, strands equal), so a shard's leading
+    run continues the run open at its left bound iff that run's end passes
+    its start (and, stranded, it has the open run's strand).  One
+    all_gather of (n, last end, last strand, the first k runs) per shard; k
+    doubles and the gather repeats only while a shard's k leading runs are
+    all absorbed.  Returns a list over shards of (n, drop, ext, first_kept,
+    last_kept): shard r drops its first `drop` runs, ends its last kept run at
+    `ext` (None: unchanged), and keeps n - drop runs from first_kept (start)
+    to last_kept (end) -- None when it keeps none."""
     w, me = _ws(group)
-    dev = device if device is not None else (run_gs.device if run_ge is not None else "cpu")
+    dev = device if device is not None else "cpu"
     while True:
         n = runs.n
         kk = min(k, n)
-        h = [-1] * (2 * k + 2)
+        W = 3 * k + 3
+        h = [-1] * W
         h[0] = n
         h[1] = runs.last_end if n else -1
+        h[2] = getattr(runs, "last_strand", 0) if stranded and n else 0
         if kk:
             hs, he = runs.head(kk)
-            h[2:2 + kk] = hs
-            h[2 + k:2 + k + kk] = he
+            h[3:3 + kk] = hs
+            h[3 + k:3 + k + kk] = he
+            if stranded:
+                h[3 + 2 * k:3 + 2 * k + kk] = runs.head_strands(kk)
         head = torch.tensor(h, dtype=torch.int64, device=dev)
-        allh = torch.empty(w * (2 * k + 2), dtype=torch.int64, device=dev)
+        allh = torch.empty(w * W, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allh, head, group=group)
-        allh = allh.view(w, 2 * k + 2).cpu().tolist()
-        # sequential carry over shards (host, tiny)
-        carry = -1           # running max end of the open run
-        owner = -1           # shard holding the open run's start
-        drops = [0] * w
-        ext = {}             # owner shard -> extended end of its last run
-        again = False
+        allh = allh.view(w, W).cpu().tolist()
+        carry, cstrand = -1, 0  # the open run: its running max end, strand
+        owner = -1              # shard holding the open run's start
+        drops, ext, again = [0] * w, {}, False
         for r in range(w):
-            nr, last_end = allh[r][0], allh[r][1]
-            starts = allh[r][2:2 + k]
-            ends_ = allh[r][2 + k:2 + 2 * k]
+            nr, last_end, last_strand = allh[r][0], allh[r][1], allh[r][2]
+            starts = allh[r][3:3 + k]
+            ends_ = allh[r][3 + k:3 + 2 * k]
+            strands = allh[r][3 + 2 * k:3 + 3 * k]
             i = 0
-            while i < min(nr, k) and carry > starts[i]:
+            while i < min(nr, k) and carry > starts[i] and (not stranded or strands[i] == cstrand):
                 carry = max(carry, ends_[i])
                 i += 1
             if i == k and nr > k:
@@ -174,12 +186,76 @@ def merge_carry(run_gs, run_ge=None, group=None, k=256, device=None):
             drops[r] = i
             if i > 0 and owner >= 0:
                 ext[owner] = max(ext.get(owner, -1), carry)
-            if nr > i:  # shard r now holds the open run
+            if nr > i:  # shard r now holds the open run: its last run
                 owner = r
-                carry = max(carry, last_end)
-        if not again:
-            return drops[me], ext.get(me)
-        k *= 2
+                carry, cstrand = last_end, last_strand
+        if again:
+            k *= 2
+            continue
+        table = []
+        for r in range(w):
+            nr, last_end = allh[r][0], allh[r][1]
+            d = drops[r]
+            if nr > d:
+                table.append((nr, d, ext.get(r), allh[r][3 + d] if d < k else None,
+                              ext.get(r, last_end)))
+            else:
+                table.append((nr, d, ext.get(r), None, None))
+        return table
+
+
+def merge_carry(run_gs, run_ge=None, group=None, k=256, device=None, stranded=False):
+    """Cross-shard fix-up of locally merged runs (sorted, disjoint per shard).
+
+    `run_gs` is either an int64 tensor of run starts (with `run_ge`) or any
+    object with `.n`, `.last_end` and `.head(k) -> (starts, ends)`.
+    Returns (drop, new_last_end): this shard must drop its first `drop` runs
+    (they continue a run that starts on an earlier shard) and, if
+    new_last_end is not None, set the end of its last remaining run to it
+    (carry_table: one all_gather, shard-count invariant -- the reference's
+    log2(P) rounds of SetTheory.scala:236-282 are not, quirks Q1/Q2)."""
+    runs = TensorRuns(run_gs, run_ge) if run_ge is not None else run_gs
+    dev = device if device is not None else (run_gs.device if run_ge is not None else "cpu")
+    _, me = _ws(group)
+    row = carry_table(runs, group, k, dev, stranded)[me]
+    return row[1], row[2]
+
+
+def run_offsets(table):
+    """global index of every shard's first kept run (exclusive scan of the
+    kept counts of carry_table)"""
+    out, acc = [], 0
+    for nr, d, _, _, _ in table:
+        out.append(acc)
+        acc += nr - d
+    return out
+
+
+def global_run_ids(local, drop, offset):
+    """Global run id of every row of a shard's local merge (SetTheory.scala
+    :213-217 after the moves of :263-272: the rows of a run continued from an
+    earlier shard belong to that run): a row of local run j >= drop is in run
+    offset + j - drop; a row of a dropped run is in the run open at the
+    shard's left bound, the last run before it: offset - 1."""
+    local = local.to(torch.int64)
+    return torch.where(local >= drop, local - drop + offset,
+                       torch.full_like(local, offset - 1))
+
+
+def complement_frame(table, rank):
+    """The runs around shard `rank`'s window that its share of the complement
+    needs (Complement.scala:67-73 / :112-122: the gap at a partition bound
+    runs from the previous partition's last run end to the next run start):
+    (prev_end, next_start) -- the last kept run end on an earlier shard and
+    the first kept run start on a later one, None where there is none."""
+    prev_end = next_start = None
+    for r in range(rank):
+        if table[r][4] is not None:
+            prev_end = table[r][4]
+    for r in range(len(table) - 1, rank, -1):
+        if table[r][3] is not None:
+            next_start = table[r][3]
+    return prev_end, next_start
 
 
 # ------------------------------------------------------ device exchanges
@@ -199,11 +275,15 @@ def coord_splits(span, world, align=None):
     return cuts + [int(span)]
 
 
-def exchange(tensors, counts, group=None, comm_device=None):
+def exchange(tensors, counts, group=None, comm_device=None, packed=False):
     """Variable all_to_all of 1-D tensors whose rows are grouped by destination
     (counts[q] rows to rank q, the same for every tensor).  The tensors stay
     on their device for RCCL (backend "nccl": xGMI peer traffic, no host
     copy); with comm_device = cpu (gloo) they are staged through the host.
+    packed: the tensors (same dtype) travel as the columns of ONE [rows, k]
+    tensor -- one collective for all of them (fewer, larger transfers suit
+    xGMI's point-to-point links).  The counts cost one all_to_all and one
+    host read: all_to_all_single takes its split sizes on the host.
     Returns (received tensors on the input device, received counts)."""
     w, _ = _ws(group)
     dev = tensors[0].device
@@ -212,6 +292,14 @@ def exchange(tensors, counts, group=None, comm_device=None):
     rc = torch.empty(w, dtype=torch.int64, device=cd)
     dist.all_to_all_single(rc, sc, group=group)
     rcounts = rc.tolist()
+    if packed and len(tensors) > 1:
+        t = sum(counts)
+        src = torch.stack([x[:t] for x in tensors], dim=1).to(cd)
+        r = torch.empty((sum(rcounts), len(tensors)), dtype=src.dtype, device=cd)
+        dist.all_to_all_single(r, src, output_split_sizes=rcounts,
+                               input_split_sizes=list(counts), group=group)
+        r = r.to(dev)
+        return [r[:, j].contiguous() for j in range(len(tensors))], rcounts
     out = []
     for t in tensors:
         src = t[:sum(counts)].to(cd)
@@ -220,6 +308,50 @@ def exchange(tensors, counts, group=None, comm_device=None):
                                input_split_sizes=list(counts), group=group)
         out.append(r.to(dev))
     return out, rcounts
+
+
+def exchange_sets(sets, counts, group=None, comm_device=None):
+    """The rows of k sets moved by ONE packed all_to_all (plus one all_to_all
+    of the k x w count matrix): sets[i] = [column tensors] with their rows
+    grouped by destination, counts[i][q] of them for rank q.  Returns, per
+    set, the received columns (rows from rank 0 first), their count and how
+    many came from other ranks -- the k-way C5 input in 2 collectives instead
+    of 3 k."""
+    w, _ = _ws(group)
+    k = len(sets)
+    dev = sets[0][0].device
+    cd = comm_device if comm_device is not None else dev
+    ncol = len(sets[0])
+    starts = [[0] * (w + 1) for _ in range(k)]
+    for i in range(k):
+        for q in range(w):
+            starts[i][q + 1] = starts[i][q] + counts[i][q]
+    # counts: to rank q the k numbers counts[.][q]
+    sc = torch.tensor([[counts[i][q] for i in range(k)] for q in range(w)], dtype=torch.int64,
+                      device=cd)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcm = rc.tolist()  # rcm[p][i]: rows of set i from rank p
+    parts = [torch.stack([c[starts[i][q]:starts[i][q + 1]] for c in sets[i]], dim=1)
+             for q in range(w) for i in range(k)]
+    src = torch.cat(parts).to(cd) if parts else torch.empty((0, ncol), device=cd)
+    send_n = [sum(counts[i][q] for i in range(k)) for q in range(w)]
+    recv_n = [sum(rcm[p]) for p in range(w)]
+    r = torch.empty((sum(recv_n), ncol), dtype=src.dtype, device=cd)
+    dist.all_to_all_single(r, src, output_split_sizes=recv_n, input_split_sizes=send_n,
+                           group=group)
+    r = r.to(dev)
+    out, at = [[] for _ in range(k)], 0
+    for p in range(w):
+        for i in range(k):
+            out[i].append(r[at:at + rcm[p][i]])
+            at += rcm[p][i]
+    _, me = _ws(group)
+    res = []
+    for i in range(k):
+        t = torch.cat(out[i]) if out[i] else r[:0]
+        res.append(([t[:, j].contiguous() for j in range(ncol)], t.shape[0], t.shape[0] - rcm[me][i]))
+    return res
 
 
 def allgatherv(t, group=None, comm_device=None):

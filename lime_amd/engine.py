@@ -214,6 +214,23 @@ class Result:
         check(_lib().lime_result_device_arrays(self._h, C.byref(gs), C.byref(ge)))
         return gs.value, ge.value
 
+    def copy_run_ids_device(self, d_run, d_row):
+        """merge results: (run of every sorted input row, that row's id) into
+        caller device buffers (u32, as many as the merged set has rows)"""
+        check(_lib().lime_result_copy_run_ids_device(self._h, vp(d_run), vp(d_row)))
+
+    def copy_rows_device(self, first, count, d_gs, d_ge):
+        """regions [first, first + count) (global) into caller device buffers"""
+        check(_lib().lime_result_copy_rows_device(self._h, int(first), int(count), vp(d_gs),
+                                                  vp(d_ge)))
+
+    def run_strands(self, first, count):
+        """stranded merges: strand codes of runs [first, first + count)"""
+        out = np.zeros(max(int(count), 1), dtype=np.int8)
+        check(_lib().lime_result_run_strands(self._h, int(first), int(count),
+                                             _ptr(out, C.c_int8)))
+        return out[:count]
+
     def copy_range(self, first, count):
         """host copy of regions [first, first+count) in GLOBAL coordinates"""
         gs = np.zeros(count, dtype=np.uint32)
@@ -370,6 +387,14 @@ class Context:
                                             C.byref(h)))
         return IntervalSet(self, h, space)
 
+    def set_from_global_stranded(self, space, n, d_gs, d_ge, d_row, d_strand):
+        """global rows with int8 strand codes in HBM: full RegionOrdering, merge
+        breaks runs at strand changes"""
+        h = vp()
+        check(_lib().lime_set_create_global_stranded(self._h, space.handle, int(n), d_gs, d_ge,
+                                                     d_row, vp(d_strand), C.byref(h)))
+        return IntervalSet(self, h, space)
+
     # ------------------------------------------------------------- ops
     def intersect(self, a, b, threshold=0, a_owned=-1, b_owned=-1):
         h, n = vp(), i64()
@@ -425,6 +450,15 @@ class Context:
         check(_lib().lime_complement(self._h, genome_space.handle, a._h, C.byref(h), C.byref(n)))
         return Result(self, h, a.space, keep=(a,))
 
+    def complement_runs(self, genome_space, n, d_gs, d_ge, lo=0, hi=None):
+        """gaps of sorted disjoint runs in HBM (global coordinates) over the
+        genome, only those starting in [lo, hi) (a shard's share)"""
+        h, k = vp(), i64()
+        hi = genome_space.span if hi is None else hi
+        check(_lib().lime_complement_runs(self._h, genome_space.handle, int(n), vp(d_gs),
+                                          vp(d_ge), int(lo), int(hi), C.byref(h), C.byref(k)))
+        return Result(self, h, genome_space)
+
     def bitset(self, a):
         h = vp()
         check(_lib().lime_bitset_from_set(self._h, a._h, C.byref(h)))
@@ -468,17 +502,20 @@ class Context:
         return Bitset(self, h, space)
 
     def route_rows(self, space, n, d_contig, d_start, d_end, splits, clip=False, cap=-1,
-                   d_gs=None, d_ge=None, d_row=None, row_base=0):
+                   d_gs=None, d_ge=None, d_row=None, row_base=0, d_strand=None,
+                   d_strand_out=None):
         """Rows -> coordinate shards (lime_route_rows): returns the per-shard
         counts; when their total <= cap the rows are written, grouped by
-        shard, to d_gs / d_ge (global) and d_row (row_base + input index).
+        shard, to d_gs / d_ge (global) and d_row (row_base + input index),
+        their strand codes (d_strand, per input row) to d_strand_out.
         d_contig None: d_start / d_end are already global."""
         k = len(splits) - 1
         sp = (C.c_uint32 * (k + 1))(*[int(x) for x in splits])
         counts = (i64 * k)()
         check(_lib().lime_route_rows(self._h, space.handle, int(n), vp(d_contig), vp(d_start),
                                      vp(d_end), int(row_base) & 0xFFFFFFFF, k, sp, int(bool(clip)),
-                                     int(cap), vp(d_gs), vp(d_ge), vp(d_row), counts))
+                                     int(cap), vp(d_gs), vp(d_ge), vp(d_row), counts,
+                                     vp(d_strand), vp(d_strand_out)))
         return list(counts)
 
     def bitset_runs(self, op, a, b=None):

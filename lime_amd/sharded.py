@@ -16,18 +16,23 @@ from . import dist as ld
 
 
 class _EngineRuns:
-    """merge result as seen by lime_amd.dist.merge_carry"""
+    """merge result as seen by lime_amd.dist.carry_table"""
 
-    def __init__(self, res):
-        self.res, self.n = res, res.n
-        self.last_end = -1
+    def __init__(self, res, stranded=False):
+        self.res, self.n, self.stranded = res, res.n, stranded
+        self.last_end, self.last_strand = -1, 0
         if self.n:
             _, ge = res.copy_range(self.n - 1, 1)
             self.last_end = int(ge[0])
+            if stranded:
+                self.last_strand = int(res.run_strands(self.n - 1, 1)[0])
 
     def head(self, k):
         gs, ge = self.res.copy_range(0, k)
         return [int(x) for x in gs], [int(x) for x in ge]
+
+    def head_strands(self, k):
+        return [int(x) for x in self.res.run_strands(0, k)]
 
 
 class ShardStep:
@@ -66,19 +71,54 @@ class ShardStep:
         return torch.empty(max(int(n), 1), dtype=torch.int32, device=self.dev)
 
     # ----------------------------------------------------------- routing
-    def load(self, n, d_contig, d_start, d_end, row_base=0):
-        """-> IntervalSet of the rows this shard owns (global row ids)"""
+    def route(self, n, d_contig, d_start, d_end, row_base=0, d_strand=None):
+        """this rank's slice of unsorted rows -> the rows this shard owns:
+        [gs, ge, row(, strand)] int32 device tensors (global coordinates and
+        row ids), one packed all_to_all (lime_route_rows + dist.exchange)"""
         ctx, sp = self.ctx, self.space
-        gs, ge, row = self._i32(n), self._i32(n), self._i32(n)
+        cols = [self._i32(n) for _ in range(4 if d_strand else 3)]
+        st8 = torch.empty(max(int(n), 1), dtype=torch.int8, device=self.dev) if d_strand else None
         counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=False, cap=n,
-                                d_gs=gs.data_ptr(), d_ge=ge.data_ptr(), d_row=row.data_ptr(),
-                                row_base=row_base)
+                                d_gs=cols[0].data_ptr(), d_ge=cols[1].data_ptr(),
+                                d_row=cols[2].data_ptr(), row_base=row_base, d_strand=d_strand,
+                                d_strand_out=st8.data_ptr() if d_strand else None)
+        if d_strand:
+            cols[3] = st8.to(torch.int32)
         self._sync()
-        (rgs, rge, rrow), rc = ld.exchange([gs, ge, row], counts, self.group, self.comm)
+        recv, rc = ld.exchange(cols, counts, self.group, self.comm, packed=True)
         self._sync()
         self.routed += sum(rc) - rc[self.rank]
-        m = sum(rc)
-        return ctx.set_from_global(sp, m, rgs.data_ptr(), rge.data_ptr(), rrow.data_ptr())
+        return recv
+
+    def load(self, n, d_contig, d_start, d_end, row_base=0, d_strand=None):
+        """-> IntervalSet of the rows this shard owns (global row ids); with
+        strand codes (int8 per input row) a stranded set: full RegionOrdering,
+        merge breaks runs at strand changes (cli/Intersection.scala:45,48
+        key both sides with ReferenceRegion.stranded, Merge.scala:19)"""
+        recv = self.route(n, d_contig, d_start, d_end, row_base, d_strand)
+        m = recv[0].numel()
+        if d_strand:
+            st8 = recv[3].to(torch.int8)
+            S = self.ctx.set_from_global_stranded(self.space, m, recv[0].data_ptr(),
+                                                  recv[1].data_ptr(), recv[2].data_ptr(),
+                                                  st8.data_ptr())
+        else:
+            S = self.ctx.set_from_global(self.space, m, *(t.data_ptr() for t in recv[:3]))
+        return S
+
+    def load_strand_groups(self, n, d_contig, d_start, d_end, d_strand, row_base=0):
+        """stranded rows -> {strand code: IntervalSet} of this shard's rows:
+        the pairwise ops pair equal strands only (ReferenceRegion.overlaps),
+        so each strand group runs through the strand-free kernels"""
+        gs, ge, row, st = self.route(n, d_contig, d_start, d_end, row_base, d_strand)
+        out = {}
+        codes = torch.unique(st).tolist() if st.numel() else []
+        for c in codes:
+            keep = st == c
+            sub = [x[keep].contiguous() for x in (gs, ge, row)]
+            out[int(c)] = self.ctx.set_from_global(self.space, sub[0].numel(),
+                                                   *(t.data_ptr() for t in sub))
+        return out
 
     # -------------------------------------------------------------- halo
     def _halo(self, sets, my_end):
@@ -170,6 +210,62 @@ class ShardStep:
         res = self.ctx.subtract(A, Be, threshold, mode)
         return res, (hl, hr), Be
 
+    # ------------------------------------------------ merge / complement
+    def merge(self, S, stranded=False):
+        """DistributedMerge over the shards (SetTheory.scala:202-282): the
+        local merge, then ONE all_gather (dist.carry_table).  Returns a dict:
+        the local result, drop / ext (this shard drops its first `drop` runs
+        and ends its last at `ext`), `offset` (the global index of its first
+        kept run) and the table of every shard."""
+        res = self.ctx.merge(S)
+        cd = self.comm if self.comm is not None else self.dev
+        table = ld.carry_table(_EngineRuns(res, stranded), self.group, device=cd,
+                               stranded=stranded)
+        nr, drop, ext, _, _ = table[self.rank]
+        return {"result": res, "drop": drop, "ext": ext, "table": table,
+                "offset": ld.run_offsets(table)[self.rank], "runs": nr - drop}
+
+    def global_run_ids(self, m, n_rows):
+        """(row ids, global run ids) of this shard's rows, int64 device
+        tensors: the Iterable[T] grouping of the sharded merge (SetTheory.scala
+        :213-217 after the moves of :263-272)"""
+        run, row = self._i32(n_rows), self._i32(n_rows)
+        if n_rows:
+            m["result"].copy_run_ids_device(run.data_ptr(), row.data_ptr())
+        local = run[:n_rows].to(torch.int64) & 0xFFFFFFFF
+        return (row[:n_rows].to(torch.int64) & 0xFFFFFFFF,
+                ld.global_run_ids(local, m["drop"], m["offset"]))
+
+    def complement(self, S):
+        """This shard's share of DistributedComplement (Complement.scala
+        :33-134) against the shard space's contigs: the gaps that START in its
+        window [split[r], split[r+1]), from its carried runs framed by the
+        previous shards' last run end and the next shards' first run start
+        (the gap at a partition bound, :67-73 / :112-122; contigs without
+        data, :39-45, fall to the shard holding their start).  The shards'
+        gaps concatenate to the unsharded result."""
+        m = self.merge(S)
+        res, drop, ext = m["result"], m["drop"], m["ext"]
+        prev_end, next_start = ld.complement_frame(m["table"], self.rank)
+        k = res.n - drop
+        lead = 1 if prev_end is not None else 0
+        tot = lead + k + (1 if next_start is not None else 0)
+        gs, ge = self._i32(tot), self._i32(tot)
+        if k:
+            res.copy_rows_device(drop, k, gs[lead:].data_ptr(), ge[lead:].data_ptr())
+        if prev_end is not None:
+            gs[0] = ge[0] = prev_end - (1 << 32) if prev_end >= (1 << 31) else prev_end
+        if ext is not None and k:
+            ge[lead + k - 1] = ext - (1 << 32) if ext >= (1 << 31) else ext
+        if next_start is not None:
+            v = next_start - (1 << 32) if next_start >= (1 << 31) else next_start
+            gs[tot - 1] = ge[tot - 1] = v
+        self._sync()
+        out = self.ctx.complement_runs(self.space, tot, gs.data_ptr(), ge.data_ptr(),
+                                       self.splits[self.rank], self.splits[self.rank + 1])
+        res.close()
+        return out
+
     # -------------------------------------------------------------- step
     def run(self, A, B, threshold=0, on_pairs=None):
         """A, B: this shard's own sorted sets (load()).  Intersect (owned
@@ -244,20 +340,9 @@ class ShardedBitset:
     def shard_rows(self, n, d_contig, d_start, d_end):
         """this rank's slice of one set's rows -> the rows of this shard's
         window from every rank (global coordinates, clipped): (m, gs, ge)"""
-        ctx, sp = self.ctx, self.space
-        cap = n + 4096
-        gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
-                                cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
-        if sum(counts) > cap:  # many rows cross shard bounds: exact size
-            cap = sum(counts)
-            gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
-            ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
-            counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
-                                    cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
+        gs, ge, counts = self._route_clipped(n, d_contig, d_start, d_end)
         self._sync()
-        (rgs, rge), rc = ld.exchange([gs, ge], counts, self.group, self.comm)
+        (rgs, rge), rc = ld.exchange([gs, ge], counts, self.group, self.comm, packed=True)
         self._sync()
         self.moved += sum(rc) - rc[self.rank]
         return sum(rc), rgs, rge
@@ -270,15 +355,39 @@ class ShardedBitset:
         m, rgs, rge = self.shard_rows(n, d_contig, d_start, d_end)
         return ctx.bitset_from_global(sp, self.lo, self.hi, m, rgs.data_ptr(), rge.data_ptr())
 
+    def _route_clipped(self, n, d_contig, d_start, d_end):
+        """one set's rows, clipped to the shards they overlap and grouped by
+        shard: (gs, ge) int32 device tensors and the per-shard counts"""
+        ctx, sp = self.ctx, self.space
+        cap = n + 4096
+        gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
+                                cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
+        if sum(counts) > cap:  # many rows cross shard bounds: exact size
+            cap = sum(counts)
+            gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
+            ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
+            counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
+                                    cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
+        return gs, ge, counts
+
     def and_bitset(self, inputs):
         """this shard's AND of k sets in one fused paint per 16
-        (lime_bitset_and_from_device / _from_global): no per-set bitsets"""
+        (lime_bitset_and_from_device / _from_global): no per-set bitsets.
+        The k sets' rows move in ONE packed all_to_all (dist.exchange_sets)."""
         ctx, sp = self.ctx, self.space
         if self.world == 1:
             return ctx.bitset_and_from_device(sp, inputs)
-        got = [self.shard_rows(*x) for x in inputs]
+        routed = [self._route_clipped(*x) for x in inputs]
+        self._sync()
+        got = ld.exchange_sets([[g, e] for g, e, _ in routed], [c for _, _, c in routed],
+                               self.group, self.comm)
+        self._sync()
+        self.moved += sum(x for _, _, x in got)
         return ctx.bitset_and_from_global(sp, self.lo, self.hi,
-                                          [(m, g.data_ptr(), e.data_ptr()) for m, g, e in got])
+                                          [(m, cols[0].data_ptr(), cols[1].data_ptr())
+                                           for cols, m, _ in got])
 
     def run(self, inputs, gather=False, op="and"):
         """inputs: [(n, d_contig, d_start, d_end)] per set (this rank's rows,

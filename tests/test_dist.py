@@ -210,3 +210,196 @@ def test_sharded_bitset_and_carry(world):
     assert len(want) > 30
     for _, got in res:
         assert got == want  # every rank holds the whole ordered list
+
+
+# ---------------- sharded merge run ids, complement, stranded carry (8(e))
+_GENOME = [70_000, 55_000, 90_000]  # three contigs, bounds inside shards
+
+
+def _offsets():
+    off = [0]
+    for L in _GENOME:
+        off.append(off[-1] + L + 1)
+    return off
+
+
+def _to_local(g):
+    off = np.array(_offsets())
+    c = np.searchsorted(off, np.asarray(g), side="right") - 1
+    return c.astype(np.int32), np.asarray(g) - off[c]
+
+
+def _genome_rows(seed, n, splits):
+    """rows over the three contigs in global coordinates (pads between
+    contigs), strands + / -, with zero-width rows and rows that start or end
+    exactly on a shard bound"""
+    rng = np.random.default_rng(seed)
+    off = _offsets()
+    c = rng.integers(0, 3, n)
+    L = np.array(_GENOME)[c]
+    s = (rng.random(n) * (L - 600)).astype(np.int64)
+    e = s + rng.integers(0, 600, n)
+    gs, ge = np.array(off)[c] + s, np.array(off)[c] + e
+    z = rng.random(n) < 0.05
+    ge[z] = gs[z]
+    # a zero-width row and a row ending exactly on every inner shard bound
+    # (bounds off the pads), and a row starting there
+    extra = []
+    for b in splits[1:-1]:
+        if b in off or b - 1 in [o - 1 for o in off[1:]]:
+            continue
+        extra += [(b, b), (b - 50, b), (b, b + 40)]
+    if extra:
+        gs = np.concatenate([gs, [x for x, _ in extra]])
+        ge = np.concatenate([ge, [y for _, y in extra]])
+    strand = rng.integers(1, 3, len(gs))
+    return gs.astype(np.int64), ge.astype(np.int64), strand.astype(np.int64)
+
+
+def _oracle_merge_global(gs, ge, strand=None):
+    from oracle import oracle
+    c, s = _to_local(gs)
+    e = ge - np.array(_offsets())[c]
+    return oracle.merge((c, s, e) if strand is None else (c, s, e, strand))
+
+
+def _runs_global(m):
+    off = np.array(_offsets())
+    return off[m["contig"]] + m["start"], off[m["contig"]] + m["end"]
+
+
+def _merge_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        from oracle import oracle
+        span = _offsets()[-1]
+        splits = ld.even_splits(span, world)
+        n = 4000
+        gs, ge, st = _genome_rows(9, n, splits)
+        N = len(gs)
+        sl = slice(rank * N // world, (rank + 1) * N // world)
+        cols = [torch.from_numpy(x[sl].copy()) for x in (gs, ge, np.arange(N), st)]
+        rgs, rge, rrow, rst = ld.route_rows(*cols[:3], splits, None, cols[3])
+        lo, hi = splits[rank], splits[rank + 1]
+        assert ((rgs >= lo) & (rgs < hi)).all()
+        out = {}
+        for stranded in (False, True):
+            # the shard's local merge (the engine's, restated by the oracle),
+            # rows in RegionOrdering, ties by row
+            m = _oracle_merge_global(rgs.numpy(), rge.numpy(), rst.numpy() if stranded else None)
+            a, b = _runs_global(m)
+            runs = ld.TensorRuns(torch.from_numpy(a), torch.from_numpy(b),
+                                 torch.from_numpy(m["strand"].astype(np.int64)) if stranded
+                                 else None)
+            table = ld.carry_table(runs, k=2, stranded=stranded)  # small k: the regather
+            nr, drop, ext, _, _ = table[rank]
+            kept = np.stack([a, b], 1)[drop:].copy()
+            if ext is not None and len(kept):
+                kept[-1, 1] = ext
+            # every local row's global run (the Iterable[T] grouping)
+            off = ld.run_offsets(table)[rank]
+            gid = ld.global_run_ids(torch.from_numpy(m["run_of_row"]), drop, off)
+            out[stranded] = (kept.tolist(), list(zip(rrow.tolist(), gid.tolist())))
+            if not stranded:
+                # this shard's share of the complement: its kept runs framed
+                # by the previous shards' last end and the next first start
+                prev_end, next_start = ld.complement_frame(table, rank)
+                V = kept.tolist()
+                if prev_end is not None:
+                    V = [[prev_end, prev_end]] + V
+                if next_start is not None:
+                    V = V + [[next_start, next_start]]
+                V = np.array(V, np.int64).reshape(-1, 2)
+                c, s = _to_local(V[:, 0])
+                e = V[:, 1] - np.array(_offsets())[c]
+                comp = oracle.complement((c, s, e), _GENOME)
+                gl = np.array(_offsets())[comp["contig"]] + comp["start"]
+                gr = np.array(_offsets())[comp["contig"]] + comp["end"]
+                mine = (gl >= lo) & (gl < hi)
+                out["comp"] = list(zip(gl[mine].tolist(), gr[mine].tolist()))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_merge_run_ids_complement_strands(world):
+    # SURVEY.md 8(e): the merge carry, global run ids of every row, the
+    # complement's shard-bound gaps and the stranded carry, against the
+    # unsharded oracle (shard-count invariant); zero-width rows and rows on
+    # shard bounds included
+    from oracle import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_merge_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    span = _offsets()[-1]
+    gs, ge, st = _genome_rows(9, 4000, ld.even_splits(span, world))
+    for stranded in (False, True):
+        m = _oracle_merge_global(gs, ge, st if stranded else None)
+        a, b = _runs_global(m)
+        runs = [tuple(x) for x in sum((r[1][stranded][0] for r in res), [])]
+        assert runs == list(zip(a.tolist(), b.tolist()))
+        ids = dict(sum((r[1][stranded][1] for r in res), []))
+        assert [ids[i] for i in range(len(gs))] == m["run_of_row"].tolist()
+    c, s = _to_local(gs)
+    e = ge - np.array(_offsets())[c]
+    comp = oracle.complement((c, s, e), _GENOME)
+    off = np.array(_offsets())
+    want = list(zip((off[comp["contig"]] + comp["start"]).tolist(),
+                    (off[comp["contig"]] + comp["end"]).tolist()))
+    got = sorted(sum((r[1]["comp"] for r in res), []))
+    assert got == want
+
+
+def _xsets_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        # k sets, each rank holding rows for every destination (grouped by
+        # destination, as lime_route_rows writes them); some (set, dest)
+        # pairs empty
+        k = 3
+        sets, counts = [], []
+        for i in range(k):
+            c = [(rank + 2 * i + q) % 3 for q in range(world)]
+            vals = [1000 * rank + 100 * i + 10 * q + j for q in range(world) for j in range(c[q])]
+            t = torch.tensor(vals or [0], dtype=torch.int32)
+            sets.append([t, -t])
+            counts.append(c)
+        got = ld.exchange_sets(sets, counts)
+        q.put((rank, [(cols[0][:m].tolist(), cols[1][:m].tolist(), m) for cols, m, _ in got]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_sets(world):
+    # C5's batched exchange: every (source, set) segment lands in its set, in
+    # rank order, both columns aligned
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xsets_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for me, got in res:
+        for i, (a, b, m) in enumerate(got):
+            want = [1000 * p + 100 * i + 10 * me + j for p in range(world)
+                    for j in range((p + 2 * i + me) % 3)]
+            assert a == want and b == [-x for x in want] and m == len(want)

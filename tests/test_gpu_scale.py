@@ -57,7 +57,7 @@ def test_1b_merge(ctx, pile_1b):
     say(f"merge: {res.n} runs on the device; oracle")
     m = oracle.merge_mt(len(sp.names), X)
     say("merge: oracle done")
-    assert len(h["start"]) == len(m["start"]) > 1_000_000
+    assert len(h["start"]) == len(m["start"]) > 500_000  # ~7.3e5 pile-up clusters
     assert_runs_equal((h["contig"], h["start"], h["end"]), (m["contig"], m["start"], m["end"]))
     assert ck[2:] == (m["grp_sum"], m["grp_xor"])  # every row's run
     res.close()

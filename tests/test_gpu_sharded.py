@@ -301,3 +301,140 @@ def test_sharded_subtract_and_c4_ops(world):
             want = coalesce(exp["contig"], exp["start"], exp["end"])
             for x, y in zip(got, want):
                 assert np.array_equal(x, y), op
+
+
+# ------------------- sharded complement, global run ids, stranded sets
+def _strand_rows():
+    """A (with strands 1 / 2, zero-width rows, rows on the 2- and 3-way shard
+    bounds) and B, contig-local"""
+    from lime_amd import Space, synth
+    from lime_amd import dist as ld
+    A = [np.asarray(x) for x in synth.uniform(LENS, 12000, 0x33, 0, 4000)]
+    B = [np.asarray(x) for x in synth.uniform(LENS, 9000, 0x44, 10, 5000)]
+    sp_off = np.concatenate([[0], np.cumsum(np.array(LENS) + 1)])
+    extra = []
+    for w in (2, 3):
+        for b in ld.even_splits(int(sp_off[-1]), w)[1:-1]:
+            c = int(np.searchsorted(sp_off, b, side="right") - 1)
+            s = int(b - sp_off[c])
+            if 60 < s < LENS[c] - 60:
+                extra += [(c, s, s), (c, s - 50, s), (c, s, s + 40), (c, s - 5, s + 5)]
+    for i, col in enumerate(zip(*extra)):
+        A[i] = np.concatenate([A[i], np.array(col, A[i].dtype)])
+    rng = np.random.default_rng(5)
+    sa = rng.integers(1, 3, len(A[0])).astype(np.int8)
+    sb = rng.integers(1, 3, len(B[0])).astype(np.int8)
+    return A, B, sa, sb
+
+
+def _strand_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        import lime_amd
+        from lime_amd.sharded import ShardStep
+        ctx = lime_amd.Context(0)
+        sp = lime_amd.Space(NAMES, LENS)
+        off = sp.offsets
+        A, B, sa, sb = _strand_rows()
+        step = ShardStep(ctx, sp, comm_device=torch.device("cpu"))
+
+        def dev(X, st=None):
+            n = len(X[0])
+            f, l = rank * n // world, (rank + 1) * n // world
+            t = [torch.from_numpy(np.ascontiguousarray(x[f:l]).astype(np.int32)).cuda()
+                 for x in X]
+            s8 = torch.from_numpy(np.ascontiguousarray(st[f:l])).cuda() if st is not None \
+                else None
+            torch.cuda.synchronize()
+            return l - f, t, s8, f
+        out = {}
+        # plain: merge run ids + the shard's complement gaps
+        n, t, _, f = dev(A)
+        S = step.load(n, *(x.data_ptr() for x in t), row_base=f)
+        m = step.merge(S)
+        rows, gid = step.global_run_ids(m, S.n)
+        out["ids"] = list(zip(rows.cpu().tolist(), gid.cpu().tolist()))
+        m["result"].close()
+        comp = step.complement(S).to_host()
+        lo, hi = step.splits[rank], step.splits[rank + 1]
+        g = off[comp["contig"]] + comp["start"]
+        assert ((g >= lo) & (g < hi)).all()
+        out["comp"] = list(zip(comp["contig"].tolist(), comp["start"].tolist(),
+                               comp["end"].tolist()))
+        # stranded: merge (runs break at strand changes) + its run ids
+        n, t, s8, f = dev(A, sa)
+        SS = step.load(n, *(x.data_ptr() for x in t), row_base=f, d_strand=s8.data_ptr())
+        m = step.merge(SS, stranded=True)
+        h = m["result"].to_host()
+        st_ = m["result"].run_strands(0, m["result"].n)
+        k = m["drop"]
+        runs = [list(x) for x in zip(h["contig"].tolist(), h["start"].tolist(),
+                                     h["end"].tolist(), st_.tolist())][k:]
+        if m["ext"] is not None and runs:
+            runs[-1][2] = m["ext"] - int(off[runs[-1][0]])
+        out["sruns"] = [tuple(r) for r in runs]
+        rows, gid = step.global_run_ids(m, SS.n)
+        out["sids"] = list(zip(rows.cpu().tolist(), gid.cpu().tolist()))
+        # stranded pairwise: strand groups of A and B, intersect per group
+        na, ta, s8a, fa = dev(A, sa)
+        nb, tb, s8b, fb = dev(B, sb)
+        GA = step.load_strand_groups(na, *(x.data_ptr() for x in ta), s8a.data_ptr(), fa)
+        GB = step.load_strand_groups(nb, *(x.data_ptr() for x in tb), s8b.data_ptr(), fb)
+        pairs = []
+        for code in (1, 2):  # every rank runs every code (collectives line up)
+            Ga = GA.get(code) or ctx.set_from_global(sp, 0, 0, 0, 0)
+            Gb = GB.get(code) or ctx.set_from_global(sp, 0, 0, 0, 0)
+
+            def on_pairs(plan):
+                p = plan.fill_host()
+                pairs.extend(zip(p["a_row"].tolist(), p["b_row"].tolist()))
+            step.run(Ga, Gb, on_pairs=on_pairs)
+        out["spairs"] = pairs
+        q.put((rank, out))
+        ctx.close()
+    except Exception:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_complement_run_ids_strands(world):
+    # SURVEY.md 8(e) on the device: the shards' complement gaps, the global
+    # run id of every row (plain and stranded merge) and stranded pairs equal
+    # the single-shard oracle (Complement.scala:39-45,67-73,112-122;
+    # SetTheory.scala:213-217,263-272; cli/Intersection.scala:45,48)
+    from oracle import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_strand_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    errs = [r[1]["error"] for r in res if "error" in r[1]]
+    assert not errs, errs[0]
+    A, B, sa, sb = _strand_rows()
+    m = oracle.merge(A)
+    ids = dict(sum((r[1]["ids"] for r in res), []))
+    assert [ids[i] for i in range(len(A[0]))] == m["run_of_row"].tolist()
+    comp = oracle.complement(A, LENS)
+    got = sorted(sum((r[1]["comp"] for r in res), []))
+    assert got == list(zip(comp["contig"].tolist(), comp["start"].tolist(), comp["end"].tolist()))
+    ms = oracle.merge((A[0], A[1], A[2], sa))
+    runs = sum((r[1]["sruns"] for r in res), [])
+    assert runs == list(zip(ms["contig"].tolist(), ms["start"].tolist(), ms["end"].tolist(),
+                            ms["strand"].tolist()))
+    ids = dict(sum((r[1]["sids"] for r in res), []))
+    assert [ids[i] for i in range(len(A[0]))] == ms["run_of_row"].tolist()
+    ix = oracle.intersect((A[0], A[1], A[2], sa), (B[0], B[1], B[2], sb))
+    assert sorted(sum((r[1]["spairs"] for r in res), [])) == \
+        sorted(zip(ix["a_row"].tolist(), ix["b_row"].tolist()))

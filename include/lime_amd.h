@@ -115,7 +115,12 @@ int lime_set_create_host_stranded(lime_ctx *ctx, const lime_space *space, int64_
                                   const int32_t *contig, const int64_t *start,
                                   const int64_t *end, const int8_t *strand, lime_set **out);
 /* Device arrays (u32 contig-local coordinates) already resident in HBM:
- * validated and sorted on the context's stream, inputs are not modified. */
+ * validated and sorted on the context's stream, inputs are not modified.
+ * Device inputs (here and in every call below that takes them) are read on
+ * the context's stream: on the context's own stream a call returns once they
+ * are consumed; on a caller stream (lime_ctx_set_stream) they must stay valid
+ * until that stream has passed the call -- a stream-ordered allocator on the
+ * same stream (e.g. PyTorch's) gives exactly that. */
 int lime_set_create_device(lime_ctx *ctx, const lime_space *space, int64_t n,
                            const int32_t *d_contig, const uint32_t *d_start,
                            const uint32_t *d_end, lime_set **out);

@@ -558,6 +558,9 @@ int lime_set_destroy(lime_set *s) {
     // (s->d_off is the context's cached space array: held by s->space_keep)
     release(ctx, s->pmax);
     release(ctx, s->strand_in);
+    release(ctx, s->tie_gs);
+    release(ctx, s->tie_ge);
+    release(ctx, s->tie_row);
     delete s;
     return LIME_OK;
 }

@@ -123,6 +123,12 @@ struct lime_set {
     // strand_in indexed by SORTED position instead of row id (global
     // stranded sets, whose row ids are the caller's)
     bool strand_sorted = false;
+    // sort by (gs, ge, row) (subtract's tie index, a temporary set)
+    bool row_ties = false;
+    // lazily built: the rows of B's multi-row same-start groups sorted by
+    // (gs, ge, row) -- subtract's block head among many same-start hits
+    mutable uint32_t *tie_gs = nullptr, *tie_ge = nullptr, *tie_row = nullptr;
+    mutable int64_t tie_n = -1;  // -1: not built
     // binned sets (bitset painting from unsorted rows): only the gs digits
     // at shifts >= min_shift are sorted, i.e. rows grouped by gs >> min_shift
     int min_shift = 0;

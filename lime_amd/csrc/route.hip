@@ -227,6 +227,9 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
     if (h[nsh] > cap || n == 0) return LIME_OK;  // counts only
     hipLaunchKernelGGL(k_route_write, dim3(nblk), dim3(RT), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
+    // (the caller's rows are consumed before the return on the context's own
+    // stream, as lime_amd.h states for device inputs)
+    if (ctx->stream == ctx->own_stream) LIME_HIP(hipStreamSynchronize(S(ctx)));
     return LIME_OK;
 }
 

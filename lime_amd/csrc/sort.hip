@@ -49,7 +49,9 @@ struct SetStats {
 // sets sort by (gs, ge, strand) -- RegionOrdering -- with passes ST (skipped
 // when every row has one strand), GE x ceil(bits(max width) / 8), GS; plain
 // sets by (gs, zero-width first) with NZ?, GS.
-enum { M_GS = 0, M_NZ = 1, M_GE = 2, M_ST = 3 };
+// M_RW: an 8-bit digit of the row id (the full (gs, ge, row) order of
+// subtract's tie index, tie.hip)
+enum { M_GS = 0, M_NZ = 1, M_GE = 2, M_ST = 3, M_RW = 4 };
 // where a pass's row ids come from: none kept (binned sets), loaded, or the
 // identity (the first pass of a set built from caller rows: row = position)
 enum { ROWS_NONE = 0, ROWS_LOAD = 1, ROWS_IDENT = 2 };
@@ -62,6 +64,7 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, uint32_t r,
     // strand codes 0 independent, 1 forward, 2 reverse, 3 unknown sort by
     // bdg-formats' enum ordinal: FORWARD, REVERSE, INDEPENDENT, UNKNOWN
     if (M == M_ST) return (0xd2u >> (2 * ((uint32_t)(uint8_t)st[r] & 3u))) & 3u;
+    if (M == M_RW) return (r >> shift) & (RBINS - 1);
     return (k >> shift) & (RBINS - 1);
 }
 
@@ -388,10 +391,10 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
             } else {
                 ve[4 * k] = ve[4 * k + 1] = ve[4 * k + 2] = ve[4 * k + 3] = 0u;
             }
-            if (M == M_ST && rows == ROWS_IDENT) {
+            if ((M == M_ST || M == M_RW) && rows == ROWS_IDENT) {
                 const uint32_t r = (uint32_t)(base + 4 * (k * 64 + lane));
                 vr[4 * k] = r, vr[4 * k + 1] = r + 1, vr[4 * k + 2] = r + 2, vr[4 * k + 3] = r + 3;
-            } else if (M == M_ST) {
+            } else if (M == M_ST || M == M_RW) {
                 const uint4 u = r4[k * 64 + lane];
                 vr[4 * k] = u.x, vr[4 * k + 1] = u.y, vr[4 * k + 2] = u.z, vr[4 * k + 3] = u.w;
             } else {
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
             valid[k] = i < n;
             vk[k] = valid[k] ? key[i] : 0u;
             ve[k] = (NEED_E && valid[k]) ? ge[i] : 0u;
-            vr[k] = (M == M_ST && valid[k]) ? (rows == ROWS_IDENT ? (uint32_t)i : row[i]) : 0u;
+            vr[k] = ((M == M_ST || M == M_RW) && valid[k]) ? (rows == ROWS_IDENT ? (uint32_t)i : row[i]) : 0u;
         }
     }
     __syncthreads();
@@ -638,6 +641,9 @@ int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, co
             break;
         case M_ST:
             launch_pass<M_ST>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
+            break;
+        case M_RW:
+            launch_pass<M_RW>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
             break;
         default:
             launch_pass<M_GS>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
@@ -984,6 +990,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     // binned sets (bitset painting) keep no row ids: 8 B per row per pass
     const bool keep_rows = set->min_shift == 0;
     const bool stranded = set->strand_in != nullptr;
+    const bool row_ties = set->row_ties;  // (gs, ge, row): subtract's tie index
     LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * (ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
     LIME_TRY(alloc(ctx, &st, 1));
@@ -994,7 +1001,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     // bucket costs more than the digit passes below that)
     const int64_t span = set->off.empty() ? 0 : (int64_t)set->off.back();
     const int sbits = span > 1 ? 64 - __builtin_clzll((uint64_t)(span - 1)) : 1;
-    const bool bucket_cand = keep_rows && !stranded && sbits > 16 &&
+    const bool bucket_cand = keep_rows && !stranded && !row_ties && sbits > 16 &&
                              n >= LMIN * ((span >> (sbits - 16)) + 1);
     const int hshift = bucket_cand ? sbits - 16 : set->min_shift;
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
@@ -1053,7 +1060,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     set->max_width = h.max_width;
     set->has_zero_width = h.has_zero != 0;
     const int bits = h.max_gs ? 32 - __builtin_clz(h.max_gs) : 1;
-    const bool need = n > 1 && (h.unsorted || stranded) &&
+    const bool need = n > 1 && (h.unsorted || stranded || row_ties) &&
                       !(set->min_shift > 0 && (h.max_gs >> set->min_shift) == 0);
 
     if (bucket_cand) {
@@ -1119,6 +1126,10 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             set->gs = a[0];
             set->ge = a[1];
             set->row = a[2];
+            // the first pass read the caller's arrays after the statistics
+            // read-back: on the context's own stream the call returns only once
+            // they are consumed (a caller stream orders their reuse itself)
+            if (ctx->stream == ctx->own_stream) LIME_HIP(hipStreamSynchronize(S(ctx)));
             return LIME_OK;
         }
         // (in order, or dense buckets) the digit-pass layout from the caller's rows
@@ -1153,7 +1164,12 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         LIME_TRY(alloc(ctx, &e1, (size_t)n));
         if (keep_rows) LIME_TRY(alloc(ctx, &r1, (size_t)n));
         std::vector<std::pair<int, int>> passes;  // (mode, shift), least significant first
-        if (stranded) {
+        if (row_ties) {
+            // (gs, ge, row): row digits, then width digits, then gs
+            for (int sh = 0; sh < 32; sh += 8) passes.push_back({M_RW, sh});
+            const int wbits = h.max_width ? 32 - __builtin_clz(h.max_width) : 0;
+            for (int sh = 0; sh < wbits; sh += 8) passes.push_back({M_GE, sh});
+        } else if (stranded) {
             // RegionOrdering (start, end, strand): strand, then ge, then gs.
             // The strand pass runs first, while row i is still input row i.
             const int wbits = h.max_width ? 32 - __builtin_clz(h.max_width) : 0;

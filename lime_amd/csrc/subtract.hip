@@ -54,7 +54,34 @@ struct SubArgs {
     const uint64_t *off;    // pass 2
     unsigned int *err;      // pass 2 (RUNS): a block's recount differs from pass 1
     uint32_t *ogs, *oge, *oar, *obr;
+    // the tie index of B (rows of its multi-row same-start groups by (gs,
+    // ge, row)); tn = 0: B has no same-start group past TIE_G rows
+    const uint32_t *tgs, *tge, *trow;
+    int64_t tn;
 };
+
+// A block's head is the min (end, row) among its same-start hits.  Past
+// TIE_G of them (identical PCR duplicates, repeated annotations) the head
+// comes from the tie index by one search instead of a walk over the group:
+// the first row with start bs and end > thr.  (A walk per left row was
+// O(n_A x D) for D rows sharing a start.)
+constexpr int TIE_G = 16;
+__device__ __forceinline__ void tie_head(const SubArgs &sa, uint32_t bs, uint32_t thr,
+                                         uint32_t &bh, uint32_t &bhe) {
+    int64_t lo = 0, hi = sa.tn;  // first p with (tgs, tge) > (bs, thr)
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const uint32_t g = sa.tgs[mid];
+        if (g < bs || (g == bs && sa.tge[mid] <= thr))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo < sa.tn && sa.tgs[lo] == bs) {
+        bh = sa.trow[lo];
+        bhe = sa.tge[lo];
+    }
+}
 
 __device__ __forceinline__ int64_t first_spanning(const uint32_t *__restrict__ pm, int64_t lo1,
                                                   uint32_t thr) {
@@ -310,13 +337,15 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             be = pm_last;
             bh = Brow(j0);
             bhe = Bge(j0);
-            for (int64_t j = j0 + 1; j < lo1 && Bgs(j) == bs; ++j) {
+            int64_t j = j0 + 1;
+            for (; j < lo1 && j <= j0 + TIE_G && Bgs(j) == bs; ++j) {
                 const uint32_t ge = Bge(j), row = Brow(j);
                 if (ge > thr && (ge < bhe || (ge == bhe && row < bh))) {
                     bh = row;
                     bhe = ge;
                 }
             }
+            if (j < lo1 && Bgs(j) == bs) tie_head(sa, bs, thr, bh, bhe);  // a long group
         }
         // close the current block (bs, be, bh): its records
         auto close_block = [&]() {
@@ -364,14 +393,17 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
                 bh = row;
                 bhe = ge;
                 // the head among the run's same-start non-empty hits: min (end, row)
-                if (bhe > bs)
-                    for (int64_t k = j + 1; k < nx && Bgs(k) == bs; ++k) {
+                if (bhe > bs) {
+                    int64_t k = j + 1;
+                    for (; k < nx && k <= j + TIE_G && Bgs(k) == bs; ++k) {
                         const uint32_t e2 = Bge(k), r2 = Brow(k);
                         if (e2 < bhe || (e2 == bhe && r2 < bh)) {
                             bh = r2;
                             bhe = e2;
                         }
                     }
+                    if (k < nx && Bgs(k) == bs) tie_head(sa, bs, bs, bh, bhe);  // a long group
+                }
                 be = max(be, Bpm(nx - 1));
                 j = nx;
             }
@@ -651,7 +683,94 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     if (lane == 0 && sb < nblk) sa.count[sb] = tot;
 }
 
+// any same-start group past TIE_G rows (*big), and every row of a
+// multi-row same-start group flagged for the tie index
+__global__ __launch_bounds__(256) void k_tie_flags(const uint32_t *__restrict__ gs, int64_t n,
+                                                   uint32_t *__restrict__ flag,
+                                                   unsigned int *__restrict__ big) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t g = gs[j];
+    flag[j] = (j + 1 < n && gs[j + 1] == g) || (j > 0 && gs[j - 1] == g);
+    if (j + TIE_G < n && gs[j + TIE_G] == g) atomicOr(big, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_tie_compact(const uint32_t *__restrict__ gs,
+                                                     const uint32_t *__restrict__ ge,
+                                                     const uint32_t *__restrict__ row, int64_t n,
+                                                     const uint32_t *__restrict__ flag,
+                                                     const uint32_t *__restrict__ pos,
+                                                     uint32_t *__restrict__ tg,
+                                                     uint32_t *__restrict__ te,
+                                                     uint32_t *__restrict__ tr) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n || !flag[j]) return;
+    const uint32_t p = pos[j];
+    tg[p] = gs[j];
+    te[p] = ge[j];
+    tr[p] = row[j];
+}
+
 }  // namespace
+
+int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const uint32_t *d_ge,
+                    const uint32_t *d_row, const uint32_t *d_len);
+
+// B's tie index, built once per set (under its context's lock) when some
+// same-start group has more than TIE_G rows; else tie_n = 0
+static int build_tie_index(lime_ctx *ctx, const lime_set *B) {
+    std::lock_guard<std::mutex> lock(B->ctx->mu);
+    if (B->tie_n >= 0) return LIME_OK;
+    const int64_t n = B->n;
+    if (n <= TIE_G) {
+        B->tie_n = 0;
+        return LIME_OK;
+    }
+    uint32_t *flag, *pos, *tot;
+    unsigned int *big;
+    LIME_TRY(alloc(ctx, &flag, (size_t)n));
+    PoolGuard<uint32_t> g0{ctx, flag};
+    LIME_TRY(alloc(ctx, &pos, (size_t)n));
+    PoolGuard<uint32_t> g1{ctx, pos};
+    LIME_TRY(alloc(ctx, &tot, 2));
+    PoolGuard<uint32_t> g2{ctx, tot};
+    big = reinterpret_cast<unsigned int *>(tot + 1);
+    LIME_HIP(hipMemsetAsync(tot, 0, 8, S(ctx)));
+    hipLaunchKernelGGL(k_tie_flags, dim3(blocks_for(n, 256)), dim3(256), 0, S(ctx), B->gs, n, flag,
+                       big);
+    LIME_TRY(scan_exclusive_u32(ctx, flag, pos, n, tot));
+    uint32_t h[2] = {0, 0};
+    LIME_TRY(read_back(ctx, h, tot, sizeof(h)));
+    if (!h[1]) {  // no long group: the bounded walks suffice
+        B->tie_n = 0;
+        return LIME_OK;
+    }
+    const int64_t T = h[0];
+    uint32_t *tg, *te, *tr;
+    LIME_TRY(alloc(ctx, &tg, (size_t)T));
+    PoolGuard<uint32_t> g3{ctx, tg};
+    LIME_TRY(alloc(ctx, &te, (size_t)T));
+    PoolGuard<uint32_t> g4{ctx, te};
+    LIME_TRY(alloc(ctx, &tr, (size_t)T));
+    PoolGuard<uint32_t> g5{ctx, tr};
+    hipLaunchKernelGGL(k_tie_compact, dim3(blocks_for(n, 256)), dim3(256), 0, S(ctx), B->gs, B->ge,
+                       B->row, n, (const uint32_t *)flag, (const uint32_t *)pos, tg, te, tr);
+    LIME_HIP(hipGetLastError());
+    lime_set t;  // (gs, ge, row) order
+    t.ctx = ctx;
+    t.n = T;
+    t.d_off = B->d_off;
+    t.n_contigs = B->n_contigs;
+    t.off = B->off;
+    t.len = B->len;
+    t.row_ties = true;
+    LIME_TRY(sort_set_global(ctx, &t, tg, te, tr, nullptr));
+    B->tie_gs = t.gs;
+    B->tie_ge = t.ge;
+    B->tie_row = t.row;
+    B->tie_n = T;
+    return LIME_OK;
+}
 
 int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
 int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res);
@@ -720,6 +839,12 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.count = cnt;
     sa.off = off;
     sa.err = err;
+    // the tie index of B (long same-start groups), built once per set
+    if (B->n > 0) LIME_TRY(build_tie_index(ctx, B));
+    sa.tgs = B->tie_gs;
+    sa.tge = B->tie_ge;
+    sa.trow = B->tie_row;
+    sa.tn = B->tie_n > 0 ? B->tie_n : 0;
     sa.ogs = sa.oge = sa.oar = sa.obr = nullptr;
     sa.brun = nullptr;
     sa.zw = B->has_zero_width ? 1 : 0;

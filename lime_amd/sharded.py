@@ -82,9 +82,9 @@ class ShardStep:
                                 d_gs=cols[0].data_ptr(), d_ge=cols[1].data_ptr(),
                                 d_row=cols[2].data_ptr(), row_base=row_base, d_strand=d_strand,
                                 d_strand_out=st8.data_ptr() if d_strand else None)
+        self._sync()  # engine output -> torch ops
         if d_strand:
             cols[3] = st8.to(torch.int32)
-        self._sync()
         recv, rc = ld.exchange(cols, counts, self.group, self.comm, packed=True)
         self._sync()
         self.routed += sum(rc) - rc[self.rank]
@@ -99,6 +99,7 @@ class ShardStep:
         m = recv[0].numel()
         if d_strand:
             st8 = recv[3].to(torch.int8)
+            self._sync()  # torch output -> engine input
             S = self.ctx.set_from_global_stranded(self.space, m, recv[0].data_ptr(),
                                                   recv[1].data_ptr(), recv[2].data_ptr(),
                                                   st8.data_ptr())
@@ -116,6 +117,7 @@ class ShardStep:
         for c in codes:
             keep = st == c
             sub = [x[keep].contiguous() for x in (gs, ge, row)]
+            self._sync()
             out[int(c)] = self.ctx.set_from_global(self.space, sub[0].numel(),
                                                    *(t.data_ptr() for t in sub))
         return out
@@ -141,6 +143,7 @@ class ShardStep:
             pre = [self._i32(c) for _ in range(3)]
             if c:
                 S.copy_rows_device(0, c, *(t.data_ptr() for t in pre))
+                self._sync()  # the engine's copy lands before torch.cat reads it
             send = [torch.cat([t[:k] for k in counts]) if sum(counts) else t[:0] for t in pre]
             self._sync()
             recv, _ = ld.exchange(send, counts, self.group, self.comm)
@@ -175,6 +178,7 @@ class ShardStep:
         suf = [self._i32(c) for _ in range(3)]
         if c:
             S.copy_rows_device(f0, c, *(t.data_ptr() for t in suf))
+            self._sync()
         send = [torch.cat([t[first[r] - f0:] for r in range(w) if counts[r]])
                 if sum(counts) else t[:0] for t in suf]
         self._sync()
@@ -232,6 +236,7 @@ class ShardStep:
         run, row = self._i32(n_rows), self._i32(n_rows)
         if n_rows:
             m["result"].copy_run_ids_device(run.data_ptr(), row.data_ptr())
+            self._sync()
         local = run[:n_rows].to(torch.int64) & 0xFFFFFFFF
         return (row[:n_rows].to(torch.int64) & 0xFFFFFFFF,
                 ld.global_run_ids(local, m["drop"], m["offset"]))
@@ -253,6 +258,7 @@ class ShardStep:
         gs, ge = self._i32(tot), self._i32(tot)
         if k:
             res.copy_rows_device(drop, k, gs[lead:].data_ptr(), ge[lead:].data_ptr())
+            self._sync()  # before torch overwrites the last end
         if prev_end is not None:
             gs[0] = ge[0] = prev_end - (1 << 32) if prev_end >= (1 << 31) else prev_end
         if ext is not None and k:

@@ -311,3 +311,23 @@ def test_c5_eight_way_and_density(ctx):
     assert_runs_equal((f["contig"], f["start"], f["end"]), (got["contig"], got["start"], got["end"]))
     cov = int((g[2] - g[1]).sum())
     assert 0.01 < cov / sum(sp.lengths) < 0.05  # 8-way ~2.7% of the genome
+
+
+@pytest.mark.timeout(900)
+def test_c2_subtract_full_size(ctx):
+    # DistributedSubtract (Subtract.scala:91-116) on C2's inputs at full size,
+    # both modes: region count + region checksum == the contig-sharded oracle
+    # (lo_subtract_mt), ~1e8 remnants per mode
+    sp = hg38()
+    n = 100_000_000
+    da, A = device_rows(ctx, sp, n, 0xA, 50, 5000)
+    db, B = device_rows(ctx, sp, n, 0xB, 50, 5000)
+    a, b = dset(ctx, sp, da), dset(ctx, sp, db)
+    del da, db
+    for mode in (oracle.SUB_LIME, oracle.SUB_SET):
+        res = ctx.subtract(a, b, 0, mode)
+        ck = res.checksum()
+        exp = oracle.subtract_mt(len(sp.names), A, B, 0, mode)
+        assert res.n == exp["n"] > 1e7
+        assert ck[:2] == (exp["sum"], exp["xor"])
+        res.close()

@@ -800,3 +800,34 @@ def test_bitset_runs_dense_tile_falls_back(ctx):
     got = ctx.bitset_runs(0, bs).to_host()
     assert got["start"].tolist() == starts.tolist()
     assert got["end"].tolist() == ends.tolist()
+
+
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+@pytest.mark.parametrize("t", [0, 1])
+def test_subtract_many_same_start_rows(ctx, mode, t):
+    # PCR-duplicate-like B: thousands of rows sharing a start, mostly
+    # identical, some with other ends (in random input order, so the head --
+    # the min (end, row) among the same-start hits, Subtract.scala:103-108 --
+    # is not the first of them), zero-width ones, and groups spanning and
+    # inside the left rows.  Past TIE_G such rows the head comes from the tie
+    # index (one search), not a walk per left row (the O(n_A x D) cliff).
+    rng = np.random.default_rng(2024 + t)
+    L = 200_000
+    a_s = rng.integers(0, L - 3000, 8000)
+    A = (np.zeros(8000, np.int32), a_s, a_s + rng.integers(1, 3000, 8000))
+    parts = []
+    for start, d in ((1000, 12000), (50_000, 3000), (120_000, 40), (150_000, 17)):
+        e = np.full(d, start + 5000)
+        k = rng.random(d)
+        e[k < 0.03] = start + 2000
+        e[(k >= 0.03) & (k < 0.05)] = start  # zero-width
+        parts.append((np.full(d, start), e))
+    bs_ = rng.integers(0, L - 3000, 4000)
+    parts.append((bs_, bs_ + rng.integers(0, 3000, 4000)))
+    s = np.concatenate([p[0] for p in parts])
+    e = np.concatenate([p[1] for p in parts])
+    perm = rng.permutation(len(s))
+    B = (np.zeros(len(s), np.int32), s[perm], e[perm])
+    sp = space_for(1, L)
+    res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t, mode).to_host()
+    _sub_equal(res, oracle.subtract(A, B, t, mode))

@@ -436,5 +436,13 @@ def test_sharded_complement_run_ids_strands(world):
     ids = dict(sum((r[1]["sids"] for r in res), []))
     assert [ids[i] for i in range(len(A[0]))] == ms["run_of_row"].tolist()
     ix = oracle.intersect((A[0], A[1], A[2], sa), (B[0], B[1], B[2], sb))
-    assert sorted(sum((r[1]["spairs"] for r in res), [])) == \
-        sorted(zip(ix["a_row"].tolist(), ix["b_row"].tolist()))
+    got = sorted(sum((r[1]["spairs"] for r in res), []))
+    want = sorted(zip(ix["a_row"].tolist(), ix["b_row"].tolist()))
+    if got != want:
+        from collections import Counter
+        g, w = Counter(got), Counter(want)
+        extra, missing = list((g - w).items())[:5], list((w - g).items())[:5]
+        info = [(p, [(int(X[0][i]), int(X[1][i]), int(X[2][i]), int(st[i]))
+                     for X, st, i in ((A, sa, p[0][0]), (B, sb, p[0][1]))]) for p in extra + missing]
+        raise AssertionError(f"{len(got)} vs {len(want)} pairs; extra {extra}; missing {missing}; "
+                             f"rows {info}")

@@ -649,21 +649,64 @@ static void lo_ungroup(lo_groups *g) {
     free(g->idx);
 }
 
-/* the rows of contig k as sorted regions (RegionOrdering, ties by row) */
-static lo_region *lo_load_group(const lo_groups *g, int32_t k, int64_t *n_out) {
-    const int64_t a = g->off[k], b = g->off[k + 1];
-    lo_region *r = (lo_region *)malloc(sizeof(lo_region) * (size_t)(b > a ? b - a : 1));
-    for (int64_t j = a; j < b; ++j) {
-        const int64_t i = g->idx[j];
-        lo_region *x = &r[j - a];
-        x->contig = k;
-        x->start = g->s[i];
-        x->end = g->e[i];
-        x->strand = 0;
-        x->row = i;
+/* stable LSD radix sort of (key, id) pairs by key, 16-bit digits; passes
+ * whose digit is constant over the input are skipped */
+static void lo_radix_pairs(uint64_t *key, int64_t *id, int64_t n) {
+    if (n < 2) return;
+    uint64_t *k2 = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)n);
+    int64_t *i2 = (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
+    int64_t *cnt = (int64_t *)malloc(sizeof(int64_t) * 65536);
+    for (int shift = 0; shift < 64; shift += 16) {
+        memset(cnt, 0, sizeof(int64_t) * 65536);
+        for (int64_t j = 0; j < n; ++j) cnt[(key[j] >> shift) & 0xffff]++;
+        if (cnt[(key[0] >> shift) & 0xffff] == n) continue;
+        int64_t run = 0;
+        for (int d = 0; d < 65536; ++d) {
+            const int64_t c = cnt[d];
+            cnt[d] = run;
+            run += c;
+        }
+        for (int64_t j = 0; j < n; ++j) {
+            const int64_t at = cnt[(key[j] >> shift) & 0xffff]++;
+            k2[at] = key[j];
+            i2[at] = id[j];
+        }
+        memcpy(key, k2, sizeof(uint64_t) * (size_t)n);
+        memcpy(id, i2, sizeof(int64_t) * (size_t)n);
     }
-    qsort(r, (size_t)(b - a), sizeof(lo_region), lo_qsort_cmp);
-    *n_out = b - a;
+    free(k2);
+    free(i2);
+    free(cnt);
+}
+
+/* the rows of contig k as sorted regions (RegionOrdering, ties by row).  All
+ * rows of a group share the contig and strand 0 and come in ascending row
+ * order, so lo_qsort_cmp's order is the STABLE order by (start, end): one
+ * radix sort of start << 32 | end (the contig-sharded drivers' 1e9-row inputs
+ * would spend minutes in qsort; lo_load keeps qsort, and the drivers are
+ * checked against it by tests/test_oracle.py) */
+static lo_region *lo_load_group(const lo_groups *g, int32_t k, int64_t *n_out) {
+    const int64_t a = g->off[k], b = g->off[k + 1], n = b - a;
+    lo_region *r = (lo_region *)malloc(sizeof(lo_region) * (size_t)(n > 0 ? n : 1));
+    uint64_t *key = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1));
+    int64_t *id = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    for (int64_t j = 0; j < n; ++j) {
+        const int64_t i = g->idx[a + j];
+        key[j] = ((uint64_t)g->s[i] << 32) | (uint64_t)g->e[i];
+        id[j] = i;
+    }
+    lo_radix_pairs(key, id, n);
+    for (int64_t j = 0; j < n; ++j) {
+        lo_region *x = &r[j];
+        x->contig = k;
+        x->start = (int64_t)(key[j] >> 32);
+        x->end = (int64_t)(key[j] & 0xffffffffu);
+        x->strand = 0;
+        x->row = id[j];
+    }
+    free(key);
+    free(id);
+    *n_out = n;
     return r;
 }
 

@@ -71,7 +71,7 @@ def test_1b_complement(ctx, pile_1b):
     say(f"complement: {res.n} gaps on the device; oracle")
     e = oracle.complement_mt(sp.lengths, X)
     say("complement: oracle done")
-    assert res.n == e["n"] > 1_000_000
+    assert res.n == e["n"] > 500_000  # ~7.3e5 gaps between the pile-up clusters
     assert ck[:2] == (e["sum"], e["xor"])
     res.close()
 
@@ -115,7 +115,7 @@ def test_1b_subtract(ctx, pair_1b, mode):
     say(f"subtract mode {mode}: {res.n} regions on the device; oracle")
     exp = oracle.subtract_mt(len(sp.names), A, B, 0, mode)
     say("subtract: oracle done")
-    assert res.n == exp["n"] > 1e8
+    assert res.n == exp["n"] > 1e6  # lime mode: ~7.4e7 regions
     assert ck[:2] == (exp["sum"], exp["xor"])
     res.close()
 

@@ -317,7 +317,8 @@ def test_c5_eight_way_and_density(ctx):
 def test_c2_subtract_full_size(ctx):
     # DistributedSubtract (Subtract.scala:91-116) on C2's inputs at full size,
     # both modes: region count + region checksum == the contig-sharded oracle
-    # (lo_subtract_mt), ~1e8 remnants per mode
+    # (lo_subtract_mt).  At C2's depth (~160x coverage by B) only a handful
+    # of A's bases escape B: 16 remnants per mode on the GPU box
     sp = hg38()
     n = 100_000_000
     da, A = device_rows(ctx, sp, n, 0xA, 50, 5000)
@@ -328,6 +329,6 @@ def test_c2_subtract_full_size(ctx):
         res = ctx.subtract(a, b, 0, mode)
         ck = res.checksum()
         exp = oracle.subtract_mt(len(sp.names), A, B, 0, mode)
-        assert res.n == exp["n"] > 1e7
+        assert res.n == exp["n"] > 0
         assert ck[:2] == (exp["sum"], exp["xor"])
         res.close()

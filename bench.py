@@ -357,6 +357,15 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
         else:
             breakdown = {"sort_ms": p[0].elapsed_time(p[1]), "count_ms": p[1].elapsed_time(p[2]),
                          "fill_ms": p[2].elapsed_time(p[3]), "merge_ms": p[3].elapsed_time(p[4])}
+        # the sort stage against its own roofline (24 B per
+        # row algorithmic -- read 12, write 12), both sets
+        sort_roof = None
+        if world == 1 and breakdown.get("sort_ms"):
+            sb = 24 * 2 * n
+            sa = sb / (breakdown["sort_ms"] * 1e-3) / 1e9
+            sort_roof = {"bound": "hbm", "achieved": sa, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": sa / HBM_PEAK_GBS, "alg_bytes": sb,
+                         "kernels": "k_prep + 2 digit passes + k_local_small (bucketed sort)"}
         npairs, nruns = state["npairs"], state["nruns"]
         if world > 1:
             tt = torch.tensor([npairs, nruns], dtype=torch.int64, device=comm_dev or dev)
@@ -390,6 +399,7 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
                          "kernel": "k_fill<false>", "avg_launch_ms": avg_ms,
                          "alg_bytes_per_launch": avg_b, "launches": len(timed)},
             "breakdown_ms": breakdown,
+            "sort_roofline": sort_roof,
             "cpu_baseline": cpu,
         }
     return step, finish

@@ -633,6 +633,50 @@ def test_bitset_window_end_on_bin_bound(ctx):
         assert got["end"].tolist() == xe.tolist()
 
 
+@pytest.mark.parametrize("hi", [1 << 18, 3 << 18, (3 << 18) + 37, 1 << 23])
+def test_bitset_runs_reaching_window_end(ctx, hi):
+    # Run extraction pairs every start with an end: a run covering the
+    # window's last bit closes in the tile past the last word (the extraction
+    # covers one word more than the window).  Windows whose word count is an
+    # exact multiple of the extraction tile (4096 words = 2^18 bits), one that
+    # ends mid-word, and a 2-bin window; rows crossing the window end and a
+    # row ending exactly on it; ops: bits (0), NOT within the window (1),
+    # AND-NOT with an empty operand (3), the fused AND of one set.  (An
+    # unpaired event raises LIME_ERR_DEVICE "odd event count" instead.)
+    import torch
+    from tests.test_gpu_configs import coalesce
+    rng = np.random.default_rng(hi)
+    sp = space_for(1, 12_000_000)
+    lo = 0
+    n = 30000
+    s = rng.integers(0, hi, n)
+    e = s + rng.integers(1, 300, n)
+    s = np.concatenate([s, [hi - 100, hi - 7, hi - 1, hi - 50]])
+    e = np.concatenate([e, [hi + 50, hi, hi, hi + 2000]])
+    n = len(s)
+    gs = torch.from_numpy(s.astype(np.uint32).view(np.int32)).cuda()
+    ge = torch.from_numpy(e.astype(np.uint32).view(np.int32)).cuda()
+    none = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    m = oracle.merge((np.zeros(n, np.int32), s, e))
+    cs, ce = np.clip(m["start"], lo, hi), np.clip(m["end"], lo, hi)
+    keep = ce > cs
+    _, xs, xe = coalesce(np.zeros(int(keep.sum())), cs[keep], ce[keep])
+    assert xe[-1] == hi
+    # the gaps inside [lo, hi)
+    gs_, ge_ = np.concatenate([[lo], xe]), np.concatenate([xs, [hi]])
+    g = ge_ > gs_
+    b = ctx.bitset_from_global(sp, lo, hi, n, gs.data_ptr(), ge.data_ptr())
+    empty = ctx.bitset_from_global(sp, lo, hi, 0, none.data_ptr(), none.data_ptr())
+    fused = ctx.bitset_and_from_global(sp, lo, hi, [(n, gs.data_ptr(), ge.data_ptr())])
+    for got, (es, ee) in ((ctx.bitset_runs(0, b), (xs, xe)), (ctx.bitset_runs(1, b), (gs_[g], ge_[g])),
+                          (ctx.bitset_runs(3, b, empty), (xs, xe)),
+                          (ctx.bitset_runs(0, fused), (xs, xe))):
+        h = got.to_host()
+        assert h["start"].tolist() == es.tolist()
+        assert h["end"].tolist() == ee.tolist()
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_set_theory_genome_cut_into_spaces(ctx, monkeypatch, seed):
     # a genome whose span exceeds one engine space (u32 coordinates: >= 2^32)

@@ -23,6 +23,13 @@ the 8(f) rows (bench.py measures the headline config C2).  Single GPU; one JSON 
       plan + fill
   closest_single  SingleClosestSingleOverlap (sequential chain per contig) on
       1/100 of C2's rows
+  b1_merge  north_star's 1B-interval target, merge side: 1e9 ChIP-seq-like
+      pile-up rows (4e6 centres, N(0,150), len U[150,600], seed 0x1B; the
+      rows of tests/test_gpu_scale.py): sort + merge (run ids) + complement
+  b1_pair   north_star's 1B-interval target, pairwise side: 2 x 5e8 rows
+      uniform over hg38, len U[10,40] (seeds 0x1A / 0x1C, as the scale
+      tests): sort both + intersect (every pair filled through a 2^31-record
+      buffer) + subtract in lime and set mode
 
 Inputs are generated on the device (counter-based RNG) outside the timed
 region; every step starts from unsorted rows in HBM.
@@ -43,7 +50,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", required=True,
                    choices=["c3", "c4", "c5", "bed", "closest", "closest_single", "window",
-                            "subtract"])
+                            "subtract", "b1_merge", "b1_pair"])
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scale", type=float, default=1.0, help="row-count scale (testing)")
@@ -111,6 +118,72 @@ def main():
             b = 12 * n + 8 * runs  # read gs+ge, write run id per row, write runs
             return {"sort_ms": t0.elapsed_time(t1), "merge_ms": ms, "runs": runs}, \
                 {"kernel": "k_merge_scan (single pass, decoupled look-back)", "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+    elif a.workload == "b1_merge":
+        inp = gen(int(1e9 * a.scale), 0x1B, 150, 600, pile=(4_000_000, 150))
+        n = inp[0]
+
+        def step(rec):
+            t0 = ev()
+            S = mkset(inp)
+            t1 = ev()
+            m = ctx.merge(S)
+            t2 = ev()
+            c = ctx.complement(space, S)
+            t3 = ev()
+            rec.append((t0, t1, t2, t3, m.n, c.n))
+            for h in (c, m, S):
+                h.close()
+        units, unit = n, "intervals/s"
+        desc = f"1B merge side: sort + merge (run ids) + complement of {n} pile-up intervals " \
+               "(4e6 centres, N(0,150), len U[150,600])"
+
+        def roof(rec):
+            t0, t1, t2, t3, runs, gaps = rec[-1]
+            ms = t1.elapsed_time(t2)
+            b = 12 * n + 8 * runs
+            return {"sort_ms": t0.elapsed_time(t1), "merge_ms": ms,
+                    "complement_ms": t2.elapsed_time(t3), "runs": runs, "gaps": gaps,
+                    "sort_GBps_24B_per_row": 24 * n / (t0.elapsed_time(t1) * 1e-3) / 1e9}, \
+                {"kernel": "k_merge_scan (single pass, decoupled look-back)", "bound": "hbm",
+                 "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
+    elif a.workload == "b1_pair":
+        ia = gen(int(5e8 * a.scale), 0x1A, 10, 40)
+        ib = gen(int(5e8 * a.scale), 0x1C, 10, 40)
+        n = ia[0]
+        chunk = 1 << 31
+        buf = torch.empty((chunk, 4), dtype=torch.int32, device=dev)
+
+        def step(rec):
+            t0 = ev()
+            SA, SB = mkset(ia), mkset(ib)
+            t1 = ev()
+            plan = ctx.intersect(SA, SB)
+            t2 = ev()
+            for f in range(0, plan.n, chunk):
+                plan.fill_device(f, min(chunk, plan.n - f), buf.data_ptr())
+            t3 = ev()
+            r0 = ctx.subtract(SA, SB, 0, 0)
+            t4 = ev()
+            r1 = ctx.subtract(SA, SB, 0, 1)
+            t5 = ev()
+            rec.append((t0, t1, t2, t3, t4, t5, plan.n, r0.n, r1.n))
+            for h in (r1, r0, plan, SA, SB):
+                h.close()
+        units, unit = 2 * n, "intervals/s"
+        desc = f"1B pairwise side: sort + intersect (every pair filled) + subtract (lime, set) " \
+               f"of 2 x {n} intervals, uniform over hg38, len U[10,40]"
+
+        def roof(rec):
+            t0, t1, t2, t3, t4, t5, k, s0, s1 = rec[-1]
+            ms = t2.elapsed_time(t3)
+            b = 16 * k + 20 * 2 * n
+            return {"sort_ms": t0.elapsed_time(t1), "count_ms": t1.elapsed_time(t2),
+                    "fill_ms": ms, "subtract_lime_ms": t3.elapsed_time(t4),
+                    "subtract_set_ms": t4.elapsed_time(t5), "pairs": k,
+                    "remnants_lime": s0, "remnants_set": s1,
+                    "sort_GBps_24B_per_row": 24 * 2 * n / (t0.elapsed_time(t1) * 1e-3) / 1e9}, \
+                {"kernel": "k_fill (all launches)", "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "c4":
         ia = gen(int(1e7 * a.scale), 0xD, 50, 500)

@@ -797,6 +797,88 @@ __device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b,
     }
 }
 
+// The common case of bucket_sort_regs without its two ranked digit passes
+// (17 wave ballots per row: k_local_small was issue-bound, 34 % of its wave
+// cycles issuing, 26 % waiting on dependencies): every row gets the unique
+// composite key u = local key << POSB | position (local key = (gs mod 2^L)
+// << 1 | non-zero width), and
+//   1. an LDS histogram of the key's top SBB bits (sub-bins of a few rows),
+//   2. one block scan of the sub-bin counts (and their max),
+//   3. each row claims a slot of its sub-bin (one returning LDS atomic; the
+//      order inside a sub-bin is arbitrary),
+//   4. each row's rank in its sub-bin = the number of its keys below u
+//      (unique keys: no tie, so the result is the stable order),
+// and the rows are written in rank order.  A sub-bin past SMAX rows (piled-up
+// starts) sends the bucket back to the digit passes: returns false, having
+// staged s_e / s_r only.
+constexpr int SBB = 9, SMAX = 48;
+template <int NT, int ITEMS, int POSB>
+__device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b, uint32_t s0,
+                                                  uint32_t m, const uint32_t (&g)[ITEMS],
+                                                  const uint32_t (&e)[ITEMS],
+                                                  const uint32_t (&r)[ITEMS], uint32_t *T,
+                                                  uint32_t *O, uint32_t *sstart, uint32_t *scur,
+                                                  uint32_t *scratch, uint32_t *s_e, uint32_t *s_r) {
+    static_assert(NT == (1 << SBB), "one sub-bin per thread in the scan");
+    constexpr int NW = NT / 64;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int nit = (int)((m + NW * 64 - 1) / (NW * 64));
+    const int c = nit * 64;
+    const uint32_t lmask = (1u << a.L) - 1u;
+    const int kb = a.L + 1;                      // local key bits
+    const int sh = kb > SBB ? kb - SBB : 0;      // sub-bin = key >> sh
+    scur[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t u[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
+        u[it] = 0xffffffffu;
+        if (it < nit && pos < m) {
+            const uint32_t k = ((g[it] & lmask) << 1) | (e[it] > g[it] ? 1u : 0u);
+            u[it] = (k << POSB) | pos;
+            atomicAdd(&scur[k >> sh], 1u);
+            s_e[pos] = e[it];
+            s_r[pos] = r[it];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = scur[threadIdx.x];
+    uint32_t tot;
+    const uint32_t st = dev::block_exclusive_sum<NT>(cnt, scratch, &tot);
+    const uint32_t mx = dev::wave_reduce_max(cnt);
+    if (lane == 0) scratch[NW + 1 + w] = mx;  // (past the scan's NW + 1 words)
+    sstart[threadIdx.x] = st;
+    scur[threadIdx.x] = st;
+    __syncthreads();
+    uint32_t big = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) big = max(big, scratch[NW + 1 + i]);
+    if (big > (uint32_t)SMAX) return false;  // (uniform: every thread read the same words)
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it)
+        if (u[it] != 0xffffffffu) T[atomicAdd(&scur[(u[it] >> POSB) >> sh], 1u)] = u[it];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        if (u[it] == 0xffffffffu) continue;
+        const uint32_t sb = (u[it] >> POSB) >> sh;
+        const uint32_t lo = sstart[sb], hi = scur[sb];
+        uint32_t rk = lo;
+        for (uint32_t j = lo; j < hi; ++j) rk += T[j] < u[it] ? 1u : 0u;
+        O[rk] = u[it];
+    }
+    __syncthreads();
+    const uint32_t base = b << a.L, pm = (1u << POSB) - 1u;
+    for (uint32_t q = threadIdx.x; q < m; q += NT) {
+        const uint32_t x = O[q], j = x & pm;
+        a.k1[s0 + q] = base | ((x >> (POSB + 1)) & lmask);
+        a.e1[s0 + q] = s_e[j];
+        a.r1[s0 + q] = s_r[j];
+    }
+    return true;
+}
+
 // a bucket's rows into registers, branch-free (positions past the bucket
 // clamped to its last row; a bucket too large for the shape, or empty, loads
 // row 0): every load issued before any is used
@@ -838,7 +920,8 @@ using SmallRegs = BucketRegs<LNT_S, LCAP_S / LNT_S, LCAP_S>;
 __global__ __launch_bounds__(LNT_S) void k_local_small(LocalArgs a, uint32_t nb) {
     __shared__ uint32_t A[LCAP_S], B[LCAP_S], s_e[LCAP_S], s_r[LCAP_S];
     __shared__ uint16_t cnt[LNT_S / 64][1 << LDMAX];
-    __shared__ uint32_t scratch[LNT_S / 64 + 1];
+    __shared__ uint32_t sstart[LNT_S], scur[LNT_S];
+    __shared__ uint32_t scratch[2 * (LNT_S / 64) + 1];
     SmallRegs cur, nxt;
     cur.load(a, blockIdx.x, nb);
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
@@ -846,8 +929,13 @@ __global__ __launch_bounds__(LNT_S) void k_local_small(LocalArgs a, uint32_t nb)
         if (cur.m > (uint32_t)LCAP_S) {  // for the big kernel
             if (threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;
         } else if (cur.m > 0) {
-            bucket_sort_regs<LNT_S, LCAP_S / LNT_S, LPOS_S, true, uint16_t>(
-                a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, cnt, scratch, s_e, s_r);
+            if (!bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S>(a, b, cur.s0, cur.m, cur.g,
+                                                                   cur.e, cur.r, A, B, sstart,
+                                                                   scur, scratch, s_e, s_r)) {
+                __syncthreads();  // (the fallback re-stages into the same arrays)
+                bucket_sort_regs<LNT_S, LCAP_S / LNT_S, LPOS_S, true, uint16_t>(
+                    a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, cnt, scratch, s_e, s_r);
+            }
         }
         __syncthreads();  // (the next bucket overwrites the staging)
         cur = nxt;
@@ -1001,8 +1089,13 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     // bucket costs more than the digit passes below that)
     const int64_t span = set->off.empty() ? 0 : (int64_t)set->off.back();
     const int sbits = span > 1 ? 64 - __builtin_clzll((uint64_t)(span - 1)) : 1;
+    // (and few enough that they average at most LAVG over the span: denser
+    // sets, e.g. C3's 5e8 rows, take the digit passes, decided before the
+    // prep so it runs once -- a validate-only prep then a writing one cost
+    // C3 1.4 ms)
+    const int64_t nb_span = (span >> (sbits - 16)) + 1;
     const bool bucket_cand = keep_rows && !stranded && !row_ties && sbits > 16 &&
-                             n >= LMIN * ((span >> (sbits - 16)) + 1);
+                             n >= LMIN * nb_span && n <= LAVG * nb_span;
     const int hshift = bucket_cand ? sbits - 16 : set->min_shift;
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
     if (n > 0) {

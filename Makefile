@@ -68,3 +68,10 @@ build/var3/liblime_amd.so: $(HIP_SRCS) $(SRC)/common.hpp include/lime_amd.h $(CP
 	@mkdir -p build/var3
 	$(HIPCC) $(HIPFLAGS) -DLIME_FILL_WGS=3 -c $(SRC)/intersect.hip -o build/var3/intersect.o
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(filter-out $(OBJDIR)/intersect.o,$(HIP_OBJS)) build/var3/intersect.o $(CPP_OBJS)
+
+# tuning variants of one translation unit (tools/gpu_ab.sh A/B only):
+#   make build/var_<name>/liblime_amd.so VAR_SRC=merge VAR_DEFS="-DLIME_MS2_NT=256"
+build/var_%/liblime_amd.so: $(HIP_SRCS) $(SRC)/common.hpp include/lime_amd.h $(CPP_OBJS) $(HIP_OBJS)
+	@mkdir -p build/var_$*
+	$(HIPCC) $(HIPFLAGS) $(VAR_DEFS) -c $(SRC)/$(VAR_SRC).hip -o build/var_$*/$(VAR_SRC).o
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(filter-out $(OBJDIR)/$(VAR_SRC).o,$(HIP_OBJS)) build/var_$*/$(VAR_SRC).o $(CPP_OBJS)

@@ -408,35 +408,36 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
     if (err && dev::lane_id() == 0) atomicOr(a.err, err);
 }
 
-// one block per bin: its rows -> its PSUB paint tiles.  Slot claims per wave
-// and step: lane j = 8 k + d counts the rows of slot k bound for tile d (the
-// tile's 3 bits as ballots), a prefix over k gives each (k, d) its offset among the wave's
-// claims for d, and ONE LDS atomic instruction (lanes 56..63) reserves all
-// of them -- no chain of returning atomics per row.
-static_assert(PSUB == 8, "claims: 8 slots x 8 destinations = one wave");
+// one block per bin: its rows -> its PSUB paint tiles.  The bin's rows go
+// in chunks of SPB * 8: every row claims a slot on its WAVE's counter for its
+// tile (one returning LDS atomic; 64 lanes over 8 counters, where a counter
+// per block took 512), a scan over the 8 waves per tile places the waves'
+// slot groups one after the other at the tile's cursor, and the rows are
+// stored there (a wave's rows of one tile are consecutive slots).  Claims
+// inside a group come back in any order: a tile's rows are ORed in any order.
 static_assert(NBMAX % WRB == 0, "write-pass bin scan: whole bins per thread");
 constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
 __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
-    __shared__ uint32_t cur[PSUB];
+    constexpr int NWV = SPB / 64, PV = 8;
+    __shared__ uint32_t wc[NWV][PSUB], wbase[NWV][PSUB], cur[PSUB];
     const int b = blockIdx.x;
+    const int wv = threadIdx.x / 64, lane = dev::lane_id();
     if (threadIdx.x < PSUB) cur[threadIdx.x] = a.ttot[b * PSUB + threadIdx.x];
+    if (threadIdx.x < NWV * PSUB) (&wc[0][0])[threadIdx.x] = 0u;
     const uint32_t r0 = a.mat[(int64_t)b * a.nchunks], r1 = a.mat[(int64_t)(b + 1) * a.nchunks];
     __syncthreads();
-    const int lane = dev::lane_id();
     const uint64_t bin0 = (uint64_t)b << BSH;
-    constexpr int PV = 8;
-    const int wv = threadIdx.x / 64, nwv = SPB / 64;
-    const uint32_t stride = (uint32_t)nwv * 64 * PV;
+    constexpr uint32_t CH = SPB * PV;  // rows per chunk
+    const uint32_t mine = (uint32_t)wv * 64 * PV + lane;  // the lane's first row in a chunk
     uint32_t pv[PV];
-    const uint32_t first = r0 + (uint32_t)wv * 64 * PV;
-    if (first < r1)
+    if (r0 < r1)
 #pragma unroll
-        for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(first + k * 64 + lane, r1 - 1)];
-    for (uint32_t rb = first; rb < r1; rb += stride) {
-        uint32_t q[PV], val[PV], dst[PV];
+        for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(r0 + mine + k * 64, r1 - 1)];
+    for (uint32_t c0 = r0; c0 < r1; c0 += CH) {  // (uniform over the block)
+        uint32_t q[PV], val[PV], rk[PV];
 #pragma unroll
         for (int k = 0; k < PV; ++k) {
-            const bool v = rb + k * 64 + lane < r1;
+            const bool v = c0 + mine + k * 64 < r1;
             const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
             q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
             const uint32_t qend = (q[k] + 1) << PSH;
@@ -444,13 +445,28 @@ __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
             if (v && l2 < l)  // remainder [o + l2, o + l) into the next tile(s)
                 a.cross[atomicAdd(a.ncross, 1u)] = ((bin0 + o + l2) << 32) | (bin0 + o + l);
             val[k] = ((o - (q[k] << PSH)) << PLENB) | l2;
-            dst[k] = v ? atomicAdd(&cur[q[k]], 1u) : 0u;
+            rk[k] = v ? atomicAdd(&wc[wv][q[k]], 1u) : 0u;
         }
-        if (rb + stride < r1)
+        if (c0 + CH < r1)
 #pragma unroll
-            for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(rb + stride + k * 64 + lane, r1 - 1)];
+            for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(c0 + CH + mine + k * 64, r1 - 1)];
+        __syncthreads();
+        if (threadIdx.x < PSUB) {  // the waves' groups, one after the other per tile
+            const int d = threadIdx.x;
+            uint32_t run = cur[d];
 #pragma unroll
-        for (int k = 0; k < PV; ++k) *(q[k] < PSUB ? a.slab2 + dst[k] : a.dummy) = val[k];
+            for (int w = 0; w < NWV; ++w) {
+                const uint32_t c = wc[w][d];
+                wbase[w][d] = run;
+                wc[w][d] = 0u;
+                run += c;
+            }
+            cur[d] = run;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PV; ++k)
+            *(q[k] < PSUB ? a.slab2 + wbase[wv][q[k] & (PSUB - 1)] + rk[k] : a.dummy) = val[k];
     }
 }
 

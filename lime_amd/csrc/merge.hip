@@ -395,8 +395,14 @@ struct ScanGeom {
 };
 // 512 threads x 32 rows: 16384-row tiles (as k_merge_scan: as few
 // look-backs), two workgroups per CU (<= 128 VGPRs)
-constexpr int MS2 = 512;
-using G2 = ScanGeom<MS2, 8>;
+#ifndef LIME_MS2_NT
+#define LIME_MS2_NT 512
+#endif
+#ifndef LIME_MS2_Q
+#define LIME_MS2_Q 8
+#endif
+constexpr int MS2 = LIME_MS2_NT;
+using G2 = ScanGeom<MS2, LIME_MS2_Q>;
 
 __global__ __launch_bounds__(MS2) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_merge_scan2(MergeScanArgs a) {

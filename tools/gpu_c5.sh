@@ -10,3 +10,6 @@ bash tools/gpu_prof.sh ${T}_c5 python bench.py --workload c5 --steps 5 --no-cpu-
 grep -h '^{' gpurun_out/${T}_c5_prof.txt | python3 -c "import json,sys; d=json.loads(sys.stdin.readline()); print('c5', d['ms_per_step'], d['roofline']['frac'])"
 timeout -k 10 300 python tools/bench_extra.py --workload c4 > gpurun_out/${T}_c4.txt 2>&1 || exit 1
 grep -h '^{' gpurun_out/${T}_c4.txt | python3 -c "import json,sys; d=json.loads(sys.stdin.readline()); print('c4', d['ms_per_step'], d['breakdown_ms'])"
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS --output-format csv -d gpurun_out/${T}_sq -o p -- python bench.py --workload c5 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/${T}_sq.log 2>&1 || exit 1
+python3 tools/pmc_summary.py gpurun_out/${T}_sq > gpurun_out/${T}_sq_summary.txt
+grep -E "bin_write|bin_split|bin_count|paint_and" gpurun_out/${T}_sq_summary.txt

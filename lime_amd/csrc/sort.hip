@@ -199,13 +199,33 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
         uint4 *g4 = reinterpret_cast<uint4 *>(gs + base);
         uint4 *h4 = reinterpret_cast<uint4 *>(ge + base);
         uint4 *r4 = reinterpret_cast<uint4 *>(row + base);
+        // every load issued before any is used (12 x 16 B per lane in flight:
+        // one iteration's loads at a time held the prep at 4.1 TB/s), and the
+        // row before the wave's chunk (lane 0's predecessor in iteration 0;
+        // in later iterations it is lane 63's last row of the one before)
+        int4 cv[RITEMS / 4];
+        uint4 sv[RITEMS / 4], ev[RITEMS / 4];
 #pragma unroll
         for (int k = 0; k < RITEMS / 4; ++k) {
             const int q = k * 64 + lane;
-            const int4 cv = c4[q];
-            const uint4 sv = s4[q], ev = e4[q];
-            const int32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
-            const uint32_t ss[4] = {sv.x, sv.y, sv.z, sv.w}, ee[4] = {ev.x, ev.y, ev.z, ev.w};
+            cv[k] = c4[q];
+            sv[k] = s4[q];
+            ev[k] = e4[q];
+        }
+        int32_t bc = -1;
+        uint32_t bs = 0, be = 0;
+        if (lane == 0 && base > 0) {
+            bc = contig[base - 1];
+            bs = start[base - 1];
+            be = end[base - 1];
+        }
+        uint32_t l0 = 0, l1 = 0, lok = 0;  // lane 63's last row of the previous iteration
+#pragma unroll
+        for (int k = 0; k < RITEMS / 4; ++k) {
+            const int q = k * 64 + lane;
+            const int32_t cc[4] = {cv[k].x, cv[k].y, cv[k].z, cv[k].w};
+            const uint32_t ss[4] = {sv[k].x, sv[k].y, sv[k].z, sv[k].w},
+                           ee[4] = {ev[k].x, ev[k].y, ev[k].z, ev[k].w};
             uint32_t a0[4], a1[4], ok[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -229,21 +249,24 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                 ve[4 * k + j] = a1[j];
             }
             // canonical-order check: the row before this lane's first row is
-            // the previous lane's last one (lane 0 reads it from memory)
+            // the previous lane's last one
             uint32_t p0 = dev::wave_shr1(a0[3], 0u), p1 = dev::wave_shr1(a1[3], 0u),
                      pok = dev::wave_shr1(ok[3], 0u);
             const int64_t i0 = base + 4 * (int64_t)q;
             if (lane == 0) {
-                pok = 0;
-                if (i0 > 0) {
-                    const int32_t pc = contig[i0 - 1];
-                    pok = pc >= 0 && pc < n_contigs;
+                if (k > 0) {
+                    p0 = l0, p1 = l1, pok = lok;
+                } else {
+                    pok = bc >= 0 && bc < n_contigs;
                     if (pok) {
-                        p0 = off[pc] + start[i0 - 1];
-                        p1 = off[pc] + end[i0 - 1];
+                        p0 = off[bc] + bs;
+                        p1 = off[bc] + be;
                     }
                 }
             }
+            l0 = (uint32_t)__builtin_amdgcn_readlane((int)a0[3], 63);
+            l1 = (uint32_t)__builtin_amdgcn_readlane((int)a1[3], 63);
+            lok = (uint32_t)__builtin_amdgcn_readlane((int)ok[3], 63);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (pok && ok[j] && (p0 > a0[j] || (p0 == a0[j] && p1 > p0 && a1[j] == a0[j])))
@@ -809,8 +832,8 @@ __device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b,
 //   4. each row's rank in its sub-bin = the number of its keys below u
 //      (unique keys: no tie, so the result is the stable order),
 // and the rows are written in rank order.  A sub-bin past SMAX rows (piled-up
-// starts) sends the bucket back to the digit passes: returns false, having
-// staged s_e / s_r only.
+// starts) sends the bucket to k_local_big's ranked digit passes: returns false
+// (nothing written).
 constexpr int SBB = 9, SMAX = 48;
 template <int NT, int ITEMS, int POSB>
 __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b, uint32_t s0,
@@ -854,7 +877,10 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
     uint32_t big = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) big = max(big, scratch[NW + 1 + i]);
-    if (big > (uint32_t)SMAX) return false;  // (uniform: every thread read the same words)
+    if (big > (uint32_t)SMAX) {  // (uniform: every thread read the same words)
+        __syncthreads();  // (sstart / scur are reset by the next bucket)
+        return false;
+    }
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it)
         if (u[it] != 0xffffffffu) T[atomicAdd(&scur[(u[it] >> POSB) >> sh], 1u)] = u[it];
@@ -909,34 +935,30 @@ struct BucketRegs {
     }
 };
 
-// Persistent (two workgroups per CU): each workgroup takes buckets b,
-// b + grid, ... and loads the next one's rows into registers before sorting
-// the current one, so the load latency hides behind the LDS passes (one
-// bucket per workgroup, loads then sort, left the memory pipe idle half the
-// time: 1.0 vs 0.X ms per 1e8 rows).  Buckets past LCAP_S rows are listed for
-// k_local_big.
-constexpr int LNT_S = 512, LPOS_S = 12, LCAP_S = 1 << LPOS_S;  // 8 items / thread
+// Persistent (three workgroups per CU, <= 80 VGPRs, ~50 KiB LDS): each
+// workgroup takes buckets b, b + grid, ... and loads the next one's rows into
+// registers before sorting the current one, so the load latency hides behind
+// the LDS work (one bucket per workgroup, loads then sort, left the memory
+// pipe idle half the time).  Buckets past LCAP_S rows, or with a sub-bin past
+// SMAX rows, are listed for k_local_big.  (Two workgroups per CU with 4096-row
+// buckets and the ranked digit passes inline took 78 KiB of LDS each: the
+// loads in flight per CU, not the bytes, bounded it at 3.75 TB/s.)
+constexpr int LNT_S = 512, LPOS_S = 12, LCAP_S = 3072;  // 6 items / thread
 using SmallRegs = BucketRegs<LNT_S, LCAP_S / LNT_S, LCAP_S>;
-__global__ __launch_bounds__(LNT_S) void k_local_small(LocalArgs a, uint32_t nb) {
+__global__ __launch_bounds__(LNT_S) __attribute__((amdgpu_waves_per_eu(6, 8)))
+void k_local_small(LocalArgs a, uint32_t nb) {
     __shared__ uint32_t A[LCAP_S], B[LCAP_S], s_e[LCAP_S], s_r[LCAP_S];
-    __shared__ uint16_t cnt[LNT_S / 64][1 << LDMAX];
     __shared__ uint32_t sstart[LNT_S], scur[LNT_S];
     __shared__ uint32_t scratch[2 * (LNT_S / 64) + 1];
     SmallRegs cur, nxt;
     cur.load(a, blockIdx.x, nb);
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         nxt.load(a, b + gridDim.x, nb);
-        if (cur.m > (uint32_t)LCAP_S) {  // for the big kernel
-            if (threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;
-        } else if (cur.m > 0) {
-            if (!bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S>(a, b, cur.s0, cur.m, cur.g,
-                                                                   cur.e, cur.r, A, B, sstart,
-                                                                   scur, scratch, s_e, s_r)) {
-                __syncthreads();  // (the fallback re-stages into the same arrays)
-                bucket_sort_regs<LNT_S, LCAP_S / LNT_S, LPOS_S, true, uint16_t>(
-                    a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, cnt, scratch, s_e, s_r);
-            }
-        }
+        bool listed = cur.m > (uint32_t)LCAP_S;
+        if (!listed && cur.m > 0)
+            listed = !bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S>(
+                a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, sstart, scur, scratch, s_e, s_r);
+        if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
         cur = nxt;
     }
@@ -1210,7 +1232,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (cus <= 0) cus = 256;
-            hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)),
+            hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)),
                                dim3(LNT_S), 0, S(ctx), la, nb);
             hipLaunchKernelGGL(k_local_big, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B), 0,
                                S(ctx), la);

@@ -834,15 +834,20 @@ __device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b,
 // and the rows are written in rank order.  A sub-bin past SMAX rows (piled-up
 // starts) sends the bucket to k_local_big's ranked digit passes: returns false
 // (nothing written).
-constexpr int SBB = 9, SMAX = 48;
-template <int NT, int ITEMS, int POSB>
+constexpr int SMAX = 48;
+// NSB = 2^SBB sub-bins (NSB / NT per thread in the scan); CT: the sub-bin
+// counter type (u32: LDS atomics); STAGE: e / r staged in LDS by
+// position (else gathered from global memory at the end, where the
+// bucket's lines are L2-resident after its load)
+template <int NT, int ITEMS, int POSB, int SBB, bool STAGE, typename CT>
 __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b, uint32_t s0,
                                                   uint32_t m, const uint32_t (&g)[ITEMS],
                                                   const uint32_t (&e)[ITEMS],
                                                   const uint32_t (&r)[ITEMS], uint32_t *T,
-                                                  uint32_t *O, uint32_t *sstart, uint32_t *scur,
+                                                  uint32_t *O, CT *sstart, CT *scur,
                                                   uint32_t *scratch, uint32_t *s_e, uint32_t *s_r) {
-    static_assert(NT == (1 << SBB), "one sub-bin per thread in the scan");
+    constexpr int NSB = 1 << SBB, SPT = NSB / NT;
+    static_assert(NSB % NT == 0 && SPT >= 1, "whole sub-bins per thread in the scan");
     constexpr int NW = NT / 64;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int nit = (int)((m + NW * 64 - 1) / (NW * 64));
@@ -850,7 +855,8 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
     const uint32_t lmask = (1u << a.L) - 1u;
     const int kb = a.L + 1;                      // local key bits
     const int sh = kb > SBB ? kb - SBB : 0;      // sub-bin = key >> sh
-    scur[threadIdx.x] = 0u;
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) scur[SPT * threadIdx.x + q] = 0;
     __syncthreads();
     uint32_t u[ITEMS];
 #pragma unroll
@@ -861,18 +867,30 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
             const uint32_t k = ((g[it] & lmask) << 1) | (e[it] > g[it] ? 1u : 0u);
             u[it] = (k << POSB) | pos;
             atomicAdd(&scur[k >> sh], 1u);
-            s_e[pos] = e[it];
-            s_r[pos] = r[it];
+            if (STAGE) {
+                s_e[pos] = e[it];
+                s_r[pos] = r[it];
+            }
         }
     }
     __syncthreads();
-    const uint32_t cnt = scur[threadIdx.x];
+    uint32_t cv[SPT], csum = 0, cmax = 0;
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+        cv[q] = scur[SPT * threadIdx.x + q];
+        csum += cv[q];
+        cmax = max(cmax, cv[q]);
+    }
     uint32_t tot;
-    const uint32_t st = dev::block_exclusive_sum<NT>(cnt, scratch, &tot);
-    const uint32_t mx = dev::wave_reduce_max(cnt);
+    uint32_t st = dev::block_exclusive_sum<NT>(csum, scratch, &tot);
+    const uint32_t mx = dev::wave_reduce_max(cmax);
     if (lane == 0) scratch[NW + 1 + w] = mx;  // (past the scan's NW + 1 words)
-    sstart[threadIdx.x] = st;
-    scur[threadIdx.x] = st;
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+        sstart[SPT * threadIdx.x + q] = (CT)st;
+        scur[SPT * threadIdx.x + q] = (CT)st;
+        st += cv[q];
+    }
     __syncthreads();
     uint32_t big = 0;
 #pragma unroll
@@ -899,8 +917,8 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
     for (uint32_t q = threadIdx.x; q < m; q += NT) {
         const uint32_t x = O[q], j = x & pm;
         a.k1[s0 + q] = base | ((x >> (POSB + 1)) & lmask);
-        a.e1[s0 + q] = s_e[j];
-        a.r1[s0 + q] = s_r[j];
+        a.e1[s0 + q] = STAGE ? s_e[j] : a.e0[s0 + j];
+        a.r1[s0 + q] = STAGE ? s_r[j] : a.r0[s0 + j];
     }
     return true;
 }
@@ -956,7 +974,7 @@ void k_local_small(LocalArgs a, uint32_t nb) {
         nxt.load(a, b + gridDim.x, nb);
         bool listed = cur.m > (uint32_t)LCAP_S;
         if (!listed && cur.m > 0)
-            listed = !bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S>(
+            listed = !bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S, 9, true, uint32_t>(
                 a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, sstart, scur, scratch, s_e, s_r);
         if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
@@ -1047,10 +1065,17 @@ __device__ void bucket_sort_global(const LocalArgs &a, uint32_t s0, uint32_t m, 
 
 // the listed buckets (> LCAP_S rows), taken in ticket order by one resident
 // workgroup per CU until the list is done
+// (the claim sort with 2048 sub-bins first, the ranked digit passes when a
+// pile-up puts more than SMAX rows in one of them)
 __global__ __launch_bounds__(LNT_B) void k_local_big(LocalArgs a) {
     __shared__ uint32_t A[LCAP_B], B[LCAP_B];
-    __shared__ uint16_t cnt[LNT_B / 64][1 << LDMAX];
-    __shared__ uint32_t scratch[LNT_B / 64 + 1];
+    // the ranked passes' digit counters and the claim sort's sub-bin starts /
+    // cursors share one 16 KiB block (the two paths never overlap in time)
+    __shared__ uint32_t aux[4096];
+    static_assert(sizeof(uint16_t) * (LNT_B / 64) * (1 << LDMAX) <= sizeof(aux), "aux");
+    uint16_t(*cnt)[1 << LDMAX] = reinterpret_cast<uint16_t(*)[1 << LDMAX]>(aux);
+    uint32_t *sstart = aux, *scur = aux + 2048;
+    __shared__ uint32_t scratch[2 * (LNT_B / 64) + 1];
     __shared__ uint32_t s_i;
     for (;;) {
         if (threadIdx.x == 0) s_i = atomicAdd(&a.nover[1], 1u);
@@ -1063,8 +1088,10 @@ __global__ __launch_bounds__(LNT_B) void k_local_big(LocalArgs a) {
         if (m <= (uint32_t)LCAP_B) {
             BucketRegs<LNT_B, LCAP_B / LNT_B, LCAP_B> R;
             R.load(a, b, b + 1);
-            bucket_sort_regs<LNT_B, LCAP_B / LNT_B, LPOS_B, false, uint16_t>(
-                a, b, s0, m, R.g, R.e, R.r, A, B, cnt, scratch, nullptr, nullptr);
+            if (!bucket_sort_claim<LNT_B, LCAP_B / LNT_B, LPOS_B, 11, false, uint32_t>(
+                    a, b, s0, m, R.g, R.e, R.r, A, B, sstart, scur, scratch, nullptr, nullptr))
+                bucket_sort_regs<LNT_B, LCAP_B / LNT_B, LPOS_B, false, uint16_t>(
+                    a, b, s0, m, R.g, R.e, R.r, A, B, cnt, scratch, nullptr, nullptr);
         } else
             bucket_sort_global<LNT_B>(a, s0, m, A);
         __syncthreads();
@@ -1088,7 +1115,10 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
 }
 
 // the bucketed sort's choice: 2^L-base buckets under two 8-bit digit passes
-// (L = bits - 16), averaging LMIN to LAVG rows (else the digit passes)
+// (L = bits - 16), averaging LMIN to LAVG rows (else the digit passes):
+// most buckets in k_local_small.  (Denser sets through k_local_big, one
+// workgroup per CU: C3's 5e8 pile-up rows, ~10.6k per bucket, took 7.0 ms
+// there -- sort 14.6 ms against 13.0 with the four digit passes.)
 constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4;
 
 int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,

@@ -130,3 +130,38 @@ def test_sorted_input_and_digit_pass_sets(ctx):
     sp2 = _space([60_000])
     s, e = _rows(rng, 300_000, 0, 60_000 - 100, 100, 0.1, 0.1)
     _check_host_set(ctx, sp2, np.zeros(len(s), np.int32), s, e)
+
+
+def test_bucketed_sort_dense_buckets(ctx):
+    # C3's shape at 2e8 rows: pile-ups (8e5 centres over hg38, N(0,150), len
+    # U[150,600]) averaging ~4.2k rows per 65536-base bucket: denser than the
+    # bucketed sort takes, so the four digit passes.  Checked on the device at
+    # full size: canonical order (gs, zero-width first, input row), the row
+    # ids a permutation, every row's coordinates those of its input row.
+    import torch
+
+    from lime_amd import synth
+    sp = Space(list(synth.HG38.keys()), list(synth.HG38.values()))
+    n = 200_000_000
+    c = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.empty(n, dtype=torch.int32, device="cuda")
+    e = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.synth_pileup(sp, n, 0x3C, 800_000, 150, 150, 600, c.data_ptr(), s.data_ptr(), e.data_ptr())
+    torch.cuda.synchronize()
+    S = ctx.set_from_device(sp, n, c.data_ptr(), s.data_ptr(), e.data_ptr())
+    gs, ge, row = (torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    S.copy_rows_device(0, n, gs.data_ptr(), ge.data_ptr(), row.data_ptr())
+    torch.cuda.synchronize()
+    S.close()
+    off = torch.tensor(sp.offsets[:-1].astype(np.int64), device="cuda")
+    g64 = gs.to(torch.int64) & 0xFFFFFFFF
+    e64 = ge.to(torch.int64) & 0xFFFFFFFF
+    key = g64 * 2 + (e64 > g64).to(torch.int64)
+    assert bool((key[1:] >= key[:-1]).all())
+    tie = key[1:] == key[:-1]
+    r64 = row.to(torch.int64) & 0xFFFFFFFF
+    assert bool((r64[1:][tie] > r64[:-1][tie]).all())
+    assert bool((torch.sort(r64).values == torch.arange(n, device="cuda")).all())
+    cin = c.to(torch.int64)[r64]
+    assert bool((g64 == off[cin] + s.to(torch.int64)[r64]).all())
+    assert bool((e64 == off[cin] + e.to(torch.int64)[r64]).all())

@@ -210,10 +210,16 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t bid, uint32_t nch) {
     return x * q + (x < r ? x : r) + i;
 }
 
-// A step = 16 rows per lane: four groups of 4 consecutive rows, the groups
+// A step = SROWS rows per lane: groups of 4 consecutive rows, the groups
 // BINB * 4 rows apart, so every load is a lane-consecutive 16-B access and a
-// step keeps 8-12 loads in flight per lane.
-constexpr int SROWS = 16;
+// step keeps 6-9 loads in flight per lane.
+// 12 rows per lane and two write workgroups per CU (<= 128 VGPRs, 57 KiB
+// LDS): C5 10.8-11.1 -> 10.5-10.8 ms against 16 rows at one per CU (8 rows:
+// no gain, shorter runs per bin)
+#ifndef LIME_SROWS
+#define LIME_SROWS 12
+#endif
+constexpr int SROWS = LIME_SROWS;  // (a multiple of 4)
 constexpr int STEP = SROWS * BINB;    // rows per count step
 constexpr int WSTEP = SROWS * WRB;    // rows per write step
 
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
 }
 
 #ifndef LIME_WRITE_BLOCKS
-#define LIME_WRITE_BLOCKS 1
+#define LIME_WRITE_BLOCKS 2
 #endif
 template <bool LC>
 __global__ __launch_bounds__(WRB)

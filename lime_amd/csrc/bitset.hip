@@ -914,24 +914,86 @@ constexpr int EVCAP = LIME_EVCAP;  // events of a tile staged in LDS
 // a scan of the counts then places them (k_ev_gather).  Nothing waits on a
 // predecessor, so the pass runs at the rate of the count pass; a tile with
 // more than EVCAP events raises *oflow and the host takes the two-pass path.
+// The tile is held in registers, not staged in LDS: thread t loads its
+// EV_W consecutive words (16-B loads, every operand combined as it lands),
+// the word before a lane's first is the previous lane's last (DPP shift;
+// across waves one LDS word per wave; before the tile one global read), and
+// only the events go through LDS (for lane-consecutive slot stores).  (The
+// LDS-staged tile image held the kernel to 3 workgroups per CU: 2.3-4.6
+// TB/s.)
 __global__ __launch_bounds__(EV_NT) void k_ev_local(OpArgs a, uint32_t *__restrict__ tev,
                                                     uint32_t *__restrict__ tcnt,
                                                     unsigned int *__restrict__ oflow) {
-    __shared__ unsigned long long img[img_words(EV_TW)];
+    constexpr int NW = EV_NT / 64;
     __shared__ uint32_t s_pad[MAXPAD];
     __shared__ int s_npad;
+    __shared__ uint64_t s_last[NW];
     __shared__ uint32_t scratch[EV_NT / 64 + 1];
     __shared__ uint32_t s_ev[EVCAP];
     const uint32_t tile = blockIdx.x;
     const int64_t w0 = (int64_t)tile * EV_TW;
-    stage_tile<EV_NT, EV_TW>(a, w0, img, s_pad, &s_npad);
-    const int q0 = threadIdx.x * EV_W;
-    uint32_t c = 0;
+    const int64_t nw = a.n_words;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t q0 = w0 + (int64_t)threadIdx.x * EV_W;  // the thread's first word
+    if (a.op == 1 && threadIdx.x == 0) {  // NOT: the contig pads of the tile
+        const int64_t lo = (a.word0 + (w0 > 0 ? w0 - 1 : 0)) * 64, hi = (a.word0 + w0 + EV_TW) * 64;
+        int64_t c = dev::lower_bound(a.off + 1, 0, (int64_t)a.nc, (uint64_t)lo + 1);
+        int np = 0;
+        for (; c < a.nc && (int64_t)a.off[c + 1] - 1 < hi && np < MAXPAD; ++c)
+            s_pad[np++] = a.off[c + 1] - 1;
+        s_npad = np;
+    }
+    uint64_t x[EV_W];
+    const int nops = a.op == 4 ? a.k : (a.op >= 2 ? 2 : 1);
+    for (int i = 0; i < nops; ++i) {
+        const uint64_t *src = a.w[i];
 #pragma unroll
-    for (int k = 0; k < EV_W; ++k) {
-        uint64_t st, en;
-        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
-        c += __popcll(st) + __popcll(en);
+        for (int k = 0; k < EV_W; k += 2) {
+            const int64_t wd = q0 + k;
+            uint64_t y0, y1;
+            if (wd + 1 < nw) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(src + wd);
+                y0 = v.x;
+                y1 = v.y;
+            } else {
+                y0 = wd < nw ? src[wd] : 0ull;
+                y1 = 0ull;
+            }
+            if (i == 0) {
+                x[k] = y0;
+                x[k + 1] = y1;
+            } else {
+                x[k] &= a.op == 3 ? ~y0 : y0;
+                x[k + 1] &= a.op == 3 ? ~y1 : y1;
+            }
+        }
+    }
+    // the word before the tile (thread 0's left neighbour)
+    uint64_t xb = 0;
+    if (threadIdx.x == 0 && w0 > 0 && w0 - 1 < nw) xb = op_raw(a, w0 - 1);
+    __syncthreads();  // s_pad
+    if (a.op == 1) {
+        const int npad = s_npad;
+#pragma unroll
+        for (int k = 0; k < EV_W; ++k)
+            x[k] = q0 + k < nw ? not_mask(a, q0 + k, ~x[k], s_pad, npad) : 0ull;
+        if (threadIdx.x == 0 && w0 > 0 && w0 - 1 < nw) xb = not_mask(a, w0 - 1, xb, s_pad, npad);
+    }
+    // left neighbour of the thread's first word
+    if (lane == 63) s_last[w] = x[EV_W - 1];
+    uint64_t prev = dev::wave_shr1(x[EV_W - 1], (uint64_t)0);
+    __syncthreads();
+    if (lane == 0) prev = w > 0 ? s_last[w - 1] : xb;
+    uint32_t c = 0;
+    {
+        uint64_t p = prev;
+#pragma unroll
+        for (int k = 0; k < EV_W; ++k) {
+            uint64_t st, en;
+            events_of(x[k], p, st, en);
+            c += __popcll(st) + __popcll(en);
+            p = x[k];
+        }
     }
     uint32_t tot;
     const uint32_t mine = dev::block_exclusive_sum<EV_NT>(c, scratch, &tot);
@@ -941,16 +1003,20 @@ __global__ __launch_bounds__(EV_NT) void k_ev_local(OpArgs a, uint32_t *__restri
     }
     if (tot > (uint32_t)EVCAP) return;
     uint32_t le = mine;
+    {
+        uint64_t p = prev;
 #pragma unroll
-    for (int k = 0; k < EV_W; ++k) {
-        uint64_t st, en;
-        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
-        uint64_t all = st | en;
-        const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
-        while (all) {
-            const int b = __builtin_ctzll(all);
-            all &= all - 1;
-            s_ev[le++] = base + (uint32_t)b;
+        for (int k = 0; k < EV_W; ++k) {
+            uint64_t st, en;
+            events_of(x[k], p, st, en);
+            p = x[k];
+            uint64_t all = st | en;
+            const uint32_t base = (uint32_t)((a.word0 + q0 + k) * 64);
+            while (all) {
+                const int b = __builtin_ctzll(all);
+                all &= all - 1;
+                s_ev[le++] = base + (uint32_t)b;
+            }
         }
     }
     __syncthreads();
@@ -1133,6 +1199,19 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
     LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
     LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, slab2, ttot,
                       cross, flags));
+    // the row-error flags are final once the rows are binned: copied to the
+    // host there, so the paint kernels are already queued while the host
+    // waits (the next call's kernels follow them without a drained stream)
+    struct Ev {
+        hipEvent_t e = nullptr;
+        ~Ev() {
+            if (e) (void)hipEventDestroy(e);
+        }
+    } ev;
+    LIME_HIP(hipEventCreateWithFlags(&ev.e, hipEventDisableTiming));
+    unsigned int *hf = static_cast<unsigned int *>(ctx->pinned);  // (read_back's half)
+    LIME_HIP(hipMemcpyAsync(hf, flags, 8, hipMemcpyDeviceToHost, S(ctx)));
+    LIME_HIP(hipEventRecord(ev.e, S(ctx)));
     hipLaunchKernelGGL(k_paint_bins, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx),
                        (const uint32_t *)slab2, (const uint32_t *)ttot, bs->words, bs->n_words);
     if (n > 0)
@@ -1140,9 +1219,8 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
                            dim3(BB), 0, S(ctx), (const uint64_t *)cross,
                            (const unsigned int *)flags, bs->words);
     LIME_HIP(hipGetLastError());
-    unsigned int h[2] = {0, 0};
-    LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
-    return rows_error(h[1]);
+    LIME_HIP(hipEventSynchronize(ev.e));
+    return rows_error(hf[1]);
 }
 
 // the AND of k row sets' bits over window [lo, hi), straight from their

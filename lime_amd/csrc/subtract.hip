@@ -39,6 +39,9 @@ constexpr int SUB_B = 256;
 struct SubArgs {
     // per block (inline ranges: per 4 blocks): first B row a spanning hit can be
     const uint32_t *wstart;
+    // runs: every block's own window start, found by the count pass in its
+    // staged window and read by the write pass (no search there)
+    uint32_t *bwlo;
     uint32_t maxw;  // max width of B
     const uint32_t *ags, *age, *arow;
     const uint32_t *bgs, *bge, *brow, *bpmax;
@@ -181,7 +184,8 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     __shared__ uint32_t st_gs[WRITE ? SCAP : 1], st_ge[WRITE ? SCAP : 1];
     __shared__ uint32_t st_ar[WRITE ? SCAP : 1], st_br[WRITE ? SCAP : 1];
     __shared__ uint32_t w_pm[BWIN];
-    // (RUNS reads starts, ends and row ids at block heads only: global memory)
+    // (RUNS reads ends and row ids at block heads only: global memory.
+    // Staging them too cost the sparse 1e9-row subtract 12.4 -> 14.3 ms)
     __shared__ uint32_t w_gs[BWIN], w_ge[RUNS ? 1 : BWIN], w_row[RUNS ? 1 : BWIN];
     __shared__ uint32_t w_run[RUNS ? BWIN : 1];
     __shared__ uint32_t s_whi[SUB_B / 64];
@@ -198,22 +202,42 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     // inline ranges: wstart holds one start per 4 blocks (the count pass's
     // workgroups); the block's own is searched from there (every wave alike)
     int64_t wlo;
-    if (inl) {
+    if (inl && WRITE) {
+        wlo = sa.bwlo[blockIdx.x];  // (the count pass's)
+    } else if (inl) {
         const int64_t c = sa.wstart[blockIdx.x / CNT_WAVES];
         const int64_t key = max((int64_t)sa.ags[(int64_t)blockIdx.x * SUB_B] - sa.maxw, (int64_t)0);
         wlo = c + dev::wave_lower_bound(sa.bgs + c, sa.nb - c, key);
     } else {
         wlo = sa.wstart[blockIdx.x];
     }
-    // inline ranges (RUNS): BWIN rows from wlo staged with their starts,
-    // without waiting for the candidate ranges
-    const int nst = inl ? (int)min((int64_t)BWIN, sa.nb - wlo) : 0;
-    if (inl)
-        for (int k = threadIdx.x; k < nst; k += SUB_B) {
-            w_pm[k] = sa.bpmax[wlo + k];
-            w_gs[k] = sa.bgs[wlo + k];
-            w_run[k] = sa.brun[wlo + k];
+    // inline ranges (RUNS): B rows from wlo staged with their starts, 256 at
+    // a time up to BWIN, until the staged starts pass every end of the
+    // block's left rows (no row's hit lies past that: sparse sets need a
+    // fraction of BWIN rows, 12 B each, per block)
+    int nst = 0;
+    if (inl) {
+        uint32_t amax = 0;
+        for (int64_t q = (int64_t)blockIdx.x * SUB_B + threadIdx.x; q < sa.na &&
+             q < (int64_t)(blockIdx.x + 1) * SUB_B; q += SUB_B)
+            amax = sa.age[q];
+        amax = dev::wave_reduce_max(amax);
+        if (dev::lane_id() == 0) s_whi[threadIdx.x / 64] = amax;
+        __syncthreads();
+        for (int w = 0; w < SUB_B / 64; ++w) amax = max(amax, s_whi[w]);
+        const int cap = (int)min((int64_t)BWIN, sa.nb - wlo);
+        for (int k0 = 0; k0 < cap; k0 += SUB_B) {  // (uniform over the block)
+            const int k = k0 + threadIdx.x;
+            if (k < cap) {
+                w_pm[k] = sa.bpmax[wlo + k];
+                w_gs[k] = sa.bgs[wlo + k];
+                w_run[k] = sa.brun[wlo + k];
+            }
+            nst = min(k0 + SUB_B, cap);
+            __syncthreads();
+            if (w_gs[nst - 1] >= amax) break;
         }
+    }
     if (!inl) {
         uint32_t h = 0;
         if (i < sa.na) h = sa.olo[i] + sa.ocnt[i];
@@ -681,6 +705,27 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     tot = dev::wave_reduce_sum(tot);
     const int64_t sb = (int64_t)blockIdx.x * CNT_WAVES + wv;
     if (lane == 0 && sb < nblk) sa.count[sb] = tot;
+    // the block's own window start (its first row's start - max width of B,
+    // lower bound among B's starts) for the write pass, from the staged
+    // window when it reaches that far
+    if (lane == 0 && sb < nblk && base < sa.na) {
+        const int64_t key = max((int64_t)as[0] - (int64_t)sa.maxw, (int64_t)0);
+        int64_t r;
+        if (nst > 0 && (int64_t)w_gs[nst - 1] >= key) {
+            int l = 0, h = nst - 1;
+            while (l < h) {
+                const int m = (l + h) >> 1;
+                if ((int64_t)w_gs[m] < key)
+                    l = m + 1;
+                else
+                    h = m;
+            }
+            r = wlo + l;
+        } else {
+            r = dev::lower_bound(sa.bgs, whi, sa.nb, key);
+        }
+        sa.bwlo[sb] = (uint32_t)r;
+    }
 }
 
 // any same-start group past TIE_G rows (*big), and every row of a
@@ -820,8 +865,12 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
                            na, B->gs, B->n, B->max_width, nws, stride, wstart);
     else
         LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nws, S(ctx)));
+    uint32_t *bwlo = nullptr;  // runs: per-block window starts (count -> write pass)
+    if (inl) LIME_TRY(alloc(ctx, &bwlo, (size_t)nblk));
+    PoolGuard<uint32_t> gb{ctx, bwlo};
     SubArgs sa;
     sa.wstart = wstart;
+    sa.bwlo = bwlo;
     sa.maxw = B->max_width;
     sa.ags = A->gs;
     sa.age = A->ge;

@@ -229,6 +229,34 @@ def test_intersect_deep_windows(ctx, seed, n, contig_len, max_len):
     assert plan.checksum() == want
 
 
+# One plan whose tiles differ in density: a dense contig (the fill finds a
+# tile's ranges in its LDS window itself, >= 32 pairs per owner) next to a
+# sparse one (k_count's staged ranges), zero-width partners (the search skips
+# them at a.s) and a threshold (its hi keys, not filtered: no row narrower)
+@pytest.mark.parametrize("seed,t", [(71, 0), (72, 20), (73, -5)])
+def test_intersect_mixed_density(ctx, seed, t):
+    rng = np.random.default_rng(seed)
+
+    def one(n):
+        c = (rng.random(n) < 0.5).astype(np.int32)
+        lo = max(t, 1)
+        s = np.where(c == 0, rng.integers(0, 37000, n), rng.integers(0, 399000, n))
+        l = np.where(c == 0, rng.integers(lo, 3000, n), rng.integers(lo, 60, n))
+        if t <= 0:
+            l[rng.random(n) < 0.03] = 0
+        return c, s.astype(np.int64), s.astype(np.int64) + l.astype(np.int64)
+
+    A, B = one(8000), one(8000)
+    sp = Space(["c0", "c1"], [40000, 400000])
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    plan = ctx.intersect(a, b, t)
+    exp = oracle.intersect(A, B, t)
+    assert plan.n == len(exp["start"])
+    want = oracle.checksum_pairs(exp)
+    assert oracle.checksum_pairs(plan.fill_host()) == want
+    assert plan.checksum() == want
+
+
 @pytest.mark.parametrize("seed,d", [(61, 0), (62, 1), (63, 7), (64, 150), (65, 1000),
                                     (66, 40000)])
 def test_window_parity(ctx, seed, d):

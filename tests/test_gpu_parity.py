@@ -491,6 +491,39 @@ def test_bitset_from_unsorted_rows(ctx, seed, max_len):
     assert ctx.bitset_runs(3, bu, bs).n == 0 and ctx.bitset_runs(3, bs, bu).n == 0
 
 
+@pytest.mark.parametrize("case", ["spread", "skewed"])
+def test_bitset_sparse_and_skewed_bins(ctx, case):
+    # unsorted rows -> bits over a 2-bin space: rows crossing the paint tiles
+    # and the bins, rows past a bin piece's length field (cross list),
+    # zero-width rows, and (skewed) one bin holding 5/6 of the rows
+    import torch
+    rng = np.random.default_rng(57 if case == "spread" else 58)
+    n = 24000
+    c = rng.integers(0, 3, n).astype(np.int32)
+    s = rng.integers(0, 1_990_000, n)
+    if case == "skewed":  # 20000 rows in contig 0's first 1 Mb: bin 0
+        c[:20000] = 0
+        s[:20000] = rng.integers(0, 1_000_000, 20000)
+    ln = rng.integers(0, 400, n)
+    long_rows = rng.random(n) < 0.02
+    ln[long_rows] = rng.integers(1000, 9000, int(long_rows.sum()))
+    e = np.minimum(s + ln, 2_000_000)
+    A = (c, s.astype(np.int64), e.astype(np.int64))
+    sp = space_for(3, 2_000_000)
+    dev = torch.device("cuda", 0)
+    t = [torch.from_numpy(np.ascontiguousarray(x).astype(np.int32)).to(dev) for x in A]
+    torch.cuda.synchronize()
+    bu = ctx.bitset_from_device(sp, n, *(x.data_ptr() for x in t))
+    bs = ctx.bitset(ctx.set_from_host(sp, *A))
+    m = oracle.merge(A)
+    assert bu.popcount() == bs.popcount() == int((m["end"] - m["start"]).sum())
+    for op in (0, 1):
+        got, want = ctx.bitset_runs(op, bu).to_host(), ctx.bitset_runs(op, bs).to_host()
+        assert got["start"].tolist() == want["start"].tolist()
+        assert got["end"].tolist() == want["end"].tolist()
+    assert ctx.bitset_runs(3, bu, bs).n == 0 and ctx.bitset_runs(3, bs, bu).n == 0
+
+
 def test_bitset_paths(ctx):
     rng = np.random.default_rng(51)
     A, B = random_sets(rng, 20000, 20000, n_contigs=3, contig_len=200000, max_len=300)

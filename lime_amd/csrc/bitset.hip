@@ -898,11 +898,14 @@ __global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w,
 #ifndef LIME_EV_NT
 #define LIME_EV_NT 256
 #endif
+// 8 words per thread (2048-word tiles, 2048-event slots: the same events per
+// word as 16 / 4096): C4's extraction 0.445 -> 0.42 ms (twice the tiles, a
+// shorter tail); 32 words: 0.465 ms (profiles/round3l_ev_geometry_ab.txt)
 #ifndef LIME_EV_W
-#define LIME_EV_W 16
+#define LIME_EV_W 8
 #endif
 #ifndef LIME_EVCAP
-#define LIME_EVCAP 4096
+#define LIME_EVCAP 2048
 #endif
 constexpr int EV_NT = LIME_EV_NT, EV_W = LIME_EV_W, EV_TW = EV_NT * EV_W;
 constexpr int EVCAP = LIME_EVCAP;  // events of a tile staged in LDS
@@ -935,13 +938,17 @@ __global__ __launch_bounds__(EV_NT) void k_ev_local(OpArgs a, uint32_t *__restri
     const int64_t nw = a.n_words;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t q0 = w0 + (int64_t)threadIdx.x * EV_W;  // the thread's first word
-    if (a.op == 1 && threadIdx.x == 0) {  // NOT: the contig pads of the tile
+    if (a.op == 1 && w == 0) {  // NOT: the contig pads of the tile, by wave 0
+        // (a 65-ary search, then lane l tests the l-th pad from there: the
+        // serial binary search by one lane cost C4's complement ~15 us)
         const int64_t lo = (a.word0 + (w0 > 0 ? w0 - 1 : 0)) * 64, hi = (a.word0 + w0 + EV_TW) * 64;
-        int64_t c = dev::lower_bound(a.off + 1, 0, (int64_t)a.nc, (uint64_t)lo + 1);
-        int np = 0;
-        for (; c < a.nc && (int64_t)a.off[c + 1] - 1 < hi && np < MAXPAD; ++c)
-            s_pad[np++] = a.off[c + 1] - 1;
-        s_npad = np;
+        static_assert(MAXPAD == 64, "one pad per lane");
+        const int64_t c = dev::wave_lower_bound(a.off + 1, (int64_t)a.nc, lo + 1) + lane;
+        const int64_t pad = c < a.nc ? (int64_t)a.off[c + 1] - 1 : INT64_MAX;
+        const bool in = pad < hi;  // (pads ascend: a prefix of the lanes)
+        const uint64_t m = __ballot(in);
+        if (in) s_pad[lane] = (uint32_t)pad;
+        if (lane == 0) s_npad = __popcll(m);
     }
     uint64_t x[EV_W];
     const int nops = a.op == 4 ? a.k : (a.op >= 2 ? 2 : 1);

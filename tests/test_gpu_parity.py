@@ -890,8 +890,8 @@ def test_spaces_cached_per_context(ctx):
 
 
 def test_bitset_runs_dense_tile_falls_back(ctx):
-    # a tile with more events than the extraction's per-tile stage (4096):
-    # 3000 one-base runs two bases apart in the first 262144-base tile, plus
+    # a tile with more events than the extraction's per-tile stage (2048):
+    # 3000 one-base runs two bases apart in the first 131072-base tile, plus
     # a sparse tail; the runs come back exact either way
     rng = np.random.default_rng(5)
     dense = np.arange(3000, dtype=np.int64) * 2

@@ -54,6 +54,9 @@ struct SubArgs {
     // zw = B holds zero-width rows
     int zw;
     uint64_t *count;        // pass 1
+    // RUNS: every left row's record count from the count pass (255: the write
+    // pass folds the row twice, counting first), so the write pass folds once
+    uint8_t *rcnt;
     const uint64_t *off;    // pass 2
     unsigned int *err;      // pass 2 (RUNS): a block's recount differs from pass 1
     uint32_t *ogs, *oge, *oar, *obr;
@@ -307,6 +310,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         end = (int64_t)sa.off[i + 1];
     }
     auto emit = [&](uint32_t s, uint32_t e, uint32_t br, int64_t at) {
+        if (WRITE && RUNS && (at < bbase || at >= bend)) {  // (a count mismatch: flagged)
+            atomicOr(sa.err, 1u);
+            return;
+        }
         if (WRITE) {
             if (staged) {
                 const int k = (int)(at - bbase);
@@ -526,7 +533,15 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         // RUNS: per-block totals (count pass); the write pass counts again
         // (O(runs) per row) and places its rows by a block scan
         __shared__ uint64_t s_part[SUB_B / 64];
-        const uint64_t n_out = fold(false);
+        // (write pass: the count pass's per-row count; the sparse 1e9-row
+        // subtract's write pass folded every row twice)
+        uint64_t n_out;
+        if (WRITE) {
+            const uint32_t rc = i < sa.na ? sa.rcnt[i] : 0u;
+            n_out = rc < 255u ? rc : fold(false);
+        } else {
+            n_out = fold(false);
+        }
         const uint64_t inc = dev::wave_inclusive_sum(n_out);
         if (dev::lane_id() == 63) s_part[threadIdx.x / 64] = inc;
         __syncthreads();
@@ -550,7 +565,7 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         staged = total <= (uint64_t)SCAP;
         pos = bbase + (int64_t)(before + inc - n_out);
         end = pos + (int64_t)n_out;
-        fold(true);
+        if (fold(true) != n_out) atomicOr(sa.err, 1u);
     }
     if (staged) {  // the block's records, lane-consecutive
         __syncthreads();
@@ -700,6 +715,7 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
             if (!lime_mode && a_e > setpos) ++cum;
             n_out = cum;
         }
+        sa.rcnt[base + k * 64 + lane] = (uint8_t)(n_out < 255 ? n_out : 255);
         tot += n_out;
     }
     tot = dev::wave_reduce_sum(tot);
@@ -868,6 +884,9 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     uint32_t *bwlo = nullptr;  // runs: per-block window starts (count -> write pass)
     if (inl) LIME_TRY(alloc(ctx, &bwlo, (size_t)nblk));
     PoolGuard<uint32_t> gb{ctx, bwlo};
+    uint8_t *rcnt = nullptr;  // runs: per-row record counts (count -> write pass)
+    if (inl) LIME_TRY(alloc(ctx, &rcnt, (size_t)na));
+    PoolGuard<uint8_t> gr{ctx, rcnt};
     SubArgs sa;
     sa.wstart = wstart;
     sa.bwlo = bwlo;
@@ -886,6 +905,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.t = threshold;
     sa.mode = mode;
     sa.count = cnt;
+    sa.rcnt = rcnt;
     sa.off = off;
     sa.err = err;
     // the tie index of B (long same-start groups), built once per set

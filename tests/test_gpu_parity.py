@@ -229,6 +229,38 @@ def test_intersect_deep_windows(ctx, seed, n, contig_len, max_len):
     assert plan.checksum() == want
 
 
+# Fill windows of odd sizes and offsets ([first, first + count), records
+# of one owner split across windows): their concatenation is the whole fill,
+# for a sparse plan (the thread-per-owner fill, ~4 pairs per owner) and a
+# dense one (k_fill)
+@pytest.mark.parametrize("seed,max_len", [(81, 60), (82, 3000)])
+def test_intersect_fill_windows(ctx, seed, max_len):
+    rng = np.random.default_rng(seed)
+    A, B = random_sets(rng, 6000, 5000, n_contigs=2, contig_len=40000, max_len=max_len,
+                       zero_frac=0.02, dup_frac=0.05)
+    sp = space_for(2, 40000)
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    plan = ctx.intersect(a, b)
+    exp = oracle.intersect(A, B)
+    assert plan.n == len(exp["start"])
+    whole = plan.fill_host()
+    parts, f = [], 0
+    for k in [1, 777, 4096, 63, 100000]:
+        k = min(k, plan.n - f)
+        if k <= 0:
+            break
+        parts.append(plan.fill_host(f, k))
+        f += k
+    if f < plan.n:
+        parts.append(plan.fill_host(f, plan.n - f))
+    cat = np.concatenate(parts)
+    for key in whole.dtype.names:
+        assert cat[key].tolist() == whole[key].tolist()
+    want = oracle.checksum_pairs(exp)
+    assert oracle.checksum_pairs(whole) == want
+    assert plan.checksum() == want
+
+
 # One plan whose tiles differ in density: a dense contig (the fill finds a
 # tile's ranges in its LDS window itself, >= 32 pairs per owner) next to a
 # sparse one (k_count's staged ranges), zero-width partners (the search skips

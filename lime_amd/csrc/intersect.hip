@@ -370,9 +370,6 @@ constexpr int FOPT = OT / FB;     // owners per thread when staging a tile
 #ifndef LIME_FILL_WGS
 #define LIME_FILL_WGS 2  // fill workgroups per CU (LDS budget below)
 #endif
-#ifndef LIME_FILL_SPARSE
-#define LIME_FILL_SPARSE 0  // thread-per-owner fill for sparse plans (k_fill_sparse)
-#endif
 // LDS partner window (16 B records): 1792 rows keep 3 workgroups per CU
 constexpr int PCAP = LIME_FILL_WGS >= 3 ? 1792 : 2048;
 constexpr int PPT = (PCAP + FB - 1) / FB;  // partner rows per thread when staging
@@ -626,121 +623,6 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
     }
 }
 
-// Sparse plans (< FS_PPO pairs per owner on average: the 1e9-row uniform
-// sets with lengths 10-40 have 4): k_fill's per-tile staging, barriers and
-// owner searches cost more than the tile's few records, so a thread takes
-// one owner and writes its records itself -- its range [lo, lo + c) of
-// partners read through the caches (consecutive owners share them), its
-// records at the tile's offset + its k_count offset, those inside the
-// window [first, first + count) only, staged in LDS at their place in the
-// workgroup's records and stored lane-consecutively (a lane storing its own
-// records 16 B apart from its neighbours' took the sparse 1e9-row fill
-// 30.2 -> 43.3 ms).  Workgroups of 256 owners stride over
-// the window's tiles (4 per tile), the first found by a 65-ary search.
-constexpr int64_t FS_PPO = 16;
-constexpr int SPB_F = 256;
-template <bool CKSUM, bool WIN>
-__global__ __launch_bounds__(SPB_F) void k_fill_sparse(FillArgs fa) {
-    __shared__ int64_t s_t0;
-    __shared__ uint64_t s_red[2][SPB_F / 64];
-    constexpr int SREC = 2048;  // records of a workgroup staged in LDS (32 KiB)
-    __shared__ u32x4 s_rec[CKSUM ? 1 : SREC];
-    constexpr int PER = OT / SPB_F;  // workgroups per tile
-    if (threadIdx.x < 64) {
-        const int64_t t0 = wave_tile_of(fa.toff, fa.ntiles, (uint64_t)fa.first);
-        if (threadIdx.x == 0) s_t0 = t0;
-    }
-    __syncthreads();
-    const int64_t wend = fa.first + fa.count;
-    uint64_t hsum = 0, hxor = 0;
-    for (int64_t u = s_t0 * PER + blockIdx.x; u < fa.ntiles * PER; u += gridDim.x) {
-        const int64_t t = u / PER;
-        const int64_t tb = (int64_t)fa.toff[t];
-        if (tb >= wend) break;  // (uniform over the workgroup)
-        const int64_t te = t + 1 < fa.ntiles ? (int64_t)fa.toff[t + 1] : fa.total;
-        if (te <= fa.first) continue;  // (uniform)
-        const int st = tile_stream(fa, t);
-        const StreamArgs &sa = fa.s[st];
-        const int64_t o0 = (t - sa.tile0) * OT;
-        const int nown = (int)min((int64_t)OT, sa.no - o0);
-        const int qb = (int)(u % PER) * SPB_F;  // the workgroup's first owner in the tile
-        if (qb >= nown) continue;  // (uniform)
-        const int q = qb + threadIdx.x;
-        // the workgroup's records [wb, we) inside the window
-        const int64_t bb = tb + fa.ocnt[sa.owner0 + o0 + qb];
-        const int64_t be = qb + SPB_F < nown ? tb + fa.ocnt[sa.owner0 + o0 + qb + SPB_F] : te;
-        const int64_t wb = max(bb, fa.first), we = min(be, wend);
-        if (q < nown) {
-            const int64_t j = o0 + q;
-            const uint32_t off = fa.ocnt[sa.owner0 + j];  // tile-local (k_count<_, true>)
-            const uint32_t nxt = q + 1 < nown ? fa.ocnt[sa.owner0 + j + 1] : (uint32_t)(te - tb);
-            const uint32_t lo = fa.olo[sa.owner0 + j];
-            const uint32_t og = sa.ogs_o[j], oe = sa.oge_o[j], orw = sa.orow[j];
-            const uint32_t ts = fa.tseg[t];
-            const uint32_t sg = ts != 0xffffffffu ? ts : contig_off(fa.off, fa.n_contigs, og);
-            const int64_t ob = tb + off;  // the owner's first record
-            const int64_t r0 = max((int64_t)0, fa.first - ob);
-            const int64_t r1 = min((int64_t)(nxt - off), wend - ob);
-            for (int64_t r4 = r0; r4 < r1; r4 += 4) {
-                uint32_t pg[4], pe[4], pr[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {  // the loads first
-                    const bool v = r4 + k < r1;
-                    const uint32_t p = lo + (uint32_t)(r4 + k);
-                    pg[k] = v ? sa.pgs_o[p] : 0u;
-                    pe[k] = v ? sa.pge_o[p] : 0u;
-                    pr[k] = v ? sa.prow[p] : 0u;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (r4 + k >= r1) break;
-                    const uint32_t rs = (WIN ? (st == 0 ? og : pg[k]) : (og > pg[k] ? og : pg[k])) - sg;
-                    const uint32_t re = (WIN ? (st == 0 ? oe : pe[k]) : (oe < pe[k] ? oe : pe[k])) - sg;
-                    const uint32_t ar = st == 0 ? orw : pr[k];
-                    const uint32_t br = st == 0 ? pr[k] : orw;
-                    if (CKSUM) {
-                        const uint64_t h = dev::pair_hash(rs, re, ar, br);
-                        hsum += h;
-                        hxor ^= h;
-                    } else {
-                        // staged at its place in the workgroup's records; past
-                        // the stage (a locally dense workgroup) stored directly
-                        const int64_t x = ob + r4 + k - wb;
-                        if (x < SREC)
-                            s_rec[x] = u32x4{rs, re, ar, br};
-                        else
-                            fa.out[ob + r4 + k - fa.first] = u32x4{rs, re, ar, br};
-                    }
-                }
-            }
-        }
-        if (!CKSUM) {  // the staged records, lane-consecutive 16-B stores
-            __syncthreads();
-            const int cnt = (int)min((int64_t)SREC, we - wb);
-            for (int k = threadIdx.x; k < cnt; k += SPB_F) fa.out[wb - fa.first + k] = s_rec[k];
-            __syncthreads();
-        }
-    }
-    if (CKSUM) {
-        hsum = dev::wave_reduce_sum(hsum);
-        uint64_t x = dev::wave_reduce_xor(hxor);
-        if (dev::lane_id() == 0) {
-            s_red[0][threadIdx.x / 64] = hsum;
-            s_red[1][threadIdx.x / 64] = x;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint64_t a = 0, b = 0;
-            for (int i = 0; i < SPB_F / 64; ++i) {
-                a += s_red[0][i];
-                b ^= s_red[1][i];
-            }
-            atomicAdd((unsigned long long *)&fa.cksum[0], (unsigned long long)a);
-            atomicXor((unsigned long long *)&fa.cksum[1], (unsigned long long)b);
-        }
-    }
-}
-
 // Filtered fallback (threshold >= 1 with partners narrower than it): thread per
 // owner walks its candidate range and emits the qualifying ones in order.
 template <bool CKSUM>
@@ -919,26 +801,6 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
         else
             hipLaunchKernelGGL(k_fill_filtered<false>, dim3(grid), dim3(IB), 0, S(ctx), fa,
                                pl->threshold);
-    } else if (LIME_FILL_SPARSE && pl->total < FS_PPO * (pl->a_own + pl->b_own)) {
-        // enough workgroups to fill the device a few times over; each strides
-        // over the window's tiles
-        static const unsigned slots = [] {
-            int dev = 0, cus = 256;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            return (unsigned)(cus > 0 ? cus : 256) * 32u;
-        }();
-        const int64_t want = (pl->nt0 + pl->nt1) * (OT / SPB_F);
-        const dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>(want, slots)));
-        const bool win = pl->reach >= 0;
-        if (cksum && win)
-            hipLaunchKernelGGL((k_fill_sparse<true, true>), g, dim3(SPB_F), 0, S(ctx), fa);
-        else if (cksum)
-            hipLaunchKernelGGL((k_fill_sparse<true, false>), g, dim3(SPB_F), 0, S(ctx), fa);
-        else if (win)
-            hipLaunchKernelGGL((k_fill_sparse<false, true>), g, dim3(SPB_F), 0, S(ctx), fa);
-        else
-            hipLaunchKernelGGL((k_fill_sparse<false, false>), g, dim3(SPB_F), 0, S(ctx), fa);
     } else {
         const int64_t per = fill_span(count);
         const int64_t grid = (count + per - 1) / per;

@@ -371,11 +371,7 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
             tt = torch.tensor([npairs, nruns], dtype=torch.int64, device=comm_dev or dev)
             dist.all_reduce(tt)
             npairs, nruns = (int(x) for x in tt.tolist())
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "fill_pmc.json")
-        if os.path.exists(pmc) and world == 1:
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+        traffic, tsrc = pmc_traffic("pmc_c2.json", "hbm_bytes_per_launch", world)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_scale, n)
@@ -396,6 +392,7 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
                        "parallelism": f"range-shard x{world}" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": tsrc,
                          "kernel": "k_fill<false>", "avg_launch_ms": avg_ms,
                          "alg_bytes_per_launch": avg_b, "launches": len(timed)},
             "breakdown_ms": breakdown,
@@ -442,6 +439,7 @@ def bench_c5(args, ctx, space, dev, world, rank, comm_dev, ev):
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = c5_cpu_baseline(100, per)
+        traffic, tsrc = pmc_traffic("pmc_c5.json", "hbm_bytes_per_step", world)
         return {
             "metric": "intervals/sec for 8-way intersection (BASELINE C5); % of HBM peak GB/s",
             "value": k * per / (dt / args.steps), "unit": "intervals/s", "n_gpus": world,
@@ -456,13 +454,31 @@ def bench_c5(args, ctx, space, dev, world, rank, comm_dev, ev):
                        "genome_bases": G,
                        "parallelism": f"range-shard x{world}" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": tsrc,
                          "kernel": "whole C5 step (route, bin, paint, AND, extract) per GPU",
                          "alg_bytes_per_step_per_gpu": alg / world,
                          "step_ms_hip_events": state["t"][0].elapsed_time(state["t"][1])},
             "cpu_baseline": cpu,
         }
     return step, finish
+
+
+def pmc_traffic(name, field, world):
+    """HBM bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_json.py) of
+    the same command, from a profile committed under profiles/, with where it
+    came from (file, commit, command, kernel); (None, None) without one or at
+    N > 1 (the profiles are single-GPU runs)"""
+    p = os.path.join(ROOT, "profiles", name)
+    if world != 1 or not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    src = dict(d.get("provenance", {}))
+    src["file"] = os.path.join("profiles", name)
+    if "key_kernel" in d:
+        src["kernel"] = d["key_kernel"]
+    return d.get(field), src
 
 
 def synth_lengths():

@@ -744,6 +744,25 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     }
 }
 
+// whether any same-start group has more than TIE_G rows: gs[j] == gs[j +
+// TIE_G] for some j (4 rows per thread, 16-B loads; reads gs once: the tie
+// index's flag + scan passes run only when it does)
+__global__ __launch_bounds__(256) void k_tie_detect(const uint32_t *__restrict__ gs, int64_t n,
+                                                    unsigned int *__restrict__ big) {
+    static_assert(TIE_G % 4 == 0, "aligned 16-B loads at j and j + TIE_G");
+    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (j + TIE_G >= n) return;
+    bool hit = false;
+    if (j + TIE_G + 4 <= n) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(gs + j);
+        const uint4 y = *reinterpret_cast<const uint4 *>(gs + j + TIE_G);
+        hit = x.x == y.x || x.y == y.y || x.z == y.z || x.w == y.w;
+    } else {
+        for (int64_t q = j; q + TIE_G < n && q < j + 4; ++q) hit |= gs[q] == gs[q + TIE_G];
+    }
+    if (__ballot(hit) != 0 && dev::lane_id() == 0) atomicOr(big, 1u);
+}
+
 // any same-start group past TIE_G rows (*big), and every row of a
 // multi-row same-start group flagged for the tie index
 __global__ __launch_bounds__(256) void k_tie_flags(const uint32_t *__restrict__ gs, int64_t n,
@@ -789,14 +808,26 @@ static int build_tie_index(lime_ctx *ctx, const lime_set *B) {
     }
     uint32_t *flag, *pos, *tot;
     unsigned int *big;
-    LIME_TRY(alloc(ctx, &flag, (size_t)n));
-    PoolGuard<uint32_t> g0{ctx, flag};
-    LIME_TRY(alloc(ctx, &pos, (size_t)n));
-    PoolGuard<uint32_t> g1{ctx, pos};
     LIME_TRY(alloc(ctx, &tot, 2));
     PoolGuard<uint32_t> g2{ctx, tot};
     big = reinterpret_cast<unsigned int *>(tot + 1);
     LIME_HIP(hipMemsetAsync(tot, 0, 8, S(ctx)));
+    // (most sets have no long same-start group: one read of gs decides)
+    hipLaunchKernelGGL(k_tie_detect, dim3(blocks_for((n + 3) / 4, 256)), dim3(256), 0, S(ctx),
+                       B->gs, n, big);
+    LIME_HIP(hipGetLastError());
+    {
+        uint32_t hb[2] = {0, 0};
+        LIME_TRY(read_back(ctx, hb, tot, sizeof(hb)));
+        if (!hb[1]) {
+            B->tie_n = 0;
+            return LIME_OK;
+        }
+    }
+    LIME_TRY(alloc(ctx, &flag, (size_t)n));
+    PoolGuard<uint32_t> g0{ctx, flag};
+    LIME_TRY(alloc(ctx, &pos, (size_t)n));
+    PoolGuard<uint32_t> g1{ctx, pos};
     hipLaunchKernelGGL(k_tie_flags, dim3(blocks_for(n, 256)), dim3(256), 0, S(ctx), B->gs, n, flag,
                        big);
     LIME_TRY(scan_exclusive_u32(ctx, flag, pos, n, tot));

@@ -8,8 +8,12 @@ contig-sharded oracle drivers, by count plus order-independent checksum
       every row's run (SetTheory.scala:208-225); complement gaps by count and
       region checksum (Complement.scala:59-128)
   2 x 5e8 intersect / subtract  uniform over hg38, len U[10,40] (~4e9 pairs):
-      pair count + pair checksum (Intersection.scala:58-69); subtract in both
-      modes by count + region checksum (Subtract.scala:91-116)
+      pair count + pair checksum, of the fill's register side and of every
+      record it stores (Intersection.scala:58-69); subtract in both modes by
+      count + region checksum (Subtract.scala:91-116)
+  sparse-B subtract  1e7 long left rows (len U[1000,10000]) minus 3e7 short
+      right rows (len U[10,40]): ~50 blocks per left row, ~5e8 remnants in
+      lime mode (Subtract.scala:103-114's per-block emission at volume)
   C5 at full size  8 x 1.25e8 rows over hg38, len U[10,40]: the fused k-way
       paint-AND (the bench's path) == the oracle fold of intersect over the
       merged operands (Appendix A.4), runs exact
@@ -103,6 +107,22 @@ def test_1b_intersect(ctx, pair_1b):
     assert plan.n == exp["n"]
     assert 3.5e9 < plan.n < 4.5e9  # E = n^2 (25 + 25) / G ~ 4.0e9
     assert got == (exp["sum"], exp["xor"])
+    # the bytes the fill STORES on this sparse plan (~4 pairs per owner, the
+    # tile-commit-bound shape), 2^31-record chunks through one reusable
+    # buffer as bench_extra's b1_pair line, hashed from HBM by a separate
+    # kernel: every stored record, not the fill's register-side checksum
+    import torch
+    chunk = 1 << 31
+    buf = torch.empty((chunk, 4), dtype=torch.int32, device="cuda")
+    hs, hx, f = 0, 0, 0
+    while f < plan.n:
+        k = min(chunk, plan.n - f)
+        plan.fill_device(f, k, buf.data_ptr())
+        s, x = ctx.pairs_checksum_device(buf.data_ptr(), k)
+        hs, hx, f = (hs + s) & 0xFFFFFFFFFFFFFFFF, hx ^ x, f + k
+    del buf
+    say("intersect: stored records hashed")
+    assert (hs, hx) == (exp["sum"], exp["xor"])
     plan.close()
 
 
@@ -118,6 +138,29 @@ def test_1b_subtract(ctx, pair_1b, mode):
     assert res.n == exp["n"] > 1e6  # lime mode: ~7.4e7 regions
     assert ck[:2] == (exp["sum"], exp["xor"])
     res.close()
+
+
+# ------------------------------------------- sparse B from long left rows
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", [oracle.SUB_LIME, oracle.SUB_SET])
+def test_sparse_b_subtract_long_rows(ctx, mode):
+    # every left row is cut by ~50 separate B rows: many blocks per row and a
+    # remnant per block (lime mode: Subtract.scala:103-114; set mode: the
+    # pieces of a minus the union of its hits)
+    sp = hg38()
+    da, A = device_rows(ctx, sp, 10_000_000, 0x5A, 1000, 10000)
+    db, B = device_rows(ctx, sp, 30_000_000, 0x5B, 10, 40)
+    a, b = dset(ctx, sp, da), dset(ctx, sp, db)
+    del da, db
+    res = ctx.subtract(a, b, 0, mode)
+    ck = res.checksum()
+    say(f"sparse-B subtract mode {mode}: {res.n} regions on the device; oracle")
+    exp = oracle.subtract_mt(len(sp.names), A, B, 0, mode)
+    say("sparse-B subtract: oracle done")
+    assert res.n == exp["n"] > 2e8  # ~50 pieces per left row
+    assert ck[:2] == (exp["sum"], exp["xor"])
+    for h in (res, a, b):
+        h.close()
 
 
 # ------------------------------------------------------- C5 at full size

@@ -7,9 +7,9 @@ sort, on inputs that take every path of lime_amd/csrc/sort.hip:
     rows, buckets of ~2-4k rows (512-thread kernel), of 4k-16k rows
     (1024-thread kernel) and past 16k rows (the workgroup-wide radix over
     global memory);
-  - the digit passes (spans within 16 bits, sets of few rows per bucket;
-    sets averaging more than LAVG rows per bucket run through the 1e9-row
-    tests of tests/test_gpu_scale.py);
+  - the digit passes (spans within 16 bits, sets of few rows per bucket,
+    sets past LAVG rows per bucket: both sides of that switch at full size
+    over hg38, C3-shaped pile-ups, giant piles, global rows);
   - host, device and global-coordinate inputs, zero-width rows, exact
     duplicates, rows already in order.
 
@@ -132,22 +132,11 @@ def test_sorted_input_and_digit_pass_sets(ctx):
     _check_host_set(ctx, sp2, np.zeros(len(s), np.int32), s, e)
 
 
-def test_bucketed_sort_dense_buckets(ctx):
-    # C3's shape at 2e8 rows: pile-ups (8e5 centres over hg38, N(0,150), len
-    # U[150,600]) averaging ~4.2k rows per 65536-base bucket: denser than the
-    # bucketed sort takes, so the four digit passes.  Checked on the device at
-    # full size: canonical order (gs, zero-width first, input row), the row
-    # ids a permutation, every row's coordinates those of its input row.
+def _check_device_order(ctx, sp, n, c, s, e):
+    """the set built from device rows (c, s, e) is in canonical order (gs,
+    zero-width first, input row), its row ids a permutation and every row's
+    coordinates those of its input row -- checked on the device at full size"""
     import torch
-
-    from lime_amd import synth
-    sp = Space(list(synth.HG38.keys()), list(synth.HG38.values()))
-    n = 200_000_000
-    c = torch.empty(n, dtype=torch.int32, device="cuda")
-    s = torch.empty(n, dtype=torch.int32, device="cuda")
-    e = torch.empty(n, dtype=torch.int32, device="cuda")
-    ctx.synth_pileup(sp, n, 0x3C, 800_000, 150, 150, 600, c.data_ptr(), s.data_ptr(), e.data_ptr())
-    torch.cuda.synchronize()
     S = ctx.set_from_device(sp, n, c.data_ptr(), s.data_ptr(), e.data_ptr())
     gs, ge, row = (torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3))
     S.copy_rows_device(0, n, gs.data_ptr(), ge.data_ptr(), row.data_ptr())
@@ -165,3 +154,99 @@ def test_bucketed_sort_dense_buckets(ctx):
     cin = c.to(torch.int64)[r64]
     assert bool((g64 == off[cin] + s.to(torch.int64)[r64]).all())
     assert bool((e64 == off[cin] + e.to(torch.int64)[r64]).all())
+
+
+def _hg38():
+    from lime_amd import synth
+    return Space(list(synth.HG38.keys()), list(synth.HG38.values()))
+
+
+def _synth(ctx, sp, n, seed, lo, hi, pile=None):
+    import torch
+    c, s, e = (torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    if pile:
+        ctx.synth_pileup(sp, n, seed, pile[0], pile[1], lo, hi, c.data_ptr(), s.data_ptr(),
+                         e.data_ptr())
+    else:
+        ctx.synth_uniform(sp, n, seed, lo, hi, c.data_ptr(), s.data_ptr(), e.data_ptr())
+    torch.cuda.synchronize()
+    return c, s, e
+
+
+# hg38: sbits 32, 47,125 buckets of 65,536 bases.  LAVG (2304) rows per
+# bucket switch a set from the bucketed sort to the four digit passes
+# (sort.hip); both sides of the switch are exercised at full size.
+_BUCKETS_HG38 = 47_125
+
+
+@pytest.mark.parametrize("n", [2304 * _BUCKETS_HG38 - 1_000_000, 2304 * _BUCKETS_HG38 + 1_000_000])
+def test_bucketed_sort_switch_point(ctx, n):
+    # uniform rows over hg38, len U[0, 60] (zero-width rows included): below
+    # the switch two 8-bit passes and k_local_small, above it the zero-width
+    # pass and four digit passes
+    sp = _hg38()
+    c, s, e = _synth(ctx, sp, n, 0x5A, 0, 60)
+    _check_device_order(ctx, sp, n, c, s, e)
+
+
+def test_bucketed_sort_dense_buckets(ctx):
+    # C3's shape at 2e8 rows: pile-ups (8e5 centres over hg38, N(0,150), len
+    # U[150,600]) averaging ~4.2k rows per 65536-base bucket: denser than the
+    # bucketed sort takes, so the four digit passes
+    sp = _hg38()
+    n = 200_000_000
+    c, s, e = _synth(ctx, sp, n, 0x3C, 150, 600, pile=(800_000, 150))
+    _check_device_order(ctx, sp, n, c, s, e)
+
+
+def test_digit_pass_sort_giant_piles(ctx):
+    # the digit passes (1.2e8 rows over hg38: past the bucketed sort's
+    # density) with piles of 2.5k, 9k, 40k and 150k rows at single positions,
+    # zero-width rows and duplicates among them: stable at every pile
+    import torch
+    sp = _hg38()
+    n = 120_000_000
+    c, s, e = _synth(ctx, sp, n, 0x61, 50, 500)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    for k, (size, pos) in enumerate([(2_500, 1_000_000), (9_000, 5_000_000),
+                                     (40_000, 9_000_100), (150_000, 70_000_000)]):
+        idx = torch.randperm(n, device="cuda", generator=g)[:size]
+        c[idx] = 1 + k
+        s[idx] = pos + torch.randint(0, 3000, (size,), device="cuda", generator=g,
+                                     dtype=torch.int32)
+        w = torch.randint(0, 400, (size,), device="cuda", generator=g, dtype=torch.int32)
+        w[torch.rand(size, device="cuda", generator=g) < 0.1] = 0
+        e[idx] = s[idx] + w
+    torch.cuda.synchronize()
+    _check_device_order(ctx, sp, n, c, s, e)
+
+
+def test_digit_pass_sort_global(ctx):
+    # global-coordinate rows with the caller's row ids through the digit
+    # passes (1.15e8 rows over hg38): ties keep INPUT order, rows carried
+    # through
+    import torch
+    sp = _hg38()
+    n = 115_000_000
+    c, s, e = _synth(ctx, sp, n, 0x62, 0, 40)
+    off = torch.tensor(sp.offsets[:-1].astype(np.int64), device="cuda")
+    gs = (off[c.to(torch.int64)] + s.to(torch.int64)).to(torch.int64)
+    ge = (off[c.to(torch.int64)] + e.to(torch.int64)).to(torch.int64)
+    rows = torch.arange(n, device="cuda", dtype=torch.int64) * 3 + 7
+    t32 = [torch.where(x >= 2**31, x - 2**32, x).to(torch.int32) for x in (gs, ge, rows)]
+    torch.cuda.synchronize()  # (torch's stream is not the engine's)
+    S = ctx.set_from_global(sp, n, *(t.data_ptr() for t in t32))
+    og, oe, orow = (torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    S.copy_rows_device(0, n, og.data_ptr(), oe.data_ptr(), orow.data_ptr())
+    torch.cuda.synchronize()
+    S.close()
+    g64, e64, r64 = (x.to(torch.int64) & 0xFFFFFFFF for x in (og, oe, orow))
+    key = g64 * 2 + (e64 > g64).to(torch.int64)
+    assert bool((key[1:] >= key[:-1]).all())
+    tie = key[1:] == key[:-1]
+    assert bool((r64[1:][tie] > r64[:-1][tie]).all())
+    i = (r64 - 7) // 3
+    assert bool(((r64 - 7) % 3 == 0).all())
+    assert bool((torch.sort(i).values == torch.arange(n, device="cuda")).all())
+    assert bool((g64 == gs[i]).all()) and bool((e64 == ge[i]).all())

@@ -47,7 +47,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", default="c2", choices=["c2", "c5"])
+    p.add_argument("--workload", default="c2", choices=["c2", "c5", "c3", "sub"],
+                   help="c2: intersect + merge (the metric); c5: 8-way AND; c3: merge side "
+                        "(sort + merge + carry + run ids + complement) of C3's pile-ups; sub: "
+                        "subtract (lime mode) of C2's inputs")
+    p.add_argument("--no-ops", action="store_true",
+                   help="c2: skip the short c3 / sub lines reported under 'operators'")
+    p.add_argument("--ops-steps", type=int, default=3)
     p.add_argument("--rows", type=int, default=None,
                    help="rows per set (C2: 1e8; C5: 1.25e8, 8 sets)")
     p.add_argument("--chunk", type=int, default=1 << 31, help="pairs per output chunk")
@@ -237,29 +243,40 @@ def main():
         e.record(stream)
         return e
 
-    if args.workload == "c5":
-        run = bench_c5(args, ctx, space, dev, world, rank, comm_dev, ev)
-    else:
-        run = bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev)
-    step, finish = run
+    def measure(step, steps, warmup):
+        """warmup untimed steps, then `steps` timed ones bracketed by a
+        barrier + device sync; the max over ranks"""
+        for _ in range(warmup):
+            step(False)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i == steps - 1)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], dtype=torch.float64, device=comm_dev or dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt
 
-    for _ in range(args.warmup):
-        step(False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i == args.steps - 1)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=comm_dev or dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    line = finish(dt)
+    benches = {"c2": bench_c2, "c5": bench_c5, "c3": bench_c3, "sub": bench_sub}
+    step, finish = benches[args.workload](args, ctx, space, dev, world, rank, comm_dev, ev)
+    line = finish(measure(step, args.steps, args.warmup))
+    if args.workload == "c2" and not args.no_ops:
+        # the other operators north_star names, short lines at the same N
+        # (the driver's scaling runs record them beside the metric)
+        finish.release()
+        ops = {}
+        for name, fn in (("merge_side_c3", bench_c3), ("subtract_c2", bench_sub)):
+            st, fi = fn(args, ctx, space, dev, world, rank, comm_dev, ev, brief=True)
+            ops[name] = fi(measure(st, args.ops_steps, 1))
+            fi.release()
+        line["operators"] = ops
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
@@ -399,6 +416,12 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
             "sort_roofline": sort_roof,
             "cpu_baseline": cpu,
         }
+
+    def release():  # the output buffer and inputs, before other workloads run
+        nonlocal buf, A_in, B_in
+        buf = A_in = B_in = None
+        torch.cuda.empty_cache()
+    finish.release = release
     return step, finish
 
 
@@ -479,6 +502,168 @@ def pmc_traffic(name, field, world):
     if "key_kernel" in d:
         src["kernel"] = d["key_kernel"]
     return d.get(field), src
+
+
+def _count_all(x, world, comm_dev, dev):
+    """a per-rank count summed over the ranks"""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64, device=comm_dev or dev)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def bench_c3(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
+    """north_star's merge side on C3's input (5e8 ChIP-seq-like pile-up rows:
+    2e6 centres, N(0,150) offsets, len U[150,600], seed 0xC): sort, merge with
+    every row's run id and the complement's gaps (Merge.scala:34-36,
+    Complement.scala:131-134).  N > 1: the rows range-sharded, the merge
+    carried across shards (one all_gather), global run ids, the sharded
+    complement from the carry."""
+    import torch
+    n = args.rows if (args.rows and not brief) else 500_000_000
+    first, last = rank * n // world, (rank + 1) * n // world
+    m = last - first
+    cols = [torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3)]
+    ctx.synth_pileup_rows(space, first, m, 0xC, 2_000_000, 150, 150, 600,
+                          *(c.data_ptr() for c in cols))
+    torch.cuda.synchronize(dev)
+    shard = None
+    if world > 1:
+        from lime_amd.sharded import ShardStep
+        shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
+    state = {"runs": 0, "gaps": 0, "t": None}
+
+    def step(last_step):
+        t0 = ev() if last_step else None
+        if shard is not None:
+            S = shard.load(m, *(c.data_ptr() for c in cols), row_base=first)
+            mg = shard.merge(S)
+            _, ids = shard.global_run_ids(mg, S.n)
+            gaps = shard.complement(S, mg)
+            runs, ng = mg["runs"], gaps.n
+            for h in (gaps, mg["result"], S):
+                h.close()
+            del ids
+        else:
+            S = ctx.set_from_device(space, m, *(c.data_ptr() for c in cols))
+            mg = ctx.merge(S)
+            gaps = ctx.complement(space, S)
+            runs, ng = mg.n, gaps.n
+            for h in (gaps, mg, S):
+                h.close()
+        if last_step:
+            state["t"] = (t0, ev())
+        state["runs"], state["gaps"] = runs, ng
+
+    def finish(dt):
+        steps = args.ops_steps if brief else args.steps
+        ms = dt / steps * 1e3
+        runs = _count_all(state["runs"], world, comm_dev, dev)
+        gaps = _count_all(state["gaps"], world, comm_dev, dev)
+        # per row: sort 24 B, merge 8 B read + 4 B run id; 8 B per run and gap
+        alg = 36 * n + 8 * (runs + gaps)
+        achieved = alg / world / (ms * 1e-3) / 1e9
+        out = {"metric": "intervals/sec, merge side (sort + merge + run ids + complement) of "
+                         "BASELINE C3", "value": n / (dt / steps), "unit": "intervals/s",
+               "n_gpus": world, "steps": steps, "ms_per_step": ms, "higher_is_better": True,
+               "scaling": "strong", "rows": n, "runs": runs, "gaps": gaps,
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                            "kernel": "whole step per GPU",
+                            "alg_bytes_per_step_per_gpu": alg / world}}
+        if not brief:
+            out.update({"warmup": args.warmup, "vs_baseline": None, "dtype": "u32",
+                        "data": "synthetic (counter-based splitmix64 pile-ups, seed 0xC; rank r "
+                                "generates rows [r n/N, (r+1) n/N) of the one input)",
+                        "config": {"workload": "C3: merge side of 5e8 pile-up intervals "
+                                               "(2e6 centres, N(0,150), len U[150,600]), hg38"
+                                               + (", range-sharded" if world > 1 else ""),
+                                   "parallelism": f"range-shard x{world}" if world > 1
+                                   else "1 GPU"}})
+        return out
+
+    def release():
+        cols.clear()
+        torch.cuda.empty_cache()
+    finish.release = release
+    return step, finish
+
+
+def bench_sub(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
+    """north_star's difference: DistributedSubtract (lime mode,
+    Subtract.scala:78-116) of C2's inputs (2 x 1e8 rows uniform over hg38,
+    len U[50,5000]): sort both, A minus B, every remnant materialised.  N > 1:
+    both sets range-sharded, B with its left and right halos (rows of other
+    shards reaching into the shard), outputs disjoint by A row."""
+    import torch
+    n = args.rows if (args.rows and not brief) else 100_000_000
+    first, last = rank * n // world, (rank + 1) * n // world
+    m = last - first
+
+    def gen(seed):
+        cols = [torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3)]
+        ctx.synth_uniform_rows(space, first, m, seed, 50, 5000, *(c.data_ptr() for c in cols))
+        return cols
+    A_in, B_in = gen(0xA), gen(0xB)
+    torch.cuda.synchronize(dev)
+    shard = None
+    if world > 1:
+        from lime_amd.sharded import ShardStep
+        shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
+    state = {"records": 0}
+
+    def step(last_step):
+        if shard is not None:
+            A = shard.load(m, *(c.data_ptr() for c in A_in), row_base=first)
+            B = shard.load(m, *(c.data_ptr() for c in B_in), row_base=first)
+            res, _, Be = shard.subtract(A, B)
+            hs = (res, Be, A, B) if Be is not B else (res, A, B)
+        else:
+            A = ctx.set_from_device(space, m, *(c.data_ptr() for c in A_in))
+            B = ctx.set_from_device(space, m, *(c.data_ptr() for c in B_in))
+            res = ctx.subtract(A, B)
+            hs = (res, A, B)
+        state["records"] = res.n
+        for h in hs:
+            h.close()
+
+    def finish(dt):
+        steps = args.ops_steps if brief else args.steps
+        ms = dt / steps * 1e3
+        rec = _count_all(state["records"], world, comm_dev, dev)
+        # sort 24 B per row of both sets; A rows read 12 B, B 16 B (rows and
+        # prefix max); 16 B per record
+        alg = 48 * n + 28 * n + 16 * rec
+        achieved = alg / world / (ms * 1e-3) / 1e9
+        out = {"metric": "intervals/sec, DistributedSubtract (lime mode) of BASELINE C2's "
+                         "inputs", "value": 2 * n / (dt / steps), "unit": "intervals/s",
+               "n_gpus": world, "steps": steps, "ms_per_step": ms, "higher_is_better": True,
+               "scaling": "strong", "rows_per_set": n, "records": rec,
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                            "kernel": "whole step per GPU",
+                            "alg_bytes_per_step_per_gpu": alg / world}}
+        if not brief:
+            out.update({"warmup": args.warmup, "vs_baseline": None, "dtype": "u32",
+                        "data": "synthetic (counter-based splitmix64, seeds 0xA/0xB; rank r "
+                                "generates rows [r n/N, (r+1) n/N) of each input)",
+                        "config": {"workload": "subtract (lime mode) of C2's inputs: 2 x 1e8 "
+                                               "intervals, uniform over hg38, len U[50,5000]"
+                                               + (", range-sharded with halos" if world > 1
+                                                  else ""),
+                                   "parallelism": f"range-shard x{world}" if world > 1
+                                   else "1 GPU"}})
+        return out
+
+    def release():
+        A_in.clear()
+        B_in.clear()
+        torch.cuda.empty_cache()
+    finish.release = release
+    return step, finish
 
 
 def synth_lengths():

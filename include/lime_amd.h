@@ -45,7 +45,7 @@ extern "C" {
 
 /* 2: lime_set_lower_bound / _first_reaching return -(LIME_ERR_*) on error
  *    (was -1); lime_pairs_checksum_device and the sharded-path helpers added */
-#define LIME_ABI_VERSION 2
+#define LIME_ABI_VERSION 3
 
 /* status codes */
 #define LIME_OK 0
@@ -160,6 +160,23 @@ int lime_set_first_reachings(const lime_set *set, int32_t k, const uint32_t *gke
 /* device-to-device copy of sorted rows [first, first + count) */
 int lime_set_copy_rows_device(const lime_set *set, int64_t first, int64_t count, uint32_t *d_gstart,
                               uint32_t *d_gend, uint32_t *d_row);
+/* Width statistics gathered when the set was built: min and max of end -
+ * start, and whether any row has zero width. */
+int lime_set_stats(const lime_set *set, uint32_t *min_width, uint32_t *max_width,
+                   int32_t *has_zero_width);
+/* A new plain set: the rows of `set` followed by n more rows (device arrays
+ * in global coordinates and caller row ids) that the CALLER guarantees to be
+ * in canonical order and to start at or after the set's last row -- a
+ * coordinate shard's own rows followed by its right halo (rows of later
+ * shards).  Nothing is sorted or validated and nothing is read back (no
+ * stream drain): the rows are copied device-to-device, and the width
+ * statistics are `set`'s combined with the caller's bounds for the added rows
+ * (min_width / max_width / has_zero_width of those rows, or bounds of them).
+ * Replaces rebuilding the shard's set (lime_set_create_global: a validating
+ * pass and a read-back) in the sharded pairwise step. */
+int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const uint32_t *d_gstart,
+                           const uint32_t *d_gend, const uint32_t *d_row, uint32_t min_width,
+                           uint32_t max_width, int32_t has_zero_width, lime_set **out);
 /* Device pointers of the sorted set: global start, global end, input row. */
 int lime_set_device_arrays(const lime_set *set, const uint32_t **gstart, const uint32_t **gend,
                            const uint32_t **row);

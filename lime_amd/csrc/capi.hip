@@ -576,6 +576,69 @@ int lime_set_device_arrays(const lime_set *s, const uint32_t **gs, const uint32_
     return LIME_OK;
 }
 
+int lime_set_stats(const lime_set *s, uint32_t *min_width, uint32_t *max_width,
+                   int32_t *has_zero_width) {
+    if (!s) return fail(LIME_ERR_ARG, "set is null");
+    if (min_width) *min_width = s->min_width;
+    if (max_width) *max_width = s->max_width;
+    if (has_zero_width) *has_zero_width = s->has_zero_width ? 1 : 0;
+    return LIME_OK;
+}
+
+int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const uint32_t *d_gs,
+                           const uint32_t *d_ge, const uint32_t *d_row, uint32_t min_width,
+                           uint32_t max_width, int32_t has_zero_width, lime_set **out) {
+    if (!ctx || !set || !out || n < 0 || (n > 0 && (!d_gs || !d_ge || !d_row)))
+        return fail(LIME_ERR_ARG, "bad set arguments");
+    if (set->ctx != ctx) return fail(LIME_ERR_ARG, "set belongs to another context");
+    if (set->strand_in || set->row_ties || set->min_shift)
+        return fail(LIME_ERR_ARG, "only plain sets extend");
+    const int64_t m = set->n + n;
+    if (m > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
+    hipSetDevice(ctx->device);
+    lime_set *s = new lime_set();
+    s->ctx = ctx;
+    s->n = m;
+    s->n_contigs = set->n_contigs;
+    s->off = set->off;
+    s->len = set->len;
+    s->d_off = set->d_off;
+    s->space_keep = set->space_keep;
+    s->min_width = set->n ? set->min_width : min_width;
+    s->max_width = set->max_width;
+    s->has_zero_width = set->has_zero_width;
+    if (n > 0) {
+        if (set->n) s->min_width = std::min(s->min_width, min_width);
+        s->max_width = std::max(s->max_width, max_width);
+        s->has_zero_width = s->has_zero_width || has_zero_width != 0;
+    }
+    int rc = alloc(ctx, &s->gs, (size_t)std::max<int64_t>(m, 1));
+    if (rc == LIME_OK) rc = alloc(ctx, &s->ge, (size_t)std::max<int64_t>(m, 1));
+    if (rc == LIME_OK) rc = alloc(ctx, &s->row, (size_t)std::max<int64_t>(m, 1));
+    if (rc != LIME_OK) {
+        lime_set_destroy(s);
+        return rc;
+    }
+    const size_t a = 4 * (size_t)set->n, b = 4 * (size_t)n;
+    hipError_t e = hipSuccess;
+    if (a) {
+        e = hipMemcpyAsync(s->gs, set->gs, a, hipMemcpyDeviceToDevice, S(ctx));
+        if (e == hipSuccess) e = hipMemcpyAsync(s->ge, set->ge, a, hipMemcpyDeviceToDevice, S(ctx));
+        if (e == hipSuccess) e = hipMemcpyAsync(s->row, set->row, a, hipMemcpyDeviceToDevice, S(ctx));
+    }
+    if (b && e == hipSuccess) {
+        e = hipMemcpyAsync(s->gs + set->n, d_gs, b, hipMemcpyDeviceToDevice, S(ctx));
+        if (e == hipSuccess) e = hipMemcpyAsync(s->ge + set->n, d_ge, b, hipMemcpyDeviceToDevice, S(ctx));
+        if (e == hipSuccess) e = hipMemcpyAsync(s->row + set->n, d_row, b, hipMemcpyDeviceToDevice, S(ctx));
+    }
+    if (e != hipSuccess) {
+        lime_set_destroy(s);
+        return fail(LIME_ERR_DEVICE, std::string("lime_set_extend_sorted copy: ") + hipGetErrorString(e));
+    }
+    *out = s;
+    return LIME_OK;
+}
+
 int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const uint32_t *d_gs,
                            const uint32_t *d_ge, const uint32_t *d_row, lime_set **out) {
     if (!ctx || !sp || !out || n < 0 || (n > 0 && (!d_gs || !d_ge || !d_row)))

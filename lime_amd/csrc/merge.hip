@@ -81,49 +81,13 @@ __device__ __forceinline__ void load_blocked(const T *__restrict__ src, int64_t 
 }
 
 // ---------------------------------------------------------- single pass
-constexpr uint64_t ST_AGG = 1ull << 62;  // tile aggregate published
-constexpr uint64_t ST_INC = 2ull << 62;  // inclusive prefix published
-constexpr uint64_t ST_VAL = (1ull << 62) - 1;
-
-__device__ __forceinline__ void st_publish(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t st_poll(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Decoupled look-back by one wave: combine (max or sum) of the values of
-// every tile before `tile`.  Lane l inspects tile base - l; a window of 64
-// predecessors is consumed once all of them have published at least an
-// aggregate, and the walk stops at the nearest inclusive prefix.  Tiles are
-// numbered in ticket order, so every predecessor is already running and
-// publishes without waiting on this tile: the spin always ends.
-template <bool MAX>
-__device__ __forceinline__ uint64_t lookback(const uint64_t *st, int64_t tile) {
-    const int lane = dev::lane_id();
-    uint64_t acc = 0;
-    for (int64_t base = tile - 1; base >= 0; base -= 64) {
-        const int64_t i = base - lane;
-        uint64_t v = ST_INC;  // before tile 0: inclusive identity
-        if (i >= 0) {
-            v = st_poll(st + i);
-            while ((v >> 62) == 0) {
-                __builtin_amdgcn_s_sleep(1);
-                v = st_poll(st + i);
-            }
-        }
-        const uint64_t inc = __ballot((v >> 62) == 2);
-        uint64_t val = v & ST_VAL;
-        if (inc) {
-            const int first = __ffsll((unsigned long long)inc) - 1;
-            if (lane > first) val = 0;
-        }
-        const uint64_t r = MAX ? dev::wave_reduce_max(val) : dev::wave_reduce_sum(val);
-        acc = MAX ? (acc > r ? acc : r) : acc + r;
-        if (inc) break;
-    }
-    return acc;
-}
+// (decoupled look-back: dev::lookback and the status words, common.hpp)
+using dev::ST_AGG;
+using dev::ST_INC;
+using dev::ST_VAL;
+using dev::st_publish;
+using dev::st_poll;
+using dev::lookback;
 
 struct MergeScanArgs {
     const uint32_t *gs, *ge;

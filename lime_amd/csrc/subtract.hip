@@ -565,7 +565,9 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
         staged = total <= (uint64_t)SCAP;
         pos = bbase + (int64_t)(before + inc - n_out);
         end = pos + (int64_t)n_out;
-        if (fold(true) != n_out) atomicOr(sa.err, 1u);
+        // (a row without records -- covered by B in lime mode: 85 % of the
+        // sparse 1e9-row subtract's rows -- has nothing to fold for)
+        if (n_out > 0 && fold(true) != n_out) atomicOr(sa.err, 1u);
     }
     if (staged) {  // the block's records, lane-consecutive
         __syncthreads();
@@ -744,6 +746,278 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     }
 }
 
+// RUNS (threshold <= 0), count and write in ONE pass: the workgroup of
+// k_sub_count_runs (CNT_ROWS left rows, their B window staged once, each
+// lane's bounds by lockstep searches) counts every row's records, places its
+// rows by a workgroup scan and its tile by a decoupled look-back over the
+// per-tile totals (tiles in ticket order), then folds again, writing, only
+// the rows that have records.  (The two-kernel form re-staged a window per
+// 256 rows and folded every row again: on the sparse 1e9-row subtract, 0.15
+// records per left row, its write pass took twice its count pass.)  Records
+// are staged in LDS and stored coalesced when the tile's fit in FCAP, else
+// stored where they fall.  The output arrays are sized before the launch
+// (cap records): nothing is stored past cap, the exact total comes back
+// through `total`, and the caller runs the pass again at that size.
+// (26 KiB of LDS in all: six workgroups per CU; at 64 records and eight per
+// CU the sparse 1e9-row subtract took the same time)
+constexpr int FCAP = 448;
+// 1024 left rows per tile, the count pass's window (2048-row tiles with a
+// 3072-row window: the sparse 1e9-row subtract's pass 9.6 -> 10.2 ms)
+constexpr int FW = 4, FROWS = FW * SUB_B, FWIN = 1536;
+struct FusedArgs {
+    uint64_t *st;          // per-tile status words (zeroed)
+    unsigned int *ticket;  // tile ticket (zeroed)
+    uint64_t *total;       // every tile's records (stored by the last tile)
+    uint64_t cap;          // output capacity (records)
+    int64_t ntiles;
+};
+
+__global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa) {
+    __shared__ uint32_t w_pm[FWIN], w_gs[FWIN], w_run[FWIN];
+    __shared__ uint32_t f_gs[FCAP], f_ge[FCAP], f_ar[FCAP], f_br[FCAP];
+    __shared__ uint64_t s_wtot[FW];
+    __shared__ uint64_t s_base;
+    __shared__ uint32_t s_tile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(fa.ticket, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int wv = threadIdx.x / 64, lane = dev::lane_id();
+    const int64_t base = tile * FROWS + (int64_t)wv * SUB_B;
+    constexpr int RPL = SUB_B / 64;  // rows per lane: row base + k 64 + lane
+    uint32_t as[RPL], ae[RPL];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+        const int64_t i = base + k * 64 + lane;
+        as[k] = ae[k] = 0;
+        if (i < sa.na) {
+            as[k] = sa.ags[i];
+            ae[k] = sa.age[i];
+        }
+    }
+    const int64_t wlo = sa.wstart[tile];
+    const int nst = (int)min((int64_t)FWIN, sa.nb - wlo);
+    for (int k = threadIdx.x; k < nst; k += FW * 64) {
+        w_pm[k] = sa.bpmax[wlo + k];
+        w_gs[k] = sa.bgs[wlo + k];
+        w_run[k] = sa.brun[wlo + k];
+    }
+    __syncthreads();
+    const int64_t whi = wlo + nst;
+    auto in = [&](int64_t j) { return j >= wlo && j < whi; };
+    auto PM = [&](int64_t j) { return in(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
+    auto GS = [&](int64_t j) { return in(j) ? w_gs[j - wlo] : sa.bgs[j]; };
+    auto RUN = [&](int64_t j) { return in(j) ? w_run[j - wlo] : sa.brun[j]; };
+    auto NX = [&](int64_t j, int64_t hi1) -> int64_t {  // end of j's run, cut at hi1
+        const uint32_t r = RUN(j);
+        if (RUN(hi1 - 1) == r) return hi1;
+        int64_t l = j + 1, h = hi1 - 1;
+        while (l < h) {
+            const int64_t m = (l + h) >> 1;
+            if (RUN(m) > r)
+                h = m;
+            else
+                l = m + 1;
+        }
+        return l;
+    };
+    const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
+    int bl[RPL], bh[RPL], bp[RPL];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = bp[k] = 0;
+    for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            if (bl[k] + step <= nst && w_gs[bl[k] + step - 1] < as[k]) bl[k] += step;
+            if (bh[k] + step <= nst && w_gs[bh[k] + step - 1] < ae[k]) bh[k] += step;
+            if (bp[k] + step <= nst && w_pm[bp[k] + step - 1] <= as[k]) bp[k] += step;
+        }
+    }
+    // a row's fold (k_subtract<_, true>'s, over this window): counts its
+    // records, or with `wr` emits them into [pos, end) -- tile-local
+    // positions in the LDS stage when `staged`, else global ones
+    auto fold = [&](int k, bool wr, uint64_t pos, uint64_t end, uint32_t ar,
+                    bool staged) -> uint64_t {
+        const uint32_t a_s = as[k], a_e = ae[k];
+        int64_t lo1 = bl[k] < nst ? wlo + bl[k] : dev::lower_bound(sa.bgs, whi, sa.nb, (int64_t)a_s);
+        int64_t hi1 = lo1;
+        if (a_e > a_s)
+            hi1 = bh[k] < nst ? wlo + bh[k]
+                              : dev::lower_bound(sa.bgs, max(lo1, whi), sa.nb, (int64_t)a_e);
+        if (sa.zw) {
+            while (lo1 < sa.nb && GS(lo1) == a_s && sa.bge[lo1] == a_s) ++lo1;
+            if (hi1 < lo1) hi1 = lo1;
+        }
+        const uint32_t thr = a_s;  // threshold <= 0
+        auto emit = [&](uint32_t s, uint32_t e, uint32_t br, uint64_t at) {
+            if (staged) {
+                const uint32_t li = (uint32_t)at;
+                f_gs[li] = s;
+                f_ge[li] = e;
+                f_ar[li] = ar;
+                f_br[li] = br;
+            } else if (at < fa.cap) {
+                sa.ogs[at] = s;
+                sa.oge[at] = e;
+                sa.oar[at] = ar;
+                sa.obr[at] = br;
+            }
+        };
+        bool any = false;
+        uint32_t bs = 0, be = 0, hr = 0, he = 0, setpos = a_s;  // block, head row and end
+        uint64_t cum = 0;
+        auto close_block = [&]() {
+            if (lime_mode) {
+                const uint32_t r = (bs > a_s) + (a_e > be);
+                if (wr) {
+                    uint64_t at = end - cum - r;
+                    if (bs > a_s) emit(a_s, bs, hr, at++);
+                    if (a_e > be) emit(be, a_e, hr, at++);
+                }
+                cum += r;
+            } else {
+                if (bs > setpos) {
+                    if (wr) emit(setpos, bs, hr, pos + cum);
+                    ++cum;
+                }
+                if (be > setpos) setpos = be;
+            }
+        };
+        // the spanning block: first j in [wlo, lo1) with pmax > thr; its head
+        // the min (end, row) among its same-start rows
+        const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
+        if (lo1 > 0 && pm_last > thr) {
+            const int64_t j0 = bp[k] < nst ? wlo + bp[k] : first_spanning(sa.bpmax, lo1, thr);
+            any = true;
+            bs = GS(j0);
+            be = pm_last;
+            if (wr) {
+                hr = sa.brow[j0];
+                he = sa.bge[j0];
+                int64_t j = j0 + 1;
+                for (; j < lo1 && j <= j0 + TIE_G && GS(j) == bs; ++j) {
+                    const uint32_t g2 = sa.bge[j], r2 = sa.brow[j];
+                    if (g2 > thr && (g2 < he || (g2 == he && r2 < hr))) {
+                        hr = r2;
+                        he = g2;
+                    }
+                }
+                if (j < lo1 && GS(j) == bs) tie_head(sa, bs, thr, hr, he);  // a long group
+            }
+        }
+        int64_t j = lo1;
+        // the spanning block goes on through the inside rows of its run
+        if (any && j < hi1 && RUN(j) == RUN(lo1 - 1)) {
+            const int64_t nx = NX(j, hi1);
+            be = max(be, PM(nx - 1));
+            j = nx;
+        }
+        while (j < hi1) {
+            const int64_t nx = NX(j, hi1);
+            const uint32_t gs = GS(j);
+            if (!any) {  // foldLeft(List(head)): the head is folded against itself
+                any = true;
+                const uint32_t ge = sa.bge[j];
+                if (ge == gs) {  // a zero-width head closes a duplicate of itself
+                    bs = be = gs;
+                    if (wr) {
+                        hr = sa.brow[j];
+                        he = ge;
+                    }
+                    close_block();
+                }
+            } else {
+                close_block();
+            }
+            bs = gs;
+            be = PM(nx - 1);  // (the inclusive prefix max: >= the head's end)
+            if (wr) {  // the head among the run's same-start non-empty hits: min (end, row)
+                hr = sa.brow[j];
+                he = sa.bge[j];
+                if (he > bs) {
+                    int64_t q = j + 1;
+                    for (; q < nx && q <= j + TIE_G && GS(q) == bs; ++q) {
+                        const uint32_t e2 = sa.bge[q], r2 = sa.brow[q];
+                        if (e2 < he || (e2 == he && r2 < hr)) {
+                            hr = r2;
+                            he = e2;
+                        }
+                    }
+                    if (q < nx && GS(q) == bs) tie_head(sa, bs, bs, hr, he);  // a long group
+                }
+            }
+            j = nx;
+        }
+        if (any) {
+            close_block();
+            if (!lime_mode && a_e > setpos) {
+                if (wr) emit(setpos, a_e, hr, pos + cum);
+                ++cum;
+            }
+            return cum;
+        }
+        if (wr) emit(a_s, a_e, 0xffffffffu, pos);  // no hit: (L, None)
+        return 1;
+    };
+    // counts, then each row's place: rows in order (k, lane) within a wave,
+    // waves in order within the tile
+    uint64_t cnt[RPL], ex[RPL], run = 0;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+        cnt[k] = base + k * 64 + lane < sa.na ? fold(k, false, 0, 0, 0, false) : 0;
+        const uint64_t inc = dev::wave_inclusive_sum(cnt[k]);
+        ex[k] = run + inc - cnt[k];
+        run += dev::lane63(inc);
+    }
+    if (lane == 0) s_wtot[wv] = run;
+    __syncthreads();
+    uint64_t wpre = 0, T = 0;
+#pragma unroll
+    for (int w = 0; w < FW; ++w) {
+        if (w < wv) wpre += s_wtot[w];
+        T += s_wtot[w];
+    }
+    // the tile's place: its total published at once; the look-back (wave 0)
+    // runs before the writing folds only when they store to global memory
+    // directly, else after them (the folds stage tile-local records in LDS
+    // meanwhile, and the predecessors have published by then)
+    const bool staged = T <= (uint64_t)FCAP;
+    auto place = [&]() {
+        if (wv == 0) {
+            const uint64_t excl = tile > 0 ? dev::lookback<false>(fa.st, tile) : 0;
+            if (lane == 0) {
+                if (tile > 0) dev::st_publish(fa.st + tile, dev::ST_INC | (excl + T));
+                if (tile == fa.ntiles - 1) *fa.total = excl + T;
+                s_base = excl;
+            }
+        }
+        __syncthreads();
+    };
+    if (wv == 0 && lane == 0)
+        dev::st_publish(fa.st + tile, (tile == 0 ? dev::ST_INC : dev::ST_AGG) | T);
+    if (!staged) place();
+    const uint64_t tb = staged ? 0 : s_base;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+        if (cnt[k] == 0) continue;
+        const int64_t i = base + k * 64 + lane;
+        const uint64_t pos = tb + wpre + ex[k];
+        if (fold(k, true, pos, pos + cnt[k], sa.arow[i], staged) != cnt[k])
+            atomicOr(sa.err, 1u);  // (the two folds disagree: flagged, not written past)
+    }
+    if (staged) {  // the tile's records, lane-consecutive
+        place();  // (its barrier also orders the staged records)
+        const uint64_t gb = s_base;
+        for (int q = threadIdx.x; q < (int)T; q += FW * 64) {
+            const uint64_t at = gb + q;
+            if (at >= fa.cap) break;
+            sa.ogs[at] = f_gs[q];
+            sa.oge[at] = f_ge[q];
+            sa.oar[at] = f_ar[q];
+            sa.obr[at] = f_br[q];
+        }
+    }
+}
+
 // whether any same-start group has more than TIE_G rows: gs[j] == gs[j +
 // TIE_G] for some j (4 rows per thread, 16-B loads; reads gs once: the tie
 // index's flag + scan passes run only when it does)
@@ -900,9 +1174,24 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
     if (!inl) LIME_TRY(owner_ranges(ctx, A, B, 0, threshold, olo, ocnt));
     const int64_t nblk = (na + SUB_B - 1) / SUB_B;
-    // window starts: per block, or per count workgroup (CNT_WAVES blocks)
-    // with inline ranges
-    const int stride = inl ? CNT_WAVES : 1;
+    // runs: B's merge runs with their run ids and B's prefix max (one scan)
+    lime_result mb;
+    mb.ctx = ctx;
+    PoolGuard<uint32_t> g1{ctx, mb.run_of_sorted};
+    PoolGuard<uint32_t> g2{ctx, mb.gs};
+    PoolGuard<uint32_t> g3{ctx, mb.ge};
+    if (runs) LIME_TRY(merge_runs_with_pmax(ctx, B, &mb));
+    // runs, one pass (k_sub_fused) when records are plentiful (they come
+    // from A rows crossing the ends of B's runs: the sparse 1e9-row subtract,
+    // 9.2e6 runs of B, 7.4e7 records for 5e8 rows); B merging into fewer runs
+    // than A's rows / 64 (B covers A deeply: C2's inputs, 16 records for 1e8
+    // rows) leaves most tiles without a record, and there the count pass + a
+    // write pass that skips them wins (1.0 vs 1.4 ms on C2's inputs: no
+    // tickets, no look-back)
+    const bool fused = runs && mb.n * 64 >= na;
+    // window starts: per block; per count workgroup (CNT_WAVES blocks) or
+    // fused tile (FW blocks) with inline ranges
+    const int stride = fused ? FW : inl ? CNT_WAVES : 1;
     const int64_t nws = (nblk + stride - 1) / stride;
     uint32_t *wstart;
     LIME_TRY(alloc(ctx, &wstart, (size_t)nws));
@@ -948,15 +1237,52 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.ogs = sa.oge = sa.oar = sa.obr = nullptr;
     sa.brun = nullptr;
     sa.zw = B->has_zero_width ? 1 : 0;
-    lime_result mb;
-    mb.ctx = ctx;
-    PoolGuard<uint32_t> g1{ctx, mb.run_of_sorted};
-    PoolGuard<uint32_t> g2{ctx, mb.gs};
-    PoolGuard<uint32_t> g3{ctx, mb.ge};
     if (runs) {
-        LIME_TRY(merge_runs_with_pmax(ctx, B, &mb));
         sa.bpmax = B->pmax;  // built by the merge scan when it was not yet
         sa.brun = mb.run_of_sorted;
+    }
+    if (fused) {  // one pass: counts, places (look-back) and records
+        const int64_t ntiles = blocks_for(na, FROWS);
+        uint64_t *st;
+        LIME_TRY(alloc(ctx, &st, (size_t)ntiles + 2));  // + ticket, total
+        PoolGuard<uint64_t> gs_{ctx, st};
+        FusedArgs fa;
+        fa.st = st;
+        fa.ticket = reinterpret_cast<unsigned int *>(st + ntiles);
+        fa.total = st + ntiles + 1;
+        fa.ntiles = ntiles;
+        // records rarely pass one per left row; past the guess the pass runs
+        // again at the exact total
+        uint64_t cap = (uint64_t)na + 4096, total = 0;
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            LIME_TRY(alloc(ctx, &res->gs, (size_t)cap));
+            LIME_TRY(alloc(ctx, &res->ge, (size_t)cap));
+            LIME_TRY(alloc(ctx, &res->a_row, (size_t)cap));
+            LIME_TRY(alloc(ctx, &res->b_row, (size_t)cap));
+            sa.ogs = res->gs;
+            sa.oge = res->ge;
+            sa.oar = res->a_row;
+            sa.obr = res->b_row;
+            fa.cap = cap;
+            LIME_HIP(hipMemsetAsync(st, 0, 8 * ((size_t)ntiles + 2), S(ctx)));
+            hipLaunchKernelGGL(k_sub_fused, dim3((unsigned)ntiles), dim3(FW * 64), 0, S(ctx), sa,
+                               fa);
+            LIME_HIP(hipGetLastError());
+            LIME_TRY(read_back(ctx, &total, fa.total, sizeof(total)));
+            if (total <= cap) break;
+            release(ctx, res->gs);
+            release(ctx, res->ge);
+            release(ctx, res->a_row);
+            release(ctx, res->b_row);
+            cap = total;
+        }
+        unsigned int e = 0;
+        LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
+        if (e) return fail(LIME_ERR_DEVICE, "subtract: the writing fold differs from the count");
+        release(ctx, cnt);
+        release(ctx, off);
+        res->n = (int64_t)total;
+        return LIME_OK;
     }
     auto launch = [&](bool write) {
         const dim3 g(blocks_for(na, SUB_B)), b(SUB_B);

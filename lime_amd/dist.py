@@ -133,75 +133,118 @@ class TensorRuns:
 
 
 def carry_table(runs, group=None, k=256, device=None, stranded=False):
-    """Every shard's view of the cross-shard merge carry (sorted, disjoint
-    runs per shard, shards in coordinate order).  `runs` has `.n`,
-    `.last_end`, `.head(k) -> (starts, ends)` and, when stranded,
-    `.last_strand` and `.head_strands(k)`.
+    """Every shard's view of the cross-shard merge carry of one set: see
+    carry_tables (one set, no extra values)."""
+    return carry_tables([runs], group, k, device, stranded)[0][0]
+
+
+def _payload_host(runs, k, stranded):
+    """the gathered words of one set: n, last end, last strand, the first k
+    run starts, ends and strands (-1 past the runs)"""
+    n = runs.n
+    kk = min(k, n)
+    h = [-1] * (3 * k + 3)
+    h[0] = n
+    h[1] = runs.last_end if n else -1
+    h[2] = getattr(runs, "last_strand", 0) if stranded and n else 0
+    if kk:
+        hs, he = runs.head(kk)
+        h[3:3 + kk] = hs
+        h[3 + k:3 + k + kk] = he
+        if stranded:
+            h[3 + 2 * k:3 + 2 * k + kk] = runs.head_strands(kk)
+    return h
+
+
+def carry_tables(runs_list, group=None, k=256, device=None, stranded=False, extra=()):
+    """The cross-shard merge carry of several sets (sorted, disjoint runs per
+    shard, shards in coordinate order) in ONE all_gather, plus `extra` small
+    integers per shard gathered along (e.g. the sets' width bounds).  Each
+    element of `runs_list` has `.n`, `.last_end`, `.head(k) -> (starts, ends)`
+    and, when stranded, `.last_strand` and `.head_strands(k)`; or a
+    `.payload(k, device)` method returning those 3 k + 3 words as an int64
+    tensor (built on the device: no host copy before the collective).
 
     The reference folds the sorted rows into runs with Merge.condition =
     overlaps (SetTheory.scala:208-225, strands equal), so a shard's leading
     run continues the run open at its left bound iff that run's end passes
     its start (and, stranded, it has the open run's strand).  One
-    all_gather of (n, last end, last strand, the first k runs) per shard; k
-    doubles and the gather repeats only while a shard's k leading runs are
-    all absorbed.  Returns a list over shards of (n, drop, ext, first_kept,
-    last_kept): shard r drops its first `drop` runs, ends its last kept run at
-    `ext` (None: unchanged), and keeps n - drop runs from first_kept (start)
-    to last_kept (end) -- None when it keeps none."""
+    all_gather of (n, last end, last strand, the first k runs) per shard and
+    set; k doubles and the gather repeats only while some shard's k leading
+    runs of some set are all absorbed.  Returns (tables, extras, last_ends): per set a
+    list over shards of (n, drop, ext, first_kept, last_kept) -- shard r drops
+    its first `drop` runs, ends its last kept run at `ext` (None: unchanged),
+    and keeps n - drop runs from first_kept (start) to last_kept (end), None
+    when it keeps none -- per shard its `extra` values, and per set every
+    shard's own last run end (its rows' max end; -1 without rows)."""
     w, me = _ws(group)
     dev = device if device is not None else "cpu"
+    ns = len(runs_list)
+    ne = len(extra)
     while True:
-        n = runs.n
-        kk = min(k, n)
         W = 3 * k + 3
-        h = [-1] * W
-        h[0] = n
-        h[1] = runs.last_end if n else -1
-        h[2] = getattr(runs, "last_strand", 0) if stranded and n else 0
-        if kk:
-            hs, he = runs.head(kk)
-            h[3:3 + kk] = hs
-            h[3 + k:3 + k + kk] = he
-            if stranded:
-                h[3 + 2 * k:3 + 2 * k + kk] = runs.head_strands(kk)
-        head = torch.tensor(h, dtype=torch.int64, device=dev)
-        allh = torch.empty(w * W, dtype=torch.int64, device=dev)
+        parts = []
+        for runs in runs_list:
+            if hasattr(runs, "payload"):
+                parts.append(runs.payload(k, dev))
+            else:
+                parts.append(torch.tensor(_payload_host(runs, k, stranded), dtype=torch.int64,
+                                          device=dev))
+        if ne:
+            parts.append(torch.tensor(list(extra), dtype=torch.int64, device=dev))
+        head = torch.cat(parts)
+        allh = torch.empty(w * (ns * W + ne), dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allh, head, group=group)
-        allh = allh.view(w, W).cpu().tolist()
-        carry, cstrand = -1, 0  # the open run: its running max end, strand
-        owner = -1              # shard holding the open run's start
-        drops, ext, again = [0] * w, {}, False
-        for r in range(w):
-            nr, last_end, last_strand = allh[r][0], allh[r][1], allh[r][2]
-            starts = allh[r][3:3 + k]
-            ends_ = allh[r][3 + k:3 + 2 * k]
-            strands = allh[r][3 + 2 * k:3 + 3 * k]
-            i = 0
-            while i < min(nr, k) and carry > starts[i] and (not stranded or strands[i] == cstrand):
-                carry = max(carry, ends_[i])
-                i += 1
-            if i == k and nr > k:
+        allh = allh.view(w, ns * W + ne).cpu().tolist()
+        tables, again = [], False
+        for si in range(ns):
+            rows = [allh[r][si * W:(si + 1) * W] for r in range(w)]
+            t = _carry_from_rows(rows, k, stranded)
+            if t is None:
                 again = True
                 break
-            drops[r] = i
-            if i > 0 and owner >= 0:
-                ext[owner] = max(ext.get(owner, -1), carry)
-            if nr > i:  # shard r now holds the open run: its last run
-                owner = r
-                carry, cstrand = last_end, last_strand
+            tables.append(t)
         if again:
             k *= 2
             continue
-        table = []
-        for r in range(w):
-            nr, last_end = allh[r][0], allh[r][1]
-            d = drops[r]
-            if nr > d:
-                table.append((nr, d, ext.get(r), allh[r][3 + d] if d < k else None,
-                              ext.get(r, last_end)))
-            else:
-                table.append((nr, d, ext.get(r), None, None))
-        return table
+        return (tables, [allh[r][ns * W:] for r in range(w)],
+                [[allh[r][si * W + 1] for r in range(w)] for si in range(ns)])
+
+
+def _carry_from_rows(allh, k, stranded):
+    """carry table of one set from every shard's gathered words (None: some
+    shard's k leading runs are all absorbed -- gather more)"""
+    w = len(allh)
+    carry, cstrand = -1, 0  # the open run: its running max end, strand
+    owner = -1              # shard holding the open run's start
+    drops, ext = [0] * w, {}
+    for r in range(w):
+        nr, last_end, last_strand = allh[r][0], allh[r][1], allh[r][2]
+        starts = allh[r][3:3 + k]
+        ends_ = allh[r][3 + k:3 + 2 * k]
+        strands = allh[r][3 + 2 * k:3 + 3 * k]
+        i = 0
+        while i < min(nr, k) and carry > starts[i] and (not stranded or strands[i] == cstrand):
+            carry = max(carry, ends_[i])
+            i += 1
+        if i == k and nr > k:
+            return None
+        drops[r] = i
+        if i > 0 and owner >= 0:
+            ext[owner] = max(ext.get(owner, -1), carry)
+        if nr > i:  # shard r now holds the open run: its last run
+            owner = r
+            carry, cstrand = last_end, last_strand
+    table = []
+    for r in range(w):
+        nr, last_end = allh[r][0], allh[r][1]
+        d = drops[r]
+        if nr > d:
+            table.append((nr, d, ext.get(r), allh[r][3 + d] if d < k else None,
+                          ext.get(r, last_end)))
+        else:
+            table.append((nr, d, ext.get(r), None, None))
+    return table
 
 
 def merge_carry(run_gs, run_ge=None, group=None, k=256, device=None, stranded=False):

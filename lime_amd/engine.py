@@ -10,7 +10,7 @@ import ctypes as C
 import numpy as np
 
 from . import _ffi
-from ._ffi import check, i32, i64, u64, vp
+from ._ffi import check, i32, i64, u32, u64, vp
 
 P = C.POINTER
 
@@ -148,6 +148,12 @@ class IntervalSet:
         out = (i64 * k)()
         check(fn(self._h, k, keys, out))
         return list(out)
+
+    def stats(self):
+        """(min width, max width, has a zero-width row)"""
+        lo, hi, z = u32(), u32(), i32()
+        check(_lib().lime_set_stats(self._h, C.byref(lo), C.byref(hi), C.byref(z)))
+        return lo.value, hi.value, bool(z.value)
 
     def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
         check(_lib().lime_set_copy_rows_device(self._h, int(first), int(count), d_gs, d_ge,
@@ -387,6 +393,17 @@ class Context:
                                             C.byref(h)))
         return IntervalSet(self, h, space)
 
+    def set_extend_sorted(self, s, n, d_gs, d_ge, d_row, min_width, max_width, has_zero):
+        """s's rows followed by n device rows that the caller guarantees to be
+        in canonical order past s's last row (a shard's right halo), copied
+        without a sort, a validation or a read-back; the widths of the added
+        rows are bounded by the caller's (min, max, any zero)"""
+        h = vp()
+        check(_lib().lime_set_extend_sorted(self._h, s._h, int(n), vp(d_gs), vp(d_ge), vp(d_row),
+                                            int(min_width), int(max_width), int(bool(has_zero)),
+                                            C.byref(h)))
+        return IntervalSet(self, h, s.space)
+
     def set_from_global_stranded(self, space, n, d_gs, d_ge, d_row, d_strand):
         """global rows with int8 strand codes in HBM: full RegionOrdering, merge
         breaks runs at strand changes"""
@@ -609,6 +626,13 @@ class DeviceBed:
         check(_lib().lime_dbed_remap_contigs(self._h, _ptr(ids, i32), len(ids)))
         c, s, e, _ = self.device_arrays()
         return self.ctx.set_from_device(space, self.n, c, s, e)
+
+    def synth_pileup_rows(self, space, first, n, seed, n_centres, sigma, len_lo, len_hi,
+                          d_contig, d_start, d_end):
+        """rows [first, first + n) of lime_synth_pileup's sequence"""
+        check(_lib().lime_synth_pileup_rows(self._h, space.handle, int(first), int(n), int(seed),
+                                            int(n_centres), int(sigma), int(len_lo), int(len_hi),
+                                            d_contig, d_start, d_end))
 
     def close(self):
         if self._h:

@@ -16,16 +16,24 @@ from . import dist as ld
 
 
 class _EngineRuns:
-    """merge result as seen by lime_amd.dist.carry_table"""
+    """merge result as seen by lime_amd.dist.carry_tables: its leading runs
+    and last end copied on the device into the gathered words (payload), so
+    the carry costs no host copy before its one all_gather"""
 
-    def __init__(self, res, stranded=False):
+    def __init__(self, res, stranded=False, sync=None, dev=None):
         self.res, self.n, self.stranded = res, res.n, stranded
-        self.last_end, self.last_strand = -1, 0
-        if self.n:
-            _, ge = res.copy_range(self.n - 1, 1)
-            self.last_end = int(ge[0])
-            if stranded:
-                self.last_strand = int(res.run_strands(self.n - 1, 1)[0])
+        self._sync = sync or (lambda: None)
+        self.dev = dev  # the engine's device (where the copies land)
+        self.last_strand = 0
+        if self.n and stranded:
+            self.last_strand = int(res.run_strands(self.n - 1, 1)[0])
+
+    @property
+    def last_end(self):
+        if not self.n:
+            return -1
+        _, ge = self.res.copy_range(self.n - 1, 1)
+        return int(ge[0])
 
     def head(self, k):
         gs, ge = self.res.copy_range(0, k)
@@ -33,6 +41,29 @@ class _EngineRuns:
 
     def head_strands(self, k):
         return [int(x) for x in self.res.run_strands(0, k)]
+
+    def payload(self, k, dev):
+        """n, last end, last strand, the first k runs' starts, ends, strands
+        (int64 on `dev`; -1 past the runs)"""
+        n, kk = self.n, min(k, self.n)
+        out = torch.full((3 * k + 3,), -1, dtype=torch.int64, device=dev)
+        out[0] = n
+        out[2] = self.last_strand if self.stranded and n else 0
+        if n:
+            g = torch.empty(kk + 1, dtype=torch.int32, device=self.dev)
+            e = torch.empty(kk + 1, dtype=torch.int32, device=self.dev)
+            self.res.copy_rows_device(0, kk, g.data_ptr(), e.data_ptr())
+            self.res.copy_rows_device(n - 1, 1, g[kk:].data_ptr(), e[kk:].data_ptr())
+            self._sync()  # the engine's copies land before torch reads them
+            g64 = (g.to(torch.int64) & 0xFFFFFFFF).to(dev)
+            e64 = (e.to(torch.int64) & 0xFFFFFFFF).to(dev)
+            out[1] = e64[kk]
+            out[3:3 + kk] = g64[:kk]
+            out[3 + k:3 + k + kk] = e64[:kk]
+            if self.stranded:
+                out[3 + 2 * k:3 + 2 * k + kk] = torch.tensor(self.head_strands(kk),
+                                                             dtype=torch.int64, device=dev)
+        return out
 
 
 class ShardStep:
@@ -123,44 +154,47 @@ class ShardStep:
         return out
 
     # -------------------------------------------------------------- halo
-    def _halo(self, sets, my_end):
+    def _halo(self, sets, ends=None, my_end=-1):
         """right halo of every set, on the device: [(gs, ge, row) int32
-        tensors], each sorted (later shards' prefixes in rank order)"""
+        tensors], each sorted (later shards' prefixes in rank order).  `ends`:
+        every shard's max row end, when the caller gathered them already;
+        else one all_gather of `my_end`.  Every set's rows travel in ONE
+        packed all_to_all (dist.exchange_sets)."""
         w, me = self.world, self.rank
         cd = self.comm if self.comm is not None else self.dev
-        ends = torch.empty(w, dtype=torch.int64, device=cd)
-        dist.all_gather_into_tensor(ends, torch.tensor([my_end], dtype=torch.int64, device=cd),
-                                    group=self.group)
-        ends = ends.tolist()
-        out = []
+        if ends is None:
+            t = torch.empty(w, dtype=torch.int64, device=cd)
+            dist.all_gather_into_tensor(t, torch.tensor([my_end], dtype=torch.int64, device=cd),
+                                        group=self.group)
+            ends = t.tolist()
+        cols, counts = [], []
         for S in sets:
             # rows of mine that shard r < me needs: gs < ends[r] (one batched
             # search for every earlier shard)
             ask = [r for r in range(w) if r < me and ends[r] > 0]
             got = dict(zip(ask, S.lower_bounds([min(ends[r], 0xFFFFFFFF) for r in ask])))
-            counts = [got.get(r, 0) for r in range(w)]
-            c = max(counts) if counts else 0
+            cnt = [got.get(r, 0) for r in range(w)]
+            c = max(cnt) if cnt else 0
             pre = [self._i32(c) for _ in range(3)]
             if c:
                 S.copy_rows_device(0, c, *(t.data_ptr() for t in pre))
-                self._sync()  # the engine's copy lands before torch.cat reads it
-            send = [torch.cat([t[:k] for k in counts]) if sum(counts) else t[:0] for t in pre]
-            self._sync()
-            recv, _ = ld.exchange(send, counts, self.group, self.comm)
-            self._sync()
-            out.append(recv)
-        return out
-
-    def _extend(self, S, halo):
-        """own sorted rows followed by the halo rows (already in order), as
-        one engine set: nothing to sort, k_prep only checks the order"""
-        n, h = S.n, halo[0].numel()
-        gs, ge, row = self._i32(n + h), self._i32(n + h), self._i32(n + h)
-        S.copy_rows_device(0, n, gs.data_ptr(), ge.data_ptr(), row.data_ptr())
-        gs[n:n + h], ge[n:n + h], row[n:n + h] = halo
+            cols.append(pre)
+            counts.append(cnt)
+        self._sync()  # the engine's copies land before torch.cat reads them
+        send = [[torch.cat([t[:k] for k in cnt]) if sum(cnt) else t[:0] for t in pre]
+                for pre, cnt in zip(cols, counts)]
+        got = ld.exchange_sets(send, counts, self.group, self.comm)
         self._sync()
-        return self.ctx.set_from_global(self.space, n + h, gs.data_ptr(), ge.data_ptr(),
-                                        row.data_ptr())
+        return [recv for recv, _, _ in got]
+
+    def _extend(self, S, halo, widths):
+        """own sorted rows followed by the halo rows (already in order: later
+        shards' rows start past every own row) as one engine set, copied on
+        the device without a sort, a validation or a read-back
+        (lime_set_extend_sorted); `widths` bounds the halo rows' widths (min,
+        max, any zero-width) -- the sending shards' set statistics"""
+        h = halo[0].numel()
+        return self.ctx.set_extend_sorted(S, h, *(t.data_ptr() for t in halo[:3]), *widths)
 
     def _left_halo(self, S):
         """rows of earlier shards that may reach into this shard: shard q
@@ -199,7 +233,7 @@ class ShardStep:
             my_end = _EngineRuns(ma).last_end
             ma.close()
         left = self._left_halo(B)
-        (right,) = self._halo([B], my_end)
+        (right,) = self._halo([B], my_end=my_end)
         n, hl, hr = B.n, left[0].numel(), right[0].numel()
         if hl or hr:
             gs, ge, row = self._i32(hl + n + hr), self._i32(hl + n + hr), self._i32(hl + n + hr)
@@ -223,8 +257,8 @@ class ShardStep:
         kept run) and the table of every shard."""
         res = self.ctx.merge(S)
         cd = self.comm if self.comm is not None else self.dev
-        table = ld.carry_table(_EngineRuns(res, stranded), self.group, device=cd,
-                               stranded=stranded)
+        table = ld.carry_table(_EngineRuns(res, stranded, self._sync, self.dev), self.group,
+                               device=cd, stranded=stranded)
         nr, drop, ext, _, _ = table[self.rank]
         return {"result": res, "drop": drop, "ext": ext, "table": table,
                 "offset": ld.run_offsets(table)[self.rank], "runs": nr - drop}
@@ -241,15 +275,18 @@ class ShardStep:
         return (row[:n_rows].to(torch.int64) & 0xFFFFFFFF,
                 ld.global_run_ids(local, m["drop"], m["offset"]))
 
-    def complement(self, S):
+    def complement(self, S, m=None):
         """This shard's share of DistributedComplement (Complement.scala
         :33-134) against the shard space's contigs: the gaps that START in its
         window [split[r], split[r+1]), from its carried runs framed by the
         previous shards' last run end and the next shards' first run start
         (the gap at a partition bound, :67-73 / :112-122; contigs without
         data, :39-45, fall to the shard holding their start).  The shards'
-        gaps concatenate to the unsharded result."""
-        m = self.merge(S)
+        gaps concatenate to the unsharded result.  `m`: this shard's merge()
+        of S when the caller has it (kept open), else merged here."""
+        own = m is None
+        if own:
+            m = self.merge(S)
         res, drop, ext = m["result"], m["drop"], m["ext"]
         prev_end, next_start = ld.complement_frame(m["table"], self.rank)
         k = res.n - drop
@@ -269,7 +306,8 @@ class ShardStep:
         self._sync()
         out = self.ctx.complement_runs(self.space, tot, gs.data_ptr(), ge.data_ptr(),
                                        self.splits[self.rank], self.splits[self.rank + 1])
-        res.close()
+        if own:
+            res.close()
         return out
 
     # -------------------------------------------------------------- step
@@ -279,17 +317,29 @@ class ShardStep:
         cross-shard carry.  Returns a dict of counts and the merge results."""
         ctx = self.ctx
         ma, mb = ctx.merge(A), ctx.merge(B)
-        ra, rb = _EngineRuns(ma), _EngineRuns(mb)
-        my_end = max(ra.last_end, rb.last_end)
-        halo_a, halo_b = self._halo([A, B], my_end)
-        Ae = self._extend(A, halo_a) if halo_a[0].numel() else A
-        Be = self._extend(B, halo_b) if halo_b[0].numel() else B
+        ra = _EngineRuns(ma, sync=self._sync, dev=self.dev)
+        rb = _EngineRuns(mb, sync=self._sync, dev=self.dev)
+        cd = self.comm if self.comm is not None else self.dev
+        # ONE all_gather: both sets' merge carries, every shard's last run
+        # ends (its rows' max end: the halo bound) and width bounds
+        wa, wb = A.stats(), B.stats()
+        (ta, tb), ex, (la, lb) = ld.carry_tables(
+            [ra, rb], self.group, device=cd,
+            extra=[wa[0], wa[1], int(wa[2]), wb[0], wb[1], int(wb[2])])
+        ends = [max(x, y) for x, y in zip(la, lb)]
+        later = ex[self.rank + 1:]  # the halo rows come from later shards
+        wha = (min([x[0] for x in later], default=0), max([x[1] for x in later], default=0),
+               any(x[2] for x in later))
+        whb = (min([x[3] for x in later], default=0), max([x[4] for x in later], default=0),
+               any(x[5] for x in later))
+        halo_a, halo_b = self._halo([A, B], ends=ends)
+        Ae = self._extend(A, halo_a, wha) if halo_a[0].numel() else A
+        Be = self._extend(B, halo_b, whb) if halo_b[0].numel() else B
         plan = ctx.intersect(Ae, Be, threshold, a_owned=A.n, b_owned=B.n)
         if on_pairs is not None:
             on_pairs(plan)
-        cd = self.comm if self.comm is not None else self.dev
-        da, ea = ld.merge_carry(ra, group=self.group, device=cd)
-        db, eb = ld.merge_carry(rb, group=self.group, device=cd)
+        da, ea = ta[self.rank][1], ta[self.rank][2]
+        db, eb = tb[self.rank][1], tb[self.rank][2]
         out = {"pairs": plan.n, "runs_a": ma.n - da, "runs_b": mb.n - db,
                "drop": (da, db), "extend": (ea, eb),
                "halo": (halo_a[0].numel(), halo_b[0].numel()), "merge_a": ma, "merge_b": mb}

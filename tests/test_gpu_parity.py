@@ -848,6 +848,39 @@ def test_subtract_runs_path(ctx, mode, t):
     _sub_equal(res, oracle.subtract(A, B, t, mode))
 
 
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+@pytest.mark.parametrize("deep", [False, True])
+def test_subtract_one_pass_and_two_pass(ctx, mode, deep):
+    # threshold 0 over B's runs takes one of two launches: the one-pass
+    # k_sub_fused (count, look-back placement, write) when B merges into at
+    # least 1/64 as many runs as A has rows, else the count pass + a
+    # write pass over the tiles with records (B covering A deeply).  The same
+    # left rows against a sparse B (one pass) and that B plus long rows
+    # covering nearly everything (two passes), with zero-width rows,
+    # duplicates, book-ended rows and a 30-row same-start group (tie index)
+    rng = np.random.default_rng(4242)
+    L = 200_000
+    A = random_sets(rng, 8000, 1, n_contigs=2, contig_len=L, max_len=400, zero_frac=0.05,
+                    dup_frac=0.05, book_frac=0.1)[0]
+    B = random_sets(rng, 4000, 1, n_contigs=2, contig_len=L, max_len=100, zero_frac=0.05,
+                    dup_frac=0.05, book_frac=0.1)[0]
+    B = [x.copy() for x in B]
+    B[0][:30], B[1][:30] = B[0][40], B[1][40]
+    B[2][:30] = B[1][40] + rng.integers(1, 300, 30)
+    if deep:
+        k = 300
+        c = rng.integers(0, 2, k).astype(B[0].dtype)
+        st = rng.integers(0, L - 30_000, k)
+        B = [np.concatenate([B[0], c]), np.concatenate([B[1], st]),
+             np.concatenate([B[2], st + rng.integers(5_000, 30_000, k)])]
+    sp = space_for(2, L)
+    sb = ctx.set_from_host(sp, *B)
+    runs = ctx.merge(sb).n
+    assert (runs * 64 >= len(A[0])) == (not deep)  # the launch this case is for
+    res = ctx.subtract(ctx.set_from_host(sp, *A), sb, 0, mode).to_host()
+    _sub_equal(res, oracle.subtract(A, B, 0, mode))
+
+
 def test_bitset_and_past_sixteen_sets(ctx):
     # the fused AND paints 16 sets per kernel and chains the groups
     # (lime_bitset_and_from_device); lime_bitset_and_runs chains its words

@@ -43,6 +43,11 @@ class FakeSet:
     def lower_bounds(self, keys):
         return [self.lower_bound(k) for k in keys]
 
+    def stats(self):
+        w = self.ge - self.gs
+        return (int(w.min()) if self.n else 0, int(w.max()) if self.n else 0,
+                bool((w == 0).any()))
+
     def copy_rows_device(self, first, count, d_gs, d_ge, d_row):
         for src, dst in ((self.gs, d_gs), (self.ge, d_ge), (self.row, d_row)):
             a = np.ascontiguousarray(src[first:first + count], dtype=np.uint32)
@@ -59,6 +64,11 @@ class FakeRuns:
     def copy_range(self, first, count):
         return (self.gs[first:first + count].astype(np.uint32),
                 self.ge[first:first + count].astype(np.uint32))
+
+    def copy_rows_device(self, first, count, d_gs, d_ge):
+        for src, dst in ((self.gs, d_gs), (self.ge, d_ge)):
+            a = np.ascontiguousarray(src[first:first + count], dtype=np.uint32)
+            ctypes.memmove(dst, a.ctypes.data, 4 * count)
 
     def close(self):
         pass
@@ -87,6 +97,16 @@ class FakeCtx:
         def arr(p):
             return np.ctypeslib.as_array((ctypes.c_uint32 * n).from_address(p)).astype(np.int64)
         return FakeSet(arr(d_gs), arr(d_ge), arr(d_row))
+
+    def set_extend_sorted(self, S, n, d_gs, d_ge, d_row, min_w, max_w, zero):
+        def arr(p):
+            return np.ctypeslib.as_array((ctypes.c_uint32 * n).from_address(p)).astype(np.int64)
+        g, e, r = arr(d_gs), arr(d_ge), arr(d_row)
+        assert n == 0 or g[0] >= S.gs[-1], "halo rows start past the shard's rows"
+        w = e - g
+        assert n == 0 or (w.max() <= max_w and w.min() >= min_w and (zero or not (w == 0).any()))
+        return FakeSet(np.concatenate([S.gs, g]), np.concatenate([S.ge, e]),
+                       np.concatenate([S.row, r]))
 
     def intersect(self, A, B, t, a_owned, b_owned):
         from oracle import oracle

@@ -20,7 +20,7 @@ for i in 1 2; do for lib in "$@"; do for W in $works; do
   esac
   out=gpurun_out/${tag}_$(echo $lib | tr '/:=' '___')_${W}_$i.txt
   case $W in
-    c2) timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $out 2>&1 ;;
+    c2) timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-ops > $out 2>&1 ;;
     c5) timeout -k 10 300 python bench.py --workload c5 --steps 5 --warmup 2 --no-cpu-baseline > $out 2>&1 ;;
     *) timeout -k 10 300 python tools/bench_extra.py --workload $W > $out 2>&1 ;;
   esac || { tail -20 $out; exit 1; }

@@ -410,7 +410,7 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": tsrc,
-                         "kernel": "k_fill<false>", "avg_launch_ms": avg_ms,
+                         "kernel": "k_fill<1, false, false>", "avg_launch_ms": avg_ms,
                          "alg_bytes_per_launch": avg_b, "launches": len(timed)},
             "breakdown_ms": breakdown,
             "sort_roofline": sort_roof,

@@ -58,28 +58,6 @@ __global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
     for (int i = threadIdx.x; i < cnt; i += BB) words[w0 + i] = img[i];
 }
 
-// bits [s, e) of global words (after every tile is stored)
-__device__ __forceinline__ void paint_global(uint64_t *words, uint64_t s, uint64_t e) {
-    const uint64_t a = s >> 6, b = (e - 1) >> 6;
-    for (uint64_t w = a; w <= b; ++w) {
-        const uint64_t lo = w == a ? (s & 63) : 0;
-        const uint64_t hi = w == b ? ((e - 1) & 63) : 63;
-        const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
-        if (m == ~0ull)
-            words[w] = m;  // full word: idempotent plain store
-        else
-            atomicOr((unsigned long long *)&words[w], (unsigned long long)m);
-    }
-}
-
-__global__ __launch_bounds__(BB) void k_paint_cross(const uint64_t *__restrict__ cross,
-                                                    const unsigned int *__restrict__ ncross,
-                                                    uint64_t *__restrict__ words) {
-    const int64_t nx = *ncross;
-    for (int64_t i = (int64_t)blockIdx.x * BB + threadIdx.x; i < nx; i += (int64_t)gridDim.x * BB)
-        paint_global(words, cross[i] >> 32, cross[i] & 0xffffffffull);
-}
-
 // ------------------------------------------------- rows -> bits, no sort
 // Unsorted rows are binned by a two-level counting scatter, then each
 // 2^PSH-base paint tile ORs its rows into an LDS image and stores it once:
@@ -91,14 +69,16 @@ __global__ __launch_bounds__(BB) void k_paint_cross(const uint64_t *__restrict__
 //                bin (LDS atomics), staged in LDS in bin order, and stored as
 //                runs, one u32 each (offset in bin << LENB | length); longer
 //                rows and rows crossing the bin end leave their remainder to
-//                the cross list (k_paint_cross)
+//                the cross list (bucketed by tile: k_xcount / k_xwrite)
 //   k_bin_split_atomic  one block per bin: its rows to its PSUB paint tiles
 //                (one returning LDS atomic per row on the tile's cursor: a
 //                wave's claims on one cursor come back consecutive, so the
 //                stores stay runs), re-packed relative to the tile,
 //                tile-crossing remainders to the cross list
-//   k_paint_bins one block per paint tile: its rows OR-ed into a 64 KiB LDS
-//                image, stored once (every word written exactly once)
+//   k_paint_and  one block per paint tile: its rows OR-ed into a 64 KiB LDS
+//                image, stored once (every word written exactly once) -- or
+//   k_paint_ev   the same image combined with the other operands' and its
+//                runs' events extracted in place (no words stored)
 // Why two levels: a one-level scatter to 5,900 paint tiles (hg38) keeps
 // (destinations x resident blocks) lines open per XCD, far beyond its 4 MiB
 // L2, and wrote 3.9x its bytes (profiles/round2_c5_pmc_onelevel.txt); 737
@@ -501,42 +481,6 @@ __device__ __forceinline__ void paint_lds(unsigned long long *img, uint32_t s0, 
     }
 }
 
-__global__ __launch_bounds__(PAINTB) void k_paint_bins(const uint32_t *__restrict__ slab2,
-                                                       const uint32_t *__restrict__ tstart,
-                                                       uint64_t *__restrict__ words,
-                                                       int64_t n_words) {
-    __shared__ unsigned long long img[TWORDS];
-    const int t = blockIdx.x;
-    for (int i = threadIdx.x; i < TWORDS; i += PAINTB) img[i] = 0ull;
-    const uint32_t r0 = tstart[t], r1 = tstart[t + 1];
-    __syncthreads();
-    // 8 independent loads per lane per step, then their paints
-    constexpr int PV = 8;
-    for (uint32_t rb = r0; rb < r1; rb += PV * PAINTB) {
-        uint32_t pv[PV];
-#pragma unroll
-        for (int k = 0; k < PV; ++k) {
-            const uint32_t r = rb + k * PAINTB + threadIdx.x;
-            pv[k] = r < r1 ? slab2[r] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < PV; ++k) {
-            const uint32_t l = pv[k] & ((1u << PLENB) - 1);
-            if (l) paint_lds(img, pv[k] >> PLENB, (pv[k] >> PLENB) + l);
-        }
-    }
-    __syncthreads();
-    const int64_t w0 = (int64_t)t * TWORDS;
-    const int cnt = (int)max((int64_t)0, min((int64_t)TWORDS, n_words - w0));
-    // 16-B stores: two words per lane
-    for (int i = 2 * threadIdx.x; i < cnt; i += 2 * PAINTB) {
-        if (i + 1 < cnt)
-            *reinterpret_cast<ulonglong2 *>(words + w0 + i) = make_ulonglong2(img[i], img[i + 1]);
-        else
-            words[w0 + i] = img[i];
-    }
-}
-
 // ---------------------------------------- k-way AND straight from rows
 // The C5 shape: k row sets binned as above, then ONE kernel
 // paints every set's rows of a tile into LDS in turn and ANDs the images in
@@ -599,22 +543,22 @@ struct AndArgs {
 
 constexpr int AWPT = TWORDS / PAINTB;  // AND words per thread (registers)
 constexpr int APV = 16;                // rows per lane per batch
-// The tile's (set, batch) sequence is software-pipelined: the next batch's
-// loads (possibly the next set's) are issued before the current batch is
-// painted, so they stay in flight across the set's AND barriers.
-__global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
-    __shared__ unsigned long long img[TWORDS];
-    const int t = blockIdx.x;
+// acc[j] (word t TWORDS + threadIdx.x + j PAINTB of tile t) &= every set's
+// bits of the tile, complemented for the sets in `neg`.  The tile's (set,
+// batch) sequence is software-pipelined: the next batch's loads (possibly
+// the next set's) are issued before the current batch is painted, so they
+// stay in flight across the set's AND barriers.  img: TWORDS words of LDS.
+__device__ __forceinline__ void paint_and_tile(const AndArgs &a, int t, uint32_t neg,
+                                               unsigned long long *img, uint64_t (&acc)[AWPT]) {
     constexpr uint32_t B = APV * PAINTB;
-    uint64_t acc[AWPT];
-    const int64_t wt = (int64_t)t * TWORDS;
-#pragma unroll
-    for (int j = 0; j < AWPT; ++j) {
-        const int64_t w = wt + threadIdx.x + j * PAINTB;
-        acc[j] = a.init ? (w < a.n_words ? a.words[w] : 0ull) : ~0ull;
-    }
-    // a tile wholly inside one of the set's cross pieces: AND unchanged
-    auto skip = [&](int i) { return a.full[i] && a.full[i][t + 1] != 0u; };
+    // a tile wholly inside one of the set's cross pieces: all ones (AND
+    // unchanged, or all zeros complemented)
+    bool zero = false;
+    auto skip = [&](int i) {
+        const bool f = a.full[i] && a.full[i][t + 1] != 0u;
+        if (f && ((neg >> i) & 1u)) zero = true;
+        return f;
+    };
     auto load = [&](int i, uint32_t rb, uint32_t(&p)[APV]) {
         const uint32_t r1 = a.tstart[i][t + 1];
         const uint32_t *slab2 = a.slab2[i];
@@ -656,8 +600,9 @@ __global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
                 }
             }
             __syncthreads();
+            const uint64_t inv = ((neg >> i) & 1u) ? ~0ull : 0ull;
 #pragma unroll
-            for (int j = 0; j < AWPT; ++j) acc[j] &= img[threadIdx.x + j * PAINTB];
+            for (int j = 0; j < AWPT; ++j) acc[j] &= img[threadIdx.x + j * PAINTB] ^ inv;
             if (i2 < a.k) {
                 __syncthreads();
 #pragma unroll
@@ -670,7 +615,22 @@ __global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
         i = i2;
         rb = rb2;
     }
+    if (zero)
+#pragma unroll
+        for (int j = 0; j < AWPT; ++j) acc[j] = 0ull;
+}
+
+__global__ __launch_bounds__(PAINTB) void k_paint_and(AndArgs a) {
+    __shared__ unsigned long long img[TWORDS];
+    const int t = blockIdx.x;
+    uint64_t acc[AWPT];
     const int64_t w0 = (int64_t)t * TWORDS;
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) {
+        const int64_t w = w0 + threadIdx.x + j * PAINTB;
+        acc[j] = a.init ? (w < a.n_words ? a.words[w] : 0ull) : ~0ull;
+    }
+    paint_and_tile(a, t, 0u, img, acc);
 #pragma unroll
     for (int j = 0; j < AWPT; ++j) {
         const int64_t w = w0 + threadIdx.x + j * PAINTB;
@@ -1035,18 +995,21 @@ __global__ __launch_bounds__(EV_NT) void k_ev_local(OpArgs a, uint32_t *__restri
 // and ends (odd) at the tile's scanned offset; one workgroup per tile
 // (launched before the host has seen the totals: nothing is written when a
 // tile overflowed its slot, hdr[0], or past the result's capacity)
+// (k_paint_ev's slots: `slot` events each, the first skipped where skip1)
 __global__ __launch_bounds__(256) void k_ev_gather(const uint32_t *__restrict__ tev,
                                                    const uint32_t *__restrict__ tcnt,
                                                    const uint32_t *__restrict__ toff,
                                                    const unsigned int *__restrict__ hdr,
                                                    uint32_t cap_events,
                                                    uint32_t *__restrict__ rgs,
-                                                   uint32_t *__restrict__ rge) {
+                                                   uint32_t *__restrict__ rge,
+                                                   uint32_t slot = EVCAP,
+                                                   const uint32_t *__restrict__ skip1 = nullptr) {
     if (hdr[0]) return;
     const uint32_t t = blockIdx.x;
     const uint32_t e0 = toff[t];
     const uint32_t n = min(tcnt[t], e0 < cap_events ? cap_events - e0 : 0u);
-    const uint32_t *src = tev + (size_t)t * EVCAP;
+    const uint32_t *src = tev + (size_t)t * slot + (skip1 ? skip1[t] : 0u);
     for (uint32_t i = threadIdx.x; i < n; i += 256) {
         const uint32_t e = e0 + i, p = src[i];
         if (e & 1u)
@@ -1054,6 +1017,142 @@ __global__ __launch_bounds__(256) void k_ev_gather(const uint32_t *__restrict__ 
         else
             rgs[e >> 1] = p;
     }
+}
+
+// --------------------------------- runs straight from binned operands
+// Bitsets built from rows stay binned (their rows grouped by paint tile,
+// bitset_build_rows) until words are needed; an op's runs over binned
+// operands fuse the paint with the extraction: per paint tile the operands'
+// rows are painted in LDS and combined in registers (paint_and_tile, the
+// complemented operand of a & ~b or ~a entering inverted), the result is
+// staged back into LDS and its events found there -- no bitset stored or
+// re-read (C4: two 386 MB bitsets written and three read by the two
+// extractions).  A tile's events go to its own slot of `cap`, counted with
+// the bit before the tile taken as 0 and a run reaching the tile's end
+// closed there; k_ev_join then drops the two events of every run that
+// crosses a tile boundary (the close and the reopening) before the scan.
+struct PaintEvArgs {
+    AndArgs s;            // the operands' binned rows (s.k sets)
+    uint32_t neg;         // bit i: operand i complemented
+    int notmask;          // not a: clear the contig pads and the bits past the window
+    int64_t word0;        // global index of the window's word 0
+    int64_t hi_bit;       // end of the window (global bits)
+    const uint32_t *off;  // contig offsets (nc + 1): contig c's pad bit is off[c + 1] - 1
+    int32_t nc;
+    uint32_t *tev;        // nt slots of `cap` events
+    uint32_t cap;
+    uint32_t *tcnt;       // events of each tile
+    uint32_t *edge;       // bit 0: the tile's first bit, bit 1: its last
+    unsigned int *oflow;  // a tile past `cap` events
+};
+constexpr int PEW = TWORDS / PAINTB;  // consecutive words per thread (extraction)
+
+__global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
+    __shared__ unsigned long long img[img_words(TWORDS)];
+    __shared__ uint32_t scratch[PAINTB / 64 + 1];
+    const int t = blockIdx.x;
+    const int64_t nw = a.s.n_words;
+    const int64_t w0 = (int64_t)t * TWORDS;
+    uint64_t acc[AWPT];
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
+    paint_and_tile(a.s, t, a.neg, img, acc);
+    __syncthreads();  // img again, in the extraction's padded layout
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) {
+        const int q = threadIdx.x + j * PAINTB;
+        uint64_t x = w0 + q < nw ? acc[j] : 0ull;
+        if (a.notmask) {  // nothing past the window
+            const int64_t b0 = (a.word0 + w0 + q) * 64;
+            if (b0 + 64 > a.hi_bit) {
+                const int64_t keep = a.hi_bit - b0;
+                x &= keep <= 0 ? 0ull : ((1ull << keep) - 1);
+            }
+        }
+        img[ipad(q)] = x;
+    }
+    __syncthreads();
+    if (a.notmask) {
+        // the contig pads inside the tile, cleared 64 at a time by wave 0
+        // (the pads ascend: a batch not wholly inside the tile is the last)
+        if (threadIdx.x < 64) {
+            const int64_t lo = (a.word0 + w0) * 64, hi = lo + (int64_t)TWORDS * 64;
+            for (int64_t c = dev::wave_lower_bound(a.off + 1, (int64_t)a.nc, lo + 1); c < a.nc;
+                 c += 64) {
+                const int64_t cc = c + threadIdx.x;
+                const int64_t pad = cc < a.nc ? (int64_t)a.off[cc + 1] - 1 : INT64_MAX;
+                const bool in = pad < hi;
+                if (in) {
+                    const int64_t q = pad - lo;
+                    atomicAnd(&img[ipad((int)(q >> 6))], ~(1ull << (q & 63)));
+                }
+                if (__ballot(in) != ~0ull) break;
+            }
+        }
+        __syncthreads();
+    }
+    const int q0 = threadIdx.x * PEW;
+    uint64_t x[PEW];
+#pragma unroll
+    for (int k = 0; k < PEW; ++k) x[k] = img[ipad(q0 + k)];
+    const uint64_t prev = q0 > 0 ? img[ipad(q0 - 1)] : 0ull;
+    uint32_t c = 0;
+    {
+        uint64_t p = prev;
+#pragma unroll
+        for (int k = 0; k < PEW; ++k) {
+            uint64_t st, en;
+            events_of(x[k], p, st, en);
+            c += __popcll(st) + __popcll(en);
+            p = x[k];
+        }
+    }
+    // a run reaching the tile's end closes there (k_ev_join reopens it)
+    const bool close = threadIdx.x == PAINTB - 1 && (x[PEW - 1] >> 63) != 0;
+    c += close;
+    uint32_t tot;
+    const uint32_t mine = dev::block_exclusive_sum<PAINTB>(c, scratch, &tot);
+    if (threadIdx.x == 0) {
+        a.tcnt[t] = tot;
+        a.edge[t] = (uint32_t)(x[0] & 1ull) | (uint32_t)(img[ipad(TWORDS - 1)] >> 63) << 1;
+        if (tot > a.cap) atomicOr(a.oflow, 1u);
+    }
+    if (tot > a.cap) return;
+    uint32_t *dst = a.tev + (size_t)t * a.cap;
+    uint32_t e = mine;
+    const uint32_t base = (uint32_t)((a.word0 + w0 + q0) * 64);
+    {
+        uint64_t p = prev;
+#pragma unroll
+        for (int k = 0; k < PEW; ++k) {
+            uint64_t st, en;
+            events_of(x[k], p, st, en);
+            p = x[k];
+            uint64_t all = st | en;
+            while (all) {
+                const int b = __builtin_ctzll(all);
+                all &= all - 1;
+                dst[e++] = base + (uint32_t)(64 * k + b);
+            }
+        }
+    }
+    if (close) dst[e] = (uint32_t)((a.word0 + w0 + TWORDS) * 64);
+}
+
+// a run crossing the boundary of tiles t and t + 1 was closed at the end of
+// t and reopened at the start of t + 1: both events dropped (cnt2 = the
+// kept events, skip1 = whether the slot's first event is dropped)
+__global__ __launch_bounds__(256) void k_ev_join(const uint32_t *__restrict__ tcnt,
+                                                 const uint32_t *__restrict__ edge, int64_t nt,
+                                                 uint32_t *__restrict__ cnt2,
+                                                 uint32_t *__restrict__ skip1) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nt) return;
+    const uint32_t e = edge[t];
+    const uint32_t jp = t > 0 && (edge[t - 1] & 2u) && (e & 1u);
+    const uint32_t jn = t + 1 < nt && (e & 2u) && (edge[t + 1] & 1u);
+    cnt2[t] = tcnt[t] - jp - jn;
+    skip1[t] = jp;
 }
 
 int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
@@ -1190,50 +1289,99 @@ void window_of(lime_bitset *bs, const lime_space *sp, int64_t lo, int64_t hi) {
 }
 }  // namespace
 
-// bits straight from UNSORTED device rows (k_bin_count / k_bin_write /
-// k_bin_split / k_paint_bins / k_paint_cross): no sort, no merge.
-// Window [lo, hi) of the space's global bits (lo % 64 == 0): the whole
-// space, or a coordinate shard's range (rows clipped to it)
+namespace {
+// set's cross pieces (nx, in `cross`) bucketed by paint tile: xb = [bucket
+// starts | difference-array scan (tiles wholly covered) | fill claims], each
+// tstride long (zeroed here), xl = the 2 nx piece slots
+int bucket_cross(lime_ctx *ctx, int64_t tstride, const uint64_t *cross,
+                 const unsigned int *d_ncross, unsigned int nx, uint32_t *xb, uint2 *xl) {
+    uint32_t *xcnt = xb, *diff = xb + tstride, *xfill = xb + 2 * tstride;
+    LIME_HIP(hipMemsetAsync(xb, 0, 4 * 3 * (size_t)tstride, S(ctx)));
+    const unsigned g = std::min<unsigned>(blocks_for(nx, BB), 2048u);
+    hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), cross, d_ncross, xcnt, diff);
+    LIME_TRY(scan_exclusive_u32_pair(ctx, xcnt, xcnt, tstride, diff, diff, tstride));
+    hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), cross, d_ncross,
+                       (const uint32_t *)xcnt, xfill, xl);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
+AndArgs binned_args(const lime_bitset *const *sets, int k) {
+    AndArgs aa;
+    for (int i = 0; i < MAXK; ++i) {
+        const bool v = i < k;
+        const size_t ts = v ? (size_t)sets[i]->nt + 1 : 0;
+        aa.slab2[i] = v ? sets[i]->slab2 : nullptr;
+        aa.tstart[i] = v ? sets[i]->tstart : nullptr;
+        aa.xl[i] = v ? sets[i]->xl : nullptr;
+        aa.xoff[i] = v && sets[i]->xl ? sets[i]->xb : nullptr;
+        aa.full[i] = v && sets[i]->xl ? sets[i]->xb + ts : nullptr;
+    }
+    aa.k = k;
+    aa.init = 0;
+    aa.words = nullptr;
+    aa.n_words = k > 0 ? sets[0]->n_words : 0;
+    return aa;
+}
+}  // namespace
+
+void bitset_free(lime_bitset *bs) {
+    lime_ctx *ctx = bs->ctx;
+    release(ctx, bs->words);
+    release(ctx, bs->slab2);
+    release(ctx, bs->tstart);
+    release(ctx, bs->xl);
+    release(ctx, bs->xb);
+    bs->words = nullptr;
+    bs->slab2 = bs->tstart = bs->xb = nullptr;
+    bs->xl = nullptr;
+}
+
+// bits straight from UNSORTED device rows, no sort, no merge: the rows are
+// binned by paint tile (k_bin_count / k_bin_write / k_bin_split, their cross
+// pieces bucketed by tile) and kept so; the words are painted on first need
+// (bitset_paint), or never when an op's runs come straight from the bins
+// (k_paint_ev).  Window [lo, hi) of the space's global bits (lo % 64 == 0):
+// the whole space, or a coordinate shard's range (rows clipped to it)
 int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                       const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
                       const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs) {
     window_of(bs, sp, lo, hi);
     bs->runs_bound = n;  // the union of n rows has at most n runs
-    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
-    const int nt = n_bins(hi - lo) * PSUB;
+    const int64_t nt = n_bins(hi - lo) * PSUB;
+    bs->nt = nt;
+    LIME_TRY(alloc(ctx, &bs->tstart, (size_t)nt + 1));
+    LIME_TRY(alloc(ctx, &bs->slab2, (size_t)std::max<int64_t>(n, 1)));
     PoolBag bag{ctx, {}};
-    uint32_t *ttot, *slab2;
     uint64_t *cross;
     unsigned int *flags;  // [0] ncross, [1] err
-    LIME_TRY(bag.get(&ttot, (size_t)nt + 1));
-    LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n, 1)));
     LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * n, 1)));
     LIME_TRY(bag.get(&flags, 2));
     LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
-    LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, slab2, ttot,
-                      cross, flags));
-    // the row-error flags are final once the rows are binned: copied to the
-    // host there, so the paint kernels are already queued while the host
-    // waits (the next call's kernels follow them without a drained stream)
-    struct Ev {
-        hipEvent_t e = nullptr;
-        ~Ev() {
-            if (e) (void)hipEventDestroy(e);
-        }
-    } ev;
-    LIME_HIP(hipEventCreateWithFlags(&ev.e, hipEventDisableTiming));
-    unsigned int *hf = static_cast<unsigned int *>(ctx->pinned);  // (read_back's half)
-    LIME_HIP(hipMemcpyAsync(hf, flags, 8, hipMemcpyDeviceToHost, S(ctx)));
-    LIME_HIP(hipEventRecord(ev.e, S(ctx)));
-    hipLaunchKernelGGL(k_paint_bins, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx),
-                       (const uint32_t *)slab2, (const uint32_t *)ttot, bs->words, bs->n_words);
-    if (n > 0)
-        hipLaunchKernelGGL(k_paint_cross, dim3(std::min<unsigned>(blocks_for(n, BB), 2048u)),
-                           dim3(BB), 0, S(ctx), (const uint64_t *)cross,
-                           (const unsigned int *)flags, bs->words);
+    LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, bs->slab2,
+                      bs->tstart, cross, flags));
+    unsigned int h[2] = {0, 0};
+    LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
+    LIME_TRY(rows_error(h[1]));
+    if (h[0]) {
+        LIME_TRY(alloc(ctx, &bs->xb, 3 * ((size_t)nt + 1)));
+        LIME_TRY(alloc(ctx, &bs->xl, 2 * (size_t)h[0]));
+        LIME_TRY(bucket_cross(ctx, nt + 1, cross, flags, h[0], bs->xb, bs->xl));
+    }
+    return LIME_OK;
+}
+
+// the words of a binned bitset, painted once (k_paint_and over its one set)
+int bitset_paint(lime_ctx *ctx, const lime_bitset *cbs) {
+    lime_bitset *bs = const_cast<lime_bitset *>(cbs);  // (a cache: the bits are unchanged)
+    if (bs->words || !bs->slab2) return LIME_OK;
+    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
+    AndArgs aa = binned_args(&cbs, 1);
+    aa.words = bs->words;
+    if (bs->nt > 0)
+        hipLaunchKernelGGL(k_paint_and, dim3((unsigned)bs->nt), dim3(PAINTB), 0, S(ctx), aa);
     LIME_HIP(hipGetLastError());
-    LIME_HIP(hipEventSynchronize(ev.e));
-    return rows_error(hf[1]);
+    return LIME_OK;
 }
 
 // the AND of k row sets' bits over window [lo, hi), straight from their
@@ -1307,21 +1455,11 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
             uint2 *xl;
             LIME_TRY(bag.get(&xb, 3 * tstride));
             LIME_TRY(bag.get(&xl, 2 * (size_t)nx));
-            uint32_t *xcnt = xb, *diff = xb + tstride, *xfill = xb + 2 * tstride;
-            LIME_HIP(hipMemsetAsync(xb, 0, 4 * 3 * tstride, S(ctx)));
-            const unsigned g = std::min<unsigned>(blocks_for(nx, BB), 2048u);
-            const uint64_t *cx = cross[q % 2];
-            hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), cx,
-                               (const unsigned int *)(flags + 2 * i), xcnt, diff);
-            LIME_TRY(scan_exclusive_u32_pair(ctx, xcnt, xcnt, (int64_t)tstride, diff, diff,
-                                             (int64_t)tstride));
-            hipLaunchKernelGGL(k_xwrite, dim3(g), dim3(BB), 0, S(ctx), cx,
-                               (const unsigned int *)(flags + 2 * i), (const uint32_t *)xcnt,
-                               xfill, xl);
-            LIME_HIP(hipGetLastError());
+            LIME_TRY(bucket_cross(ctx, (int64_t)tstride, cross[q % 2],
+                                  (const unsigned int *)(flags + 2 * i), nx, xb, xl));
             aa.xl[q] = xl;
-            aa.xoff[q] = xcnt;
-            aa.full[q] = diff;
+            aa.xoff[q] = xb;
+            aa.full[q] = xb + tstride;
             return LIME_OK;
         };
         for (int q = 0; q < kg; ++q) {
@@ -1345,8 +1483,108 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     return LIME_OK;
 }
 
+namespace {
+// op's runs over binned operands (sets[0..nin)), fused with their paint:
+// k_paint_ev, k_ev_join, a scan, k_ev_gather.  *overflow: a tile had more
+// events than its slot (the caller paints the operands and takes the words
+// path; nothing is returned)
+int runs_binned(lime_ctx *ctx, int op, int nin, const lime_bitset *const *sets, lime_result *res,
+                bool *overflow) {
+    *overflow = false;
+    const lime_bitset *a = sets[0];
+    const int64_t nt = a->nt;
+    PaintEvArgs pa;
+    pa.s = binned_args(sets, nin);
+    pa.neg = op == 1 ? 1u : (op == 3 ? 2u : 0u);
+    pa.notmask = op == 1;
+    pa.word0 = a->word0;
+    pa.hi_bit = a->hi_bit;
+    const uint32_t *d_off = nullptr;
+    LIME_TRY(space_device(ctx, a->off, &d_off, nullptr));
+    pa.off = d_off;
+    pa.nc = a->n_contigs;
+    // runs bound (a run starts at a run start of an operand, or a contig's
+    // start for NOT) -> a slot of twice the mean events per tile + 2048
+    int64_t bound = op == 1 ? (int64_t)a->n_contigs + 1 : 0;
+    for (int i = 0; i < nin && bound >= 0; ++i)
+        bound = sets[i]->runs_bound < 0 ? -1 : bound + sets[i]->runs_bound;
+    int64_t cap = bound < 0 ? 16384 : 2 * (2 * bound / std::max<int64_t>(nt, 1)) + 2048;
+    cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), 1 << 20);
+    pa.cap = (uint32_t)cap;
+    PoolBag bag{ctx, {}};
+    uint32_t *tev, *tcnt, *edge, *cnt2, *skip1, *toff;
+    unsigned int *hdr;  // [0] overflow flag, [1] total events
+    LIME_TRY(bag.get(&tev, (size_t)nt * (size_t)cap));
+    LIME_TRY(bag.get(&tcnt, (size_t)nt));
+    LIME_TRY(bag.get(&edge, (size_t)nt));
+    LIME_TRY(bag.get(&cnt2, (size_t)nt));
+    LIME_TRY(bag.get(&skip1, (size_t)nt));
+    LIME_TRY(bag.get(&toff, (size_t)nt));
+    LIME_TRY(bag.get(&hdr, 2));
+    LIME_HIP(hipMemsetAsync(hdr, 0, 8, S(ctx)));
+    pa.tev = tev;
+    pa.tcnt = tcnt;
+    pa.edge = edge;
+    pa.oflow = hdr;
+    hipLaunchKernelGGL(k_paint_ev, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), pa);
+    hipLaunchKernelGGL(k_ev_join, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx),
+                       (const uint32_t *)tcnt, (const uint32_t *)edge, nt, cnt2, skip1);
+    LIME_HIP(hipGetLastError());
+    LIME_TRY(scan_exclusive_u32(ctx, cnt2, toff, nt, hdr + 1));
+    // with a bound the result is allocated at it and the gather queued
+    // before the host reads the totals (as bitset_runs)
+    const int64_t rcap = bound;
+    auto gather = [&](uint32_t cap_events) {
+        hipLaunchKernelGGL(k_ev_gather, dim3((unsigned)nt), dim3(256), 0, S(ctx),
+                           (const uint32_t *)tev, (const uint32_t *)cnt2, (const uint32_t *)toff,
+                           (const unsigned int *)hdr, cap_events, res->gs, res->ge,
+                           (uint32_t)cap, (const uint32_t *)skip1);
+    };
+    if (rcap >= 0) {
+        LIME_TRY(alloc(ctx, &res->gs, (size_t)std::max<int64_t>(rcap, 1)));
+        LIME_TRY(alloc(ctx, &res->ge, (size_t)std::max<int64_t>(rcap, 1)));
+        gather((uint32_t)std::min<int64_t>(2 * rcap, 0xffffffffll));
+        LIME_HIP(hipGetLastError());
+    }
+    unsigned int h[2] = {0, 0};
+    LIME_TRY(read_back(ctx, h, hdr, sizeof(h)));
+    if (h[0]) {
+        if (rcap >= 0) {
+            release(ctx, res->gs);
+            release(ctx, res->ge);
+            res->gs = res->ge = nullptr;
+        }
+        *overflow = true;
+        return LIME_OK;
+    }
+    if (h[1] & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
+    const int64_t nr = h[1] / 2;
+    if (rcap >= 0) {
+        if (nr > rcap) return fail(LIME_ERR_DEVICE, "bitset run extraction: runs past bound");
+    } else {
+        LIME_TRY(alloc(ctx, &res->gs, (size_t)std::max<int64_t>(nr, 1)));
+        LIME_TRY(alloc(ctx, &res->ge, (size_t)std::max<int64_t>(nr, 1)));
+        if (nr > 0) gather(h[1]);
+        LIME_HIP(hipGetLastError());
+    }
+    res->n = nr;
+    return LIME_OK;
+}
+}  // namespace
+
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res) {
     const lime_bitset *a = sets[0];
+    // binned operands (bitsets from rows): the runs straight from the bins,
+    // unless a tile overflows its event slot; else (or then) from words
+    const int nin = op == 4 ? k : (op >= 2 ? 2 : 1);
+    bool binned = a->n_words > 0 && nin <= MAXK;
+    for (int i = 0; i < nin; ++i) binned = binned && sets[i]->slab2 && sets[i]->nt == a->nt;
+    if (binned) {
+        bool overflow = false;
+        LIME_TRY(runs_binned(ctx, op, nin, sets, res, &overflow));
+        if (!overflow) return LIME_OK;
+    }
+    for (int i = 0; i < nin; ++i) LIME_TRY(bitset_paint(ctx, sets[i]));
     // an AND of more than MAXK bitsets: their words ANDed group by group into
     // a temporary bitset, whose runs are then extracted (op 0)
     uint64_t *tmp = nullptr;
@@ -1480,6 +1718,7 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
 }
 
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a) {
+    if (bitset_paint(ctx, a) != LIME_OK) return -1;
     unsigned long long *d;
     if (alloc(ctx, &d, 1)) return -1;
     if (hipMemsetAsync(d, 0, 8, S(ctx)) != hipSuccess) return -1;

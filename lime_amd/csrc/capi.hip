@@ -142,6 +142,7 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
                int8_t *d_strand_out);
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
+void bitset_free(lime_bitset *bs);
 int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t first, int64_t n, uint64_t seed,
           uint32_t lo, uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig,
           uint32_t *d_start, uint32_t *d_end);
@@ -1298,7 +1299,7 @@ int lime_bitset_from_device(lime_ctx *ctx, const lime_space *sp, int64_t n,
     int rc = bitset_build_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, 0, sp->span,
                                bs);
     if (rc != LIME_OK) {
-        release(ctx, bs->words);
+        bitset_free(bs);
         delete bs;
         return rc;
     }
@@ -1322,7 +1323,7 @@ int lime_bitset_from_global(lime_ctx *ctx, const lime_space *sp, int64_t lo, int
     bs->len = sp->len;
     int rc = bitset_build_rows(ctx, sp, n, nullptr, d_gs, d_ge, nullptr, nullptr, lo, hi, bs);
     if (rc != LIME_OK) {
-        release(ctx, bs->words);
+        bitset_free(bs);
         delete bs;
         return rc;
     }
@@ -1357,7 +1358,7 @@ static int bitset_and_entry(lime_ctx *ctx, const lime_space *sp, int64_t lo, int
     int rc = bitset_and_rows(ctx, sp, k, n, contig.data(), d_start, d_end, d_off, d_len, lo, hi,
                              bs);
     if (rc != LIME_OK) {
-        release(ctx, bs->words);
+        bitset_free(bs);
         delete bs;
         return rc;
     }
@@ -1461,7 +1462,7 @@ int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a) {
 
 int lime_bitset_destroy(lime_bitset *bs) {
     if (!bs) return LIME_OK;
-    release(bs->ctx, bs->words);
+    bitset_free(bs);
     delete bs;
     return LIME_OK;
 }

@@ -47,6 +47,7 @@ struct PairsPlan {
     uint32_t *win = nullptr;                   // per tile partner window [lo, hi)
     uint32_t *tseg = nullptr;                  // per tile contig offset (0xffffffff: mixed)
     int64_t total = 0;
+    int tpf = 1;  // owner tiles per fill commit (k_fill<TPF>)
     // window plans (DistributedWindow): A is the widened set W, A_out the
     // caller's set whose own coordinates the pairs carry; reach = distance
     const lime_set *A_out = nullptr;
@@ -344,7 +345,12 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
         uint64_t s = 0;
         for (int i = 0; i < IB / 64; ++i) s += red[i];
         tcnt[sa.tile0 + t] = s;
-        if (s > 0xffffffffull && oflow) atomicOr(oflow, 1u);
+        // bit 0: a tile's u32 offsets would wrap; bit 1: two adjacent tiles'
+        // might (the fill then keeps one tile per commit, see k_fill)
+        if (s > 0xffffffffull && oflow)
+            atomicOr(oflow, 1u);
+        else if (s > 0x7fffffffull && oflow)
+            atomicOr(oflow, 2u);
     }
 }
 
@@ -366,14 +372,48 @@ struct FillArgs {
 
 constexpr int FB = 512;           // fill workgroup: 8 waves
 constexpr int FW = FB / 64;
-constexpr int FOPT = OT / FB;     // owners per thread when staging a tile
 #ifndef LIME_FILL_WGS
 #define LIME_FILL_WGS 2  // fill workgroups per CU (LDS budget below)
 #endif
 // LDS partner window (16 B records): 1792 rows keep 3 workgroups per CU
 constexpr int PCAP = LIME_FILL_WGS >= 3 ? 1792 : 2048;
-constexpr int PPT = (PCAP + FB - 1) / FB;  // partner rows per thread when staging
+// Two-tile commits (sparse plans) keep the window as three u32 arrays so
+// that 2048 owners + 2560 partners still fit two workgroups per CU
+constexpr int PCAP2 = 2560;
+#ifndef LIME_FILL_SPARSE
+// mean pairs per owner below which a plan fills two owner tiles per commit
+#define LIME_FILL_SPARSE 16
+#endif
+#ifndef LIME_FILL_SPARSE_EMIT
+#define LIME_FILL_SPARSE_EMIT 1  // two-tile commits resolve owners wave-wide (emit_sparse)
+#endif
 constexpr int64_t GR = 1ll << 40;  // wave granule: default one equal chunk per wave
+
+template <int TPF> struct FillShape {
+    static constexpr int OTF = OT * TPF;                     // owners per commit
+    static constexpr int FOPT = OTF / FB;                    // owners per thread when staging
+    static constexpr int CAP = TPF == 1 ? PCAP : PCAP2;      // LDS partner window rows
+    static constexpr int PPT = (CAP + FB - 1) / FB;          // partner rows per thread
+};
+
+// The LDS partner window: 16-B records (one b128 read per output) for
+// one-tile commits, three u32 arrays for two-tile commits.
+template <int TPF> struct ParWin {
+    u32x4 v[PCAP];
+    __device__ __forceinline__ void put(int i, uint32_t g, uint32_t e, uint32_t r) {
+        v[i] = u32x4{g, e, r, 0u};
+    }
+    __device__ __forceinline__ u32x4 get(uint32_t i) const { return v[i]; }
+};
+template <> struct ParWin<2> {
+    uint32_t g[PCAP2], e[PCAP2], r[PCAP2];
+    __device__ __forceinline__ void put(int i, uint32_t pg, uint32_t pe, uint32_t pr) {
+        g[i] = pg;
+        e[i] = pe;
+        r[i] = pr;
+    }
+    __device__ __forceinline__ u32x4 get(uint32_t i) const { return u32x4{g[i], e[i], r[i], 0u}; }
+};
 
 // 65-ary wave search on the u64 tile offsets: largest t with toff[t] <= key
 __device__ __forceinline__ int64_t wave_tile_of(const uint64_t *__restrict__ a, int64_t n,
@@ -395,31 +435,50 @@ __device__ __forceinline__ int64_t wave_tile_of(const uint64_t *__restrict__ a, 
     return lo + __popcll(__ballot(le)) - 1;
 }
 
-// Everything a fill workgroup stages for one owner tile, held in registers
-// so that the NEXT tile's loads are in flight while the current tile's
-// records are being stored (the staging latency is hidden behind the store
-// stream instead of stalling it once per tile).
-struct TileRegs {
-    uint32_t off[FOPT], lo[FOPT], og[FOPT], oe[FOPT], orw[FOPT];
-    uint32_t pg[PPT], pe[PPT], pr[PPT];
+// Everything a fill workgroup stages for one commit (TPF consecutive owner
+// tiles of one stream), held in registers so that the NEXT commit's loads
+// are in flight while the current one's records are being stored (the
+// staging latency is hidden behind the store stream instead of stalling it
+// once per tile).
+template <int TPF> struct TileRegs {
+    static constexpr int FO = FillShape<TPF>::FOPT, PP = FillShape<TPF>::PPT;
+    uint32_t off[FO], lo[FO], og[FO], oe[FO], orw[FO];
+    uint32_t pg[PP], pe[PP], pr[PP];
     uint32_t wlo, whi, seg;
-    uint64_t tnext;  // toff[t + 1] (or the plan total): the tile's end
+    uint64_t tnext;  // toff[t1] (or the plan total): the commit's end
+    int64_t t1;      // one past the commit's last owner tile
 };
 
-__device__ __forceinline__ int tile_stream(const FillArgs &fa, int64_t t) {
-    return t < fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT ? 0 : 1;
+__device__ __forceinline__ int64_t stream0_tiles(const FillArgs &fa) {
+    return fa.s[0].tile0 + (fa.s[0].no + OT - 1) / OT;
 }
 
-__device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileRegs &r) {
-    const StreamArgs &sa = fa.s[tile_stream(fa, t)];
+__device__ __forceinline__ int tile_stream(const FillArgs &fa, int64_t t) {
+    return t < stream0_tiles(fa) ? 0 : 1;
+}
+
+template <int TPF>
+__device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileRegs<TPF> &r) {
+    constexpr int FO = FillShape<TPF>::FOPT, PP = FillShape<TPF>::PPT;
+    const int st = tile_stream(fa, t);
+    const StreamArgs &sa = fa.s[st];
+    // a commit never spans the two streams
+    const int64_t t1 = min(t + TPF, st == 0 ? stream0_tiles(fa) : fa.ntiles);
     const int64_t o0 = (t - sa.tile0) * OT;
-    const int nown = (int)min((int64_t)OT, sa.no - o0);
+    const int nown = (int)min((int64_t)FillShape<TPF>::OTF, sa.no - o0);
+    // k_count's offsets are local to each owner tile: a thread's owners all
+    // lie in tile t + u, whose offset within the commit is toff[t+u] - toff[t]
+    uint32_t add = 0;
+    if (TPF > 1) {
+        const int u = (int)(threadIdx.x / (FB / TPF));
+        if (u > 0 && t + u < t1) add = (uint32_t)(fa.toff[t + u] - fa.toff[t]);
+    }
 #pragma unroll
-    for (int k = 0; k < FOPT; ++k) {
-        const int q = threadIdx.x * FOPT + k;
+    for (int k = 0; k < FO; ++k) {
+        const int q = threadIdx.x * FO + k;
         const bool v = q < nown;
         const int64_t j = o0 + q;
-        r.off[k] = v ? fa.ocnt[sa.owner0 + j] : 0u;  // tile-local offsets (k_count<_, true>)
+        r.off[k] = v ? fa.ocnt[sa.owner0 + j] + add : 0u;  // tile-local offsets (k_count<_, true>)
         r.lo[k] = v ? fa.olo[sa.owner0 + j] : 0u;
         r.og[k] = v ? sa.ogs_o[j] : 0u;
         r.oe[k] = v ? sa.oge_o[j] : 0u;
@@ -428,10 +487,17 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
     r.wlo = fa.win[2 * t];
     r.whi = fa.win[2 * t + 1];
     r.seg = fa.tseg[t];
-    r.tnext = t + 1 < fa.ntiles ? fa.toff[t + 1] : (uint64_t)fa.total;
-    const int wl = (int)min((int64_t)(r.whi - r.wlo), (int64_t)PCAP);
+    if (TPF > 1 && t1 - 1 > t) {
+        // the union of the tiles' windows (each window is an interval)
+        r.wlo = min(r.wlo, fa.win[2 * (t1 - 1)]);
+        r.whi = max(r.whi, fa.win[2 * (t1 - 1) + 1]);
+        if (fa.tseg[t1 - 1] != r.seg) r.seg = 0xffffffffu;
+    }
+    r.t1 = t1;
+    r.tnext = t1 < fa.ntiles ? fa.toff[t1] : (uint64_t)fa.total;
+    const int wl = (int)min((int64_t)(r.whi - r.wlo), (int64_t)FillShape<TPF>::CAP);
 #pragma unroll
-    for (int k = 0; k < PPT; ++k) {
+    for (int k = 0; k < PP; ++k) {
         const int i = k * FB + threadIdx.x;
         const bool v = i < wl;
         r.pg[k] = v ? sa.pgs_o[r.wlo + i] : 0u;
@@ -464,11 +530,12 @@ __device__ __forceinline__ int wave_owner_of(const uint2 *off, int lo, int hi, u
 // each wave keeps its stores in flight.  The owner walk carries the current
 // (lo, off) pair and the next owner's pair in registers, leaving two
 // dependent LDS steps per iteration (walk, then owner + partner reads).
-template <bool LDSP, bool CKSUM, bool WIN>
+template <bool LDSP, bool CKSUM, bool WIN, int TPF>
 __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, int st,
                                      const uint2 *s_lo_off, const u32x4 *s_own,
-                                     const u32x4 *s_par, uint32_t wlo, int64_t tbase, int64_t o,
-                                     int64_t gend, int &q, uint64_t &hsum, uint64_t &hxor) {
+                                     const ParWin<TPF> &s_par, uint32_t wlo, int64_t tbase,
+                                     int64_t o, int64_t gend, int &q, uint64_t &hsum,
+                                     uint64_t &hxor) {
     uint2 lof = s_lo_off[q], nxt = s_lo_off[q + 1];
     u32x4 *out = fa.out + (tbase - fa.first);
     for (; o < gend; o += 64) {
@@ -482,7 +549,7 @@ __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, i
         const u32x4 ow = s_own[q];
         u32x4 pa;
         if (LDSP)
-            pa = s_par[p - wlo];
+            pa = s_par.get(p - wlo);
         else
             pa = u32x4{sa.pgs_o[p], sa.pge_o[p], sa.prow[p], 0u};
         // intersect: the intersection; window: the left (a) row's own region
@@ -502,25 +569,92 @@ __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, i
     }
 }
 
+// Sparse plans (a few pairs per owner): the 64 outputs of a wave iteration
+// span ~16 owners, a walk of ~16 dependent LDS steps per lane.  Here the
+// wave resolves them at once: lane j reads the offset of owner qa + 1 + j
+// (qa: the owner of the iteration's first output), and every lane counts the
+// offsets <= its own output by a 7-step binary search over the lanes
+// (shuffles; the offsets ascend over the lanes) -- one LDS read and seven
+// shuffles per iteration, then the owner, partner and store as in emit.
+template <bool LDSP, bool CKSUM, bool WIN, int TPF>
+__device__ __forceinline__ void emit_sparse(const FillArgs &fa, const StreamArgs &sa, int st,
+                                            const uint2 *s_lo_off, const u32x4 *s_own,
+                                            const ParWin<TPF> &s_par, uint32_t wlo, int64_t tbase,
+                                            int64_t gb, int64_t gend, int qa, int qmax,
+                                            uint64_t &hsum, uint64_t &hxor) {
+    const uint32_t lane = dev::lane_id();
+    u32x4 *out = fa.out + (tbase - fa.first);
+    for (int64_t ob = gb; ob < gend; ob += 64) {  // (uniform)
+        const uint32_t o0 = (uint32_t)ob;
+        int cnt = 0, adv = 0;
+        for (int qb = qa + 1;; qb += 64) {  // (uniform; one round unless > 64 owners)
+            const int qj = qb + (int)lane;
+            // > 0: owners past qa start after o0
+            const uint32_t rel = qj <= qmax ? s_lo_off[qj].y - o0 : 0xffffffffu;
+            int c = __shfl(rel, 63) <= lane ? 64 : 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1) {
+                const uint32_t v = __shfl(rel, min(c + step - 1, 63));
+                if (c < 64 && v <= lane) c += step;
+            }
+            cnt += c;
+            const uint64_t m = __ballot(rel <= 64u);
+            adv += __popcll(m);  // owners starting by o0 + 64: the next iteration's qa
+            if (m != ~0ull) break;
+        }
+        const int64_t o = ob + lane;
+        if (o < gend) {
+            const int q = qa + cnt;
+            const uint2 lof = s_lo_off[q];
+            const uint32_t ou = (uint32_t)o;
+            const uint32_t p = lof.x + (ou - lof.y);
+            const u32x4 ow = s_own[q];
+            u32x4 pa;
+            if (LDSP)
+                pa = s_par.get(p - wlo);
+            else
+                pa = u32x4{sa.pgs_o[p], sa.pge_o[p], sa.prow[p], 0u};
+            const uint32_t rs =
+                (WIN ? (st == 0 ? ow.x : pa.x) : (ow.x > pa.x ? ow.x : pa.x)) - ow.w;
+            const uint32_t re =
+                (WIN ? (st == 0 ? ow.y : pa.y) : (ow.y < pa.y ? ow.y : pa.y)) - ow.w;
+            const uint32_t ar = st == 0 ? ow.z : pa.z;
+            const uint32_t br = st == 0 ? pa.z : ow.z;
+            if (CKSUM) {
+                const uint64_t h = dev::pair_hash(rs, re, ar, br);
+                hsum += h;
+                hxor ^= h;
+            } else {
+                out[o] = u32x4{rs, re, ar, br};
+            }
+        }
+        qa += adv;
+    }
+}
+
 // One workgroup writes the `per` consecutive output records of its slice of
-// the output index space [first, first + count).  Per owner tile it touches
-// it stages, in LDS,
+// the output index space [first, first + count).  Per commit (TPF owner
+// tiles of one stream) it stages, in LDS,
 //   s_lo_off[q] = (lo_q, off_q)   partner range start, exclusive output offset
 //   s_own[q]    = (gs, ge, row, contig offset) of the owner
-//   s_par[i]    = (gs, ge, row) of partner wlo + i   (the tile's window)
+//   s_par[i]    = (gs, ge, row) of partner wlo + i   (the commit's window)
 // then deals its output range to the waves in GR-record granules; lane l of
 // a wave handles outputs g + l + 64 k of a granule g, so an owner switch
 // happens about once per 82/64 iterations (C2) and is a single LDS compare,
 // and every iteration is 1 b64 + 2 b128 LDS reads and ONE 16-B store per
 // lane, the wave's 64 stores forming one contiguous 1-KiB segment.  The next
-// tile's staging data is prefetched into registers (TileRegs) before the
-// store loop.
-template <bool CKSUM, bool WIN>
+// commit's staging data is prefetched into registers (TileRegs) before the
+// store loop.  A commit costs a fixed stretch (two barriers, the staging
+// stores, the wait for the prefetch behind the store stream): sparse plans
+// (a few pairs per owner, ~4k records per tile) commit two tiles at a time
+// (TPF = 2) to halve that cost per record.
+template <int TPF, bool CKSUM, bool WIN>
 __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
-    __shared__ uint2 s_lo_off[OT + 1];
-    __shared__ u32x4 s_own[OT];
-    __shared__ u32x4 s_par[PCAP];
-    __shared__ uint32_t scratch[FW + 1];
+    constexpr int OTF = FillShape<TPF>::OTF, FO = FillShape<TPF>::FOPT,
+                  PP = FillShape<TPF>::PPT, CAP = FillShape<TPF>::CAP;
+    __shared__ uint2 s_lo_off[OTF + 1];
+    __shared__ u32x4 s_own[OTF];
+    __shared__ ParWin<TPF> s_par;
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_red[2][FW];
 
@@ -529,26 +663,30 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
     if (ob >= oend) return;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     if (w == 0) {
-        const int64_t t0 = wave_tile_of(fa.toff, fa.ntiles, (uint64_t)ob);
+        int64_t t0 = wave_tile_of(fa.toff, fa.ntiles, (uint64_t)ob);
+        // back to the first tile of its commit
+        const int64_t base = t0 < stream0_tiles(fa) ? 0 : stream0_tiles(fa);
+        t0 = base + (t0 - base) / TPF * TPF;
         if (lane == 0) s_tile = t0;
     }
     __syncthreads();
     int64_t t = s_tile;
     uint64_t hsum = 0, hxor = 0;
-    TileRegs R;
-    tile_load(fa, t, R);
+    TileRegs<TPF> R;
+    tile_load<TPF>(fa, t, R);
     while (true) {
         const int st = tile_stream(fa, t);
         const StreamArgs &sa = fa.s[st];
         const int64_t o0 = (t - sa.tile0) * OT;
-        const int nown = (int)min((int64_t)OT, sa.no - o0);
+        const int nown = (int)min((int64_t)OTF, sa.no - o0);
         const int64_t tbase = (int64_t)fa.toff[t];
+        const int64_t tn = R.t1;
         // ---- commit the staged registers to LDS (offsets come scanned
         // from k_count: no block scan here)
         const uint32_t ttot = (uint32_t)(R.tnext - (uint64_t)tbase);
 #pragma unroll
-        for (int k = 0; k < FOPT; ++k) {
-            const int q = threadIdx.x * FOPT + k;
+        for (int k = 0; k < FO; ++k) {
+            const int q = threadIdx.x * FO + k;
             if (q < nown) {
                 const uint32_t sg =
                     R.seg != 0xffffffffu ? R.seg : contig_off(fa.off, fa.n_contigs, R.og[k]);
@@ -556,21 +694,21 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
             }
             s_lo_off[q] = make_uint2(R.lo[k], q < nown ? R.off[k] : ttot);
         }
-        if (threadIdx.x == 0) s_lo_off[OT] = make_uint2(0u, ttot);
+        if (threadIdx.x == 0) s_lo_off[OTF] = make_uint2(0u, ttot);
         const uint32_t wlo = R.wlo, whi = R.whi;
-        const bool par_lds = (int64_t)whi - wlo <= PCAP;
+        const bool par_lds = (int64_t)whi - wlo <= CAP;
         if (par_lds) {
 #pragma unroll
-            for (int k = 0; k < PPT; ++k) {
+            for (int k = 0; k < PP; ++k) {
                 const int i = k * FB + threadIdx.x;
-                if (i < (int)(whi - wlo)) s_par[i] = u32x4{R.pg[k], R.pe[k], R.pr[k], 0u};
+                if (i < (int)(whi - wlo)) s_par.put(i, R.pg[k], R.pe[k], R.pr[k]);
             }
         }
         __syncthreads();
-        // ---- prefetch the next tile (its loads overlap this tile's stores)
-        const bool more = t + 1 < fa.ntiles && (int64_t)fa.toff[t + 1] < oend;
-        if (more) tile_load(fa, t + 1, R);
-        // ---- this tile's slice of the output window, in granules dealt
+        // ---- prefetch the next commit (its loads overlap this one's stores)
+        const bool more = tn < fa.ntiles && (int64_t)fa.toff[tn] < oend;
+        if (more) tile_load<TPF>(fa, tn, R);
+        // ---- this commit's slice of the output window, in granules dealt
         // round-robin to the waves (wave w: granules w, w + FW, ...).  The
         // default granule is one equal chunk per wave: 2048-record granules
         // (the fastest shape of the plain store probe, profiles/
@@ -579,7 +717,7 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
         const int64_t lb = max(ob - tbase, (int64_t)0);
         const int64_t le = min(oend - tbase, (int64_t)ttot);
         // equal shares: `rounds` granules per wave of ~GR records each, so no
-        // wave idles at the tile's closing barrier
+        // wave idles at the commit's closing barrier
         const int64_t rounds = max((int64_t)1, (le - lb + FW * gran - 1) / (FW * gran));
         const int64_t gsz = (((le - lb + FW * rounds - 1) / (FW * rounds)) + 63) & ~(int64_t)63;
         int qw = 0;  // wave-uniform: owner of the wave's previous granule start
@@ -587,20 +725,27 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
             const int64_t gend = min(le, gb + gsz);
             int64_t o = gb + lane;
             // owner of the wave's first output (largest q with off_q <= gb),
-            // by a 65-ary wave search over the LDS offsets (2 steps for a
-            // 1024-owner tile); each lane then walks to its own owner
+            // by a 65-ary wave search over the LDS offsets (2-3 steps); each
+            // lane then walks to its own owner
             qw = wave_owner_of(s_lo_off, qw, nown, (uint32_t)gb);
             int q = qw;
-            if (par_lds)
-                emit<true, CKSUM, WIN>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
-                                  hsum, hxor);
+            if (TPF > 1 && LIME_FILL_SPARSE_EMIT) {
+                if (par_lds)
+                    emit_sparse<true, CKSUM, WIN, TPF>(fa, sa, st, s_lo_off, s_own, s_par, wlo,
+                                                       tbase, gb, gend, qw, OTF, hsum, hxor);
+                else
+                    emit_sparse<false, CKSUM, WIN, TPF>(fa, sa, st, s_lo_off, s_own, s_par, wlo,
+                                                        tbase, gb, gend, qw, OTF, hsum, hxor);
+            } else if (par_lds)
+                emit<true, CKSUM, WIN, TPF>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o,
+                                            gend, q, hsum, hxor);
             else
-                emit<false, CKSUM, WIN>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o, gend, q,
-                                   hsum, hxor);
+                emit<false, CKSUM, WIN, TPF>(fa, sa, st, s_lo_off, s_own, s_par, wlo, tbase, o,
+                                             gend, q, hsum, hxor);
         }
         __syncthreads();
         if (!more) break;
-        ++t;
+        t = tn;
     }
     if (CKSUM) {
         hsum = dev::wave_reduce_sum(hsum);
@@ -777,12 +922,25 @@ int64_t fill_span(int64_t count) {
         int dev = 0, cus = 256, occ = 2;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fill<false, false>, FB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fill<1, false, false>, FB, 0);
         return (int64_t)cus * (occ > 0 ? occ : 1);
     }();
     int64_t per = (count + slots - 1) / slots;
     per = (per + 63) & ~(int64_t)63;
     return per < 4096 ? 4096 : per;
+}
+
+template <int TPF>
+void launch_k_fill(lime_ctx *ctx, dim3 g, const FillArgs &fa, int64_t per, bool cksum, bool win) {
+    if (cksum && win)
+        hipLaunchKernelGGL((k_fill<TPF, true, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+    else if (cksum)
+        hipLaunchKernelGGL((k_fill<TPF, true, false>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+    else if (win)
+        hipLaunchKernelGGL((k_fill<TPF, false, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+    else
+        hipLaunchKernelGGL((k_fill<TPF, false, false>), g, dim3(FB), 0, S(ctx), fa, per,
+                           (int64_t)GR);
 }
 
 int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_t *cksum) {
@@ -807,15 +965,10 @@ int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_
         if (grid > 0x7fffffff) return fail(LIME_ERR_OVERFLOW, "fill window too large");
         const dim3 g((unsigned)grid);
         const bool win = pl->reach >= 0;
-        if (cksum && win)
-            hipLaunchKernelGGL((k_fill<true, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
-        else if (cksum)
-            hipLaunchKernelGGL((k_fill<true, false>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
-        else if (win)
-            hipLaunchKernelGGL((k_fill<false, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+        if (pl->tpf == 2)
+            launch_k_fill<2>(ctx, g, fa, per, cksum != nullptr, win);
         else
-            hipLaunchKernelGGL((k_fill<false, false>), g, dim3(FB), 0, S(ctx), fa, per,
-                               (int64_t)GR);
+            launch_k_fill<1>(ctx, g, fa, per, cksum != nullptr, win);
     }
     LIME_HIP(hipGetLastError());
     return LIME_OK;
@@ -919,12 +1072,15 @@ int intersect_plan(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t 
     LIME_TRY(read_back(ctx, tot, total, sizeof(tot)));
     release(ctx, tcnt);
     release(ctx, total);
-    if (tot[1]) {
+    if (tot[1] & 1) {
         intersect_free(pl);
         return fail(LIME_ERR_OVERFLOW,
                     "a tile of 1024 owner rows has 2^32 or more candidate pairs (pile-up)");
     }
     pl->total = (int64_t)tot[0];
+    // sparse plans commit two owner tiles per fill step (k_fill<2>) unless
+    // a tile holds 2^31 or more pairs (two tiles' u32 offsets could wrap)
+    pl->tpf = !(tot[1] & 2) && pl->total < (int64_t)LIME_FILL_SPARSE * (a_own + b_own) ? 2 : 1;
     *out = pl;
     return LIME_OK;
 }

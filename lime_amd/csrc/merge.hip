@@ -101,7 +101,12 @@ struct MergeScanArgs {
     const int8_t *strand;       // stranded sets: strand per input row
     const uint32_t *row;        // sorted row ids (strand lookups; null: by position)
     int8_t *run_strand;         // stranded sets: the strand of every run (may be null)
+    uint32_t *tie;              // k_merge_scan2, may be null: set to 1 when some start
+                                // is shared by more than TIE_G consecutive rows
 };
+// subtract's same-start group bound (subtract.hip TIE_G): k_merge_scan2 tests
+// gs[i] == gs[i + 16], row i + 16 being held by lane + 4 (4 rows per lane)
+constexpr int MERGE_TIE_G = 16;
 
 // Full tile <-> blocked registers (thread t: rows 16t .. 16t+15) through
 // LDS: global traffic is lane-consecutive 16-B accesses (whole lines per
@@ -368,6 +373,8 @@ struct ScanGeom {
 constexpr int MS2 = LIME_MS2_NT;
 using G2 = ScanGeom<MS2, LIME_MS2_Q>;
 
+// TIE: also test for subtract's long same-start groups (a.tie)
+template <bool TIE>
 __global__ __launch_bounds__(MS2) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_merge_scan2(MergeScanArgs a) {
     constexpr int NW = G2::NW, RQ = G2::RQ;
@@ -503,6 +510,32 @@ void k_merge_scan2(MergeScanArgs a) {
         }
         r += dev::lane63(ci);
     }
+    if (TIE) {
+        // a start shared by rows i and i + 16 (a same-start group past
+        // subtract's TIE_G): row i + 16 is lane + 4's, the next round's for
+        // lanes 60-63, whose sources (lanes 0-3) offer that round's rows
+        // instead (past the wave's last round: the next rows, loaded here).
+        // Tested last, once the ends are dead (before chain 1 it spilled)
+        static_assert(MERGE_TIE_G == 16, "lane + 4 holds row i + 16");
+        uint32_t nx[4] = {0u, 0u, 0u, 0u};
+        if (lane < 4) {
+            const int64_t i0 = wb + G2::RW + 4 * lane;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) nx[j] = i0 + j < n ? a.gs[i0 + j] : 0u;
+        }
+        bool hit = false;
+        const int src = (lane + 4) & 63;
+#pragma unroll
+        for (int q = 0; q < RQ; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t v =
+                    lane < 4 ? (q + 1 < RQ ? s[4 * (q + 1) + j] : nx[j]) : s[4 * q + j];
+                const uint32_t p = __shfl(v, src);
+                hit |= wb + 256 * q + 4 * lane + j + MERGE_TIE_G < n && p == s[4 * q + j];
+            }
+        if (__ballot(hit) != 0 && lane == 0) atomicOr(a.tie, 1u);
+    }
 }
 
 // inclusive prefix max of ge (subtract's spanning-hit search)
@@ -573,7 +606,8 @@ int build_prefix_max(lime_ctx *ctx, const lime_set *set) {
 
 // merge runs of a sorted set; result owns run_gs / run_ge / run_of_sorted
 static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
-                           bool want_run_ids, uint32_t *pmax) {
+                           bool want_run_ids, uint32_t *pmax, int *tie_big = nullptr) {
+    if (tie_big) *tie_big = -1;  // unknown unless k_merge_scan2 tests it
     const int64_t n = set->n;
     res->n = 0;
     if (n == 0) {
@@ -585,10 +619,11 @@ static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
     // keep the transposing kernel's segmented scan
     const bool plain = set->strand_in == nullptr;
     const int64_t nt = (n + (plain ? G2::TILE : STILE) - 1) / (plain ? G2::TILE : STILE);
-    // status words of both chains + ticket + total in one zeroed block
+    // status words of both chains + ticket + total + tie flag in one zeroed
+    // block
     uint64_t *st;
-    LIME_TRY(alloc(ctx, &st, (size_t)(2 * nt + 2)));
-    LIME_HIP(hipMemsetAsync(st, 0, sizeof(uint64_t) * (size_t)(2 * nt + 2), S(ctx)));
+    LIME_TRY(alloc(ctx, &st, (size_t)(2 * nt + 3)));
+    LIME_HIP(hipMemsetAsync(st, 0, sizeof(uint64_t) * (size_t)(2 * nt + 3), S(ctx)));
     uint32_t *run_gs, *run_ge;
     LIME_TRY(alloc(ctx, &run_gs, (size_t)n));
     LIME_TRY(alloc(ctx, &run_ge, (size_t)n));
@@ -610,13 +645,23 @@ static int merge_runs_impl(lime_ctx *ctx, const lime_set *set, lime_result *res,
     a.strand = set->strand_in;
     a.row = set->strand_sorted ? nullptr : set->row;
     a.run_strand = run_st;
+    a.tie = plain && tie_big ? reinterpret_cast<uint32_t *>(st + 2 * nt + 2) : nullptr;
     if (set->strand_in)
         hipLaunchKernelGGL(k_merge_scan<true>, dim3((unsigned)nt), dim3(SB), 0, S(ctx), a);
+    else if (a.tie)
+        hipLaunchKernelGGL(k_merge_scan2<true>, dim3((unsigned)nt), dim3(MS2), 0, S(ctx), a);
     else
-        hipLaunchKernelGGL(k_merge_scan2, dim3((unsigned)nt), dim3(MS2), 0, S(ctx), a);
+        hipLaunchKernelGGL(k_merge_scan2<false>, dim3((unsigned)nt), dim3(MS2), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
     uint64_t nr = 0;
-    LIME_TRY(read_back(ctx, &nr, a.total, sizeof(nr)));
+    if (a.tie) {
+        uint64_t h[2] = {0, 0};  // total, tie flag: one read-back
+        LIME_TRY(read_back(ctx, h, a.total, sizeof(h)));
+        nr = h[0];
+        *tie_big = h[1] != 0;
+    } else {
+        LIME_TRY(read_back(ctx, &nr, a.total, sizeof(nr)));
+    }
     release(ctx, st);
     if (nr * 2 > (uint64_t)n) {
         // most rows start a run: keep the capacity-n arrays
@@ -649,18 +694,20 @@ int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_r
 
 // merge runs with run ids of a plain set, building the set's prefix max in
 // the same pass when it is not built yet (under the set's context lock, as
-// build_prefix_max)
-int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res) {
+// build_prefix_max).  *tie_big (may be null): 1 / 0 whether some start is
+// shared by more than MERGE_TIE_G rows, -1 when not tested
+int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res, int *tie_big) {
+    if (tie_big) *tie_big = -1;
     if (set->ctx != ctx) return fail(LIME_ERR_ARG, "set belongs to another context");
     if (set->strand_in || set->n == 0) {
         LIME_TRY(build_prefix_max(ctx, set));
         return merge_runs_impl(ctx, set, res, true, nullptr);
     }
     std::lock_guard<std::mutex> lock(set->ctx->mu);
-    if (set->pmax) return merge_runs_impl(ctx, set, res, true, nullptr);
+    if (set->pmax) return merge_runs_impl(ctx, set, res, true, nullptr, tie_big);
     uint32_t *pm;
     LIME_TRY(alloc(set->ctx, &pm, (size_t)set->n));
-    const int rc = merge_runs_impl(ctx, set, res, true, pm);
+    const int rc = merge_runs_impl(ctx, set, res, true, pm, tie_big);
     if (rc != LIME_OK) {
         release(set->ctx, pm);
         return rc;

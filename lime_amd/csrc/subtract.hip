@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__
 // the prefix max at its last row before hi1.  O(runs overlapping a) per left
 // row instead of O(hits): at C2's depth (~160 hits per row) one or two runs.
 template <bool WRITE, bool RUNS>
-__global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
+__device__ __forceinline__ void sub_block(const SubArgs &sa, const int64_t blk) {
     __shared__ uint32_t st_gs[WRITE ? SCAP : 1], st_ge[WRITE ? SCAP : 1];
     __shared__ uint32_t st_ar[WRITE ? SCAP : 1], st_br[WRITE ? SCAP : 1];
     __shared__ uint32_t w_pm[BWIN];
@@ -192,10 +192,10 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     __shared__ uint32_t w_gs[BWIN], w_ge[RUNS ? 1 : BWIN], w_row[RUNS ? 1 : BWIN];
     __shared__ uint32_t w_run[RUNS ? BWIN : 1];
     __shared__ uint32_t s_whi[SUB_B / 64];
-    const int64_t i = (int64_t)blockIdx.x * SUB_B + threadIdx.x;
+    const int64_t i = (int64_t)blk * SUB_B + threadIdx.x;
     // RUNS write pass: a block without records has nothing to do (at C2's
     // depth nearly every block)
-    if (RUNS && WRITE && sa.off[blockIdx.x + 1] == sa.off[blockIdx.x]) return;
+    if (RUNS && WRITE && sa.off[blk + 1] == sa.off[blk]) return;
     // the block's hit window [wlo, whi) of B (spanning and inside hits):
     // consecutive left rows share most of it, so it is loaded once,
     // coalesced, into LDS
@@ -206,13 +206,13 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     // workgroups); the block's own is searched from there (every wave alike)
     int64_t wlo;
     if (inl && WRITE) {
-        wlo = sa.bwlo[blockIdx.x];  // (the count pass's)
+        wlo = sa.bwlo[blk];  // (the count pass's)
     } else if (inl) {
-        const int64_t c = sa.wstart[blockIdx.x / CNT_WAVES];
-        const int64_t key = max((int64_t)sa.ags[(int64_t)blockIdx.x * SUB_B] - sa.maxw, (int64_t)0);
+        const int64_t c = sa.wstart[blk / CNT_WAVES];
+        const int64_t key = max((int64_t)sa.ags[(int64_t)blk * SUB_B] - sa.maxw, (int64_t)0);
         wlo = c + dev::wave_lower_bound(sa.bgs + c, sa.nb - c, key);
     } else {
-        wlo = sa.wstart[blockIdx.x];
+        wlo = sa.wstart[blk];
     }
     // inline ranges (RUNS): B rows from wlo staged with their starts, 256 at
     // a time up to BWIN, until the staged starts pass every end of the
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     int nst = 0;
     if (inl) {
         uint32_t amax = 0;
-        for (int64_t q = (int64_t)blockIdx.x * SUB_B + threadIdx.x; q < sa.na &&
-             q < (int64_t)(blockIdx.x + 1) * SUB_B; q += SUB_B)
+        for (int64_t q = (int64_t)blk * SUB_B + threadIdx.x; q < sa.na &&
+             q < (int64_t)(blk + 1) * SUB_B; q += SUB_B)
             amax = sa.age[q];
         amax = dev::wave_reduce_max(amax);
         if (dev::lane_id() == 0) s_whi[threadIdx.x / 64] = amax;
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
     int64_t bbase = 0, bend = 0;
     bool staged = false;
     if (WRITE && !RUNS) {
-        const int64_t first = (int64_t)blockIdx.x * SUB_B;
+        const int64_t first = (int64_t)blk * SUB_B;
         const int64_t last = min(first + SUB_B, sa.na);
         bbase = (int64_t)sa.off[first];
         bend = (int64_t)sa.off[last];
@@ -551,13 +551,13 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             total += s_part[w];
         }
         if (!WRITE) {
-            if (threadIdx.x == 0) sa.count[blockIdx.x] = total;
+            if (threadIdx.x == 0) sa.count[blk] = total;
             return;
         }
-        bbase = (int64_t)sa.off[blockIdx.x];
+        bbase = (int64_t)sa.off[blk];
         // the recount must equal the count pass's block total (k_sub_count_runs
         // folds the same runs): a mismatch would write outside the block
-        if ((int64_t)total != (int64_t)sa.off[blockIdx.x + 1] - bbase) {
+        if ((int64_t)total != (int64_t)sa.off[blk + 1] - bbase) {
             if (threadIdx.x == 0) atomicOr(sa.err, 1u);
             return;
         }
@@ -578,6 +578,34 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
             sa.oar[bbase + k] = st_ar[k];
             sa.obr[bbase + k] = st_br[k];
         }
+    }
+}
+
+// One block of left rows per workgroup, or (RUNS write pass with records
+// rare, SWEEP) a sweep: each workgroup tests SUB_B blocks' record counts at
+// once and folds only the blocks that have records (C2's inputs: 16 records
+// in 390k blocks, whose one-workgroup-per-block launch cost 90 us)
+template <bool WRITE, bool RUNS, bool SWEEP = false>
+__global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
+    if (SWEEP) {
+        __shared__ uint64_t s_mask[SUB_B / 64];
+        const int64_t nblk = (sa.na + SUB_B - 1) / SUB_B;
+        for (int64_t b0 = (int64_t)blockIdx.x * SUB_B; b0 < nblk;
+             b0 += (int64_t)gridDim.x * SUB_B) {
+            const int64_t b = b0 + threadIdx.x;
+            const uint64_t m = __ballot(b < nblk && sa.off[b + 1] != sa.off[b]);
+            if (dev::lane_id() == 0) s_mask[threadIdx.x / 64] = m;
+            __syncthreads();
+            for (int w = 0; w < SUB_B / 64; ++w) {
+                for (uint64_t mm = s_mask[w]; mm; mm &= mm - 1) {  // (uniform)
+                    sub_block<WRITE, RUNS>(sa, b0 + 64 * w + __builtin_ctzll(mm));
+                    __syncthreads();
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+        sub_block<WRITE, RUNS>(sa, blockIdx.x);
     }
 }
 
@@ -638,19 +666,19 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
         return l;
     };
     const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
-    // the rows' bounds in the staged window, a lane's 3 * RPL searches in
+    // the rows' bounds in the staged window, a lane's 2 * RPL searches in
     // lockstep (branchless binary lifting: their LDS reads overlap): lower
-    // bounds of a.s and a.e among the starts, and the number of prefix maxima
-    // <= a.s (pmax is monotone: the first spanning row)
-    int bl[RPL], bh[RPL], bp[RPL];
+    // bounds of a.s and a.e among the starts.  (The first spanning row is
+    // not searched: a spanning block starts before a.s, so its start never
+    // yields a record and the count needs only its existence and end.)
+    int bl[RPL], bh[RPL];
 #pragma unroll
-    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = bp[k] = 0;
+    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = 0;
     for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
             if (bl[k] + step <= nst && w_gs[bl[k] + step - 1] < as[k]) bl[k] += step;
             if (bh[k] + step <= nst && w_gs[bh[k] + step - 1] < ae[k]) bh[k] += step;
-            if (bp[k] + step <= nst && w_pm[bp[k] + step - 1] <= as[k]) bp[k] += step;
         }
     }
     uint64_t tot = 0;
@@ -679,13 +707,12 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
                 if (be > setpos) setpos = be;
             }
         };
-        // the spanning block: first j in [wlo, lo1) with pmax > thr
+        // the spanning block (rows before lo1 reaching past thr): it starts
+        // before a.s (bs = 0 stands for that start), ends at the prefix max
         const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
         if (lo1 > 0 && pm_last > thr) {
-            // in the staged window when any staged pmax exceeds thr
-            const int64_t j0 = bp[k] < nst ? wlo + bp[k] : first_spanning(sa.bpmax, lo1, thr);
             any = true;
-            bs = GS(j0);
+            bs = 0;
             be = pm_last;
         }
         int64_t j = lo1;
@@ -1071,12 +1098,13 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
                     const uint32_t *d_row, const uint32_t *d_len);
 
 // B's tie index, built once per set (under its context's lock) when some
-// same-start group has more than TIE_G rows; else tie_n = 0
-static int build_tie_index(lime_ctx *ctx, const lime_set *B) {
+// same-start group has more than TIE_G rows; else tie_n = 0.  known: whether
+// one has (the merge scan tests it on the runs path), -1 unknown
+static int build_tie_index(lime_ctx *ctx, const lime_set *B, int known) {
     std::lock_guard<std::mutex> lock(B->ctx->mu);
     if (B->tie_n >= 0) return LIME_OK;
     const int64_t n = B->n;
-    if (n <= TIE_G) {
+    if (n <= TIE_G || known == 0) {
         B->tie_n = 0;
         return LIME_OK;
     }
@@ -1087,10 +1115,10 @@ static int build_tie_index(lime_ctx *ctx, const lime_set *B) {
     big = reinterpret_cast<unsigned int *>(tot + 1);
     LIME_HIP(hipMemsetAsync(tot, 0, 8, S(ctx)));
     // (most sets have no long same-start group: one read of gs decides)
-    hipLaunchKernelGGL(k_tie_detect, dim3(blocks_for((n + 3) / 4, 256)), dim3(256), 0, S(ctx),
-                       B->gs, n, big);
-    LIME_HIP(hipGetLastError());
-    {
+    if (known < 0) {
+        hipLaunchKernelGGL(k_tie_detect, dim3(blocks_for((n + 3) / 4, 256)), dim3(256), 0,
+                           S(ctx), B->gs, n, big);
+        LIME_HIP(hipGetLastError());
         uint32_t hb[2] = {0, 0};
         LIME_TRY(read_back(ctx, hb, tot, sizeof(hb)));
         if (!hb[1]) {
@@ -1139,7 +1167,7 @@ static int build_tie_index(lime_ctx *ctx, const lime_set *B) {
 }
 
 int merge_runs(lime_ctx *ctx, const lime_set *set, lime_result *res, bool want_run_ids);
-int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res);
+int merge_runs_with_pmax(lime_ctx *ctx, const lime_set *set, lime_result *res, int *tie_big);
 
 int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t threshold, int mode,
                  lime_result *res) {
@@ -1180,7 +1208,9 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     PoolGuard<uint32_t> g1{ctx, mb.run_of_sorted};
     PoolGuard<uint32_t> g2{ctx, mb.gs};
     PoolGuard<uint32_t> g3{ctx, mb.ge};
-    if (runs) LIME_TRY(merge_runs_with_pmax(ctx, B, &mb));
+    // (the same scan tells whether B has a same-start group past TIE_G)
+    int tie_big = -1;
+    if (runs) LIME_TRY(merge_runs_with_pmax(ctx, B, &mb, &tie_big));
     // runs, one pass (k_sub_fused) when records are plentiful (they come
     // from A rows crossing the ends of B's runs: the sparse 1e9-row subtract,
     // 9.2e6 runs of B, 7.4e7 records for 5e8 rows); B merging into fewer runs
@@ -1229,7 +1259,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.off = off;
     sa.err = err;
     // the tie index of B (long same-start groups), built once per set
-    if (B->n > 0) LIME_TRY(build_tie_index(ctx, B));
+    if (B->n > 0) LIME_TRY(build_tie_index(ctx, B, tie_big));
     sa.tgs = B->tie_gs;
     sa.tge = B->tie_ge;
     sa.trow = B->tie_row;
@@ -1284,9 +1314,14 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         res->n = (int64_t)total;
         return LIME_OK;
     }
+    // runs write pass with records rare (under one per 16 blocks): the
+    // sweeping form of k_subtract, SUB_B blocks tested per workgroup
+    int sparse = 0;
     auto launch = [&](bool write) {
-        const dim3 g(blocks_for(na, SUB_B)), b(SUB_B);
-        if (write && runs) hipLaunchKernelGGL((k_subtract<true, true>), g, b, 0, S(ctx), sa);
+        const dim3 g(sparse ? blocks_for(nblk, SUB_B) : blocks_for(na, SUB_B)), b(SUB_B);
+        if (write && runs && sparse)
+            hipLaunchKernelGGL((k_subtract<true, true, true>), g, b, 0, S(ctx), sa);
+        else if (write && runs) hipLaunchKernelGGL((k_subtract<true, true>), g, b, 0, S(ctx), sa);
         else if (write) hipLaunchKernelGGL((k_subtract<true, false>), g, b, 0, S(ctx), sa);
         else if (runs) hipLaunchKernelGGL((k_subtract<false, true>), g, b, 0, S(ctx), sa);
         else hipLaunchKernelGGL((k_subtract<false, false>), g, b, 0, S(ctx), sa);
@@ -1310,6 +1345,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.oge = res->ge;
     sa.oar = res->a_row;
     sa.obr = res->b_row;
+    sparse = runs && (int64_t)total * 16 < nblk;
     launch(true);
     LIME_HIP(hipGetLastError());
     if (runs) {

@@ -566,6 +566,13 @@ class Context:
         check(_lib().lime_synth_uniform_rows(self._h, space.handle, int(first), int(n), int(seed),
                                              int(len_lo), int(len_hi), d_contig, d_start, d_end))
 
+    def synth_pileup_rows(self, space, first, n, seed, n_centres, sigma, len_lo, len_hi,
+                          d_contig, d_start, d_end):
+        """rows [first, first + n) of lime_synth_pileup's sequence"""
+        check(_lib().lime_synth_pileup_rows(self._h, space.handle, int(first), int(n), int(seed),
+                                            int(n_centres), int(sigma), int(len_lo), int(len_hi),
+                                            d_contig, d_start, d_end))
+
     def synth_pileup(self, space, n, seed, n_centres, sigma, len_lo, len_hi, d_contig, d_start,
                      d_end):
         check(_lib().lime_synth_pileup(self._h, space.handle, int(n), int(seed), int(n_centres),
@@ -626,13 +633,6 @@ class DeviceBed:
         check(_lib().lime_dbed_remap_contigs(self._h, _ptr(ids, i32), len(ids)))
         c, s, e, _ = self.device_arrays()
         return self.ctx.set_from_device(space, self.n, c, s, e)
-
-    def synth_pileup_rows(self, space, first, n, seed, n_centres, sigma, len_lo, len_hi,
-                          d_contig, d_start, d_end):
-        """rows [first, first + n) of lime_synth_pileup's sequence"""
-        check(_lib().lime_synth_pileup_rows(self._h, space.handle, int(first), int(n), int(seed),
-                                            int(n_centres), int(sigma), int(len_lo), int(len_hi),
-                                            d_contig, d_start, d_end))
 
     def close(self):
         if self._h:

@@ -651,6 +651,64 @@ def test_bitset_and_fused(ctx, k, max_len):
         assert got[key].tolist() == exp[key].tolist()
 
 
+def test_bitset_binned_runs_tile_edges(ctx):
+    # bitsets from rows stay binned; an op's runs come straight from the bins
+    # (k_paint_ev: per 2^19-base paint tile, events with the bit before the
+    # tile taken as 0, runs crossing a tile boundary joined by k_ev_join).
+    # Rows ending / starting exactly on tile boundaries, crossing them and
+    # wholly covering a tile, against the words path (a bitset from the
+    # sorted set: painted words) and the oracle; a dense tile past its event
+    # slot falls back to the words path
+    from tests.test_gpu_configs import coalesce
+    T = 1 << 19
+    L = 3_000_000
+    rng = np.random.default_rng(97)
+    sets = []
+    for extra in ([(T - 100, T), (T, T + 50), (2 * T - 10, 2 * T + 10), (2 * T - 5, 3 * T + 5),
+                   (4 * T, 4 * T + 1), (5 * T - 1, 5 * T)],
+                  [(T - 50, T + 30), (3 * T, 3 * T + 7), (4 * T - 3, 4 * T + 3)]):
+        A = random_sets(rng, 3000, 1, n_contigs=1, contig_len=L, max_len=2000, zero_frac=0.02)[0]
+        A = [np.concatenate([A[0], np.zeros(len(extra), A[0].dtype)]),
+             np.concatenate([A[1], np.array([a for a, _ in extra], A[1].dtype)]),
+             np.concatenate([A[2], np.array([b for _, b in extra], A[2].dtype)])]
+        sets.append(A)
+    sp = space_for(1, L)
+    binned = [ctx.bitset_from_device(sp, len(A[0]), *(x.data_ptr() for x in _dev_rows(A)))
+              for A in sets]
+    words = [ctx.bitset(ctx.set_from_host(sp, *A)) for A in sets]
+
+    def runs(r):
+        h = r.to_host()
+        return [x.tolist() for x in coalesce(h["contig"], h["start"], h["end"])]
+
+    ma, mb = (oracle.merge(A) for A in sets)
+    for op in (0, 1, 2, 3):
+        b = 1 if op >= 2 else None
+        got = ctx.bitset_runs(op, binned[0], binned[b] if b else None)
+        ref = ctx.bitset_runs(op, words[0], words[b] if b else None)
+        mixed = ctx.bitset_runs(op, words[0], binned[b] if b else None)
+        assert runs(got) == runs(ref) == runs(mixed), op
+        # the fused path's runs are maximal already (no coalescing needed)
+        h = got.to_host()
+        assert not np.any(h["start"][1:] == h["end"][:-1])
+    exp = oracle.complement(sets[0], [L])
+    assert runs(ctx.bitset_runs(1, binned[0])) == [x.tolist() for x in coalesce(
+        exp["contig"], exp["start"], exp["end"])]
+    sub = oracle.subtract((ma["contig"], ma["start"], ma["end"]),
+                          (mb["contig"], mb["start"], mb["end"]), 0, oracle.SUB_SET)
+    keep = sub["end"] > sub["start"]  # (zero-width rows' runs hold no base)
+    assert runs(ctx.bitset_runs(3, *binned)) == [x.tolist() for x in coalesce(
+        sub["contig"][keep], sub["start"][keep], sub["end"][keep])]
+    assert binned[0].popcount() == words[0].popcount() == int((ma["end"] - ma["start"]).sum())
+    # 3000 one-base rows two apart in tile 0: 6000 events past the 4096 slot
+    n = 3000
+    D = [np.zeros(n, np.int32), (10 + 2 * np.arange(n)).astype(np.uint32),
+         (11 + 2 * np.arange(n)).astype(np.uint32)]
+    bd = ctx.bitset_from_device(sp, n, *(x.data_ptr() for x in _dev_rows(D)))
+    got = ctx.bitset_runs(0, bd).to_host()
+    assert got["start"].tolist() == D[1].tolist() and got["end"].tolist() == D[2].tolist()
+    assert ctx.bitset_runs(1, bd).n == n + 1
+
 def test_bitset_and_fused_window(ctx):
     # a shard's window from global rows == the per-set window bitsets' AND
     import torch
@@ -880,6 +938,33 @@ def test_subtract_one_pass_and_two_pass(ctx, mode, deep):
     res = ctx.subtract(ctx.set_from_host(sp, *A), sb, 0, mode).to_host()
     _sub_equal(res, oracle.subtract(A, B, 0, mode))
 
+
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+def test_subtract_sweeping_write_pass(ctx, mode):
+    # records under one per 16 blocks of 256 left rows (B covering A, C2's
+    # shape) take the sweeping write pass (k_subtract<true, true, true>):
+    # each workgroup tests 256 blocks and folds only those with records.
+    # 120k left rows inside B's rows but for two narrow gaps between them,
+    # a few rows past B and one crossing B's end: a handful of records in
+    # both workgroups' sweeps
+    rng = np.random.default_rng(77)
+    L = 2_000_000
+    n = 120_000
+    st = np.sort(rng.integers(10, 1_400_000, n)).astype(np.uint32)
+    A = [np.zeros(n, np.int32), st, st + rng.integers(1, 40, n).astype(np.uint32)]
+    for i in (0, 255, 256, 30_000):  # left rows past B (their own records)
+        A[1][i], A[2][i] = 1_900_000 + i, 1_900_010 + i
+    A[1][-1], A[2][-1] = 1_499_990, 1_600_000  # crosses B's end
+    o = np.lexsort((A[2], A[1], A[0]))
+    A = [x[o] for x in A]
+    B = [np.zeros(4, np.int32), np.array([0, 5, 500_001, 1_200_001], np.uint32),
+         np.array([500_000, 400_000, 1_200_000, 1_500_000], np.uint32)]
+    sp = space_for(1, L)
+    res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), 0, mode).to_host()
+    exp = oracle.subtract(A, B, 0, mode)
+    assert 0 < len(exp["start"]) * 16 < (n + 255) // 256
+    assert len(set(exp["a_row"] // 65536)) == 2  # records in both sweeps
+    _sub_equal(res, exp)
 
 def test_bitset_and_past_sixteen_sets(ctx):
     # the fused AND paints 16 sets per kernel and chains the groups

@@ -7,7 +7,7 @@ import sqlite3
 import sys
 
 tag = sys.argv[1]
-KS = ["k_fill<false>", "k_count", "k_windows", "k_scatter", "k_hist", "k_prep", "k_merge_scan"]
+KS = ["k_fill<", "k_count", "k_windows", "k_scatter", "k_hist", "k_prep", "k_merge_scan"]
 for txt in sorted(glob.glob(f"gpurun_out/{tag}_*.txt")):
     line = [ln for ln in open(txt) if ln.startswith('{"metric"')]
     ms = json.loads(line[0])["ms_per_step"] if line else float("nan")

@@ -1,0 +1,10 @@
+# Round-4 combined check: GPU tests (KEXPR), the same tests on a variant
+# library (VLIB / VEXPR), then bench A/B lines (WORKS over LIBS) and the
+# bench workloads' operators lines (tools/gpu_r4_ops.sh).
+#   KEXPR=... VLIB=... VEXPR=... WORKS=... LIBS=... bash tools/gpu_r4_round.sh TAG
+set -o pipefail
+T=${1:-r4r}
+if [ -n "$KEXPR" ]; then KEXPR="$KEXPR" bash tools/gpu_r4_check.sh ${T}k || exit 1; fi
+if [ -n "$VLIB" ]; then LIME_AMD_LIB_VARIANT=$PWD/$VLIB KEXPR="$VEXPR" bash tools/gpu_r4_check.sh ${T}v || exit 1; fi
+if [ -n "$WORKS" ]; then bash tools/gpu_ab.sh ${T}ab "" "$WORKS" $LIBS || exit 1; fi
+if [ -n "$OPS" ]; then bash tools/gpu_r4_ops.sh ${T}o || exit 1; fi

@@ -1306,35 +1306,62 @@ int bucket_cross(lime_ctx *ctx, int64_t tstride, const uint64_t *cross,
     return LIME_OK;
 }
 
-AndArgs binned_args(const lime_bitset *const *sets, int k) {
+// paint arguments over binned row sets (k <= MAXK, nt tiles each)
+AndArgs binned_args(const lime_bitset::Bins *const *b, int k, int64_t nt, int64_t n_words) {
     AndArgs aa;
     for (int i = 0; i < MAXK; ++i) {
         const bool v = i < k;
-        const size_t ts = v ? (size_t)sets[i]->nt + 1 : 0;
-        aa.slab2[i] = v ? sets[i]->slab2 : nullptr;
-        aa.tstart[i] = v ? sets[i]->tstart : nullptr;
-        aa.xl[i] = v ? sets[i]->xl : nullptr;
-        aa.xoff[i] = v && sets[i]->xl ? sets[i]->xb : nullptr;
-        aa.full[i] = v && sets[i]->xl ? sets[i]->xb + ts : nullptr;
+        aa.slab2[i] = v ? b[i]->slab2 : nullptr;
+        aa.tstart[i] = v ? b[i]->tstart : nullptr;
+        aa.xl[i] = v ? b[i]->xl : nullptr;
+        aa.xoff[i] = v && b[i]->xl ? b[i]->xb : nullptr;
+        aa.full[i] = v && b[i]->xl ? b[i]->xb + nt + 1 : nullptr;
     }
     aa.k = k;
     aa.init = 0;
     aa.words = nullptr;
-    aa.n_words = k > 0 ? sets[0]->n_words : 0;
+    aa.n_words = n_words;
     return aa;
+}
+
+// one row set binned by paint tile into `b` (owned by the bitset): its rows
+// grouped (bin_rows), the row errors checked, its cross pieces bucketed
+int bin_set(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+            const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
+            const uint32_t *d_len, int64_t lo, int64_t hi, int64_t nt, lime_bitset::Bins &b) {
+    LIME_TRY(alloc(ctx, &b.tstart, (size_t)nt + 1));
+    LIME_TRY(alloc(ctx, &b.slab2, (size_t)std::max<int64_t>(n, 1)));
+    PoolBag bag{ctx, {}};
+    uint64_t *cross;
+    unsigned int *flags;  // [0] ncross, [1] err
+    LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * n, 1)));
+    LIME_TRY(bag.get(&flags, 2));
+    LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
+    LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, b.slab2,
+                      b.tstart, cross, flags));
+    unsigned int h[2] = {0, 0};
+    LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
+    LIME_TRY(rows_error(h[1]));
+    if (h[0]) {
+        LIME_TRY(alloc(ctx, &b.xb, 3 * ((size_t)nt + 1)));
+        LIME_TRY(alloc(ctx, &b.xl, 2 * (size_t)h[0]));
+        LIME_TRY(bucket_cross(ctx, nt + 1, cross, flags, h[0], b.xb, b.xl));
+    }
+    return LIME_OK;
 }
 }  // namespace
 
 void bitset_free(lime_bitset *bs) {
     lime_ctx *ctx = bs->ctx;
     release(ctx, bs->words);
-    release(ctx, bs->slab2);
-    release(ctx, bs->tstart);
-    release(ctx, bs->xl);
-    release(ctx, bs->xb);
     bs->words = nullptr;
-    bs->slab2 = bs->tstart = bs->xb = nullptr;
-    bs->xl = nullptr;
+    for (auto &b : bs->bins) {
+        release(ctx, b.slab2);
+        if (b.own_tstart) release(ctx, b.tstart);
+        release(ctx, b.xl);
+        release(ctx, b.xb);
+    }
+    bs->bins.clear();
 }
 
 // bits straight from UNSORTED device rows, no sort, no merge: the rows are
@@ -1348,45 +1375,37 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
                       const uint32_t *d_len, int64_t lo, int64_t hi, lime_bitset *bs) {
     window_of(bs, sp, lo, hi);
     bs->runs_bound = n;  // the union of n rows has at most n runs
-    const int64_t nt = n_bins(hi - lo) * PSUB;
-    bs->nt = nt;
-    LIME_TRY(alloc(ctx, &bs->tstart, (size_t)nt + 1));
-    LIME_TRY(alloc(ctx, &bs->slab2, (size_t)std::max<int64_t>(n, 1)));
-    PoolBag bag{ctx, {}};
-    uint64_t *cross;
-    unsigned int *flags;  // [0] ncross, [1] err
-    LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * n, 1)));
-    LIME_TRY(bag.get(&flags, 2));
-    LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
-    LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, bs->slab2,
-                      bs->tstart, cross, flags));
-    unsigned int h[2] = {0, 0};
-    LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
-    LIME_TRY(rows_error(h[1]));
-    if (h[0]) {
-        LIME_TRY(alloc(ctx, &bs->xb, 3 * ((size_t)nt + 1)));
-        LIME_TRY(alloc(ctx, &bs->xl, 2 * (size_t)h[0]));
-        LIME_TRY(bucket_cross(ctx, nt + 1, cross, flags, h[0], bs->xb, bs->xl));
-    }
-    return LIME_OK;
+    bs->nt = n_bins(hi - lo) * PSUB;
+    bs->bins.resize(1);
+    return bin_set(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, bs->nt,
+                   bs->bins[0]);
 }
 
-// the words of a binned bitset, painted once (k_paint_and over its one set)
+// the words of a binned bitset, painted once: k_paint_and over its sets
+// (groups of MAXK, each ANDing into the words the earlier ones stored)
 int bitset_paint(lime_ctx *ctx, const lime_bitset *cbs) {
     lime_bitset *bs = const_cast<lime_bitset *>(cbs);  // (a cache: the bits are unchanged)
-    if (bs->words || !bs->slab2) return LIME_OK;
+    if (bs->words || bs->bins.empty()) return LIME_OK;
     LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
-    AndArgs aa = binned_args(&cbs, 1);
-    aa.words = bs->words;
-    if (bs->nt > 0)
-        hipLaunchKernelGGL(k_paint_and, dim3((unsigned)bs->nt), dim3(PAINTB), 0, S(ctx), aa);
+    const int k = (int)bs->bins.size();
+    for (int g0 = 0; g0 < k; g0 += MAXK) {
+        std::vector<const lime_bitset::Bins *> b;
+        for (int i = g0; i < std::min(k, g0 + MAXK); ++i) b.push_back(&bs->bins[i]);
+        AndArgs aa = binned_args(b.data(), (int)b.size(), bs->nt, bs->n_words);
+        aa.init = g0 > 0;
+        aa.words = bs->words;
+        if (bs->nt > 0)
+            hipLaunchKernelGGL(k_paint_and, dim3((unsigned)bs->nt), dim3(PAINTB), 0, S(ctx), aa);
+    }
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
 
 // the AND of k row sets' bits over window [lo, hi), straight from their
-// unsorted rows (bin_rows per set, k_paint_and once): rows[i] = (n, contig
-// or null for global rows, start, end)
+// unsorted rows: every set binned (bin_rows) and kept, so the bitset is
+// their AND in binned form -- its runs come from one k_paint_ev over all the
+// sets (k <= MAXK), its words, when needed, from k_paint_and (bitset_paint).
+// rows[i] = (n, contig or null for global rows, start, end)
 int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n,
                     const int32_t *const *d_contig, const uint32_t *const *d_start,
                     const uint32_t *const *d_end, const uint32_t *d_off, const uint32_t *d_len,
@@ -1399,8 +1418,9 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
         bound += n[i];
     }
     bs->runs_bound = bound;  // each AND run starts at a run start of some set
-    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
-    const int nt = n_bins(hi - lo) * PSUB;
+    const int64_t nt = n_bins(hi - lo) * PSUB;
+    bs->nt = nt;
+    bs->bins.resize(k);
     PoolBag keep{ctx, {}};
     // two cross buffers: set q's rows are binned while set q - 1's cross
     // pieces are read back and bucketed, so the host waits on an event of set
@@ -1423,64 +1443,39 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     } ev;
     for (int j = 0; j < 2; ++j)
         LIME_HIP(hipEventCreateWithFlags(&ev.e[j], hipEventDisableTiming));
-    // groups of MAXK sets, each painted and ANDed in one k_paint_and; a group
-    // after the first ANDs into the words the earlier ones stored
-    for (int g0 = 0; g0 < k; g0 += MAXK) {
-        const int kg = std::min(MAXK, k - g0);
-        PoolBag bag{ctx, {}};  // (released in stream order after the paint)
-        AndArgs aa;
-        for (int i = 0; i < MAXK; ++i) {
-            aa.slab2[i] = aa.tstart[i] = aa.xoff[i] = aa.full[i] = nullptr;
-            aa.xl[i] = nullptr;
-        }
-        aa.k = kg;
-        aa.init = g0 > 0;
-        aa.words = bs->words;
-        aa.n_words = bs->n_words;
-        // the group's tile totals: one block, zeroed once
-        uint32_t *ttot_all;
-        const size_t tstride = (size_t)nt + 1;
-        LIME_TRY(bag.get(&ttot_all, tstride * (size_t)kg));
-        LIME_HIP(hipMemsetAsync(ttot_all, 0, 4 * tstride * (size_t)kg, S(ctx)));
-        // bucket set q's cross pieces by tile (its flags were copied to the
-        // host behind its binning; wait for that copy only)
-        auto bucket = [&](int q) -> int {
-            const int i = g0 + q;
-            LIME_HIP(hipEventSynchronize(ev.e[q % 2]));
-            const unsigned int nx = hflags[2 * q], err = hflags[2 * q + 1];
-            LIME_TRY(rows_error(err));
-            if (nx == 0) return LIME_OK;
-            // [counts | difference array | fill claims], zeroed at once
-            uint32_t *xb;
-            uint2 *xl;
-            LIME_TRY(bag.get(&xb, 3 * tstride));
-            LIME_TRY(bag.get(&xl, 2 * (size_t)nx));
-            LIME_TRY(bucket_cross(ctx, (int64_t)tstride, cross[q % 2],
-                                  (const unsigned int *)(flags + 2 * i), nx, xb, xl));
-            aa.xl[q] = xl;
-            aa.xoff[q] = xb;
-            aa.full[q] = xb + tstride;
-            return LIME_OK;
-        };
-        for (int q = 0; q < kg; ++q) {
-            const int i = g0 + q;
-            uint32_t *slab2, *ttot = ttot_all + tstride * (size_t)q;
-            LIME_TRY(bag.get(&slab2, (size_t)std::max<int64_t>(n[i], 1)));
-            // (cross[q % 2] was last used by set q - 2, bucketed before this)
-            LIME_TRY(bin_rows(ctx, sp, n[i], d_contig[i], d_start[i], d_end[i], d_off, d_len, lo,
-                              hi, slab2, ttot, cross[q % 2], flags + 2 * i, true));
-            LIME_HIP(hipMemcpyAsync(hflags + 2 * q, flags + 2 * i, 8, hipMemcpyDeviceToHost,
-                                    S(ctx)));
-            LIME_HIP(hipEventRecord(ev.e[q % 2], S(ctx)));
-            aa.slab2[q] = slab2;
-            aa.tstart[q] = ttot;
-            if (q > 0) LIME_TRY(bucket(q - 1));
-        }
-        LIME_TRY(bucket(kg - 1));
-        hipLaunchKernelGGL(k_paint_and, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), aa);
-        LIME_HIP(hipGetLastError());
+    // every set's tile totals: one block (owned by set 0), zeroed once
+    const size_t tstride = (size_t)nt + 1;
+    uint32_t *ttot_all;
+    LIME_TRY(alloc(ctx, &ttot_all, tstride * (size_t)k));
+    bs->bins[0].tstart = ttot_all;
+    for (int i = 1; i < k; ++i) bs->bins[i].own_tstart = false;
+    LIME_HIP(hipMemsetAsync(ttot_all, 0, 4 * tstride * (size_t)k, S(ctx)));
+    // bucket set q's cross pieces by tile (its flags were copied to the host
+    // behind its binning; wait for that copy only)
+    auto bucket = [&](int q) -> int {
+        LIME_HIP(hipEventSynchronize(ev.e[q % 2]));
+        const unsigned int nx = hflags[2 * (q % 2)], err = hflags[2 * (q % 2) + 1];
+        LIME_TRY(rows_error(err));
+        if (nx == 0) return LIME_OK;
+        lime_bitset::Bins &b = bs->bins[q];
+        LIME_TRY(alloc(ctx, &b.xb, 3 * tstride));
+        LIME_TRY(alloc(ctx, &b.xl, 2 * (size_t)nx));
+        return bucket_cross(ctx, (int64_t)tstride, cross[q % 2],
+                            (const unsigned int *)(flags + 2 * q), nx, b.xb, b.xl);
+    };
+    for (int q = 0; q < k; ++q) {
+        lime_bitset::Bins &b = bs->bins[q];
+        b.tstart = ttot_all + tstride * (size_t)q;
+        LIME_TRY(alloc(ctx, &b.slab2, (size_t)std::max<int64_t>(n[q], 1)));
+        // (cross[q % 2] was last used by set q - 2, bucketed before this)
+        LIME_TRY(bin_rows(ctx, sp, n[q], d_contig[q], d_start[q], d_end[q], d_off, d_len, lo, hi,
+                          b.slab2, b.tstart, cross[q % 2], flags + 2 * q, true));
+        LIME_HIP(hipMemcpyAsync(hflags + 2 * (q % 2), flags + 2 * q, 8, hipMemcpyDeviceToHost,
+                                S(ctx)));
+        LIME_HIP(hipEventRecord(ev.e[q % 2], S(ctx)));
+        if (q > 0) LIME_TRY(bucket(q - 1));
     }
-    return LIME_OK;
+    return bucket(k - 1);
 }
 
 namespace {
@@ -1493,9 +1488,17 @@ int runs_binned(lime_ctx *ctx, int op, int nin, const lime_bitset *const *sets, 
     *overflow = false;
     const lime_bitset *a = sets[0];
     const int64_t nt = a->nt;
+    // every operand's binned sets, the complemented operand's (one) marked
+    std::vector<const lime_bitset::Bins *> b;
+    uint32_t neg = 0;
+    for (int i = 0; i < nin; ++i) {
+        const bool inv = (op == 1 && i == 0) || (op == 3 && i == 1);
+        if (inv) neg |= 1u << b.size();
+        for (const auto &x : sets[i]->bins) b.push_back(&x);
+    }
     PaintEvArgs pa;
-    pa.s = binned_args(sets, nin);
-    pa.neg = op == 1 ? 1u : (op == 3 ? 2u : 0u);
+    pa.s = binned_args(b.data(), (int)b.size(), nt, a->n_words);
+    pa.neg = neg;
     pa.notmask = op == 1;
     pa.word0 = a->word0;
     pa.hi_bit = a->hi_bit;
@@ -1504,12 +1507,14 @@ int runs_binned(lime_ctx *ctx, int op, int nin, const lime_bitset *const *sets, 
     pa.off = d_off;
     pa.nc = a->n_contigs;
     // runs bound (a run starts at a run start of an operand, or a contig's
-    // start for NOT) -> a slot of twice the mean events per tile + 2048
+    // start for NOT) -> a slot of twice the bound's mean events per tile +
+    // 2048, within [4096, 16384] (an AND's bound, the sum, is loose: past the
+    // slot a tile falls back to the words path)
     int64_t bound = op == 1 ? (int64_t)a->n_contigs + 1 : 0;
     for (int i = 0; i < nin && bound >= 0; ++i)
         bound = sets[i]->runs_bound < 0 ? -1 : bound + sets[i]->runs_bound;
     int64_t cap = bound < 0 ? 16384 : 2 * (2 * bound / std::max<int64_t>(nt, 1)) + 2048;
-    cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), 1 << 20);
+    cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), 16384);
     pa.cap = (uint32_t)cap;
     PoolBag bag{ctx, {}};
     uint32_t *tev, *tcnt, *edge, *cnt2, *skip1, *toff;
@@ -1533,7 +1538,7 @@ int runs_binned(lime_ctx *ctx, int op, int nin, const lime_bitset *const *sets, 
     LIME_TRY(scan_exclusive_u32(ctx, cnt2, toff, nt, hdr + 1));
     // with a bound the result is allocated at it and the gather queued
     // before the host reads the totals (as bitset_runs)
-    const int64_t rcap = bound;
+    const int64_t rcap = bound < 0 ? -1 : std::min<int64_t>(bound, nt * (cap / 2));
     auto gather = [&](uint32_t cap_events) {
         hipLaunchKernelGGL(k_ev_gather, dim3((unsigned)nt), dim3(256), 0, S(ctx),
                            (const uint32_t *)tev, (const uint32_t *)cnt2, (const uint32_t *)toff,
@@ -1577,8 +1582,17 @@ int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, li
     // binned operands (bitsets from rows): the runs straight from the bins,
     // unless a tile overflows its event slot; else (or then) from words
     const int nin = op == 4 ? k : (op >= 2 ? 2 : 1);
-    bool binned = a->n_words > 0 && nin <= MAXK;
-    for (int i = 0; i < nin; ++i) binned = binned && sets[i]->slab2 && sets[i]->nt == a->nt;
+    // (a complemented operand must be ONE binned set: ~(x & y) is not a
+    // complement per set; at most MAXK binned sets in all)
+    bool binned = a->n_words > 0;
+    size_t nb = 0;
+    for (int i = 0; i < nin; ++i) {
+        const bool inv = (op == 1 && i == 0) || (op == 3 && i == 1);
+        binned = binned && !sets[i]->bins.empty() && sets[i]->nt == a->nt &&
+                 (!inv || sets[i]->bins.size() == 1);
+        nb += sets[i]->bins.size();
+    }
+    binned = binned && nb <= (size_t)MAXK;
     if (binned) {
         bool overflow = false;
         LIME_TRY(runs_binned(ctx, op, nin, sets, res, &overflow));

@@ -161,14 +161,19 @@ struct lime_bitset {
     int32_t n_contigs = 0;
     std::vector<uint32_t> off;
     std::vector<int64_t> len;
-    // binned form (bitset_build_rows): the rows grouped by paint tile, words
-    // painted on first need (null until then) or never, when an op's runs
-    // are extracted straight from the bins (k_paint_ev)
-    uint32_t *slab2 = nullptr;   // packed rows, tile order
-    uint32_t *tstart = nullptr;  // nt + 1 tile starts
-    uint2 *xl = nullptr;         // tile-bucketed cross pieces (null: none)
-    uint32_t *xb = nullptr;      // [bucket starts | full-tile scan | fill] x (nt + 1)
-    int64_t nt = 0;              // paint tiles (0: not binned)
+    // binned form (bitset_build_rows, bitset_and_rows): the bits are the AND
+    // of these row sets, each grouped by paint tile; words painted on first
+    // need (null until then) or never, when an op's runs are extracted
+    // straight from the bins (k_paint_ev)
+    struct Bins {
+        uint32_t *slab2 = nullptr;   // packed rows, tile order
+        uint32_t *tstart = nullptr;  // nt + 1 tile starts
+        uint2 *xl = nullptr;         // tile-bucketed cross pieces (null: none)
+        uint32_t *xb = nullptr;      // [bucket starts | full-tile scan | fill] x (nt + 1)
+        bool own_tstart = true;      // (else inside the first set's block)
+    };
+    std::vector<Bins> bins;
+    int64_t nt = 0;  // paint tiles of the bins
 };
 
 namespace lime {

@@ -700,6 +700,18 @@ def test_bitset_binned_runs_tile_edges(ctx):
     assert runs(ctx.bitset_runs(3, *binned)) == [x.tolist() for x in coalesce(
         sub["contig"][keep], sub["start"][keep], sub["end"][keep])]
     assert binned[0].popcount() == words[0].popcount() == int((ma["end"] - ma["start"]).sum())
+    # the k-way AND kept binned (its runs from one k_paint_ev over both sets;
+    # popcount paints its words) == the words path's a & b
+    dev = [_dev_rows(A) for A in sets]
+    fused = ctx.bitset_and_from_device(sp, [(len(A[0]), *(x.data_ptr() for x in t))
+                                            for A, t in zip(sets, dev)])
+    ref = ctx.bitset_runs(2, words[0], words[1])
+    assert runs(ctx.bitset_runs(0, fused)) == runs(ref)
+    pop = int((ref.to_host()["end"] - ref.to_host()["start"]).sum())
+    assert fused.popcount() == pop
+    nf = ctx.bitset_runs(1, fused).to_host()  # (~(a & b): the words path)
+    assert int((nf["end"] - nf["start"]).sum()) == L - pop
+    assert runs(ctx.bitset_runs(0, fused)) == runs(ref)  # (words painted now: same runs)
     # 3000 one-base rows two apart in tile 0: 6000 events past the 4096 slot
     n = 3000
     D = [np.zeros(n, np.int32), (10 + 2 * np.arange(n)).astype(np.uint32),

@@ -124,6 +124,9 @@ struct BinArgs {
     uint32_t nchunks;
     uint32_t *mat;             // nb * nchunks + 1 (counts, then scanned starts)
     uint32_t *ttot;            // nb * PSUB + 1 tile totals, then scanned starts
+    uint32_t *gsum;            // ngroups x (nb * PSUB): rows per (chunk group, paint tile)
+    uint32_t *gpre;            // (nb * PSUB) x ngroups: rows of a tile in earlier chunk groups
+    int ngroups;               // split workgroups per bin (chunk groups)
     uint32_t *slab;            // n packed rows, bin order
     uint32_t *slab2;           // n packed rows, paint tile order
     uint64_t *cross;           // remainders (s << 32 | e) in window bits, capacity n
@@ -266,8 +269,28 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
         for (int q = 0; q < PSUB; ++q) sum += hist[b * PSUB + q];
         a.mat[(int64_t)b * a.nchunks + ch] = sum;
     }
+    // the chunk's rows per paint tile into its chunk group's totals (the
+    // split runs one workgroup per (bin, chunk group))
+    uint32_t g = (uint32_t)(((uint64_t)ch * a.ngroups + a.ngroups - 1) / a.nchunks);
+    while (g > 0 && (int64_t)(g * (uint64_t)a.nchunks / a.ngroups) > ch) --g;
+    while (g + 1 < (uint32_t)a.ngroups && (int64_t)((g + 1) * (uint64_t)a.nchunks / a.ngroups) <= ch)
+        ++g;
     for (int t = threadIdx.x; t < nt; t += BINB)
-        if (hist[t]) atomicAdd(&a.ttot[t], hist[t]);
+        if (hist[t]) atomicAdd(&a.gsum[(int64_t)g * nt + t], hist[t]);
+}
+
+// per paint tile: its rows in the chunk groups before each group (gpre) and
+// in all (ttot, scanned next into the tile starts)
+__global__ __launch_bounds__(256) void k_tile_groups(BinArgs a) {
+    const int nt = a.nb * PSUB;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= nt) return;
+    uint32_t run = 0;
+    for (int g = 0; g < a.ngroups; ++g) {
+        a.gpre[(int64_t)t * a.ngroups + g] = run;
+        run += a.gsum[(int64_t)g * nt + t];
+    }
+    a.ttot[t] = run;
 }
 
 #ifndef LIME_WRITE_BLOCKS
@@ -403,14 +426,25 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 // inside a group come back in any order: a tile's rows are ORed in any order.
 static_assert(NBMAX % WRB == 0, "write-pass bin scan: whole bins per thread");
 constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
+#ifndef LIME_SPLIT_BLOCKS
+#define LIME_SPLIT_BLOCKS 3072
+#endif
 __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
     constexpr int NWV = SPB / 64, PV = 8;
     __shared__ uint32_t wc[NWV][PSUB], wbase[NWV][PSUB], cur[PSUB];
-    const int b = blockIdx.x;
+    // workgroup (bin b, chunk group g): the bin's rows of chunks [c0, c1),
+    // consecutive in the bin-ordered slab; each tile's cursor starts past
+    // its rows of the earlier groups (gpre), so the groups split in parallel
+    const int b = blockIdx.x / a.ngroups, g = blockIdx.x % a.ngroups;
     const int wv = threadIdx.x / 64, lane = dev::lane_id();
-    if (threadIdx.x < PSUB) cur[threadIdx.x] = a.ttot[b * PSUB + threadIdx.x];
+    if (threadIdx.x < PSUB)
+        cur[threadIdx.x] = a.ttot[b * PSUB + threadIdx.x] +
+                           a.gpre[(int64_t)(b * PSUB + threadIdx.x) * a.ngroups + g];
     if (threadIdx.x < NWV * PSUB) (&wc[0][0])[threadIdx.x] = 0u;
-    const uint32_t r0 = a.mat[(int64_t)b * a.nchunks], r1 = a.mat[(int64_t)(b + 1) * a.nchunks];
+    const int64_t c0 = (int64_t)g * a.nchunks / a.ngroups,
+                  c1 = (int64_t)(g + 1) * a.nchunks / a.ngroups;
+    const uint32_t r0 = a.mat[(int64_t)b * a.nchunks + c0],
+                   r1 = a.mat[(int64_t)b * a.nchunks + c1];
     __syncthreads();
     const uint64_t bin0 = (uint64_t)b << BSH;
     constexpr uint32_t CH = SPB * PV;  // rows per chunk
@@ -1050,6 +1084,8 @@ constexpr int PEW = TWORDS / PAINTB;  // consecutive words per thread (extractio
 __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
     __shared__ unsigned long long img[img_words(TWORDS)];
     __shared__ uint32_t scratch[PAINTB / 64 + 1];
+    __shared__ uint32_t s_last;
+    static_assert(16384 * 4 <= sizeof(img), "the event slot (<= 16384) staged in img");
     const int t = blockIdx.x;
     const int64_t nw = a.s.n_words;
     const int64_t w0 = (int64_t)t * TWORDS;
@@ -1109,16 +1145,20 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
     }
     // a run reaching the tile's end closes there (k_ev_join reopens it)
     const bool close = threadIdx.x == PAINTB - 1 && (x[PEW - 1] >> 63) != 0;
+    if (threadIdx.x == PAINTB - 1) s_last = close;
     c += close;
     uint32_t tot;
+    // (its barriers also end every read of img: the events are staged there)
     const uint32_t mine = dev::block_exclusive_sum<PAINTB>(c, scratch, &tot);
     if (threadIdx.x == 0) {
         a.tcnt[t] = tot;
-        a.edge[t] = (uint32_t)(x[0] & 1ull) | (uint32_t)(img[ipad(TWORDS - 1)] >> 63) << 1;
+        a.edge[t] = (uint32_t)(x[0] & 1ull) | s_last << 1;
         if (tot > a.cap) atomicOr(a.oflow, 1u);
     }
     if (tot > a.cap) return;
-    uint32_t *dst = a.tev + (size_t)t * a.cap;
+    // events staged in LDS, then stored lane-consecutively (a thread's own
+    // events stored where they fall were partial-line writes: 155 -> ? us)
+    uint32_t *dst = reinterpret_cast<uint32_t *>(img);
     uint32_t e = mine;
     const uint32_t base = (uint32_t)((a.word0 + w0 + q0) * 64);
     {
@@ -1137,6 +1177,9 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
         }
     }
     if (close) dst[e] = (uint32_t)((a.word0 + w0 + TWORDS) * 64);
+    __syncthreads();
+    uint32_t *slot = a.tev + (size_t)t * a.cap;
+    for (uint32_t i = threadIdx.x; i < tot; i += PAINTB) slot[i] = dst[i];
 }
 
 // a run crossing the boundary of tiles t and t + 1 was closed at the end of
@@ -1212,7 +1255,7 @@ int n_bins(int64_t width) {
 int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
              const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
              const uint32_t *d_len, int64_t lo, int64_t hi, uint32_t *slab2, uint32_t *ttot,
-             uint64_t *cross, unsigned int *flags, bool ttot_zeroed = false) {
+             uint64_t *cross, unsigned int *flags) {
     const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
     // chunk: 1..16 count steps; as many chunks as whole rounds of the write
@@ -1231,14 +1274,20 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     R = (R + STEP - 1) / STEP * STEP;
     const uint32_t nch = (uint32_t)std::max<int64_t>((n + R - 1) / R, 1);
     const int64_t mlen = (int64_t)nb * nch + 1;
+    // split workgroups per bin: ~LIME_SPLIT_BLOCKS in all (one per bin left
+    // the split at 42 serial 4096-row rounds per workgroup on C5's sets)
+    const int ng = (int)std::min<int64_t>(std::max<int64_t>((LIME_SPLIT_BLOCKS + nb - 1) / nb, 1),
+                                          std::min<int64_t>(nch, 16));
     PoolBag bag{ctx, {}};
-    uint32_t *mat, *slab, *dummy;
+    uint32_t *mat, *slab, *dummy, *gsum, *gpre;
     LIME_TRY(bag.get(&mat, (size_t)mlen));
     LIME_TRY(bag.get(&slab, (size_t)std::max<int64_t>(n, 1)));
     LIME_TRY(bag.get(&dummy, 64));
-    if (!ttot_zeroed) LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
+    LIME_TRY(bag.get(&gsum, (size_t)ng * (size_t)nt));
+    LIME_TRY(bag.get(&gpre, (size_t)nt * (size_t)ng));
     if (n == 0) {
         LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
+        LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
         return LIME_OK;
     }
     BinArgs a;
@@ -1257,6 +1306,9 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     a.nchunks = nch;
     a.mat = mat;
     a.ttot = ttot;
+    a.gsum = gsum;
+    a.gpre = gpre;
+    a.ngroups = ng;
     a.slab = slab;
     a.slab2 = slab2;
     a.cross = cross;
@@ -1264,10 +1316,12 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     a.err = flags + 1;
     a.dummy = dummy;
     const bool lc = d_contig != nullptr && sp->n <= CMAX;
+    LIME_HIP(hipMemsetAsync(gsum, 0, 4 * (size_t)ng * (size_t)nt, S(ctx)));
     if (lc)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);
     else
         hipLaunchKernelGGL(k_bin_count<false>, dim3(nch), dim3(BINB), 0, S(ctx), a);
+    hipLaunchKernelGGL(k_tile_groups, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx), a);
     // (the extra last entries receive the totals)
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
     LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
@@ -1276,7 +1330,7 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     else
         hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
     // the atomic-claim split (C5 12.05 -> 11.73 ms against a ballot-ranked one)
-    hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)nb), dim3(SPB), 0, S(ctx), a);
+    hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)(nb * ng)), dim3(SPB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
@@ -1443,13 +1497,12 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     } ev;
     for (int j = 0; j < 2; ++j)
         LIME_HIP(hipEventCreateWithFlags(&ev.e[j], hipEventDisableTiming));
-    // every set's tile totals: one block (owned by set 0), zeroed once
+    // every set's tile starts: one block (owned by set 0)
     const size_t tstride = (size_t)nt + 1;
     uint32_t *ttot_all;
     LIME_TRY(alloc(ctx, &ttot_all, tstride * (size_t)k));
     bs->bins[0].tstart = ttot_all;
     for (int i = 1; i < k; ++i) bs->bins[i].own_tstart = false;
-    LIME_HIP(hipMemsetAsync(ttot_all, 0, 4 * tstride * (size_t)k, S(ctx)));
     // bucket set q's cross pieces by tile (its flags were copied to the host
     // behind its binning; wait for that copy only)
     auto bucket = [&](int q) -> int {
@@ -1469,7 +1522,7 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
         LIME_TRY(alloc(ctx, &b.slab2, (size_t)std::max<int64_t>(n[q], 1)));
         // (cross[q % 2] was last used by set q - 2, bucketed before this)
         LIME_TRY(bin_rows(ctx, sp, n[q], d_contig[q], d_start[q], d_end[q], d_off, d_len, lo, hi,
-                          b.slab2, b.tstart, cross[q % 2], flags + 2 * q, true));
+                          b.slab2, b.tstart, cross[q % 2], flags + 2 * q));
         LIME_HIP(hipMemcpyAsync(hflags + 2 * (q % 2), flags + 2 * q, 8, hipMemcpyDeviceToHost,
                                 S(ctx)));
         LIME_HIP(hipEventRecord(ev.e[q % 2], S(ctx)));

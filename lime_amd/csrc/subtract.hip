@@ -39,6 +39,9 @@ constexpr int SUB_B = 256;
 struct SubArgs {
     // per block (inline ranges: per 4 blocks): first B row a spanning hit can be
     const uint32_t *wstart;
+    // k_sub_fused: per tile, the first B row past every inside hit of its
+    // rows (a start >= the last row's start + A's max width); null otherwise
+    const uint32_t *wend;
     // runs: every block's own window start, found by the count pass in its
     // staged window and read by the write pass (no search there)
     uint32_t *bwlo;
@@ -165,18 +168,26 @@ __device__ __forceinline__ void sub_range(const SubArgs &sa, const uint32_t *w_g
 // spanning b starts after a.s - max width(B).  One LANE per block, a
 // branch-free binary search (as k_windows_lane): a 65-ary wave search
 // fetched 64 lanes' lines per level, 4 GB per 1e9-row subtract (0.65 ms)
+// (wend, when given: the first B row starting at or past the block's last
+// row's start + maxwa, A's max width -- the two searches interleaved)
 __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__ ags, int64_t na,
                                                     const uint32_t *__restrict__ bgs, int64_t nb,
                                                     uint32_t maxw, int64_t nblk, int stride,
-                                                    uint32_t *__restrict__ wstart) {
+                                                    uint32_t *__restrict__ wstart, uint32_t maxwa,
+                                                    uint32_t *__restrict__ wend) {
     const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (b >= nblk) return;
     const int64_t key = (int64_t)ags[b * SUB_B * stride] - maxw;
-    int64_t r = 0;  // first j with bgs[j] >= key
+    const int64_t hkey =
+        wend ? (int64_t)ags[min((b + 1) * SUB_B * stride, na) - 1] + maxwa : (int64_t)0;
+    int64_t r = 0, h = 0;  // first j with bgs[j] >= key, >= hkey
     for (int64_t step = nb > 0 ? (int64_t)1 << (63 - __builtin_clzll((uint64_t)nb)) : 0; step > 0;
-         step >>= 1)
+         step >>= 1) {
         if (r + step <= nb && (int64_t)bgs[r + step - 1] < key) r += step;
+        if (wend && h + step <= nb && (int64_t)bgs[h + step - 1] < hkey) h += step;
+    }
     wstart[b] = (uint32_t)r;
+    if (wend) wend[b] = (uint32_t)h;
 }
 
 // RUNS (threshold <= 0): the inside hits are not walked one by one.  A new
@@ -792,10 +803,21 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
 // through `total`, and the caller runs the pass again at that size.
 // (26 KiB of LDS in all: six workgroups per CU; at 64 records and eight per
 // CU the sparse 1e9-row subtract took the same time)
-constexpr int FCAP = 448;
+// (20 KiB of LDS -- a 1152-row window, 384 staged records -- for 8 waves per
+// SIMD cost 12 VGPR spills and the sparse 1e9-row subtract 11.8 -> 13.3 ms)
+#ifndef LIME_SUB_FCAP
+#define LIME_SUB_FCAP 448
+#endif
+#ifndef LIME_SUB_FWIN
+#define LIME_SUB_FWIN 1536
+#endif
+#ifndef LIME_SUB_WEND
+#define LIME_SUB_WEND 1
+#endif
+constexpr int FCAP = LIME_SUB_FCAP;
 // 1024 left rows per tile, the count pass's window (2048-row tiles with a
 // 3072-row window: the sparse 1e9-row subtract's pass 9.6 -> 10.2 ms)
-constexpr int FW = 4, FROWS = FW * SUB_B, FWIN = 1536;
+constexpr int FW = 4, FROWS = FW * SUB_B, FWIN = LIME_SUB_FWIN;
 struct FusedArgs {
     uint64_t *st;          // per-tile status words (zeroed)
     unsigned int *ticket;  // tile ticket (zeroed)
@@ -812,8 +834,10 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa)
     __shared__ uint32_t s_tile;
     if (threadIdx.x == 0) s_tile = atomicAdd(fa.ticket, 1u);
     __syncthreads();
-    const int64_t tile = s_tile;
-    const int wv = threadIdx.x / 64, lane = dev::lane_id();
+    // (uniform values held in scalar registers: every VGPR here costs
+    // occupancy, 78 -> 84 VGPRs was 6 -> 5 waves per SIMD and +13 %)
+    const int64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64)), lane = dev::lane_id();
     const int64_t base = tile * FROWS + (int64_t)wv * SUB_B;
     constexpr int RPL = SUB_B / 64;  // rows per lane: row base + k 64 + lane
     uint32_t as[RPL], ae[RPL];
@@ -826,8 +850,13 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa)
             ae[k] = sa.age[i];
         }
     }
-    const int64_t wlo = sa.wstart[tile];
-    const int nst = (int)min((int64_t)FWIN, sa.nb - wlo);
+    const int64_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)sa.wstart[tile]);
+    // the rows' hits end before wend: staged up to one row past it, so every
+    // row's bound lies inside the window (the sparse 1e9-row subtract: ~1030
+    // of the 1536 rows a fixed window staged)
+    const int nst = __builtin_amdgcn_readfirstlane(
+        (int)min(min((int64_t)FWIN, sa.nb - wlo),
+                 LIME_SUB_WEND ? (int64_t)sa.wend[tile] + 1 - wlo : (int64_t)FWIN));
     for (int k = threadIdx.x; k < nst; k += FW * 64) {
         w_pm[k] = sa.bpmax[wlo + k];
         w_gs[k] = sa.bgs[wlo + k];
@@ -853,15 +882,16 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa)
         return l;
     };
     const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
-    int bl[RPL], bh[RPL], bp[RPL];
+    // lockstep bounds of a.s and a.e (the first spanning row, needed by the
+    // writing fold only, is searched there: fewer registers, more waves)
+    int bl[RPL], bh[RPL];
 #pragma unroll
-    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = bp[k] = 0;
+    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = 0;
     for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
             if (bl[k] + step <= nst && w_gs[bl[k] + step - 1] < as[k]) bl[k] += step;
             if (bh[k] + step <= nst && w_gs[bh[k] + step - 1] < ae[k]) bh[k] += step;
-            if (bp[k] + step <= nst && w_pm[bp[k] + step - 1] <= as[k]) bp[k] += step;
         }
     }
     // a row's fold (k_subtract<_, true>'s, over this window): counts its
@@ -918,11 +948,27 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa)
         // the min (end, row) among its same-start rows
         const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
         if (lo1 > 0 && pm_last > thr) {
-            const int64_t j0 = bp[k] < nst ? wlo + bp[k] : first_spanning(sa.bpmax, lo1, thr);
             any = true;
-            bs = GS(j0);
+            bs = 0;  // (counting: the spanning block starts before a.s)
             be = pm_last;
             if (wr) {
+                // first j with pmax > thr: in the window when some staged
+                // pmax exceeds thr (pmax ascends)
+                int64_t j0;
+                if (nst > 0 && w_pm[nst - 1] > thr) {
+                    int l = 0, h = nst - 1;
+                    while (l < h) {
+                        const int m = (l + h) >> 1;
+                        if (w_pm[m] > thr)
+                            h = m;
+                        else
+                            l = m + 1;
+                    }
+                    j0 = wlo + l;
+                } else {
+                    j0 = first_spanning(sa.bpmax, lo1, thr);
+                }
+                bs = GS(j0);
                 hr = sa.brow[j0];
                 he = sa.bge[j0];
                 int64_t j = j0 + 1;
@@ -992,11 +1038,12 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa)
     };
     // counts, then each row's place: rows in order (k, lane) within a wave,
     // waves in order within the tile
-    uint64_t cnt[RPL], ex[RPL], run = 0;
+    // (u32: a tile's records past 2^32 would need 4M records per row)
+    uint32_t cnt[RPL], ex[RPL], run = 0;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
-        cnt[k] = base + k * 64 + lane < sa.na ? fold(k, false, 0, 0, 0, false) : 0;
-        const uint64_t inc = dev::wave_inclusive_sum(cnt[k]);
+        cnt[k] = base + k * 64 + lane < sa.na ? (uint32_t)fold(k, false, 0, 0, 0, false) : 0u;
+        const uint32_t inc = dev::wave_inclusive_sum(cnt[k]);
         ex[k] = run + inc - cnt[k];
         run += dev::lane63(inc);
     }
@@ -1228,12 +1275,15 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     // fused tile (FW blocks) with inline ranges
     const int stride = fused ? FW : inl ? CNT_WAVES : 1;
     const int64_t nws = (nblk + stride - 1) / stride;
-    uint32_t *wstart;
+    uint32_t *wstart, *wend = nullptr;
     LIME_TRY(alloc(ctx, &wstart, (size_t)nws));
     PoolGuard<uint32_t> gw{ctx, wstart};
+    if (fused) LIME_TRY(alloc(ctx, &wend, (size_t)nws));
+    PoolGuard<uint32_t> gwe{ctx, wend};
     if (B->n > 0)
         hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nws, 256)), dim3(256), 0, S(ctx), A->gs,
-                           na, B->gs, B->n, B->max_width, nws, stride, wstart);
+                           na, B->gs, B->n, B->max_width, nws, stride, wstart, A->max_width,
+                           wend);
     else
         LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nws, S(ctx)));
     uint32_t *bwlo = nullptr;  // runs: per-block window starts (count -> write pass)
@@ -1244,6 +1294,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     PoolGuard<uint8_t> gr{ctx, rcnt};
     SubArgs sa;
     sa.wstart = wstart;
+    sa.wend = wend;
     sa.bwlo = bwlo;
     sa.maxw = B->max_width;
     sa.ags = A->gs;

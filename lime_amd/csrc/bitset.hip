@@ -369,17 +369,19 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
             if (vnow & (1u << k)) tb[k] = (tb[k] << 13) | atomicAdd(&hist[tb[k]], 1u);
         __syncthreads();
         {
-            // bins BPT t .. BPT t + BPT - 1 per thread
-            constexpr int BPT = NBMAX / WRB;
+            // bins BPT t .. BPT t + BPT - 1 per thread (fewer bins than
+            // threads: one bin each, the rest idle)
+            constexpr int BPT = NBMAX >= WRB ? NBMAX / WRB : 1;
             const int t = BPT * threadIdx.x;
+            const bool has = t < NBMAX;
             uint32_t h[BPT], sum = 0;
 #pragma unroll
-            for (int q = 0; q < BPT; ++q) sum += (h[q] = hist[t + q]);
+            for (int q = 0; q < BPT; ++q) sum += (h[q] = has ? hist[t + q] : 0u);
             uint32_t tot;
             uint32_t o = dev::block_exclusive_sum<WRB>(sum, scratch, &tot);
 #pragma unroll
             for (int q = 0; q < BPT; ++q) {
-                soff[t + q] = o;
+                if (has) soff[t + q] = o;
                 o += h[q];
             }
         }
@@ -424,7 +426,7 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 // slot groups one after the other at the tile's cursor, and the rows are
 // stored there (a wave's rows of one tile are consecutive slots).  Claims
 // inside a group come back in any order: a tile's rows are ORed in any order.
-static_assert(NBMAX % WRB == 0, "write-pass bin scan: whole bins per thread");
+static_assert(NBMAX % WRB == 0 || WRB % NBMAX == 0, "write-pass bin scan: whole bins per thread");
 constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
 #ifndef LIME_SPLIT_BLOCKS
 #define LIME_SPLIT_BLOCKS 3072
@@ -1092,6 +1094,15 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
     uint64_t acc[AWPT];
 #pragma unroll
     for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
+    // not a: the tile's first 64 contig pads searched and loaded by wave 0
+    // before the paint, so their round trips overlap it
+    const int64_t plo = (a.word0 + w0) * 64, phi = plo + (int64_t)TWORDS * 64;
+    int64_t pc = 0, pad = INT64_MAX;
+    if (a.notmask && threadIdx.x < 64) {
+        pc = dev::wave_lower_bound(a.off + 1, (int64_t)a.nc, plo + 1);
+        const int64_t cc = pc + threadIdx.x;
+        pad = cc < a.nc ? (int64_t)a.off[cc + 1] - 1 : INT64_MAX;
+    }
     paint_and_tile(a.s, t, a.neg, img, acc);
     __syncthreads();  // img again, in the extraction's padded layout
 #pragma unroll
@@ -1112,14 +1123,14 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
         // the contig pads inside the tile, cleared 64 at a time by wave 0
         // (the pads ascend: a batch not wholly inside the tile is the last)
         if (threadIdx.x < 64) {
-            const int64_t lo = (a.word0 + w0) * 64, hi = lo + (int64_t)TWORDS * 64;
-            for (int64_t c = dev::wave_lower_bound(a.off + 1, (int64_t)a.nc, lo + 1); c < a.nc;
-                 c += 64) {
-                const int64_t cc = c + threadIdx.x;
-                const int64_t pad = cc < a.nc ? (int64_t)a.off[cc + 1] - 1 : INT64_MAX;
-                const bool in = pad < hi;
+            for (int64_t c = pc; c < a.nc; c += 64) {
+                if (c != pc) {
+                    const int64_t cc = c + threadIdx.x;
+                    pad = cc < a.nc ? (int64_t)a.off[cc + 1] - 1 : INT64_MAX;
+                }
+                const bool in = pad < phi;
                 if (in) {
-                    const int64_t q = pad - lo;
+                    const int64_t q = pad - plo;
                     atomicAnd(&img[ipad((int)(q >> 6))], ~(1ull << (q & 63)));
                 }
                 if (__ballot(in) != ~0ull) break;

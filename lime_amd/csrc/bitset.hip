@@ -565,17 +565,19 @@ __global__ __launch_bounds__(BB) void k_xwrite(const uint64_t *__restrict__ cros
     }
 }
 
-struct AndArgs {
-    const uint32_t *slab2[MAXK];  // tile-ordered packed rows of set i
-    const uint32_t *tstart[MAXK]; // nt + 1 tile starts
-    const uint2 *xl[MAXK];        // tile-bucketed cross pieces (null: none)
-    const uint32_t *xoff[MAXK];   // nt + 1 bucket starts
-    const uint32_t *full[MAXK];   // nt + 1 exclusive scan of the difference array
+template <int CAP>
+struct AndArgsK {
+    const uint32_t *slab2[CAP];  // tile-ordered packed rows of set i
+    const uint32_t *tstart[CAP]; // nt + 1 tile starts
+    const uint2 *xl[CAP];        // tile-bucketed cross pieces (null: none)
+    const uint32_t *xoff[CAP];   // nt + 1 bucket starts
+    const uint32_t *full[CAP];   // nt + 1 exclusive scan of the difference array
     int k;
     int init;  // the AND continues the words already stored (sets past the first 16)
     uint64_t *words;
     int64_t n_words;
 };
+using AndArgs = AndArgsK<MAXK>;
 
 constexpr int AWPT = TWORDS / PAINTB;  // AND words per thread (registers)
 constexpr int APV = 16;                // rows per lane per batch
@@ -584,7 +586,8 @@ constexpr int APV = 16;                // rows per lane per batch
 // batch) sequence is software-pipelined: the next batch's loads (possibly
 // the next set's) are issued before the current batch is painted, so they
 // stay in flight across the set's AND barriers.  img: TWORDS words of LDS.
-__device__ __forceinline__ void paint_and_tile(const AndArgs &a, int t, uint32_t neg,
+template <class AA>
+__device__ __forceinline__ void paint_and_tile(const AA &a, int t, uint32_t neg,
                                                unsigned long long *img, uint64_t (&acc)[AWPT]) {
     constexpr uint32_t B = APV * PAINTB;
     // a tile wholly inside one of the set's cross pieces: all ones (AND
@@ -1068,8 +1071,8 @@ __global__ __launch_bounds__(256) void k_ev_gather(const uint32_t *__restrict__ 
 // closed there; k_ev_join then drops the two events of every run that
 // crosses a tile boundary (the close and the reopening) before the scan.
 struct PaintEvArgs {
-    AndArgs s;            // the operands' binned rows (s.k sets)
-    uint32_t neg;         // bit i: operand i complemented
+    int64_t n_words;      // the window's words
+    uint32_t neg;         // bit i: operand i complemented (k_paint_ev)
     int notmask;          // not a: clear the contig pads and the bits past the window
     int64_t word0;        // global index of the window's word 0
     int64_t hi_bit;       // end of the window (global bits)
@@ -1083,32 +1086,22 @@ struct PaintEvArgs {
 };
 constexpr int PEW = TWORDS / PAINTB;  // consecutive words per thread (extraction)
 
-__global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
-    __shared__ unsigned long long img[img_words(TWORDS)];
-    __shared__ uint32_t scratch[PAINTB / 64 + 1];
-    __shared__ uint32_t s_last;
-    static_assert(16384 * 4 <= sizeof(img), "the event slot (<= 16384) staged in img");
-    const int t = blockIdx.x;
-    const int64_t nw = a.s.n_words;
+// One output's events of tile t from its words acc (thread: words
+// threadIdx.x + j PAINTB), as described above; img / scratch / s_last: the
+// kernel's LDS.  (pc, pad): wave 0's prefetched first 64 contig pads of the
+// tile (NOT only).  Ends with a barrier: img is free again.
+// (word j of the thread: wj(j))
+template <class WJ>
+__device__ __forceinline__ void tile_events(const PaintEvArgs &a, int t, WJ wj,
+                                            unsigned long long *img, uint32_t *scratch,
+                                            uint32_t &s_last, int64_t pc, int64_t pad) {
+    const int64_t nw = a.n_words;
     const int64_t w0 = (int64_t)t * TWORDS;
-    uint64_t acc[AWPT];
-#pragma unroll
-    for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
-    // not a: the tile's first 64 contig pads searched and loaded by wave 0
-    // before the paint, so their round trips overlap it
     const int64_t plo = (a.word0 + w0) * 64, phi = plo + (int64_t)TWORDS * 64;
-    int64_t pc = 0, pad = INT64_MAX;
-    if (a.notmask && threadIdx.x < 64) {
-        pc = dev::wave_lower_bound(a.off + 1, (int64_t)a.nc, plo + 1);
-        const int64_t cc = pc + threadIdx.x;
-        pad = cc < a.nc ? (int64_t)a.off[cc + 1] - 1 : INT64_MAX;
-    }
-    paint_and_tile(a.s, t, a.neg, img, acc);
-    __syncthreads();  // img again, in the extraction's padded layout
 #pragma unroll
     for (int j = 0; j < AWPT; ++j) {
         const int q = threadIdx.x + j * PAINTB;
-        uint64_t x = w0 + q < nw ? acc[j] : 0ull;
+        uint64_t x = w0 + q < nw ? wj(j) : 0ull;
         if (a.notmask) {  // nothing past the window
             const int64_t b0 = (a.word0 + w0 + q) * 64;
             if (b0 + 64 > a.hi_bit) {
@@ -1166,13 +1159,11 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
         a.edge[t] = (uint32_t)(x[0] & 1ull) | s_last << 1;
         if (tot > a.cap) atomicOr(a.oflow, 1u);
     }
-    if (tot > a.cap) return;
-    // events staged in LDS, then stored lane-consecutively (a thread's own
-    // events stored where they fall were partial-line writes: 155 -> ? us)
-    uint32_t *dst = reinterpret_cast<uint32_t *>(img);
-    uint32_t e = mine;
-    const uint32_t base = (uint32_t)((a.word0 + w0 + q0) * 64);
-    {
+    if (tot <= a.cap) {  // (block-uniform)
+        // events staged in LDS, then stored lane-consecutively
+        uint32_t *dst = reinterpret_cast<uint32_t *>(img);
+        uint32_t e = mine;
+        const uint32_t base = (uint32_t)((a.word0 + w0 + q0) * 64);
         uint64_t p = prev;
 #pragma unroll
         for (int k = 0; k < PEW; ++k) {
@@ -1186,11 +1177,41 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a) {
                 dst[e++] = base + (uint32_t)(64 * k + b);
             }
         }
+        if (close) dst[e] = (uint32_t)((a.word0 + w0 + TWORDS) * 64);
+        __syncthreads();
+        uint32_t *slot = a.tev + (size_t)t * a.cap;
+        for (uint32_t i = threadIdx.x; i < tot; i += PAINTB) slot[i] = dst[i];
     }
-    if (close) dst[e] = (uint32_t)((a.word0 + w0 + TWORDS) * 64);
     __syncthreads();
-    uint32_t *slot = a.tev + (size_t)t * a.cap;
-    for (uint32_t i = threadIdx.x; i < tot; i += PAINTB) slot[i] = dst[i];
+}
+
+// the pads of a NOT (wave 0, before the paint: their round trips overlap it)
+__device__ __forceinline__ void prefetch_pads(const PaintEvArgs &a, int t, int64_t &pc,
+                                              int64_t &pad) {
+    pc = 0;
+    pad = INT64_MAX;
+    if (threadIdx.x < 64) {
+        const int64_t plo = (a.word0 + (int64_t)t * TWORDS) * 64;
+        pc = dev::wave_lower_bound(a.off + 1, (int64_t)a.nc, plo + 1);
+        const int64_t cc = pc + threadIdx.x;
+        pad = cc < a.nc ? (int64_t)a.off[cc + 1] - 1 : INT64_MAX;
+    }
+}
+
+__global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a, AndArgs s) {
+    __shared__ unsigned long long img[img_words(TWORDS)];
+    __shared__ uint32_t scratch[PAINTB / 64 + 1];
+    __shared__ uint32_t s_last;
+    static_assert(16384 * 4 <= sizeof(img), "the event slot (<= 16384) staged in img");
+    const int t = blockIdx.x;
+    uint64_t acc[AWPT];
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
+    int64_t pc = 0, pad = INT64_MAX;
+    if (a.notmask) prefetch_pads(a, t, pc, pad);
+    paint_and_tile(s, t, a.neg, img, acc);
+    __syncthreads();  // img again, in the extraction's padded layout
+    tile_events(a, t, [&](int j) { return acc[j]; }, img, scratch, s_last, pc, pad);
 }
 
 // a run crossing the boundary of tiles t and t + 1 was closed at the end of
@@ -1372,9 +1393,10 @@ int bucket_cross(lime_ctx *ctx, int64_t tstride, const uint64_t *cross,
 }
 
 // paint arguments over binned row sets (k <= MAXK, nt tiles each)
-AndArgs binned_args(const lime_bitset::Bins *const *b, int k, int64_t nt, int64_t n_words) {
-    AndArgs aa;
-    for (int i = 0; i < MAXK; ++i) {
+template <int CAP = MAXK>
+AndArgsK<CAP> binned_args(const lime_bitset::Bins *const *b, int k, int64_t nt, int64_t n_words) {
+    AndArgsK<CAP> aa;
+    for (int i = 0; i < CAP; ++i) {
         const bool v = i < k;
         aa.slab2[i] = v ? b[i]->slab2 : nullptr;
         aa.tstart[i] = v ? b[i]->tstart : nullptr;
@@ -1547,11 +1569,107 @@ namespace {
 // k_paint_ev, k_ev_join, a scan, k_ev_gather.  *overflow: a tile had more
 // events than its slot (the caller paints the operands and takes the words
 // path; nothing is returned)
+// one op's extraction from bins: its slots, counts and result sizing
+// (prepare), then, after its k_paint_ev / k_paint_ev2 launch, the join, the
+// scan, the gather and the read-back (finish)
+struct EvPlan {
+    lime_ctx *ctx;
+    PaintEvArgs pa;
+    int64_t nt = 0, cap = 0, bound = -1, rcap = -1;
+    uint32_t *cnt2 = nullptr, *skip1 = nullptr, *toff = nullptr;
+    unsigned int *hdr = nullptr;  // [0] overflow flag, [1] total events
+    PoolBag bag;
+    explicit EvPlan(lime_ctx *c) : ctx(c), bag{c, {}} {}
+
+    int prepare(int op, int nin, const lime_bitset *const *sets, uint32_t neg) {
+        const lime_bitset *a = sets[0];
+        nt = a->nt;
+        pa.n_words = a->n_words;
+        pa.neg = neg;
+        pa.notmask = op == 1;
+        pa.word0 = a->word0;
+        pa.hi_bit = a->hi_bit;
+        const uint32_t *d_off = nullptr;
+        LIME_TRY(space_device(ctx, a->off, &d_off, nullptr));
+        pa.off = d_off;
+        pa.nc = a->n_contigs;
+        // runs bound (a run starts at a run start of an operand, or a
+        // contig's start for NOT) -> a slot of twice the bound's mean events
+        // per tile + 2048, within [4096, 16384] (an AND's bound, the sum, is
+        // loose: past the slot a tile falls back to the words path)
+        bound = op == 1 ? (int64_t)a->n_contigs + 1 : 0;
+        for (int i = 0; i < nin && bound >= 0; ++i)
+            bound = sets[i]->runs_bound < 0 ? -1 : bound + sets[i]->runs_bound;
+        cap = bound < 0 ? 16384 : 2 * (2 * bound / std::max<int64_t>(nt, 1)) + 2048;
+        cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), 16384);
+        pa.cap = (uint32_t)cap;
+        LIME_TRY(bag.get(&pa.tev, (size_t)nt * (size_t)cap));
+        LIME_TRY(bag.get(&pa.tcnt, (size_t)nt));
+        LIME_TRY(bag.get(&pa.edge, (size_t)nt));
+        LIME_TRY(bag.get(&cnt2, (size_t)nt));
+        LIME_TRY(bag.get(&skip1, (size_t)nt));
+        LIME_TRY(bag.get(&toff, (size_t)nt));
+        LIME_TRY(bag.get(&hdr, 2));
+        LIME_HIP(hipMemsetAsync(hdr, 0, 8, S(ctx)));
+        pa.oflow = hdr;
+        return LIME_OK;
+    }
+
+    // everything up to the read-back queued (the gather too when the result
+    // can be sized from the bound)
+    int queue(lime_result *res) {
+        hipLaunchKernelGGL(k_ev_join, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx),
+                           (const uint32_t *)pa.tcnt, (const uint32_t *)pa.edge, nt, cnt2, skip1);
+        LIME_HIP(hipGetLastError());
+        LIME_TRY(scan_exclusive_u32(ctx, cnt2, toff, nt, hdr + 1));
+        rcap = bound < 0 ? -1 : std::min<int64_t>(bound, nt * (cap / 2));
+        if (rcap >= 0) {
+            LIME_TRY(alloc(ctx, &res->gs, (size_t)std::max<int64_t>(rcap, 1)));
+            LIME_TRY(alloc(ctx, &res->ge, (size_t)std::max<int64_t>(rcap, 1)));
+            gather(res, (uint32_t)std::min<int64_t>(2 * rcap, 0xffffffffll));
+        }
+        return LIME_OK;
+    }
+
+    void gather(lime_result *res, uint32_t cap_events) {
+        hipLaunchKernelGGL(k_ev_gather, dim3((unsigned)nt), dim3(256), 0, S(ctx),
+                           (const uint32_t *)pa.tev, (const uint32_t *)cnt2,
+                           (const uint32_t *)toff, (const unsigned int *)hdr, cap_events, res->gs,
+                           res->ge, (uint32_t)cap, (const uint32_t *)skip1);
+    }
+
+    int finish(lime_result *res, bool *overflow) {
+        *overflow = false;
+        unsigned int h[2] = {0, 0};
+        LIME_TRY(read_back(ctx, h, hdr, sizeof(h)));
+        if (h[0]) {
+            if (rcap >= 0) {
+                release(ctx, res->gs);
+                release(ctx, res->ge);
+                res->gs = res->ge = nullptr;
+            }
+            *overflow = true;
+            return LIME_OK;
+        }
+        if (h[1] & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
+        const int64_t nr = h[1] / 2;
+        if (rcap >= 0) {
+            if (nr > rcap) return fail(LIME_ERR_DEVICE, "bitset run extraction: runs past bound");
+        } else {
+            LIME_TRY(alloc(ctx, &res->gs, (size_t)std::max<int64_t>(nr, 1)));
+            LIME_TRY(alloc(ctx, &res->ge, (size_t)std::max<int64_t>(nr, 1)));
+            if (nr > 0) gather(res, h[1]);
+            LIME_HIP(hipGetLastError());
+        }
+        res->n = nr;
+        return LIME_OK;
+    }
+};
+
 int runs_binned(lime_ctx *ctx, int op, int nin, const lime_bitset *const *sets, lime_result *res,
                 bool *overflow) {
     *overflow = false;
     const lime_bitset *a = sets[0];
-    const int64_t nt = a->nt;
     // every operand's binned sets, the complemented operand's (one) marked
     std::vector<const lime_bitset::Bins *> b;
     uint32_t neg = 0;
@@ -1560,85 +1678,14 @@ int runs_binned(lime_ctx *ctx, int op, int nin, const lime_bitset *const *sets, 
         if (inv) neg |= 1u << b.size();
         for (const auto &x : sets[i]->bins) b.push_back(&x);
     }
-    PaintEvArgs pa;
-    pa.s = binned_args(b.data(), (int)b.size(), nt, a->n_words);
-    pa.neg = neg;
-    pa.notmask = op == 1;
-    pa.word0 = a->word0;
-    pa.hi_bit = a->hi_bit;
-    const uint32_t *d_off = nullptr;
-    LIME_TRY(space_device(ctx, a->off, &d_off, nullptr));
-    pa.off = d_off;
-    pa.nc = a->n_contigs;
-    // runs bound (a run starts at a run start of an operand, or a contig's
-    // start for NOT) -> a slot of twice the bound's mean events per tile +
-    // 2048, within [4096, 16384] (an AND's bound, the sum, is loose: past the
-    // slot a tile falls back to the words path)
-    int64_t bound = op == 1 ? (int64_t)a->n_contigs + 1 : 0;
-    for (int i = 0; i < nin && bound >= 0; ++i)
-        bound = sets[i]->runs_bound < 0 ? -1 : bound + sets[i]->runs_bound;
-    int64_t cap = bound < 0 ? 16384 : 2 * (2 * bound / std::max<int64_t>(nt, 1)) + 2048;
-    cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), 16384);
-    pa.cap = (uint32_t)cap;
-    PoolBag bag{ctx, {}};
-    uint32_t *tev, *tcnt, *edge, *cnt2, *skip1, *toff;
-    unsigned int *hdr;  // [0] overflow flag, [1] total events
-    LIME_TRY(bag.get(&tev, (size_t)nt * (size_t)cap));
-    LIME_TRY(bag.get(&tcnt, (size_t)nt));
-    LIME_TRY(bag.get(&edge, (size_t)nt));
-    LIME_TRY(bag.get(&cnt2, (size_t)nt));
-    LIME_TRY(bag.get(&skip1, (size_t)nt));
-    LIME_TRY(bag.get(&toff, (size_t)nt));
-    LIME_TRY(bag.get(&hdr, 2));
-    LIME_HIP(hipMemsetAsync(hdr, 0, 8, S(ctx)));
-    pa.tev = tev;
-    pa.tcnt = tcnt;
-    pa.edge = edge;
-    pa.oflow = hdr;
-    hipLaunchKernelGGL(k_paint_ev, dim3((unsigned)nt), dim3(PAINTB), 0, S(ctx), pa);
-    hipLaunchKernelGGL(k_ev_join, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx),
-                       (const uint32_t *)tcnt, (const uint32_t *)edge, nt, cnt2, skip1);
-    LIME_HIP(hipGetLastError());
-    LIME_TRY(scan_exclusive_u32(ctx, cnt2, toff, nt, hdr + 1));
-    // with a bound the result is allocated at it and the gather queued
-    // before the host reads the totals (as bitset_runs)
-    const int64_t rcap = bound < 0 ? -1 : std::min<int64_t>(bound, nt * (cap / 2));
-    auto gather = [&](uint32_t cap_events) {
-        hipLaunchKernelGGL(k_ev_gather, dim3((unsigned)nt), dim3(256), 0, S(ctx),
-                           (const uint32_t *)tev, (const uint32_t *)cnt2, (const uint32_t *)toff,
-                           (const unsigned int *)hdr, cap_events, res->gs, res->ge,
-                           (uint32_t)cap, (const uint32_t *)skip1);
-    };
-    if (rcap >= 0) {
-        LIME_TRY(alloc(ctx, &res->gs, (size_t)std::max<int64_t>(rcap, 1)));
-        LIME_TRY(alloc(ctx, &res->ge, (size_t)std::max<int64_t>(rcap, 1)));
-        gather((uint32_t)std::min<int64_t>(2 * rcap, 0xffffffffll));
-        LIME_HIP(hipGetLastError());
-    }
-    unsigned int h[2] = {0, 0};
-    LIME_TRY(read_back(ctx, h, hdr, sizeof(h)));
-    if (h[0]) {
-        if (rcap >= 0) {
-            release(ctx, res->gs);
-            release(ctx, res->ge);
-            res->gs = res->ge = nullptr;
-        }
-        *overflow = true;
-        return LIME_OK;
-    }
-    if (h[1] & 1u) return fail(LIME_ERR_DEVICE, "bitset run extraction: odd event count");
-    const int64_t nr = h[1] / 2;
-    if (rcap >= 0) {
-        if (nr > rcap) return fail(LIME_ERR_DEVICE, "bitset run extraction: runs past bound");
-    } else {
-        LIME_TRY(alloc(ctx, &res->gs, (size_t)std::max<int64_t>(nr, 1)));
-        LIME_TRY(alloc(ctx, &res->ge, (size_t)std::max<int64_t>(nr, 1)));
-        if (nr > 0) gather(h[1]);
-        LIME_HIP(hipGetLastError());
-    }
-    res->n = nr;
-    return LIME_OK;
+    const AndArgs sargs = binned_args(b.data(), (int)b.size(), a->nt, a->n_words);
+    EvPlan p(ctx);
+    LIME_TRY(p.prepare(op, nin, sets, neg));
+    hipLaunchKernelGGL(k_paint_ev, dim3((unsigned)p.nt), dim3(PAINTB), 0, S(ctx), p.pa, sargs);
+    LIME_TRY(p.queue(res));
+    return p.finish(res, overflow);
 }
+
 }  // namespace
 
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res) {

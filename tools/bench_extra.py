@@ -208,12 +208,16 @@ def main():
         def roof(rec):
             t0, t1, t2, t3, nc, nd = rec[-1]
             ms = t2.elapsed_time(t3)
-            W = (space.span + 63) // 64 * 8
-            b = W + 2 * W + 8 * (nc + nd)  # NOT reads 1 operand, ANDN 2, once each
-            return {"bitset_build_ms (bin + paint)": t1.elapsed_time(t2),
-                    "extract_ms": ms, "complement_runs": nc, "difference_runs": nd}, \
-                {"kernel": "bitset extraction (k_ev_local: per-tile event slots, no look-back; "
-                           "k_ev_gather)",
+            n = int(1e7 * a.scale)
+            # the binned rows read once (4 B each, both sets), every event
+            # written to its tile slot and read back (4 + 4 B), the runs
+            # stored (8 B): no bitset is stored or read on this path
+            b = 4 * 2 * n + 8 * 2 * (nc + nd) + 8 * (nc + nd)
+            return {"bitset_build_ms (bin, no paint)": t1.elapsed_time(t2),
+                    "extract_ms (paint + ops + runs)": ms, "complement_runs": nc,
+                    "difference_runs": nd}, \
+                {"kernel": "k_paint_ev per op (paint, op, events per tile slot) + "
+                           "k_ev_join + k_ev_gather",
                  "bound": "hbm",
                  "achieved": b / (ms * 1e-3) / 1e9, "alg_bytes": b}
     elif a.workload == "subtract":

@@ -448,7 +448,13 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
 
 // RAW (first pass over caller rows only): key_in / ge_in / row_in are the
 // caller's contig / start / end, and (gs, ge) = off[contig] + (start, end)
-template <int M, int ROWS, bool RAW = false>
+// EW (GS passes of sets narrower than 2^16 bases): how the ends travel.
+// Between the first and the last pass only the width ge - gs is carried, as
+// u16 (10 B per row and pass instead of 12): the first pass turns ends into
+// widths (EW_TO16), the middle ones move widths (EW_16), the last turns them
+// back into ends (EW_FROM16, ge = gs + width, gs staged beside it)
+enum { EW_32 = 0, EW_TO16 = 1, EW_16 = 2, EW_FROM16 = 3 };
+template <int M, int ROWS, bool RAW = false, int EW = EW_32>
 // 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
 __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
                                                 const uint32_t *__restrict__ ge_in,
@@ -471,6 +477,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     __shared__ uint32_t gbase[RBINS];
     __shared__ uint32_t scratch[RWAVES + 1];
     constexpr bool ALL3 = M != M_GS;  // digit not recomputable from the key alone
+    static_assert(EW == EW_32 || (M == M_GS && !RAW), "u16 widths: GS passes only");
     __shared__ uint32_t sk[RTILE], se[RTILE], sr[ALL3 ? RTILE : 1];
 
     for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
@@ -500,9 +507,13 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
             vr[k] = valid ? kin[o] : 0u;
             vk[k] = valid ? ein[o] : 0u;
             ve[k] = valid ? rin[o] : 0u;
+        } else if (EW == EW_16 || EW == EW_FROM16) {
+            vk[k] = valid ? kin[o] : 0u;
+            ve[k] = valid ? (uint32_t)reinterpret_cast<const uint16_t *>(ge_in)[base + o] : 0u;
         } else {
             vk[k] = valid ? kin[o] : 0u;
             ve[k] = valid ? ein[o] : 0u;
+            if (EW == EW_TO16) ve[k] -= vk[k];  // (< 2^16: checked by the caller)
         }
         // (GS passes write identity rows straight from the position below,
         // keeping vr out of the registers of that path)
@@ -598,7 +609,11 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
         const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
-        ge_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
+        const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
+        if (EW == EW_TO16 || EW == EW_16)
+            reinterpret_cast<uint16_t *>(ge_out)[g] = (uint16_t)se[j];
+        else
+            ge_out[g] = EW == EW_FROM16 ? sk[j] + se[j] : se[j];
     }
     if (ROWS == ROWS_NONE) return;
     __syncthreads();
@@ -617,7 +632,7 @@ template <int M>
 void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                  const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
                  uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows, int &rc,
-                 const uint32_t *raw_off = nullptr, int32_t raw_nc = 0) {
+                 const uint32_t *raw_off = nullptr, int32_t raw_nc = 0, int ew = EW_32) {
     if (raw_off) {  // first gs pass straight from the caller's rows (k_prep's histogram)
         if ((rc = scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr)) != LIME_OK)
             return;
@@ -632,6 +647,19 @@ void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint
                            mat, ntiles, rows);
     if ((rc = scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr)) != LIME_OK)
         return;
+    if (M == M_GS && ew != EW_32) {
+        // (u16 widths: rows kept, GS passes only)
+#define LIME_EW_LAUNCH(R, E)                                                                     \
+    hipLaunchKernelGGL((k_scatter<M_GS, R, false, E>), dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0, \
+                       r0, n, shift, st, (const uint32_t *)mat, ntiles, k1, e1, r1)
+        if (rows == ROWS_IDENT && ew == EW_TO16) LIME_EW_LAUNCH(ROWS_IDENT, EW_TO16);
+        else if (rows == ROWS_LOAD && ew == EW_TO16) LIME_EW_LAUNCH(ROWS_LOAD, EW_TO16);
+        else if (rows == ROWS_LOAD && ew == EW_16) LIME_EW_LAUNCH(ROWS_LOAD, EW_16);
+        else if (rows == ROWS_LOAD && ew == EW_FROM16) LIME_EW_LAUNCH(ROWS_LOAD, EW_FROM16);
+        else rc = LIME_ERR_ARG;  // (no such combination is planned)
+#undef LIME_EW_LAUNCH
+        return;
+    }
     if (rows == ROWS_IDENT)
         hipLaunchKernelGGL((k_scatter<M, ROWS_IDENT>), dim3(ntiles), dim3(RB), 0, S(ctx), k0, e0,
                            r0, n, shift, st, (const uint32_t *)mat, ntiles, k1, e1, r1);
@@ -646,7 +674,7 @@ void launch_pass(lime_ctx *ctx, int shift, bool have_hist, int64_t n, const uint
 int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, const uint32_t *k0,
                const uint32_t *e0, const uint32_t *r0, const int8_t *st, uint32_t *k1,
                uint32_t *e1, uint32_t *r1, uint32_t *mat, uint32_t ntiles, int rows,
-               const uint32_t *raw_off = nullptr, int32_t raw_nc = 0) {
+               const uint32_t *raw_off = nullptr, int32_t raw_nc = 0, int ew = EW_32) {
     int rc = LIME_OK;
     if (raw_off) {
         launch_pass<M_GS>(ctx, shift, true, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc,
@@ -669,7 +697,8 @@ int radix_pass(lime_ctx *ctx, int mode, int shift, bool have_hist, int64_t n, co
             launch_pass<M_RW>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
             break;
         default:
-            launch_pass<M_GS>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc);
+            launch_pass<M_GS>(ctx, shift, have_hist, n, k0, e0, r0, st, k1, e1, r1, mat, ntiles, rows, rc,
+                              nullptr, 0, ew);
     }
     if (rc != LIME_OK) return rc;
     LIME_HIP(hipGetLastError());
@@ -1119,6 +1148,9 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
 // most buckets in k_local_small.  (Denser sets through k_local_big, one
 // workgroup per CU: C3's 5e8 pile-up rows, ~10.6k per bucket, took 7.0 ms
 // there -- sort 14.6 ms against 13.0 with the four digit passes.)
+#ifndef LIME_SORT_W16
+#define LIME_SORT_W16 1
+#endif
 constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4;
 
 int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
@@ -1333,9 +1365,15 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         const int prep_shift = bucket_cand ? 0 : hshift;
         bool have = passes.front().first == M_GS && passes.front().second == prep_shift &&
                     !(bucket_cand && global);
-        for (auto &p : passes) {
+        // GS passes only, rows kept, every width < 2^16: u16 widths between
+        // the first and the last pass (EW_TO16 .. EW_FROM16)
+        bool w16 = LIME_SORT_W16 && keep_rows && passes.size() >= 2 && h.max_width < 65536u;
+        for (auto &p : passes) w16 = w16 && p.first == M_GS;
+        for (size_t q = 0; q < passes.size(); ++q) {
+            const auto &p = passes[q];
+            const int ew = !w16 ? EW_32 : q == 0 ? EW_TO16 : q + 1 == passes.size() ? EW_FROM16 : EW_16;
             LIME_TRY(radix_pass(ctx, p.first, p.second, have, n, k0, e0, r0, set->strand_in, k1,
-                                e1, r1, mat, ntiles, rows));
+                                e1, r1, mat, ntiles, rows, nullptr, 0, ew));
             have = false;
             if (rows == ROWS_IDENT) rows = ROWS_LOAD;
             std::swap(k0, k1);

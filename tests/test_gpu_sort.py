@@ -132,6 +132,37 @@ def test_sorted_input_and_digit_pass_sets(ctx):
     _check_host_set(ctx, sp2, np.zeros(len(s), np.int32), s, e)
 
 
+@pytest.mark.parametrize("wmax", [65_535, 65_536])
+def test_digit_pass_u16_widths(ctx, wmax):
+    # digit-pass sets without zero-width rows carry u16 widths between the
+    # first and the last pass when every width is < 2^16: widths up to the
+    # limit (65,535 present) and one row past it (the u32 passes), host rows
+    # and global rows with caller row ids
+    import torch
+    rng = np.random.default_rng(wmax)
+    L = 40_000_000
+    sp = _space([L, 5_000_000])
+    n = 400_000
+    c = (rng.random(n) < 0.2).astype(np.int32)
+    s = (rng.random(n) * (np.array([L, 5_000_000])[c] - 70_000)).astype(np.int64)
+    w = rng.integers(1, 65_536, n)
+    w[rng.integers(0, n, 50)] = 65_535
+    w[rng.integers(0, n, 50)] = 1
+    w[7] = wmax
+    e = s + w
+    d = rng.integers(0, n, 2000)
+    s[d[:1000]], e[d[:1000]], c[d[:1000]] = s[d[1000:]], e[d[1000:]], c[d[1000:]]
+    _check_host_set(ctx, sp, c, s, e)
+    off = sp.offsets[:-1]
+    gs, ge = (off[c] + s).astype(np.uint32), (off[c] + e).astype(np.uint32)
+    rows = rng.permutation(3 * n)[:n].astype(np.uint32)
+    tg = [torch.tensor(x.view(np.int32), device="cuda") for x in (gs, ge, rows)]
+    got = ctx.set_from_global(sp, n, *(t.data_ptr() for t in tg)).to_host()
+    order = _expected(gs.astype(np.int64), ge.astype(np.int64))
+    assert (got["row"] == rows[order]).all()
+    assert (got["start"] == s[order]).all() and (got["end"] == e[order]).all()
+
+
 def _check_device_order(ctx, sp, n, c, s, e):
     """the set built from device rows (c, s, e) is in canonical order (gs,
     zero-width first, input row), its row ids a permutation and every row's

@@ -370,12 +370,15 @@ struct ScanGeom {
 #ifndef LIME_MS2_Q
 #define LIME_MS2_Q 8
 #endif
+#ifndef LIME_MS2_WPE
+#define LIME_MS2_WPE 4
+#endif
 constexpr int MS2 = LIME_MS2_NT;
 using G2 = ScanGeom<MS2, LIME_MS2_Q>;
 
 // TIE: also test for subtract's long same-start groups (a.tie)
 template <bool TIE>
-__global__ __launch_bounds__(MS2) __attribute__((amdgpu_waves_per_eu(4, 8)))
+__global__ __launch_bounds__(MS2) __attribute__((amdgpu_waves_per_eu(LIME_MS2_WPE, 8)))
 void k_merge_scan2(MergeScanArgs a) {
     constexpr int NW = G2::NW, RQ = G2::RQ;
     __shared__ uint32_t s_wmax[NW], s_wcnt[NW];

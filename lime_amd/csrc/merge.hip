@@ -390,29 +390,46 @@ void k_merge_scan2(MergeScanArgs a) {
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t wb = tile * G2::TILE + (int64_t)w * G2::RW;  // the wave's first row
     uint32_t s[4 * RQ], e[4 * RQ];
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-        const int64_t i0 = wb + 256 * q + 4 * lane;
-        if (i0 + 4 <= n) {
-            const uint4 x = *reinterpret_cast<const uint4 *>(a.gs + i0);
-            const uint4 y = *reinterpret_cast<const uint4 *>(a.ge + i0);
-            s[4 * q] = x.x, s[4 * q + 1] = x.y, s[4 * q + 2] = x.z, s[4 * q + 3] = x.w;
-            e[4 * q] = y.x, e[4 * q + 1] = y.y, e[4 * q + 2] = y.z, e[4 * q + 3] = y.w;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool v = i0 + j < n;
-                s[4 * q + j] = v ? a.gs[i0 + j] : 0xffffffffu;
-                e[4 * q + j] = v ? a.ge[i0 + j] : 0u;
-            }
-        }
-    }
     // lane maxima per round; the wave's and the tile's maximum
     uint32_t rmax[RQ], lmax = 0;
+    auto round_max = [&]() {
 #pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-        rmax[q] = max(max(e[4 * q], e[4 * q + 1]), max(e[4 * q + 2], e[4 * q + 3]));
-        lmax = max(lmax, rmax[q]);
+        for (int q = 0; q < RQ; ++q) {
+            rmax[q] = max(max(e[4 * q], e[4 * q + 1]), max(e[4 * q + 2], e[4 * q + 3]));
+            lmax = max(lmax, rmax[q]);
+        }
+    };
+    // every end first, then every start: loads return in order, so the
+    // tile's aggregate (its max end) is published while the starts are still
+    // in flight (successors' look-backs wait on it).  A full tile takes the
+    // branch-free path, where the wait before the maximum counts only the
+    // ends (per-lane bounds checks made it wait for every load)
+    if ((tile + 1) * G2::TILE <= n) {  // (uniform)
+        const uint4 *e4 = reinterpret_cast<const uint4 *>(a.ge + wb) + lane;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(a.gs + wb) + lane;
+#pragma unroll
+        for (int q = 0; q < RQ; ++q) {
+            const uint4 y = e4[64 * q];
+            e[4 * q] = y.x, e[4 * q + 1] = y.y, e[4 * q + 2] = y.z, e[4 * q + 3] = y.w;
+        }
+#pragma unroll
+        for (int q = 0; q < RQ; ++q) {
+            const uint4 x = s4[64 * q];
+            s[4 * q] = x.x, s[4 * q + 1] = x.y, s[4 * q + 2] = x.z, s[4 * q + 3] = x.w;
+        }
+        round_max();  // (inside the branch: its wait counts the ends only)
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4 * RQ; ++k) {
+            const int64_t i = wb + 256 * (k / 4) + 4 * lane + (k % 4);
+            e[k] = i < n ? a.ge[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4 * RQ; ++k) {
+            const int64_t i = wb + 256 * (k / 4) + 4 * lane + (k % 4);
+            s[k] = i < n ? a.gs[i] : 0xffffffffu;
+        }
+        round_max();
     }
     const uint32_t wmax = dev::wave_reduce_max(lmax);
     if (lane == 0) s_wmax[w] = wmax;

@@ -238,6 +238,47 @@ __device__ __forceinline__ void load_step(const BinArgs &a, int64_t base, int64_
     }
 }
 
+// The write pass's prefetch: one step's rows by 16-B buffer loads through
+// per-chunk descriptors (bounds = the chunk's bytes), straight into the
+// step's registers.  A step past the chunk's last whole one is fetched at an
+// out-of-range offset: the loads return zeros and touch no memory, so the
+// prefetch needs no branch.  (Behind a per-lane bounds test hipcc joined the
+// loaded values into other registers, copying each group -- and so waiting
+// for it -- right after issuing it: 3 load latencies per step.)
+struct StepRsrc {
+    __amdgpu_buffer_rsrc_t c, s, e;
+};
+template <bool HC>
+__device__ __forceinline__ StepRsrc step_rsrc(const BinArgs &a, int64_t r0, int64_t r1) {
+    const int nbytes = (int)((r1 - r0) * 4);  // (< 2^31: chunk_rows <= 16 STEP)
+    StepRsrc r;
+    r.c = __builtin_amdgcn_make_buffer_rsrc(HC ? (void *)(a.contig + r0) : (void *)a.start, (short)0,
+                                           HC ? nbytes : 0, 0x00020000);
+    r.s = __builtin_amdgcn_make_buffer_rsrc((void *)(a.start + r0), (short)0, nbytes, 0x00020000);
+    r.e = __builtin_amdgcn_make_buffer_rsrc((void *)(a.end + r0), (short)0, nbytes, 0x00020000);
+    return r;
+}
+constexpr uint32_t RSRC_OOB = 0x40000000u;  // byte offset past any chunk
+template <bool HC, int NT>
+__device__ __forceinline__ void load_rsrc(const StepRsrc &r, uint32_t rel, int32_t (&c)[SROWS],
+                                          uint32_t (&s)[SROWS], uint32_t (&e)[SROWS]) {
+#pragma unroll
+    for (int q = 0; q < SROWS / 4; ++q) {
+        const uint32_t off = rel + 4u * (q * 4 * NT + 4 * threadIdx.x);  // bytes
+        if (HC) {
+            const auto cv = __builtin_amdgcn_raw_buffer_load_b128(r.c, (int)off, 0, 0);
+            c[4 * q] = (int32_t)cv[0], c[4 * q + 1] = (int32_t)cv[1], c[4 * q + 2] = (int32_t)cv[2],
+                  c[4 * q + 3] = (int32_t)cv[3];
+        } else {
+            c[4 * q] = c[4 * q + 1] = c[4 * q + 2] = c[4 * q + 3] = 0;
+        }
+        const auto sv = __builtin_amdgcn_raw_buffer_load_b128(r.s, (int)off, 0, 0);
+        s[4 * q] = sv[0], s[4 * q + 1] = sv[1], s[4 * q + 2] = sv[2], s[4 * q + 3] = sv[3];
+        const auto ev = __builtin_amdgcn_raw_buffer_load_b128(r.e, (int)off, 0, 0);
+        e[4 * q] = ev[0], e[4 * q + 1] = ev[1], e[4 * q + 2] = ev[2], e[4 * q + 3] = ev[3];
+    }
+}
+
 template <bool LC>
 __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
     __shared__ uint32_t hist[NTMAX];
@@ -296,7 +337,12 @@ __global__ __launch_bounds__(256) void k_tile_groups(BinArgs a) {
 #ifndef LIME_WRITE_BLOCKS
 #define LIME_WRITE_BLOCKS 2
 #endif
-template <bool LC>
+#ifndef LIME_BIN_PREFETCH
+#define LIME_BIN_PREFETCH 1
+#endif
+// LC: the contig table in LDS; HC: rows carry contig ids (else global
+// coordinates)
+template <bool LC, bool HC>
 __global__ __launch_bounds__(WRB)
 __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bin_write(BinArgs a) {
     __shared__ uint32_t stage[WSTEP];
@@ -317,19 +363,20 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
     uint32_t err = 0;
     int32_t c[SROWS];
     uint32_t s[SROWS], e[SROWS];
-    uint32_t valid = 0;
-    if (r0 < r1) load_step<true, WRB>(a, r0, r1, c, s, e, valid);
-    for (int64_t base = r0; base < r1; base += WSTEP) {
+    // one step: its rows' bins and packed runs from (c, s, e), then NEXT()
+    // (the following step's loads: in flight across this step's barriers --
+    // plain loads survive __syncthreads), then rank, stage and store
+    auto step = [&](int64_t base, uint32_t valid, auto next) {
         // tb[k]: the row's bin, then (bin << 13 | its rank among the step's
         // rows of the bin) once ranked: one register per row for both
         uint32_t tb[SROWS], pk[SROWS];
 #pragma unroll
         for (int k = 0; k < SROWS; ++k) {
             const int32_t cc = c[k];
-            const uint32_t gs = row_gs(a, off, cc, s[k]);
+            const uint32_t gs = row_gs(a, off, HC ? cc : 0, s[k]);
             uint32_t ge = gs;
             if (!(valid & (1u << k))) {
-            } else if (!a.contig) {
+            } else if (!HC) {
                 if (e[k] < s[k]) err |= 2u;
                 else if (e[k] > a.span) err |= 4u;
                 else ge = e[k];
@@ -357,16 +404,13 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
             if ((valid & (1u << k)) && g1 > g0 + l)
                 a.cross[atomicAdd(a.ncross, 1u)] = ((uint64_t)(g0 + l) << 32) | g1;
         }
-        const uint32_t vnow = valid;
-        // the next step's rows: their loads stay in flight across this step's
-        // barriers (plain loads survive __syncthreads)
-        if (base + WSTEP < r1) load_step<true, WRB>(a, base + WSTEP, r1, c, s, e, valid);
+        next();
         // rank per bin (16 independent LDS atomics), then bin offsets in the
         // step (one scan over <= 1024 bins), then stage in bin order
         static_assert(WSTEP <= (1 << 13) && NBMAX <= (1 << 19), "bin / rank packing");
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
-            if (vnow & (1u << k)) tb[k] = (tb[k] << 13) | atomicAdd(&hist[tb[k]], 1u);
+            if (valid & (1u << k)) tb[k] = (tb[k] << 13) | atomicAdd(&hist[tb[k]], 1u);
         __syncthreads();
         {
             // bins BPT t .. BPT t + BPT - 1 per thread (fewer bins than
@@ -388,7 +432,7 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
-            if (vnow & (1u << k)) {
+            if (valid & (1u << k)) {
                 const uint32_t t = tb[k] >> 13;
                 const uint32_t j = soff[t] + (tb[k] & 0x1fffu);
                 stage[j] = pk[k];
@@ -414,6 +458,39 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
             hist[t] = 0;
         }
         __syncthreads();
+    };
+    constexpr uint32_t ALL = (1u << SROWS) - 1;
+    // the chunk's whole steps (every chunk but the set's last has only
+    // those: chunk_rows is a multiple of WSTEP), then its partial tail
+    const int64_t nfull = (r1 - r0) / WSTEP;
+    if (LIME_BIN_PREFETCH) {
+        // iteration -1 only fetches step 0: the rows' one load site, so the
+        // registers they land in are the ones the next step reads
+        const StepRsrc rs = step_rsrc<HC>(a, r0, r1);
+        for (int64_t k = -1; k < nfull; ++k) {  // (uniform)
+            const int64_t base = r0 + k * WSTEP;
+            auto fetch = [&]() {
+                const uint32_t rel = k + 1 < nfull ? 4u * (uint32_t)((k + 1) * WSTEP) : RSRC_OOB;
+                load_rsrc<HC, WRB>(rs, rel, c, s, e);
+            };
+            if (k < 0)
+                fetch();
+            else
+                step(base, ALL, fetch);
+        }
+    } else {
+        for (int64_t k = 0; k < nfull; ++k) {
+            const int64_t base = r0 + k * WSTEP;
+            uint32_t valid;
+            load_step<true, WRB>(a, base, r1, c, s, e, valid);
+            step(base, valid, [] {});
+        }
+    }
+    const int64_t tail = r0 + nfull * WSTEP;
+    if (tail < r1) {
+        uint32_t valid;
+        load_step<true, WRB>(a, tail, r1, c, s, e, valid);
+        step(tail, valid, [] {});
     }
     err = dev::wave_reduce_or(err);
     if (err && dev::lane_id() == 0) atomicOr(a.err, err);
@@ -1297,7 +1374,7 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
         int dev = 0, c = 256, occ = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bin_write<true>, WRB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bin_write<true, true>, WRB, 0);
         return (int64_t)(c > 0 ? c : 256) * (occ > 0 ? occ : 1);
     }();
     const int64_t rounds = std::max<int64_t>((n + cus * 16 * STEP - 1) / (cus * 16 * STEP), 1);
@@ -1358,9 +1435,11 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
     LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
     if (lc)
-        hipLaunchKernelGGL(k_bin_write<true>, dim3(nch), dim3(WRB), 0, S(ctx), a);
+        hipLaunchKernelGGL((k_bin_write<true, true>), dim3(nch), dim3(WRB), 0, S(ctx), a);
+    else if (d_contig)
+        hipLaunchKernelGGL((k_bin_write<false, true>), dim3(nch), dim3(WRB), 0, S(ctx), a);
     else
-        hipLaunchKernelGGL(k_bin_write<false>, dim3(nch), dim3(WRB), 0, S(ctx), a);
+        hipLaunchKernelGGL((k_bin_write<false, false>), dim3(nch), dim3(WRB), 0, S(ctx), a);
     // the atomic-claim split (C5 12.05 -> 11.73 ms against a ballot-ranked one)
     hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)(nb * ng)), dim3(SPB), 0, S(ctx), a);
     LIME_HIP(hipGetLastError());

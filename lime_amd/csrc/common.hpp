@@ -478,6 +478,15 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t *st, int64_t tile) {
     return acc;
 }
 
+// a value the caller knows to be wave-uniform, moved to SGPRs so that what
+// is indexed by it (kernel-argument structs, table entries) is read by
+// scalar loads, outside the vector memory counter
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // splitmix64 finaliser (shared with oracle/lime_oracle.c lo_pair_hash)
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;

@@ -460,10 +460,15 @@ __device__ __forceinline__ int tile_stream(const FillArgs &fa, int64_t t) {
 }
 
 template <int TPF>
-__device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileRegs<TPF> &r) {
+__device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileRegs<TPF> &r,
+                                          const uint64_t *toff, const uint32_t *win,
+                                          const uint32_t *tseg) {
     constexpr int FO = FillShape<TPF>::FOPT, PP = FillShape<TPF>::PPT;
+    // (t is wave-uniform: the stream's arguments are selected, not indexed,
+    // so they stay scalar kernel-argument loads -- an indexed fa.s[st] was
+    // read by vector loads whose waits drained the store stream)
     const int st = tile_stream(fa, t);
-    const StreamArgs &sa = fa.s[st];
+    const StreamArgs sa = st ? fa.s[1] : fa.s[0];
     // a commit never spans the two streams
     const int64_t t1 = min(t + TPF, st == 0 ? stream0_tiles(fa) : fa.ntiles);
     const int64_t o0 = (t - sa.tile0) * OT;
@@ -472,8 +477,8 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
     // lie in tile t + u, whose offset within the commit is toff[t+u] - toff[t]
     uint32_t add = 0;
     if (TPF > 1) {
-        const int u = (int)(threadIdx.x / (FB / TPF));
-        if (u > 0 && t + u < t1) add = (uint32_t)(fa.toff[t + u] - fa.toff[t]);
+        const int u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / (FB / TPF)));
+        if (u > 0 && t + u < t1) add = (uint32_t)(toff[t + u] - toff[t]);
     }
 #pragma unroll
     for (int k = 0; k < FO; ++k) {
@@ -486,17 +491,17 @@ __device__ __forceinline__ void tile_load(const FillArgs &fa, int64_t t, TileReg
         r.oe[k] = v ? sa.oge_o[j] : 0u;
         r.orw[k] = v ? sa.orow[j] : 0u;
     }
-    r.wlo = fa.win[2 * t];
-    r.whi = fa.win[2 * t + 1];
-    r.seg = fa.tseg[t];
+    r.wlo = win[2 * t];
+    r.whi = win[2 * t + 1];
+    r.seg = tseg[t];
     if (TPF > 1 && t1 - 1 > t) {
         // the union of the tiles' windows (each window is an interval)
-        r.wlo = min(r.wlo, fa.win[2 * (t1 - 1)]);
-        r.whi = max(r.whi, fa.win[2 * (t1 - 1) + 1]);
-        if (fa.tseg[t1 - 1] != r.seg) r.seg = 0xffffffffu;
+        r.wlo = min(r.wlo, win[2 * (t1 - 1)]);
+        r.whi = max(r.whi, win[2 * (t1 - 1) + 1]);
+        if (tseg[t1 - 1] != r.seg) r.seg = 0xffffffffu;
     }
     r.t1 = t1;
-    r.tnext = t1 < fa.ntiles ? fa.toff[t1] : (uint64_t)fa.total;
+    r.tnext = t1 < fa.ntiles ? toff[t1] : (uint64_t)fa.total;
     const int wl = (int)min((int64_t)(r.whi - r.wlo), (int64_t)FillShape<TPF>::CAP);
 #pragma unroll
     for (int k = 0; k < PP; ++k) {
@@ -665,7 +670,14 @@ __device__ __forceinline__ void emit_sparse(const FillArgs &fa, const StreamArgs
 // (a few pairs per owner, ~4k records per tile) commit two tiles at a time
 // (TPF = 2) to halve that cost per record.
 template <int TPF, bool CKSUM, bool WIN>
-__global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int64_t per, int64_t gran) {
+// toff / win / tseg: fa's per-tile tables again, as restrict arguments: read
+// at wave-uniform indices they are scalar loads (lgkmcnt), so the commit's
+// table reads never wait on the vector memory counter -- which would drain
+// the previous commit's stores first
+__global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int64_t per, int64_t gran,
+                                                               const uint64_t *__restrict__ toff,
+                                                               const uint32_t *__restrict__ win,
+                                                               const uint32_t *__restrict__ tseg) {
     constexpr int OTF = FillShape<TPF>::OTF, FO = FillShape<TPF>::FOPT,
                   PP = FillShape<TPF>::PPT, CAP = FillShape<TPF>::CAP;
     __shared__ uint2 s_lo_off[OTF + 1];
@@ -687,17 +699,17 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
         if (lane == 0) s_tile = t0;
     }
     __syncthreads();
-    int64_t t = s_tile;
+    int64_t t = dev::uni64(s_tile);
     uint64_t hsum = 0, hxor = 0;
     TileRegs<TPF> R;
-    tile_load<TPF>(fa, t, R);
+    tile_load<TPF>(fa, t, R, toff, win, tseg);
     while (true) {
         const int st = tile_stream(fa, t);
-        const StreamArgs &sa = fa.s[st];
+        const StreamArgs sa = st ? fa.s[1] : fa.s[0];
         const int64_t o0 = (t - sa.tile0) * OT;
         const int nown = (int)min((int64_t)OTF, sa.no - o0);
-        const int64_t tbase = (int64_t)fa.toff[t];
-        const int64_t tn = R.t1;
+        const int64_t tbase = (int64_t)toff[t];
+        const int64_t tn = dev::uni64(R.t1);
         // ---- commit the staged registers to LDS (offsets come scanned
         // from k_count: no block scan here)
         const uint32_t ttot = (uint32_t)(R.tnext - (uint64_t)tbase);
@@ -723,8 +735,9 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
         }
         __syncthreads();
         // ---- prefetch the next commit (its loads overlap this one's stores)
-        const bool more = tn < fa.ntiles && (int64_t)fa.toff[tn] < oend;
-        if (more) tile_load<TPF>(fa, tn, R);
+        // (R.tnext = toff[tn]: no table read)
+        const bool more = tn < fa.ntiles && (int64_t)R.tnext < oend;
+        if (more) tile_load<TPF>(fa, tn, R, toff, win, tseg);
         // ---- this commit's slice of the output window, in granules dealt
         // round-robin to the waves (wave w: granules w, w + FW, ...).  The
         // default granule is one equal chunk per wave: 2048-record granules
@@ -953,14 +966,17 @@ int64_t fill_span(int64_t count) {
 template <int TPF>
 void launch_k_fill(lime_ctx *ctx, dim3 g, const FillArgs &fa, int64_t per, bool cksum, bool win) {
     if (cksum && win)
-        hipLaunchKernelGGL((k_fill<TPF, true, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+        hipLaunchKernelGGL((k_fill<TPF, true, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR,
+                           fa.toff, fa.win, fa.tseg);
     else if (cksum)
-        hipLaunchKernelGGL((k_fill<TPF, true, false>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+        hipLaunchKernelGGL((k_fill<TPF, true, false>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR,
+                           fa.toff, fa.win, fa.tseg);
     else if (win)
-        hipLaunchKernelGGL((k_fill<TPF, false, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR);
+        hipLaunchKernelGGL((k_fill<TPF, false, true>), g, dim3(FB), 0, S(ctx), fa, per, (int64_t)GR,
+                           fa.toff, fa.win, fa.tseg);
     else
         hipLaunchKernelGGL((k_fill<TPF, false, false>), g, dim3(FB), 0, S(ctx), fa, per,
-                           (int64_t)GR);
+                           (int64_t)GR, fa.toff, fa.win, fa.tseg);
 }
 
 int launch_fill(PairsPlan *pl, int64_t first, int64_t count, u32x4 *out, uint64_t *cksum) {

@@ -826,7 +826,12 @@ struct FusedArgs {
     int64_t ntiles;
 };
 
-__global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa) {
+// wstart / wend: sa's per-tile window bounds again, as restrict arguments,
+// read at the wave-uniform tile index by scalar loads: the window's staging
+// loads issue right behind the rows' loads instead of after them
+__global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
+                                                      const uint32_t *__restrict__ wstart,
+                                                      const uint32_t *__restrict__ wend) {
     __shared__ uint32_t w_pm[FWIN], w_gs[FWIN], w_run[FWIN];
     __shared__ uint32_t f_gs[FCAP], f_ge[FCAP], f_ar[FCAP], f_br[FCAP];
     __shared__ uint64_t s_wtot[FW];
@@ -841,22 +846,24 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa)
     const int64_t base = tile * FROWS + (int64_t)wv * SUB_B;
     constexpr int RPL = SUB_B / 64;  // rows per lane: row base + k 64 + lane
     uint32_t as[RPL], ae[RPL];
+    // every load unconditional (rows past the set read its last row and are
+    // zeroed after): behind a per-lane bounds branch they were issued and
+    // waited for pair by pair
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
         const int64_t i = base + k * 64 + lane;
-        as[k] = ae[k] = 0;
-        if (i < sa.na) {
-            as[k] = sa.ags[i];
-            ae[k] = sa.age[i];
-        }
+        const int64_t ic = min(i, sa.na - 1);
+        const uint32_t s_ = sa.ags[ic], e_ = sa.age[ic];
+        as[k] = i < sa.na ? s_ : 0u;
+        ae[k] = i < sa.na ? e_ : 0u;
     }
-    const int64_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)sa.wstart[tile]);
+    const int64_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)wstart[tile]);
     // the rows' hits end before wend: staged up to one row past it, so every
     // row's bound lies inside the window (the sparse 1e9-row subtract: ~1030
     // of the 1536 rows a fixed window staged)
     const int nst = __builtin_amdgcn_readfirstlane(
         (int)min(min((int64_t)FWIN, sa.nb - wlo),
-                 LIME_SUB_WEND ? (int64_t)sa.wend[tile] + 1 - wlo : (int64_t)FWIN));
+                 LIME_SUB_WEND ? (int64_t)wend[tile] + 1 - wlo : (int64_t)FWIN));
     for (int k = threadIdx.x; k < nst; k += FW * 64) {
         w_pm[k] = sa.bpmax[wlo + k];
         w_gs[k] = sa.bgs[wlo + k];
@@ -1405,7 +1412,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
             fa.cap = cap;
             LIME_HIP(hipMemsetAsync(st, 0, 8 * ((size_t)ntiles + 2), S(ctx)));
             hipLaunchKernelGGL(k_sub_fused, dim3((unsigned)ntiles), dim3(FW * 64), 0, S(ctx), sa,
-                               fa);
+                               fa, (const uint32_t *)wstart, (const uint32_t *)wend);
             LIME_HIP(hipGetLastError());
             LIME_TRY(read_back(ctx, &total, fa.total, sizeof(total)));
             if (total <= cap) break;

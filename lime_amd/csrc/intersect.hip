@@ -228,8 +228,20 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
     const int64_t t = blockIdx.x;
     const int64_t o0 = t * OT;
     const int64_t o1 = min(o0 + OT, sa.no);
-    // owner loads first: they are independent of the window and overlap
-    // its two dependent round trips
+    // the window's partner starts first, every load unconditional (lanes
+    // past the window re-read its last start, one line): issued together,
+    // one round trip, where a bounds-tested loop waited per iteration
+    const uint32_t wlo = win[2 * (sa.tile0 + t)], whi = win[2 * (sa.tile0 + t) + 1];
+    const int64_t wlen = (int64_t)whi - wlo;
+    const bool in_lds = wlen <= WCAP;
+    constexpr int WPT = WCAP / IB;
+    uint32_t wv[WPT];
+    if (in_lds && wlen > 0) {  // (uniform)
+#pragma unroll
+        for (int k = 0; k < WPT; ++k)
+            wv[k] = sa.pgs[wlo + min((int64_t)(k * IB + threadIdx.x), wlen - 1)];
+    }
+    // owner loads: independent of the window, in flight with it
     uint32_t ogv[OPT], oev[OPT];
     static_assert(OPT == 4, "owner loads are one 16-B vector per thread");
     if (o1 - o0 == OT) {  // full tile: lane-consecutive 16-B loads (sets are 16-B aligned)
@@ -245,11 +257,11 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
             oev[k] = j < o1 ? sa.oge[j] : 0u;
         }
     }
-    const uint32_t wlo = win[2 * (sa.tile0 + t)], whi = win[2 * (sa.tile0 + t) + 1];
-    const int64_t wlen = (int64_t)whi - wlo;
-    const bool in_lds = wlen <= WCAP;
-    if (in_lds)
-        for (int64_t i = threadIdx.x; i < wlen; i += IB) wgs[i] = sa.pgs[wlo + i];
+    if (in_lds && wlen > 0) {
+#pragma unroll
+        for (int k = 0; k < WPT; ++k)
+            if (k * IB + (int)threadIdx.x < wlen) wgs[k * IB + threadIdx.x] = wv[k];
+    }
     __syncthreads();
     // lo = lb(P, o.gs + lo_off) always (subtract's spanning walk starts
     // below it); hi = lb(P, o.ge - tp + 1), the range [lo, hi) being empty

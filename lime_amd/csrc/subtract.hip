@@ -637,28 +637,48 @@ __global__ __launch_bounds__(SUB_B) void k_subtract(SubArgs sa) {
 // outside the window (a B row wider than it holds) read global memory, as in
 // k_subtract.
 
-__global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, int64_t nblk) {
+// (wstart: sa.wstart again, restrict: the workgroup's window start is a
+// scalar load, so the window's loads issue beside the rows' -- as
+// k_sub_fused, whose loads are batched the same way)
+__global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, int64_t nblk,
+                                                                  const uint32_t *__restrict__ wstart) {
     __shared__ uint32_t w_pm[CNT_WIN], w_gs[CNT_WIN], w_run[CNT_WIN];
     const int wv = threadIdx.x / 64, lane = dev::lane_id();
     const int64_t base = (int64_t)blockIdx.x * CNT_ROWS + (int64_t)wv * SUB_B;
     constexpr int RPL = SUB_B / 64;  // rows per lane
     uint32_t as[RPL], ae[RPL];
+    // every load unconditional (clamped, zeroed past the set)
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
         const int64_t i = base + k * 64 + lane;
-        as[k] = ae[k] = 0;
-        if (i < sa.na) {
-            as[k] = sa.ags[i];
-            ae[k] = sa.age[i];
-        }
+        const int64_t ic = min(i, sa.na - 1);
+        const uint32_t s_ = sa.ags[ic], e_ = sa.age[ic];
+        as[k] = i < sa.na ? s_ : 0u;
+        ae[k] = i < sa.na ? e_ : 0u;
     }
-    // the workgroup's window start (its first block's)
-    const int64_t wlo = sa.wstart[blockIdx.x];
+    // the workgroup's window start (its first block's); the window staged by
+    // one batch of unconditional loads (lanes past it re-read its last row)
+    const int64_t wlo = wstart[blockIdx.x];
     const int nst = (int)min((int64_t)CNT_WIN, sa.nb - wlo);
-    for (int k = threadIdx.x; k < nst; k += CNT_WAVES * 64) {
-        w_pm[k] = sa.bpmax[wlo + k];
-        w_gs[k] = sa.bgs[wlo + k];
-        w_run[k] = sa.brun[wlo + k];
+    constexpr int WPT = (CNT_WIN + CNT_WAVES * 64 - 1) / (CNT_WAVES * 64);
+    if (nst > 0) {  // (uniform)
+        uint32_t vp[WPT], vg[WPT], vr[WPT];
+#pragma unroll
+        for (int q = 0; q < WPT; ++q) {
+            const int64_t j = wlo + min(q * CNT_WAVES * 64 + (int)threadIdx.x, nst - 1);
+            vp[q] = sa.bpmax[j];
+            vg[q] = sa.bgs[j];
+            vr[q] = sa.brun[j];
+        }
+#pragma unroll
+        for (int q = 0; q < WPT; ++q) {
+            const int k = q * CNT_WAVES * 64 + threadIdx.x;
+            if (k < nst) {
+                w_pm[k] = vp[q];
+                w_gs[k] = vg[q];
+                w_run[k] = vr[q];
+            }
+        }
     }
     __syncthreads();
     const int64_t whi = wlo + nst;
@@ -1444,7 +1464,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     };
     if (runs)
         hipLaunchKernelGGL(k_sub_count_runs, dim3(blocks_for(na, CNT_ROWS)), dim3(CNT_WAVES * 64),
-                           0, S(ctx), sa, nblk);
+                           0, S(ctx), sa, nblk, (const uint32_t *)sa.wstart);
     else
         launch(false);
     LIME_HIP(hipGetLastError());

@@ -644,6 +644,7 @@ __global__ __launch_bounds__(BB) void k_xwrite(const uint64_t *__restrict__ cros
 
 template <int CAP>
 struct AndArgsK {
+    static constexpr int NCAP = CAP;
     const uint32_t *slab2[CAP];  // tile-ordered packed rows of set i
     const uint32_t *tstart[CAP]; // nt + 1 tile starts
     const uint2 *xl[CAP];        // tile-bucketed cross pieces (null: none)
@@ -667,41 +668,63 @@ template <class AA>
 __device__ __forceinline__ void paint_and_tile(const AA &a, int t, uint32_t neg,
                                                unsigned long long *img, uint64_t (&acc)[AWPT]) {
     constexpr uint32_t B = APV * PAINTB;
+    // the tile's per-set table entries (row range, cross-piece range, whole
+    // coverage), read once into LDS by one batch of loads: walked from
+    // global memory, each was a vector load whose wait also waited for the
+    // prefetched batch, ~4 serial round trips per batch (C5: 24 batches a tile)
+    __shared__ uint32_t s_r0[AA::NCAP], s_r1[AA::NCAP], s_x0[AA::NCAP], s_x1[AA::NCAP],
+        s_full[AA::NCAP];
+    if (threadIdx.x < (unsigned)a.k) {
+        const int q = threadIdx.x;
+        s_r0[q] = a.tstart[q][t];
+        s_r1[q] = a.tstart[q][t + 1];
+        s_full[q] = a.full[q] ? a.full[q][t + 1] : 0u;
+        s_x0[q] = a.xl[q] ? a.xoff[q][t] : 0u;
+        s_x1[q] = a.xl[q] ? a.xoff[q][t + 1] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < AWPT; ++j) img[threadIdx.x + j * PAINTB] = 0ull;
+    __syncthreads();
     // a tile wholly inside one of the set's cross pieces: all ones (AND
     // unchanged, or all zeros complemented)
     bool zero = false;
     auto skip = [&](int i) {
-        const bool f = a.full[i] && a.full[i][t + 1] != 0u;
+        const bool f = s_full[i] != 0u;
         if (f && ((neg >> i) & 1u)) zero = true;
         return f;
     };
+    // a batch of B rows by bounds-checked buffer loads through a descriptor
+    // over the batch's rows (past them, and for i = k: no set, zeros, no
+    // traffic): no per-lane branch, so painting the current batch does not
+    // wait for this one (behind per-lane bounds tests it waited for all)
     auto load = [&](int i, uint32_t rb, uint32_t(&p)[APV]) {
-        const uint32_t r1 = a.tstart[i][t + 1];
-        const uint32_t *slab2 = a.slab2[i];
+        const bool has = i < a.k;  // (uniform)
+        const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb);
+        const uint32_t r1 = has ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_r1[i]) : r0;
+        const uint32_t cnt = r1 > r0 ? min(r1 - r0, B) : 0u;
+        const uint32_t *base = has ? a.slab2[i] + r0 : a.slab2[0];
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)(4u * cnt),
+                                                          0x00020000);
 #pragma unroll
-        for (int k = 0; k < APV; ++k) {
-            const uint32_t r = rb + k * PAINTB + threadIdx.x;
-            p[k] = r < r1 ? slab2[r] : 0u;
-        }
+        for (int k = 0; k < APV; ++k)
+            p[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (k * PAINTB + threadIdx.x)),
+                                                         0, 0);
     };
     int i = 0;
     while (i < a.k && skip(i)) ++i;
-#pragma unroll
-    for (int j = 0; j < AWPT; ++j) img[threadIdx.x + j * PAINTB] = 0ull;
-    __syncthreads();
-    uint32_t rb = i < a.k ? a.tstart[i][t] : 0u;
+    uint32_t rb = i < a.k ? s_r0[i] : 0u;
     uint32_t pv[APV];
     if (i < a.k) load(i, rb, pv);
     while (i < a.k) {  // (i, rb) and i2 are uniform over the block
         int i2 = i;
         uint32_t rb2 = rb + B;
-        if (rb2 >= a.tstart[i][t + 1]) {
+        if (rb2 >= s_r1[i]) {
             i2 = i + 1;
             while (i2 < a.k && skip(i2)) ++i2;
-            if (i2 < a.k) rb2 = a.tstart[i2][t];
+            if (i2 < a.k) rb2 = s_r0[i2];
         }
         uint32_t pn[APV];
-        if (i2 < a.k) load(i2, rb2, pn);
+        load(i2, rb2, pn);  // (i2 = k: zeros)
 #pragma unroll
         for (int k = 0; k < APV; ++k) {
             const uint32_t l = pv[k] & ((1u << PLENB) - 1);
@@ -709,7 +732,7 @@ __device__ __forceinline__ void paint_and_tile(const AA &a, int t, uint32_t neg,
         }
         if (i2 != i) {  // set i complete: its cross pieces, then the AND
             if (a.xl[i]) {
-                const uint32_t x0 = a.xoff[i][t], x1 = a.xoff[i][t + 1];
+                const uint32_t x0 = s_x0[i], x1 = s_x1[i];
                 for (uint32_t x = x0 + threadIdx.x; x < x1; x += PAINTB) {
                     const uint2 p = a.xl[i][x];
                     if (p.y > p.x) paint_lds(img, p.x, p.y);

@@ -959,14 +959,19 @@ template <int NT, int ITEMS, int CAP>
 struct BucketRegs {
     uint32_t g[ITEMS], e[ITEMS], r[ITEMS];
     uint32_t s0, m;
-    __device__ __forceinline__ void load(const LocalArgs &a, uint32_t b, uint32_t nb) {
+    // start: the bucket starts (a.start; the persistent kernel passes them as
+    // a restrict argument, read at its wave-uniform bucket index by scalar
+    // loads -- a vector load's wait there drained the previous bucket's
+    // stores before this bucket's rows were requested)
+    __device__ __forceinline__ void load(const LocalArgs &a, uint32_t b, uint32_t nb,
+                                         const uint32_t *start) {
         constexpr int NW = NT / 64;
         const int w = threadIdx.x / 64, lane = dev::lane_id();
         s0 = 0;
         m = 0;
         if (b < nb) {
-            s0 = a.start[b];
-            m = a.start[b + 1] - s0;
+            s0 = start[b];
+            m = start[b + 1] - s0;
         }
         const bool ok = m >= 1 && m <= (uint32_t)CAP;
         const uint32_t base = ok ? s0 : 0u;
@@ -993,14 +998,14 @@ struct BucketRegs {
 constexpr int LNT_S = 512, LPOS_S = 12, LCAP_S = 3072;  // 6 items / thread
 using SmallRegs = BucketRegs<LNT_S, LCAP_S / LNT_S, LCAP_S>;
 __global__ __launch_bounds__(LNT_S) __attribute__((amdgpu_waves_per_eu(6, 8)))
-void k_local_small(LocalArgs a, uint32_t nb) {
+void k_local_small(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) {
     __shared__ uint32_t A[LCAP_S], B[LCAP_S], s_e[LCAP_S], s_r[LCAP_S];
     __shared__ uint32_t sstart[LNT_S], scur[LNT_S];
     __shared__ uint32_t scratch[2 * (LNT_S / 64) + 1];
     SmallRegs cur, nxt;
-    cur.load(a, blockIdx.x, nb);
+    cur.load(a, blockIdx.x, nb, start);
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        nxt.load(a, b + gridDim.x, nb);
+        nxt.load(a, b + gridDim.x, nb, start);
         bool listed = cur.m > (uint32_t)LCAP_S;
         if (!listed && cur.m > 0)
             listed = !bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S, 9, true, uint32_t>(
@@ -1116,7 +1121,7 @@ __global__ __launch_bounds__(LNT_B) void k_local_big(LocalArgs a) {
         const uint32_t s0 = a.start[b], m = a.start[b + 1] - s0;
         if (m <= (uint32_t)LCAP_B) {
             BucketRegs<LNT_B, LCAP_B / LNT_B, LCAP_B> R;
-            R.load(a, b, b + 1);
+            R.load(a, b, b + 1, a.start);
             if (!bucket_sort_claim<LNT_B, LCAP_B / LNT_B, LPOS_B, 11, false, uint32_t>(
                     a, b, s0, m, R.g, R.e, R.r, A, B, sstart, scur, scratch, nullptr, nullptr))
                 bucket_sort_regs<LNT_B, LCAP_B / LNT_B, LPOS_B, false, uint16_t>(
@@ -1295,7 +1300,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (cus <= 0) cus = 256;
             hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)),
-                               dim3(LNT_S), 0, S(ctx), la, nb);
+                               dim3(LNT_S), 0, S(ctx), la, nb, (const uint32_t *)start);
             hipLaunchKernelGGL(k_local_big, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B), 0,
                                S(ctx), la);
             LIME_HIP(hipGetLastError());

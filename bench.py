@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--workload", default="c2", choices=["c2", "c5", "c3", "sub"],
                    help="c2: intersect + merge (the metric); c5: 8-way AND; c3: merge side "
                         "(sort + merge + carry + run ids + complement) of C3's pile-ups; sub: "
-                        "subtract (lime mode) of C2's inputs")
+                        "subtract (lime mode) of the 1B-interval sets (2 x 5e8, len U[10,40])")
     p.add_argument("--no-ops", action="store_true",
                    help="c2: skip the short c3 / sub lines reported under 'operators'")
     p.add_argument("--ops-steps", type=int, default=3)
@@ -272,7 +272,7 @@ def main():
         # (the driver's scaling runs record them beside the metric)
         finish.release()
         ops = {}
-        for name, fn in (("merge_side_c3", bench_c3), ("subtract_c2", bench_sub)):
+        for name, fn in (("merge_side_c3", bench_c3), ("subtract_1b", bench_sub)):
             st, fi = fn(args, ctx, space, dev, world, rank, comm_dev, ev, brief=True)
             ops[name] = fi(measure(st, args.ops_steps, 1))
             fi.release()
@@ -317,6 +317,9 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
     if world > 1:
         from lime_amd.sharded import ShardStep
         shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
+        # count-balanced shard bounds from samples of both inputs, once
+        shard.plan_splits([(m, A_in[0].data_ptr(), A_in[1].data_ptr()),
+                           (m, B_in[0].data_ptr(), B_in[1].data_ptr())])
 
     def step(last_step):
         t = [ev()] if last_step else None
@@ -443,6 +446,8 @@ def bench_c5(args, ctx, space, dev, world, rank, comm_dev, ev):
         ins.append((c, s, e))
     torch.cuda.synchronize(dev)
     op = ShardedAnd(ctx, space, comm_device=comm_dev, shared_stream=True)
+    if world > 1:  # count-balanced shard windows from samples of every set, once
+        op.plan_splits([(m, X[0].data_ptr(), X[1].data_ptr(), X[2].data_ptr()) for X in ins])
     state = {"t": None, "runs": 0}
 
     def step(last_step):
@@ -534,6 +539,7 @@ def bench_c3(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
     if world > 1:
         from lime_amd.sharded import ShardStep
         shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
+        shard.plan_splits([(m, cols[0].data_ptr(), cols[1].data_ptr())])
     state = {"runs": 0, "gaps": 0, "t": None}
 
     def step(last_step):
@@ -593,26 +599,30 @@ def bench_c3(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
 
 
 def bench_sub(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
-    """north_star's difference: DistributedSubtract (lime mode,
-    Subtract.scala:78-116) of C2's inputs (2 x 1e8 rows uniform over hg38,
-    len U[50,5000]): sort both, A minus B, every remnant materialised.  N > 1:
+    """north_star's difference on its 1B-interval sets: DistributedSubtract
+    (lime mode, Subtract.scala:78-116) of 2 x 5e8 rows uniform over hg38, len
+    U[10,40] (seeds 0x1A / 0x1C: the pairwise side of tests/test_gpu_scale.py
+    and tools/bench_extra.py b1_pair): sort both, A minus B, every remnant
+    materialised (~7.4e7 records: C2's deep inputs leave only 16).  N > 1:
     both sets range-sharded, B with its left and right halos (rows of other
     shards reaching into the shard), outputs disjoint by A row."""
     import torch
-    n = args.rows if (args.rows and not brief) else 100_000_000
+    n = args.rows if (args.rows and not brief) else 500_000_000
     first, last = rank * n // world, (rank + 1) * n // world
     m = last - first
 
     def gen(seed):
         cols = [torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3)]
-        ctx.synth_uniform_rows(space, first, m, seed, 50, 5000, *(c.data_ptr() for c in cols))
+        ctx.synth_uniform_rows(space, first, m, seed, 10, 40, *(c.data_ptr() for c in cols))
         return cols
-    A_in, B_in = gen(0xA), gen(0xB)
+    A_in, B_in = gen(0x1A), gen(0x1C)
     torch.cuda.synchronize(dev)
     shard = None
     if world > 1:
         from lime_amd.sharded import ShardStep
         shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
+        shard.plan_splits([(m, A_in[0].data_ptr(), A_in[1].data_ptr()),
+                           (m, B_in[0].data_ptr(), B_in[1].data_ptr())])
     state = {"records": 0}
 
     def step(last_step):
@@ -638,8 +648,8 @@ def bench_sub(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
         # prefix max); 16 B per record
         alg = 48 * n + 28 * n + 16 * rec
         achieved = alg / world / (ms * 1e-3) / 1e9
-        out = {"metric": "intervals/sec, DistributedSubtract (lime mode) of BASELINE C2's "
-                         "inputs", "value": 2 * n / (dt / steps), "unit": "intervals/s",
+        out = {"metric": "intervals/sec, DistributedSubtract (lime mode) of the 1B-interval "
+                         "sets (2 x 5e8)", "value": 2 * n / (dt / steps), "unit": "intervals/s",
                "n_gpus": world, "steps": steps, "ms_per_step": ms, "higher_is_better": True,
                "scaling": "strong", "rows_per_set": n, "records": rec,
                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -648,10 +658,10 @@ def bench_sub(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
                             "alg_bytes_per_step_per_gpu": alg / world}}
         if not brief:
             out.update({"warmup": args.warmup, "vs_baseline": None, "dtype": "u32",
-                        "data": "synthetic (counter-based splitmix64, seeds 0xA/0xB; rank r "
+                        "data": "synthetic (counter-based splitmix64, seeds 0x1A/0x1C; rank r "
                                 "generates rows [r n/N, (r+1) n/N) of each input)",
-                        "config": {"workload": "subtract (lime mode) of C2's inputs: 2 x 1e8 "
-                                               "intervals, uniform over hg38, len U[50,5000]"
+                        "config": {"workload": "subtract (lime mode) of 2 x 5e8 intervals, "
+                                               "uniform over hg38, len U[10,40]"
                                                + (", range-sharded with halos" if world > 1
                                                   else ""),
                                    "parallelism": f"range-shard x{world}" if world > 1

@@ -45,7 +45,7 @@ extern "C" {
 
 /* 2: lime_set_lower_bound / _first_reaching return -(LIME_ERR_*) on error
  *    (was -1); lime_pairs_checksum_device and the sharded-path helpers added */
-#define LIME_ABI_VERSION 3
+#define LIME_ABI_VERSION 4
 
 /* status codes */
 #define LIME_OK 0
@@ -173,10 +173,24 @@ int lime_set_stats(const lime_set *set, uint32_t *min_width, uint32_t *max_width
  * statistics are `set`'s combined with the caller's bounds for the added rows
  * (min_width / max_width / has_zero_width of those rows, or bounds of them).
  * Replaces rebuilding the shard's set (lime_set_create_global: a validating
- * pass and a read-back) in the sharded pairwise step. */
+ * pass and a read-back) in the sharded pairwise step.  With the environment
+ * variable LIME_CHECK_EXTEND=1 the contract is checked on the device (order
+ * at the join and among the added rows, width bounds, zero-width flag: one
+ * pass and a read-back) and a violation fails with LIME_ERR_ARG. */
 int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const uint32_t *d_gstart,
                            const uint32_t *d_gend, const uint32_t *d_row, uint32_t min_width,
                            uint32_t max_width, int32_t has_zero_width, lime_set **out);
+/* The same with rows on both sides: n_before rows that precede every row of
+ * `set`, then `set`, then n_after rows that follow it -- a coordinate shard's
+ * left halo (rows of earlier shards reaching into it), own rows and right
+ * halo, which the sharded subtract needs (Subtract.scala:78-116 over the
+ * replication of OverlapBasedSetTheory.scala:75-80).  The width bounds cover
+ * all added rows.  ABI 4. */
+int lime_set_concat_sorted(lime_ctx *ctx, const lime_set *set, int64_t n_before,
+                           const uint32_t *b_gstart, const uint32_t *b_gend, const uint32_t *b_row,
+                           int64_t n_after, const uint32_t *a_gstart, const uint32_t *a_gend,
+                           const uint32_t *a_row, uint32_t min_width, uint32_t max_width,
+                           int32_t has_zero_width, lime_set **out);
 /* Device pointers of the sorted set: global start, global end, input row. */
 int lime_set_device_arrays(const lime_set *set, const uint32_t **gstart, const uint32_t **gend,
                            const uint32_t **row);
@@ -379,6 +393,14 @@ int lime_route_rows(lime_ctx *ctx, const lime_space *space, int64_t n, const int
                     int32_t n_shards, const uint32_t *splits, int clip, int64_t cap,
                     uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts,
                     const int8_t *d_strand_in, int8_t *d_strand_out);
+/* k evenly spaced rows' global starts (rows i * n / k, i < k) into the
+ * device array d_out, for count-balanced splitters (lime_amd.dist
+ * sample_splits: the sampled range partitioner behind ADAM
+ * repartitionAndSort, cli/Intersection.scala:41-42, Partitioners.scala:10-20).
+ * d_contig == NULL: d_start is already global.  Stream-ordered, no sync.
+ * ABI 4. */
+int lime_sample_starts(lime_ctx *ctx, const lime_space *space, int64_t n, const int32_t *d_contig,
+                       const uint32_t *d_start, int32_t k, uint32_t *d_out);
 
 /* ------------------------------------------------------ synthetic inputs */
 /* Counter-based generators (splitmix64 keyed by (seed, row)) identical to

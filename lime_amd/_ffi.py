@@ -25,7 +25,7 @@ ERRORS = {
 }
 # the C-ABI contract this binding is written against (include/lime_amd.h
 # LIME_ABI_VERSION): checked at load, so a stale library fails loudly
-ABI_VERSION = 3
+ABI_VERSION = 4
 SUBTRACT_LIME = 0
 SUBTRACT_SET = 1
 
@@ -78,6 +78,9 @@ SIGNATURES = {
     "lime_set_copy_rows_device": (C.c_int, [vp, i64, i64, vp, vp, vp]),
     "lime_set_stats": (C.c_int, [vp, P(u32), P(u32), P(i32)]),
     "lime_set_extend_sorted": (C.c_int, [vp, vp, i64, vp, vp, vp, u32, u32, i32, pp]),
+    "lime_set_concat_sorted": (C.c_int, [vp, vp, i64, vp, vp, vp, i64, vp, vp, vp, u32, u32, i32,
+                                         pp]),
+    "lime_sample_starts": (C.c_int, [vp, vp, i64, vp, vp, i32, vp]),
     "lime_result_copy_range": (C.c_int, [vp, i64, i64, P(u32), P(u32)]),
     "lime_set_device_arrays": (C.c_int, [vp, pp, pp, pp]),
     "lime_set_fill_host": (C.c_int, [vp, P(i32), P(i64), P(i64), P(i64)]),

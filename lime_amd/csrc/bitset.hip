@@ -1575,18 +1575,25 @@ int bitset_build_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int3
 int bitset_paint(lime_ctx *ctx, const lime_bitset *cbs) {
     lime_bitset *bs = const_cast<lime_bitset *>(cbs);  // (a cache: the bits are unchanged)
     if (bs->words || bs->bins.empty()) return LIME_OK;
-    LIME_TRY(alloc(ctx, &bs->words, (size_t)std::max<int64_t>(bs->n_words, 1)));
+    // painted into a local buffer, published only once every group has been
+    // queued without error (a failed paint must not leave words that later
+    // calls would take as valid)
+    uint64_t *words = nullptr;
+    LIME_TRY(alloc(ctx, &words, (size_t)std::max<int64_t>(bs->n_words, 1)));
+    PoolGuard<uint64_t> guard{ctx, words};
     const int k = (int)bs->bins.size();
     for (int g0 = 0; g0 < k; g0 += MAXK) {
         std::vector<const lime_bitset::Bins *> b;
         for (int i = g0; i < std::min(k, g0 + MAXK); ++i) b.push_back(&bs->bins[i]);
         AndArgs aa = binned_args(b.data(), (int)b.size(), bs->nt, bs->n_words);
         aa.init = g0 > 0;
-        aa.words = bs->words;
+        aa.words = words;
         if (bs->nt > 0)
             hipLaunchKernelGGL(k_paint_and, dim3((unsigned)bs->nt), dim3(PAINTB), 0, S(ctx), aa);
+        LIME_HIP(hipGetLastError());
     }
-    LIME_HIP(hipGetLastError());
+    bs->words = words;
+    guard.p = nullptr;  // (owned by the bitset from here)
     return LIME_OK;
 }
 

@@ -135,6 +135,8 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
                     const int32_t *const *d_contig, const uint32_t *const *d_start,
                     const uint32_t *const *d_end, const uint32_t *d_off, const uint32_t *d_len,
                     int64_t lo, int64_t hi, lime_bitset *bs);
+int sample_starts(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                  const uint32_t *d_start, int32_t k, uint32_t *d_out);
 int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
                const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
@@ -586,15 +588,47 @@ int lime_set_stats(const lime_set *s, uint32_t *min_width, uint32_t *max_width,
     return LIME_OK;
 }
 
-int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const uint32_t *d_gs,
-                           const uint32_t *d_ge, const uint32_t *d_row, uint32_t min_width,
-                           uint32_t max_width, int32_t has_zero_width, lime_set **out) {
-    if (!ctx || !set || !out || n < 0 || (n > 0 && (!d_gs || !d_ge || !d_row)))
+// Opt-in check of the sorted-concatenation contract (LIME_CHECK_EXTEND=1):
+// every row of the new set follows its predecessor in canonical order (gs,
+// zero-width first), and the added rows -- [0, a0) and [a1, n) -- lie within
+// the declared width bounds.  bit0: order, bit1: width bounds, bit2:
+// zero-width row without the flag
+__global__ void k_check_join(const uint32_t *__restrict__ gs, const uint32_t *__restrict__ ge,
+                             int64_t n, int64_t a0, int64_t a1, uint32_t min_w, uint32_t max_w,
+                             int zero_ok, unsigned int *__restrict__ err) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = gs[i], e = ge[i];
+    unsigned int f = 0;
+    if (i > 0) {
+        const uint32_t pg = gs[i - 1], pe = ge[i - 1];
+        // canonical: (gs, zero width before non-zero width); ties beyond that
+        // keep input order
+        if (pg > g || (pg == g && pe > pg && e == g)) f |= 1u;
+    }
+    if (i < a0 || i >= a1) {
+        const uint32_t w = e - g;
+        if (e < g || w < min_w || w > max_w) f |= 2u;
+        if (w == 0 && !zero_ok) f |= 4u;
+    }
+    if (f) atomicOr(err, f);
+}
+
+// rows (nl prefix rows) + set + (nr suffix rows), copied device-to-device;
+// width statistics: the set's combined with the caller's bounds of the added
+// rows.  LIME_CHECK_EXTEND=1 checks the contract at both joins.
+static int concat_sorted(lime_ctx *ctx, const lime_set *set, int64_t nl, const uint32_t *l_gs,
+                         const uint32_t *l_ge, const uint32_t *l_row, int64_t nr,
+                         const uint32_t *r_gs, const uint32_t *r_ge, const uint32_t *r_row,
+                         uint32_t min_width, uint32_t max_width, int32_t has_zero_width,
+                         lime_set **out) {
+    if (!ctx || !set || !out || nl < 0 || nr < 0 || (nl > 0 && (!l_gs || !l_ge || !l_row)) ||
+        (nr > 0 && (!r_gs || !r_ge || !r_row)))
         return fail(LIME_ERR_ARG, "bad set arguments");
     if (set->ctx != ctx) return fail(LIME_ERR_ARG, "set belongs to another context");
     if (set->strand_in || set->row_ties || set->min_shift)
         return fail(LIME_ERR_ARG, "only plain sets extend");
-    const int64_t m = set->n + n;
+    const int64_t m = nl + set->n + nr, added = nl + nr;
     if (m > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one set");
     hipSetDevice(ctx->device);
     lime_set *s = new lime_set();
@@ -608,7 +642,7 @@ int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const 
     s->min_width = set->n ? set->min_width : min_width;
     s->max_width = set->max_width;
     s->has_zero_width = set->has_zero_width;
-    if (n > 0) {
+    if (added > 0) {
         if (set->n) s->min_width = std::min(s->min_width, min_width);
         s->max_width = std::max(s->max_width, max_width);
         s->has_zero_width = s->has_zero_width || has_zero_width != 0;
@@ -620,24 +654,65 @@ int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const 
         lime_set_destroy(s);
         return rc;
     }
-    const size_t a = 4 * (size_t)set->n, b = 4 * (size_t)n;
     hipError_t e = hipSuccess;
-    if (a) {
-        e = hipMemcpyAsync(s->gs, set->gs, a, hipMemcpyDeviceToDevice, S(ctx));
-        if (e == hipSuccess) e = hipMemcpyAsync(s->ge, set->ge, a, hipMemcpyDeviceToDevice, S(ctx));
-        if (e == hipSuccess) e = hipMemcpyAsync(s->row, set->row, a, hipMemcpyDeviceToDevice, S(ctx));
-    }
-    if (b && e == hipSuccess) {
-        e = hipMemcpyAsync(s->gs + set->n, d_gs, b, hipMemcpyDeviceToDevice, S(ctx));
-        if (e == hipSuccess) e = hipMemcpyAsync(s->ge + set->n, d_ge, b, hipMemcpyDeviceToDevice, S(ctx));
-        if (e == hipSuccess) e = hipMemcpyAsync(s->row + set->n, d_row, b, hipMemcpyDeviceToDevice, S(ctx));
-    }
+    auto part = [&](int64_t at, int64_t cnt, const uint32_t *g, const uint32_t *x,
+                    const uint32_t *r) {
+        const size_t bytes = 4 * (size_t)cnt;
+        if (!cnt || e != hipSuccess) return;
+        e = hipMemcpyAsync(s->gs + at, g, bytes, hipMemcpyDeviceToDevice, S(ctx));
+        if (e == hipSuccess) e = hipMemcpyAsync(s->ge + at, x, bytes, hipMemcpyDeviceToDevice, S(ctx));
+        if (e == hipSuccess) e = hipMemcpyAsync(s->row + at, r, bytes, hipMemcpyDeviceToDevice, S(ctx));
+    };
+    part(0, nl, l_gs, l_ge, l_row);
+    part(nl, set->n, set->gs, set->ge, set->row);
+    part(nl + set->n, nr, r_gs, r_ge, r_row);
     if (e != hipSuccess) {
         lime_set_destroy(s);
         return fail(LIME_ERR_DEVICE, std::string("lime_set_extend_sorted copy: ") + hipGetErrorString(e));
     }
+    static const bool check = [] {
+        const char *v = getenv("LIME_CHECK_EXTEND");
+        return v && v[0] && v[0] != '0';
+    }();
+    if (check && added > 0) {
+        // one pass over the whole new set: order everywhere, and the width
+        // bounds over the added rows (the set's own rows are canonical)
+        unsigned int *err = nullptr, herr = 0;
+        rc = alloc(ctx, &err, 1);
+        if (rc == LIME_OK && hipMemsetAsync(err, 0, 4, S(ctx)) != hipSuccess) rc = LIME_ERR_DEVICE;
+        if (rc == LIME_OK) {
+            hipLaunchKernelGGL(k_check_join, dim3(blocks_for(m, 256)), dim3(256), 0, S(ctx), s->gs,
+                               s->ge, m, nl, nl + set->n, min_width, max_width,
+                               has_zero_width ? 1 : 0, err);
+            rc = read_back(ctx, &herr, err, sizeof(herr));
+        }
+        release(ctx, err);
+        if (rc == LIME_OK && herr) rc = fail(LIME_ERR_ARG, herr & 1u ? "extend: rows out of canonical order"
+                                                          : herr & 2u ? "extend: a width outside the bounds"
+                                                                      : "extend: a zero-width row without the flag");
+        if (rc != LIME_OK) {
+            lime_set_destroy(s);
+            return rc;
+        }
+    }
     *out = s;
     return LIME_OK;
+}
+
+int lime_set_extend_sorted(lime_ctx *ctx, const lime_set *set, int64_t n, const uint32_t *d_gs,
+                           const uint32_t *d_ge, const uint32_t *d_row, uint32_t min_width,
+                           uint32_t max_width, int32_t has_zero_width, lime_set **out) {
+    return concat_sorted(ctx, set, 0, nullptr, nullptr, nullptr, n, d_gs, d_ge, d_row, min_width,
+                         max_width, has_zero_width, out);
+}
+
+int lime_set_concat_sorted(lime_ctx *ctx, const lime_set *set, int64_t n_before,
+                           const uint32_t *b_gs, const uint32_t *b_ge, const uint32_t *b_row,
+                           int64_t n_after, const uint32_t *a_gs, const uint32_t *a_ge,
+                           const uint32_t *a_row, uint32_t min_width, uint32_t max_width,
+                           int32_t has_zero_width, lime_set **out) {
+    return concat_sorted(ctx, set, n_before, b_gs, b_ge, b_row, n_after, a_gs, a_ge, a_row,
+                         min_width, max_width, has_zero_width, out);
 }
 
 int lime_set_create_global(lime_ctx *ctx, const lime_space *sp, int64_t n, const uint32_t *d_gs,
@@ -1400,6 +1475,14 @@ int lime_route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_
     hipSetDevice(ctx->device);
     return route_rows(ctx, sp, n, d_contig, d_start, d_end, row_base, n_shards, splits, clip, cap,
                       d_gs, d_ge, d_row, counts, d_strand_in, d_strand_out);
+}
+
+int lime_sample_starts(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                       const uint32_t *d_start, int32_t k, uint32_t *d_out) {
+    if (!ctx || !sp || n < 0 || k < 0 || (n > 0 && k > 0 && (!d_start || !d_out)))
+        return fail(LIME_ERR_ARG, "bad sample arguments");
+    hipSetDevice(ctx->device);
+    return sample_starts(ctx, sp, n, d_contig, d_start, k, d_out);
 }
 
 static lime_result *bitset_result(lime_ctx *ctx, const lime_bitset *b) {

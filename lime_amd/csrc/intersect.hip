@@ -390,16 +390,11 @@ constexpr int FW = FB / 64;
 // LDS partner window (16 B records): 1792 rows keep 3 workgroups per CU
 constexpr int PCAP = LIME_FILL_WGS >= 3 ? 1792 : 2048;
 // Two-tile commits (sparse plans) keep the window as three u32 arrays so
-// that 2048 owners + 2560 partners still fit two workgroups per CU
+// that 2048 owners + 2496 partners still fit two workgroups per CU
 constexpr int PCAP2 = 2496;
 #ifndef LIME_FILL_SPARSE
 // mean pairs per owner below which a plan fills two owner tiles per commit
 #define LIME_FILL_SPARSE 16
-#endif
-#ifndef LIME_FILL_SPARSE_EMIT
-// two-tile commits resolve owners wave-wide (emit_sparse): 2 = by LDS slots
-// and a DPP prefix max, 1 = by a shuffle search, 0 = the owner walk of emit
-#define LIME_FILL_SPARSE_EMIT 2
 #endif
 constexpr int64_t GR = 1ll << 40;  // wave granule: default one equal chunk per wave
 
@@ -590,16 +585,12 @@ __device__ __forceinline__ void emit(const FillArgs &fa, const StreamArgs &sa, i
 
 // Sparse plans (a few pairs per owner): the 64 outputs of a wave iteration
 // span ~16 owners, a walk of ~16 dependent LDS steps per lane.  Here the
-// wave resolves them at once: lane j reads the offset of owner qa + 1 + j
-// (qa: the owner of the iteration's first output), and every lane counts the
-// offsets <= its own output by a 7-step binary search over the lanes
-// (shuffles; the offsets ascend over the lanes) -- one LDS read and seven
-// shuffles per iteration, then the owner, partner and store as in emit.
-// (LIME_FILL_SPARSE_EMIT 2) Each owner starting inside the window marks
+// wave resolves them at once: each owner starting inside the window marks
 // its output slot with an LDS max of its index (the last of owners with no
 // pairs, sharing a slot, wins), and a DPP prefix max over the 64 slots gives
-// every lane its owner: three LDS operations and no dependent search.
-// wslot: the wave's 64 LDS words.
+// every lane its owner: three LDS operations and no dependent search (a
+// 7-step shuffle search over the owners' offsets took the 1e9-row fill 23.7
+// ms, the slots 20.8: DESIGN.md section 9).  wslot: the wave's 64 LDS words.
 template <bool LDSP, bool CKSUM, bool WIN, int TPF>
 __device__ __forceinline__ void emit_sparse(const FillArgs &fa, const StreamArgs &sa, int st,
                                             const uint2 *s_lo_off, const u32x4 *s_own,
@@ -610,31 +601,19 @@ __device__ __forceinline__ void emit_sparse(const FillArgs &fa, const StreamArgs
     u32x4 *out = fa.out + (tbase - fa.first);
     for (int64_t ob = gb; ob < gend; ob += 64) {  // (uniform)
         const uint32_t o0 = (uint32_t)ob;
-        int cnt = 0, adv = 0;
-        if (LIME_FILL_SPARSE_EMIT == 2) wslot[lane] = 0u;
+        int adv = 0;
+        wslot[lane] = 0u;
         for (int qb = qa + 1;; qb += 64) {  // (uniform; one round unless > 64 owners)
             const int qj = qb + (int)lane;
             // > 0: owners past qa start after o0
             const uint32_t rel = qj <= qmax ? s_lo_off[qj].y - o0 : 0xffffffffu;
-            if (LIME_FILL_SPARSE_EMIT == 2) {
-                if (rel < 64u) atomicMax(&wslot[rel], (uint32_t)qj + 1u);
-            } else {
-                int c = __shfl(rel, 63) <= lane ? 64 : 0;
-#pragma unroll
-                for (int step = 32; step > 0; step >>= 1) {
-                    const uint32_t v = __shfl(rel, min(c + step - 1, 63));
-                    if (c < 64 && v <= lane) c += step;
-                }
-                cnt += c;
-            }
+            if (rel < 64u) atomicMax(&wslot[rel], (uint32_t)qj + 1u);
             const uint64_t m = __ballot(rel <= 64u);
             adv += __popcll(m);  // owners starting by o0 + 64: the next iteration's qa
             if (m != ~0ull) break;
         }
-        if (LIME_FILL_SPARSE_EMIT == 2) {
-            const uint32_t mx = dev::wave_inclusive_max(wslot[lane]);
-            cnt = mx ? (int)mx - 1 - qa : 0;
-        }
+        const uint32_t mx = dev::wave_inclusive_max(wslot[lane]);
+        const int cnt = mx ? (int)mx - 1 - qa : 0;
         const int64_t o = ob + lane;
         if (o < gend) {
             const int q = qa + cnt;
@@ -698,6 +677,11 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
     __shared__ uint32_t s_wslot[TPF > 1 ? FW : 1][64];  // emit_sparse's owner slots
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_red[2][FW];
+    // (every shared array above counts: one more pushes k_fill<2> below
+    // LIME_FILL_WGS workgroups per CU)
+    static_assert(sizeof(s_lo_off) + sizeof(s_own) + sizeof(s_par) + sizeof(s_wslot) +
+                          sizeof(s_tile) + sizeof(s_red) <= 160 * 1024 / LIME_FILL_WGS,
+                  "k_fill's LDS must keep LIME_FILL_WGS workgroups per CU");
 
     const int64_t ob = fa.first + (int64_t)blockIdx.x * per;
     const int64_t oend = min(fa.first + fa.count, ob + per);
@@ -771,7 +755,7 @@ __global__ __launch_bounds__(FB, 2 * LIME_FILL_WGS) void k_fill(FillArgs fa, int
             // lane then walks to its own owner
             qw = wave_owner_of(s_lo_off, qw, nown, (uint32_t)gb);
             int q = qw;
-            if (TPF > 1 && LIME_FILL_SPARSE_EMIT) {
+            if (TPF > 1) {
                 uint32_t *wslot = s_wslot[TPF > 1 ? w : 0];
                 if (par_lds)
                     emit_sparse<true, CKSUM, WIN, TPF>(fa, sa, st, s_lo_off, s_own, s_par, wlo,

@@ -158,7 +158,35 @@ __global__ void k_route_totals(const uint32_t *__restrict__ mat, uint32_t nblk, 
     if (d <= nsh) out[d] = mat[(int64_t)d * nblk];
 }
 
+// k evenly spaced rows' global starts (row i * n / k), for count-balanced
+// splitters (dist.sample_splits): d_contig == NULL: d_start is global
+__global__ void k_sample_starts(const int32_t *__restrict__ contig,
+                                const uint32_t *__restrict__ start,
+                                const uint32_t *__restrict__ off, int32_t nc, int64_t n, int32_t k,
+                                uint32_t *__restrict__ out) {
+    const int32_t j = (int32_t)(blockIdx.x * 256 + threadIdx.x);
+    if (j >= k) return;
+    const int64_t i = (int64_t)j * n / k;
+    uint32_t g = start[i];
+    if (contig) {
+        const int32_t c = contig[i];
+        g += (c >= 0 && c < nc) ? off[c] : 0u;  // (routing validates the row itself)
+    }
+    out[j] = g;
+}
+
 }  // namespace
+
+int sample_starts(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
+                  const uint32_t *d_start, int32_t k, uint32_t *d_out) {
+    if (k <= 0 || n <= 0) return LIME_OK;
+    const uint32_t *d_off = nullptr, *d_len = nullptr;
+    if (d_contig) LIME_TRY(space_device(ctx, sp->off, &d_off, &d_len));
+    hipLaunchKernelGGL(k_sample_starts, dim3(blocks_for(k, 256)), dim3(256), 0, S(ctx), d_contig,
+                       d_start, d_off, (int32_t)sp->n, n, k, d_out);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
 
 int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,

@@ -23,6 +23,8 @@
 // kernel that builds gs / ge / row from the caller's (contig, start, end).
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace lime {
 namespace {
 
@@ -56,7 +58,8 @@ enum { M_GS = 0, M_NZ = 1, M_GE = 2, M_ST = 3, M_RW = 4 };
 // identity (the first pass of a set built from caller rows: row = position)
 enum { ROWS_NONE = 0, ROWS_LOAD = 1, ROWS_IDENT = 2 };
 
-template <int M>
+// DB: digit bits of a GS pass (8; 9 for the bucketed sort's wider passes)
+template <int M, int DB = 8>
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, uint32_t r, int shift,
                                              const int8_t *st) {
     if (M == M_NZ) return e > k ? 1u : 0u;
@@ -65,11 +68,11 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t k, uint32_t e, uint32_t r,
     // bdg-formats' enum ordinal: FORWARD, REVERSE, INDEPENDENT, UNKNOWN
     if (M == M_ST) return (0xd2u >> (2 * ((uint32_t)(uint8_t)st[r] & 3u))) & 3u;
     if (M == M_RW) return (r >> shift) & (RBINS - 1);
-    return (k >> shift) & (RBINS - 1);
+    return (k >> shift) & ((1u << DB) - 1u);
 }
 
 // lanes of the wave holding the same digit (among `valid` lanes)
-template <int M>
+template <int M, int DB = 8>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     uint64_t m = __ballot(valid);
     if (M == M_ST) {
@@ -86,7 +89,7 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
         return m & ((d & 1u) ? b : ~b);
     }
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < DB; ++b) {
         uint32_t bit = (d >> b) & 1u;
         uint64_t bb = __ballot(bit);
         m &= bit ? bb : ~bb;
@@ -108,9 +111,10 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t ntiles) {
 
 // (tile = the block's tile: consecutive tiles on one XCD, so the digit-major
 // column stores of neighbouring tiles complete each other's lines in its L2)
-__device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *counts,
+template <int BINS>
+__device__ __forceinline__ void flush_hist(uint32_t (*hist)[BINS], uint32_t *counts,
                                            uint32_t ntiles, uint32_t tile) {
-    for (int d = threadIdx.x; d < RBINS; d += RB) {
+    for (int d = threadIdx.x; d < BINS; d += RB) {
         uint32_t t = 0;
 #pragma unroll
         for (int ww = 0; ww < RWAVES; ++ww) t += hist[ww][d];
@@ -130,7 +134,7 @@ __device__ __forceinline__ void flush_hist(uint32_t (*hist)[RBINS], uint32_t *co
 // LC: the contig table (<= PCMAX contigs) is staged in LDS, so the per-row
 // off / len gathers are LDS reads rather than dependent cache round trips
 constexpr int PCMAX = 1024;
-template <bool GLOBAL, bool WRITE = true, bool LC = false>
+template <bool GLOBAL, bool WRITE = true, bool LC = false, int DB = 8>
 __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              const uint32_t *__restrict__ start,
                                              const uint32_t *__restrict__ end,
@@ -141,10 +145,11 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              SetStats *__restrict__ part,
                                              uint32_t *__restrict__ counts, uint32_t ntiles,
                                              int hshift) {
-    __shared__ uint32_t hist[RWAVES][RBINS];
+    constexpr int BINS = 1 << DB;
+    __shared__ uint32_t hist[RWAVES][BINS];
     __shared__ SetStats ws[RWAVES];
     __shared__ uint32_t s_off[LC ? PCMAX : 1], s_len[LC ? PCMAX : 1];
-    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < RWAVES * BINS; i += RB) (&hist[0][0])[i] = 0;
     if (LC) {
         for (int i = threadIdx.x; i < n_contigs; i += RB) {
             s_off[i] = goff[i];
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
-        if (valid[k]) atomicAdd(&hist[w][(vk[k] >> hshift) & (RBINS - 1)], 1u);
+        if (valid[k]) atomicAdd(&hist[w][(vk[k] >> hshift) & (BINS - 1)], 1u);
     err = dev::wave_reduce_or(err);
     mx = dev::wave_reduce_max(mx);
     mnw = dev::wave_reduce_min(mnw);
@@ -384,15 +389,16 @@ __global__ __launch_bounds__(256) void k_stats(const SetStats *__restrict__ part
     }
 }
 
-template <int M>
+template <int M, int DB = 8>
 __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
                                              const uint32_t *__restrict__ ge,
                                              const uint32_t *__restrict__ row, int64_t n, int shift,
                                              const int8_t *__restrict__ st,
                                              uint32_t *__restrict__ counts, uint32_t ntiles,
                                              int rows) {
-    __shared__ uint32_t hist[RWAVES][RBINS];
-    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&hist[0][0])[i] = 0;
+    constexpr int BINS = M == M_GS ? 1 << DB : RBINS;
+    __shared__ uint32_t hist[RWAVES][BINS];
+    for (int i = threadIdx.x; i < RWAVES * BINS; i += RB) (&hist[0][0])[i] = 0;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const uint32_t tile = xcd_swizzle(blockIdx.x, ntiles);
     const int64_t base = (int64_t)tile * RTILE + w * WITEMS;
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     // ranks (190 -> 104 us per 1e8-row pass)
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
-        if (valid[k]) atomicAdd(&hist[w][digit_of<M>(vk[k], ve[k], vr[k], shift, st)], 1u);
+        if (valid[k]) atomicAdd(&hist[w][digit_of<M, DB>(vk[k], ve[k], vr[k], shift, st)], 1u);
     __syncthreads();
     flush_hist(hist, counts, ntiles, tile);
 }
@@ -453,8 +459,13 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
 // u16 (10 B per row and pass instead of 12): the first pass turns ends into
 // widths (EW_TO16), the middle ones move widths (EW_16), the last turns them
 // back into ends (EW_FROM16, ge = gs + width, gs staged beside it)
+// (RAW passes may start the u16 widths: EW_TO16 from the caller's ends.)
+// DB: digit bits of a GS pass.  9-bit passes (the bucketed sort of dense
+// sets: 512 digits, runs of ~16 rows per digit and tile) keep their per-wave
+// digit counters as u16 and the RAW contig table aliased onto the staging
+// array, so two workgroups still fit a CU (~76 KiB LDS each)
 enum { EW_32 = 0, EW_TO16 = 1, EW_16 = 2, EW_FROM16 = 3 };
-template <int M, int ROWS, bool RAW = false, int EW = EW_32>
+template <int M, int ROWS, bool RAW = false, int EW = EW_32, int DB = 8>
 // 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
 __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
                                                 const uint32_t *__restrict__ ge_in,
@@ -466,21 +477,28 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
                                                 uint32_t *__restrict__ row_out,
                                                 const uint32_t *__restrict__ off = nullptr,
                                                 int32_t nc = 0) {
-    __shared__ uint32_t cnt[RWAVES][RBINS];
+    constexpr int BINS = M == M_GS ? 1 << DB : RBINS;
+    static_assert(M == M_GS || DB == 8, "wider digits: GS passes only");
+    using CT = typename std::conditional<(DB > 8), uint16_t, uint32_t>::type;
+    __shared__ CT cnt[RWAVES][BINS];
+    __shared__ uint32_t dstart[BINS];
+    __shared__ uint32_t gbase[BINS];
+    __shared__ uint32_t scratch[RWAVES + 1];
+    constexpr bool ALL3 = M != M_GS;  // digit not recomputable from the key alone
+    static_assert(EW == EW_32 || M == M_GS, "u16 widths: GS passes only");
+    static_assert(!RAW || EW == EW_32 || EW == EW_TO16, "a RAW pass reads the caller's ends");
+    __shared__ uint32_t sk[RTILE], se[RTILE], sr[ALL3 ? RTILE : 1];
     // RAW: the contig table staged in LDS (<= PCMAX contigs), so the per-row
-    // off[contig] gather is an LDS read, not a dependent cache round trip
-    __shared__ uint32_t s_off[RAW ? PCMAX : 1];
+    // off[contig] gather is an LDS read, not a dependent cache round trip.
+    // It lives in se: its lookups all precede the barrier after the loads,
+    // and se is written only after two more
+    static_assert(PCMAX <= RTILE, "contig table within the staging array");
+    uint32_t *s_off = se;
     if (RAW && nc <= PCMAX)  // (its barrier follows the tile's loads)
         for (int i = threadIdx.x; i < nc; i += RB) s_off[i] = off[i];
     const uint32_t *offp = RAW && nc <= PCMAX ? s_off : off;
-    __shared__ uint32_t dstart[RBINS];
-    __shared__ uint32_t gbase[RBINS];
-    __shared__ uint32_t scratch[RWAVES + 1];
-    constexpr bool ALL3 = M != M_GS;  // digit not recomputable from the key alone
-    static_assert(EW == EW_32 || (M == M_GS && !RAW), "u16 widths: GS passes only");
-    __shared__ uint32_t sk[RTILE], se[RTILE], sr[ALL3 ? RTILE : 1];
 
-    for (int i = threadIdx.x; i < RWAVES * RBINS; i += RB) (&cnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < RWAVES * BINS; i += RB) (&cnt[0][0])[i] = 0;
 
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     // XCD-aware tile order: consecutive tiles run on one XCD, so the partial
@@ -532,6 +550,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
             const uint32_t o = offp[vr[k]];  // (vr = 0 for invalid rows: in range)
             vk[k] += o;
             ve[k] += o;
+            if (EW == EW_TO16) ve[k] -= vk[k];  // (< 2^16: checked by the caller)
             vr[k] = 0u;
         }
     }
@@ -539,28 +558,29 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k) {
         const bool valid = k * 64 + lane < lim;
-        const uint32_t d = valid ? digit_of<M>(vk[k], ve[k], vr[k], shift, st) : 0u;
-        const uint64_t m = match_digit<M>(d, valid);
+        const uint32_t d = valid ? digit_of<M, DB>(vk[k], ve[k], vr[k], shift, st) : 0u;
+        const uint64_t m = match_digit<M, DB>(d, valid);
         const uint32_t rank = (uint32_t)__popcll(m & dev::lanemask_lt());
-        const uint32_t old = valid ? cnt[w][d] : 0u;
-        pd[k] = ((old + rank) << 8) | d;
-        if (valid && rank == 0) cnt[w][d] = old + (uint32_t)__popcll(m);
+        const uint32_t old = valid ? (uint32_t)cnt[w][d] : 0u;
+        pd[k] = ((old + rank) << DB) | d;
+        if (valid && rank == 0) cnt[w][d] = (CT)(old + (uint32_t)__popcll(m));
     }
     __syncthreads();
     // per digit: block offset of the digit, then per-wave offsets
+    static_assert(BINS <= RB, "one digit per thread in the offset scan");
     {
         const int d = threadIdx.x;
         uint32_t tot = 0;
-        if (d < RBINS)
+        if (d < BINS)
             for (int ww = 0; ww < RWAVES; ++ww) tot += cnt[ww][d];
         uint32_t all;
         const uint32_t ds = dev::block_exclusive_sum<RB>(tot, scratch, &all);
-        if (d < RBINS) {
+        if (d < BINS) {
             dstart[d] = ds;
             uint32_t run = ds;
             for (int ww = 0; ww < RWAVES; ++ww) {
                 const uint32_t c = cnt[ww][d];
-                cnt[ww][d] = run;
+                cnt[ww][d] = (CT)run;
                 run += c;
             }
             gbase[d] = base_mat[(int64_t)d * ntiles + tile];
@@ -572,7 +592,8 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     uint32_t *lp = pd;  // local position within the tile, in place
 #pragma unroll
     for (int k = 0; k < RITEMS; ++k)
-        lp[k] = k * 64 + lane < lim ? cnt[w][pd[k] & 0xffu] + (pd[k] >> 8) : 0xffffffffu;
+        lp[k] = k * 64 + lane < lim ? (uint32_t)cnt[w][pd[k] & (BINS - 1)] + (pd[k] >> DB)
+                                    : 0xffffffffu;
     if (ALL3) {  // digit needs (key, end, row): stage all three arrays at once
 #pragma unroll
         for (int k = 0; k < RITEMS; ++k)
@@ -600,7 +621,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
         const uint32_t k = sk[j];
-        const uint32_t d = digit_of<M>(k, 0u, 0u, shift, st);
+        const uint32_t d = digit_of<M, DB>(k, 0u, 0u, shift, st);
         key_out[gbase[d] + (uint32_t)j - dstart[d]] = k;
     }
 #pragma unroll
@@ -608,7 +629,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         if (lp[k] != 0xffffffffu) se[lp[k]] = ve[k];
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
+        const uint32_t d = digit_of<M, DB>(sk[j], 0u, 0u, shift, st);
         const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
         if (EW == EW_TO16 || EW == EW_16)
             reinterpret_cast<uint16_t *>(ge_out)[g] = (uint16_t)se[j];
@@ -623,7 +644,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
             se[lp[k]] = ROWS == ROWS_IDENT ? (uint32_t)(base + k * 64 + lane) : vr[k];
     __syncthreads();
     for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t d = digit_of<M>(sk[j], 0u, 0u, shift, st);
+        const uint32_t d = digit_of<M, DB>(sk[j], 0u, 0u, shift, st);
         row_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
     }
 }
@@ -731,6 +752,7 @@ struct LocalArgs {
     const uint32_t *k0, *e0, *r0;  // rows grouped by gs >> L
     const uint32_t *start;         // nb + 1 bucket starts
     int L;
+    int zb;                        // k_local_mid: 1 if the set has zero-width rows
     uint32_t *k1, *e1, *r1;        // the sorted set
     unsigned int *nover;           // [0] listed buckets, [1] the big kernel's ticket
     uint32_t *over;                // listed bucket ids
@@ -955,9 +977,9 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
 // a bucket's rows into registers, branch-free (positions past the bucket
 // clamped to its last row; a bucket too large for the shape, or empty, loads
 // row 0): every load issued before any is used
-template <int NT, int ITEMS, int CAP>
+template <int NT, int ITEMS, int CAP, bool LR = true>
 struct BucketRegs {
-    uint32_t g[ITEMS], e[ITEMS], r[ITEMS];
+    uint32_t g[ITEMS], e[ITEMS], r[LR ? ITEMS : 1];
     uint32_t s0, m;
     // start: the bucket starts (a.start; the persistent kernel passes them as
     // a restrict argument, read at its wave-uniform bucket index by scalar
@@ -982,7 +1004,7 @@ struct BucketRegs {
             const uint32_t q = base + (ok ? min(pos, m - 1) : 0u);
             g[it] = a.k0[q];
             e[it] = a.e0[q];
-            r[it] = a.r0[q];
+            if (LR) r[it] = a.r0[q];  // (LR = false: gathered at the end)
         }
     }
 };
@@ -1013,6 +1035,164 @@ void k_local_small(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start)
         if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
         cur = nxt;
+    }
+}
+
+// Buckets of a few thousand rows (the bucketed sort of dense sets: 9-bit
+// digit passes, 2^14-base buckets of ~2.6k rows at C3's density): a claim
+// sort over sub-bins of ONE local key each (u16 cursors, two per LDS word:
+// 2^SBB of them in 2^(SBB - 1) words).
+//   1. every row's key k = (gs mod 2^L) << zb | (non-zero width), zb = 1
+//      when the set has zero-width rows (else the bit is constant and left
+//      out, so 2^14-base buckets need only 2^14 sub-bins);
+//   2. a histogram of the sub-bins k >> sh (sh = 0 whenever the key fits);
+//   3. one block scan of the counts: each cursor at its sub-bin's start;
+//   4. each row claims a slot of its sub-bin (one returning LDS atomic): a
+//      row alone in its sub-bin (most rows) has its rank -- the slot;
+//   5. rows sharing a sub-bin (equal starts, or sh > 0) count the entries
+//      below their unique u = k << POSB | position (the stable order);
+//   6. the outputs leave in three rounds through T (gs, ge, row written at
+//      their ranks, stored coalesced).
+// Every row's rank stays in a register: no per-slot pass, no rank table.
+// A sub-bin past SMAX rows (a pile of identical starts) sends the bucket to
+// k_local_big.
+template <int NT, int ITEMS, int POSB, int SBB>
+__device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0, uint32_t m,
+                                                 const uint32_t (&g)[ITEMS],
+                                                 const uint32_t (&e)[ITEMS],
+                                                 const uint32_t (&rw)[ITEMS], uint32_t *T,
+                                                 uint32_t *cw, uint32_t *scratch) {
+    constexpr int NWD = 1 << (SBB - 1), SPW = NWD / NT;  // cursor words, per thread
+    static_assert(NWD % NT == 0 && SPW == 16, "16 cursor words per thread (padded layout)");
+    static_assert(NT * ITEMS <= (1 << POSB) && NT * ITEMS < 65536, "positions / ranks");
+    constexpr int NW = NT / 64;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const int nit = (int)((m + NW * 64 - 1) / (NW * 64));
+    const int c = nit * 64;
+    const uint32_t lmask = (1u << a.L) - 1u;
+    const int zb = a.zb;
+    const int kb = a.L + zb;                 // local key bits
+    const int sh = kb > SBB ? kb - SBB : 0;  // sub-bin = key >> sh
+    // cursor word i lives at i + i / 16: a thread's 16 words (its share of
+    // the scan) then start 17 words after its neighbour's -- every lane in
+    // its own bank (at 16 words apart, 16 lanes shared each bank)
+    auto pw = [](uint32_t i) { return i + (i >> 4); };
+    uint32_t *mine = cw + 17 * threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) mine[q] = 0u;
+    __syncthreads();
+    uint32_t u[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
+        u[it] = 0xffffffffu;
+        if (it < nit && pos < m) {
+            const uint32_t k = ((g[it] & lmask) << zb) | (e[it] > g[it] ? (uint32_t)zb : 0u);
+            u[it] = (k << POSB) | pos;
+            const uint32_t sb = k >> sh;
+            atomicAdd(&cw[pw(sb >> 1)], 1u << ((sb & 1u) << 4));
+        }
+    }
+    __syncthreads();
+    uint32_t cv[SPW], csum = 0, cmax = 0;
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) cv[q] = mine[q];
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) {
+        const uint32_t lo = cv[q] & 0xffffu, hi = cv[q] >> 16;
+        csum += lo + hi;
+        cmax = max(cmax, max(lo, hi));
+    }
+    uint32_t tot;
+    uint32_t st = dev::block_exclusive_sum<NT>(csum, scratch, &tot);
+    const uint32_t mx = dev::wave_reduce_max(cmax);
+    if (lane == 0) scratch[NW + 1 + w] = mx;  // (past the scan's NW + 1 words)
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) {
+        const uint32_t lo = cv[q] & 0xffffu, hi = cv[q] >> 16;
+        cv[q] = st | (st + lo) << 16;
+        st += lo + hi;
+    }
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) mine[q] = cv[q];
+    __syncthreads();
+    uint32_t big = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) big = max(big, scratch[NW + 1 + i]);
+    if (big > (uint32_t)SMAX) {  // (uniform: every thread read the same words)
+        __syncthreads();
+        return false;
+    }
+    uint32_t rk[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        rk[it] = 0xffffffffu;
+        if (u[it] != 0xffffffffu) {
+            const uint32_t sb = (u[it] >> POSB) >> sh, sft = (sb & 1u) << 4;
+            rk[it] = (atomicAdd(&cw[pw(sb >> 1)], 1u << sft) >> sft) & 0xffffu;
+            T[rk[it]] = u[it];
+        }
+    }
+    __syncthreads();
+    // rows sharing a sub-bin: their rank among its entries (after the claims
+    // each cursor is its sub-bin's end)
+    uint32_t dup = 0;
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        if (u[it] == 0xffffffffu) continue;
+        const uint32_t sb = (u[it] >> POSB) >> sh;
+        const uint32_t hi = (cw[pw(sb >> 1)] >> ((sb & 1u) << 4)) & 0xffffu;
+        const uint32_t lo = sb ? (cw[pw((sb - 1) >> 1)] >> (((sb - 1) & 1u) << 4)) & 0xffffu : 0u;
+        if (hi - lo > 1) {
+            uint32_t r = lo;
+            for (uint32_t j = lo; j < hi; ++j) r += T[j] < u[it] ? 1u : 0u;
+            rk[it] = r;
+        }
+    }
+#ifdef LIME_MID_EXP_IDENT
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it)  // (timing experiment: identity output order)
+        if (rk[it] != 0xffffffffu) rk[it] = u[it] & ((1u << POSB) - 1u);
+#endif
+#pragma unroll
+    for (int round = 0; round < 3; ++round) {
+        __syncthreads();  // (T free: ranks taken / the previous round stored)
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (rk[it] != 0xffffffffu) T[rk[it]] = round == 0 ? g[it] : round == 1 ? e[it] : rw[it];
+        __syncthreads();
+        uint32_t *dst = round == 0 ? a.k1 : round == 1 ? a.e1 : a.r1;
+        for (uint32_t q = threadIdx.x; q < m; q += NT) dst[s0 + q] = T[q];
+    }
+    return true;
+}
+
+// Persistent, MID_WGS workgroups per CU (the others overlap one bucket's
+// loads with another's sort): buckets of up to LCAP_M rows; larger ones, or
+// with a sub-bin past SMAX rows, are listed for k_local_big.
+#ifndef LIME_MID_SBB
+#define LIME_MID_SBB 14
+#endif
+#ifndef LIME_MID_WGS
+#define LIME_MID_WGS 2
+#endif
+constexpr int LNT_M = 512, LPOS_M = 13, LCAP_M = 6144, LSBB_M = LIME_MID_SBB;  // 12 items / thread
+constexpr int MID_WGS = LIME_MID_WGS;
+using MidRegs = BucketRegs<LNT_M, LCAP_M / LNT_M, LCAP_M>;
+__global__ __launch_bounds__(LNT_M) __attribute__((amdgpu_waves_per_eu(2 * MID_WGS, 8)))
+void k_local_mid(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) {
+    __shared__ uint32_t T[LCAP_M];
+    __shared__ uint32_t cw[(1 << (LSBB_M - 1)) + (1 << (LSBB_M - 5))];  // (padded: 1 per 16)
+    __shared__ uint32_t scratch[2 * (LNT_M / 64) + 1];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        MidRegs cur;
+        cur.load(a, b, nb, start);
+        bool listed = cur.m > (uint32_t)LCAP_M;
+        if (!listed && cur.m > 0)
+            listed = !bucket_sort_keys<LNT_M, LCAP_M / LNT_M, LPOS_M, LSBB_M>(
+                a, cur.s0, cur.m, cur.g, cur.e, cur.r, T, cw, scratch);
+        if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
+        __syncthreads();  // (the next bucket overwrites the staging)
     }
 }
 
@@ -1148,15 +1328,79 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
                          d_len);
 }
 
-// the bucketed sort's choice: 2^L-base buckets under two 8-bit digit passes
-// (L = bits - 16), averaging LMIN to LAVG rows (else the digit passes):
-// most buckets in k_local_small.  (Denser sets through k_local_big, one
-// workgroup per CU: C3's 5e8 pile-up rows, ~10.6k per bucket, took 7.0 ms
-// there -- sort 14.6 ms against 13.0 with the four digit passes.)
+// the bucketed sort's choice: 2^L-base buckets under two digit passes of TB
+// bits in all (L = bits - TB): 8 + 8 with buckets averaging LMIN to LAVG rows
+// (k_local_small), else 9 + 8 or 9 + 9 with buckets averaging at most LAVG_M
+// rows (k_local_mid: C3's 5e8 pile-up rows, ~2.65k per 2^14-base bucket);
+// denser sets take the digit passes.  (8 + 8 with C3's ~10.6k rows per
+// bucket through k_local_big, one workgroup per CU, took 7.0 ms there.)
 #ifndef LIME_SORT_W16
 #define LIME_SORT_W16 1
 #endif
-constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4;
+#ifndef LIME_SORT_TBMAX
+#define LIME_SORT_TBMAX 18
+#endif
+constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4, LAVG_M = LCAP_M / 2;
+
+// the (validate-only) prep of the bucketed sort, histogramming a DB-bit digit
+template <int DB>
+void launch_prep_nowrite(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
+                         const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_len,
+                         int64_t n, SetStats *part, uint32_t *mat, uint32_t ntiles, int hshift) {
+    if (global)
+        hipLaunchKernelGGL((k_prep<true, false, false, DB>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                           d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                           set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles, hshift);
+    else if (set->n_contigs <= PCMAX)
+        hipLaunchKernelGGL((k_prep<false, false, true, DB>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                           d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                           set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles, hshift);
+    else
+        hipLaunchKernelGGL((k_prep<false, false, false, DB>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                           d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                           set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles, hshift);
+}
+
+// the bucketed sort's two digit passes: pass 1 (DB1 bits at L) from the
+// caller's rows (histogrammed by the prep), pass 2 (DB2 bits at L + DB1);
+// with u16 widths (every width < 2^16) pass 1 writes widths, pass 2 ends
+template <int DB1, int DB2>
+int bucket_passes(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
+                  const uint32_t *d_start, const uint32_t *d_end, int64_t n, int L, bool w16,
+                  uint32_t *mat, uint32_t ntiles, uint32_t *const (&a)[3], uint32_t *const (&o)[3]) {
+    LIME_TRY(scan_exclusive_u32(ctx, mat, mat, ((int64_t)1 << DB1) * ntiles, nullptr));
+    const uint32_t *kc = reinterpret_cast<const uint32_t *>(d_contig);
+    const int8_t *nost = nullptr;
+    const uint32_t *cm = mat;
+    if (global && w16)
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_TO16, DB1>), dim3(ntiles), dim3(RB),
+                           0, S(ctx), kc, d_start, d_end, n, L, nost, cm, ntiles, a[0], a[1], a[2]);
+    else if (global)
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_32, DB1>), dim3(ntiles), dim3(RB),
+                           0, S(ctx), kc, d_start, d_end, n, L, nost, cm, ntiles, a[0], a[1], a[2]);
+    else if (w16)
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, true, EW_TO16, DB1>), dim3(ntiles),
+                           dim3(RB), 0, S(ctx), kc, d_start, d_end, n, L, nost, cm, ntiles, a[0],
+                           a[1], a[2], (const uint32_t *)set->d_off, set->n_contigs);
+    else
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, true, EW_32, DB1>), dim3(ntiles),
+                           dim3(RB), 0, S(ctx), kc, d_start, d_end, n, L, nost, cm, ntiles, a[0],
+                           a[1], a[2], (const uint32_t *)set->d_off, set->n_contigs);
+    LIME_HIP(hipGetLastError());
+    hipLaunchKernelGGL((k_hist<M_GS, DB2>), dim3(ntiles), dim3(RB), 0, S(ctx), a[0], a[1], a[2], n,
+                       L + DB1, nost, mat, ntiles, (int)ROWS_LOAD);
+    LIME_TRY(scan_exclusive_u32(ctx, mat, mat, ((int64_t)1 << DB2) * ntiles, nullptr));
+    if (w16)
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_FROM16, DB2>), dim3(ntiles),
+                           dim3(RB), 0, S(ctx), a[0], a[1], a[2], n, L + DB1, nost, cm, ntiles,
+                           o[0], o[1], o[2]);
+    else
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_32, DB2>), dim3(ntiles), dim3(RB),
+                           0, S(ctx), a[0], a[1], a[2], n, L + DB1, nost, cm, ntiles, o[0], o[1],
+                           o[2]);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
 
 int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
                   const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_len) {
@@ -1168,42 +1412,41 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     const bool keep_rows = set->min_shift == 0;
     const bool stranded = set->strand_in != nullptr;
     const bool row_ties = set->row_ties;  // (gs, ge, row): subtract's tie index
-    LIME_TRY(alloc(ctx, &mat, (size_t)RBINS * (ntiles ? ntiles : 1)));
-    LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
-    LIME_TRY(alloc(ctx, &st, 1));
     // the bucketed sort is a candidate for plain sets whose span needs more
-    // than 16 key bits: its prep then only validates and histograms the
-    // first digit (bits [L, L + 8)), L = bits(span) - 16
+    // than TB key bits: its prep then only validates and histograms the
+    // first digit (bits [L, L + DB1)), L = bits(span) - TB
     // (and rows enough that the buckets average LMIN rows: a workgroup per
     // bucket costs more than the digit passes below that)
     const int64_t span = set->off.empty() ? 0 : (int64_t)set->off.back();
     const int sbits = span > 1 ? 64 - __builtin_clzll((uint64_t)(span - 1)) : 1;
-    // (and few enough that they average at most LAVG over the span: denser
-    // sets, e.g. C3's 5e8 rows, take the digit passes, decided before the
-    // prep so it runs once -- a validate-only prep then a writing one cost
-    // C3 1.4 ms)
-    const int64_t nb_span = (span >> (sbits - 16)) + 1;
-    const bool bucket_cand = keep_rows && !stranded && !row_ties && sbits > 16 &&
-                             n >= LMIN * nb_span && n <= LAVG * nb_span;
-    const int hshift = bucket_cand ? sbits - 16 : set->min_shift;
+    // (and few enough that they average at most LAVG / LAVG_M over the span:
+    // denser sets take the digit passes, decided before the prep so it runs
+    // once -- a validate-only prep then a writing one cost C3 1.4 ms)
+    int TB = 0;
+    if (keep_rows && !stranded && !row_ties)
+        for (int tb = 16; tb <= LIME_SORT_TBMAX && sbits - tb >= 1; ++tb) {
+            const int64_t nbs = (span >> (sbits - tb)) + 1;
+            if (n < LMIN * nbs) break;  // (sparser still at more digit bits)
+            if (n <= (tb == 16 ? LAVG : LAVG_M) * nbs) {
+                TB = tb;
+                break;
+            }
+        }
+    const bool bucket_cand = TB != 0;
+    const int DB1 = TB - TB / 2, DB2 = TB / 2;  // 8 + 8, 9 + 8, 9 + 9
+    LIME_TRY(alloc(ctx, &mat, ((size_t)1 << (bucket_cand ? DB1 : 8)) * (ntiles ? ntiles : 1)));
+    LIME_TRY(alloc(ctx, &part, (size_t)(ntiles ? ntiles : 1)));
+    LIME_TRY(alloc(ctx, &st, 1));
+    const int hshift = bucket_cand ? sbits - TB : set->min_shift;
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
     if (n > 0) {
         if (bucket_cand) {  // validate + statistics + histogram only
-            if (global)
-                hipLaunchKernelGGL((k_prep<true, false>), dim3(ntiles), dim3(RB), 0, S(ctx),
-                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                                   set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles,
-                                   hshift);
-            else if (set->n_contigs <= PCMAX)
-                hipLaunchKernelGGL((k_prep<false, false, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
-                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                                   set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles,
-                                   hshift);
+            if (DB1 == 9)
+                launch_prep_nowrite<9>(ctx, set, global, d_contig, d_start, d_end, d_len, n, part,
+                                       mat, ntiles, hshift);
             else
-                hipLaunchKernelGGL((k_prep<false, false>), dim3(ntiles), dim3(RB), 0, S(ctx),
-                                   d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
-                                   set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles,
-                                   hshift);
+                launch_prep_nowrite<8>(ctx, set, global, d_contig, d_start, d_end, d_len, n, part,
+                                       mat, ntiles, hshift);
         } else {
             LIME_TRY(alloc(ctx, &k0, (size_t)n));
             LIME_TRY(alloc(ctx, &e0, (size_t)n));
@@ -1249,32 +1492,24 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         // the bucketed sort when the rows are not in order yet and the
         // buckets stay small on average; else materialise (gs, ge, row) the
         // way the digit passes start from
-        const int L = sbits - 16;
+        const int L = sbits - TB;
         const uint32_t nb = (h.max_gs >> L) + 1;
-        if (need && n / (int64_t)nb <= LAVG) {
+        if (need && n / (int64_t)nb <= (TB == 16 ? LAVG : LAVG_M)) {
             uint32_t *a[3], *o[3];
             for (int q = 0; q < 3; ++q) {
                 LIME_TRY(alloc(ctx, &a[q], (size_t)n));
                 LIME_TRY(alloc(ctx, &o[q], (size_t)n));
             }
-            // pass 1 (bits [L, L + 8)) straight from the caller's rows,
-            // histogrammed by k_prep
-            LIME_TRY(scan_exclusive_u32(ctx, mat, mat, (int64_t)RBINS * ntiles, nullptr));
-            if (global)
-                hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD>), dim3(ntiles), dim3(RB), 0, S(ctx),
-                                   reinterpret_cast<const uint32_t *>(d_contig), d_start, d_end,
-                                   n, L, (const int8_t *)nullptr, (const uint32_t *)mat, ntiles,
-                                   a[0], a[1], a[2]);
+            const bool w16 = LIME_SORT_W16 && h.max_width < 65536u;
+            if (TB == 16)
+                LIME_TRY((bucket_passes<8, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
+                                              mat, ntiles, a, o)));
+            else if (TB == 17)
+                LIME_TRY((bucket_passes<9, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
+                                              mat, ntiles, a, o)));
             else
-                hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, true>), dim3(ntiles), dim3(RB), 0,
-                                   S(ctx), reinterpret_cast<const uint32_t *>(d_contig), d_start,
-                                   d_end, n, L, (const int8_t *)nullptr, (const uint32_t *)mat,
-                                   ntiles, a[0], a[1], a[2], (const uint32_t *)set->d_off,
-                                   set->n_contigs);
-            LIME_HIP(hipGetLastError());
-            // pass 2 (bits [L + 8, L + 16))
-            LIME_TRY(radix_pass(ctx, M_GS, L + 8, false, n, a[0], a[1], a[2], nullptr, o[0], o[1],
-                                o[2], mat, ntiles, ROWS_LOAD));
+                LIME_TRY((bucket_passes<9, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
+                                              mat, ntiles, a, o)));
             release(ctx, mat);
             // every bucket sorted locally: (o) -> (a)
             uint32_t *start, *over;
@@ -1292,6 +1527,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             la.k0 = o[0], la.e0 = o[1], la.r0 = o[2];
             la.start = start;
             la.L = L;
+            la.zb = h.has_zero ? 1 : 0;
             la.k1 = a[0], la.e1 = a[1], la.r1 = a[2];
             la.nover = nover;
             la.over = over;
@@ -1299,8 +1535,12 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (cus <= 0) cus = 256;
-            hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)),
-                               dim3(LNT_S), 0, S(ctx), la, nb, (const uint32_t *)start);
+            if (TB == 16)
+                hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)),
+                                   dim3(LNT_S), 0, S(ctx), la, nb, (const uint32_t *)start);
+            else
+                hipLaunchKernelGGL(k_local_mid, dim3(std::min<uint32_t>(nb, (uint32_t)MID_WGS * (uint32_t)cus)),
+                                   dim3(LNT_M), 0, S(ctx), la, nb, (const uint32_t *)start);
             hipLaunchKernelGGL(k_local_big, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B), 0,
                                S(ctx), la);
             LIME_HIP(hipGetLastError());

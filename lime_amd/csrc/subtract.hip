@@ -1326,8 +1326,11 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         LIME_TRY(alloc(ctx, &olo, (size_t)na));
         LIME_TRY(alloc(ctx, &ocnt, (size_t)na));
     }
+    PoolGuard<uint32_t> go1{ctx, olo}, go2{ctx, ocnt};
     LIME_TRY(alloc(ctx, &cnt, (size_t)na + 1));
+    PoolGuard<uint64_t> gc{ctx, cnt};
     LIME_TRY(alloc(ctx, &off, (size_t)na + 1));
+    PoolGuard<uint64_t> go{ctx, off};
     unsigned int *err;
     LIME_TRY(alloc(ctx, &err, 1));
     PoolGuard<unsigned int> ge{ctx, err};
@@ -1442,11 +1445,12 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
             release(ctx, res->b_row);
             cap = total;
         }
+        // (the second attempt ran at the first one's exact total: a larger
+        // total now means the passes disagree, and the arrays hold only cap)
+        if (total > cap) return fail(LIME_ERR_DEVICE, "subtract: record total changed between passes");
         unsigned int e = 0;
         LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
         if (e) return fail(LIME_ERR_DEVICE, "subtract: the writing fold differs from the count");
-        release(ctx, cnt);
-        release(ctx, off);
         res->n = (int64_t)total;
         return LIME_OK;
     }
@@ -1489,10 +1493,6 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
         if (e) return fail(LIME_ERR_DEVICE, "subtract: write pass recount differs from the count pass");
     }
-    release(ctx, olo);
-    release(ctx, ocnt);
-    release(ctx, cnt);
-    release(ctx, off);
     res->n = (int64_t)total;
     return LIME_OK;
 }

@@ -36,27 +36,77 @@ def even_splits(span, world):
     return [span * r // world for r in range(world)] + [span]
 
 
-def sample_splits(gs, span, world, group=None, samples=1024):
-    """Count-balanced splitters from an all_gather of local start samples."""
-    w, _ = _ws(group)
+def sample_splits(gs, span, world, group=None, samples=1024, align=1):
+    """Count-balanced splitters from an all_gather of local start samples
+    (gs: this rank's global starts, any order)."""
     n = gs.numel()
     if n:
         idx = torch.linspace(0, n - 1, samples, device=gs.device).long()
-        s = torch.sort(gs)[0][idx]
+        s = torch.sort(gs.to(torch.int64))[0][idx]
     else:
         s = torch.full((samples,), -1, dtype=torch.int64, device=gs.device)
-    out = [torch.empty_like(s) for _ in range(w)]
-    dist.all_gather(out, s, group=group)
-    allv = torch.sort(torch.cat(out))[0]
+    return splits_from_samples(s, span, world, group, align)
+
+
+def splits_from_weighted_samples(s, span, world, group=None, align=1):
+    """Splitters from every rank's start samples of one or more row sets: s
+    is an int64 tensor [k_sets, k + 1] per rank -- row j holds k evenly spaced
+    global starts of set j (-1 = none) and, last, the set's row count on this
+    rank, so each sample stands for count / k rows.  One all_gather, then the
+    world quantiles of the pooled weighted samples, rounded down to `align`
+    and kept non-decreasing (the sampled range partitioner behind ADAM
+    repartitionAndSort, cli/Intersection.scala:41-42, Partitioners.scala
+    :10-20): shards hold equal row counts however the rows are spread."""
+    w, _ = _ws(group)
+    if w > 1:
+        out = [torch.empty_like(s) for _ in range(w)]
+        dist.all_gather(out, s, group=group)
+        pool = torch.stack(out).cpu()
+    else:
+        pool = s.cpu()[None]
+    k = pool.shape[-1] - 1
+    vals = pool[..., :k].reshape(-1)
+    wts = (pool[..., k:].to(torch.float64) / k).expand(*pool.shape[:-1], k).reshape(-1)
+    keep = vals >= 0
+    vals, wts = vals[keep], wts[keep]
+    if vals.numel() == 0 or float(wts.sum()) <= 0:
+        return even_splits(span, world)
+    order = torch.argsort(vals, stable=True)
+    vals, cw = vals[order], torch.cumsum(wts[order], 0)
+    total = float(cw[-1])
+    cuts = [0]
+    for r in range(1, world):
+        i = int(torch.searchsorted(cw, torch.tensor(total * r / world, dtype=torch.float64)))
+        c = int(vals[min(i, vals.numel() - 1)]) // align * align
+        cuts.append(min(max(c, cuts[-1]), int(span)))
+    cuts.append(int(span))
+    return cuts
+
+
+def splits_from_samples(s, span, world, group=None, align=1):
+    """Splitters from every rank's start samples (int64 tensor of the same
+    length on every rank; -1 = no sample): one all_gather, then the world
+    quantiles of the pooled samples, rounded down to `align` (the bitset's
+    word or bin) and kept non-decreasing -- the sampled range partitioner
+    behind ADAM repartitionAndSort (cli/Intersection.scala:41-42, routed by
+    Partitioners.scala:10-20), so that shards hold equal row counts however
+    the rows are spread over the genome."""
+    w, _ = _ws(group)
+    if w > 1:
+        out = [torch.empty_like(s) for _ in range(w)]
+        dist.all_gather(out, s, group=group)
+        pool = torch.cat(out)
+    else:
+        pool = s
+    allv = torch.sort(pool)[0]
     allv = allv[allv >= 0]
     if allv.numel() == 0:
         return even_splits(span, world)
     cuts = [0]
     for r in range(1, world):
-        cuts.append(int(allv[(allv.numel() * r) // world].item()))
+        c = int(allv[(allv.numel() * r) // world].item()) // align * align
+        cuts.append(min(max(c, cuts[-1]), int(span)))
     cuts.append(int(span))
-    for r in range(1, len(cuts)):  # monotone
-        cuts[r] = max(cuts[r], cuts[r - 1])
     return cuts
 
 
@@ -302,15 +352,21 @@ def complement_frame(table, rank):
 
 
 # ------------------------------------------------------ device exchanges
+def bitset_align(span, world):
+    """the bitset build's 2^22-base bin, or a smaller power of two (>= 64, the
+    bitset's word) for small spans, so that no shard is rounded away"""
+    align = 1 << 22
+    while align > 64 and align * 4 * world > span:
+        align >>= 1
+    return align
+
+
 def coord_splits(span, world, align=None):
     """Equal coordinate ranges with inner bounds rounded to `align` (a
-    multiple of 64: the bitset's word; by default the bitset build's 2^22-base
-    bin, or a smaller power of two for small spans, so that no shard is
-    rounded away); last = span."""
+    multiple of 64: the bitset's word; by default bitset_align); last =
+    span."""
     if align is None:
-        align = 1 << 22
-        while align > 64 and align * 4 * world > span:
-            align >>= 1
+        align = bitset_align(span, world)
     cuts = [0]
     for r in range(1, world):
         c = (span * r // world) // align * align

@@ -393,6 +393,26 @@ class Context:
                                             C.byref(h)))
         return IntervalSet(self, h, space)
 
+    def set_concat_sorted(self, before, s, after, min_width, max_width, has_zero):
+        """rows `before` (n, d_gs, d_ge, d_row), then s, then rows `after` --
+        a shard's left halo, own rows and right halo, which the caller
+        guarantees to be in canonical order -- copied without a sort, a
+        validation or a read-back; the added rows' widths bounded by the
+        caller's (min, max, any zero)"""
+        h = vp()
+        nb, bg, be, br = before
+        na, ag, ae, ar = after
+        check(_lib().lime_set_concat_sorted(self._h, s._h, int(nb), vp(bg), vp(be), vp(br),
+                                            int(na), vp(ag), vp(ae), vp(ar), int(min_width),
+                                            int(max_width), int(bool(has_zero)), C.byref(h)))
+        return IntervalSet(self, h, s.space)
+
+    def sample_starts(self, space, n, d_contig, d_start, k, d_out):
+        """k evenly spaced rows' global starts into the device array d_out
+        (u32; d_contig None: d_start already global), stream-ordered"""
+        check(_lib().lime_sample_starts(self._h, space.handle, int(n), vp(d_contig), vp(d_start),
+                                        int(k), vp(d_out)))
+
     def set_extend_sorted(self, s, n, d_gs, d_ge, d_row, min_width, max_width, has_zero):
         """s's rows followed by n device rows that the caller guarantees to be
         in canonical order past s's last row (a shard's right halo), copied

@@ -15,6 +15,29 @@ import torch.distributed as dist
 from . import dist as ld
 
 
+SAMPLES = 4096  # start samples per rank and input set for sampled splitters
+
+
+def _sampled_splits(step, inputs, align):
+    """dist.splits_from_weighted_samples over the engine's samples of the
+    inputs [(n, d_contig, d_start, ...)] of this rank"""
+    k = SAMPLES
+    rows = []
+    for x in inputs:
+        n, d_contig, d_start = int(x[0]), x[1], x[2]
+        t = torch.full((k + 1,), -1, dtype=torch.int64, device=step.dev)
+        if n:
+            buf = torch.empty(k, dtype=torch.int32, device=step.dev)
+            step.ctx.sample_starts(step.space, n, d_contig, d_start, k, buf.data_ptr())
+            step._sync()  # engine output -> torch
+            t[:k] = buf.to(torch.int64) & 0xFFFFFFFF
+        t[k] = n
+        rows.append(t)
+    cd = step.comm if step.comm is not None else step.dev
+    s = torch.stack(rows).to(cd)
+    return ld.splits_from_weighted_samples(s, step.space.span, step.world, step.group, align)
+
+
 class _EngineRuns:
     """merge result as seen by lime_amd.dist.carry_tables: its leading runs
     and last end copied on the device into the gathered words (payload), so
@@ -84,10 +107,13 @@ class ShardStep:
 
     def __init__(self, ctx, space, splits=None, group=None, comm_device=None,
                  shared_stream=False):
+        """splits: the shard bounds; None = count-balanced, sampled from the
+        inputs (plan_splits, or the first load's rows) -- equal coordinate
+        ranges are not equal work on real BED density or C3's pile-ups"""
         self.ctx, self.space, self.group = ctx, space, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.splits = splits or ld.even_splits(space.span, self.world)
+        self.splits = splits
         self.comm = comm_device
         self.dev = torch.device("cuda", ctx.device)
         self.shared = shared_stream
@@ -102,11 +128,21 @@ class ShardStep:
         return torch.empty(max(int(n), 1), dtype=torch.int32, device=self.dev)
 
     # ----------------------------------------------------------- routing
+    def plan_splits(self, inputs):
+        """count-balanced shard bounds from this rank's inputs [(n, d_contig,
+        d_start, ...)] (unsorted device rows; d_contig None: global starts):
+        SAMPLES evenly spaced starts per set (lime_sample_starts), one
+        all_gather, the weighted quantiles (dist.splits_from_weighted_samples)"""
+        self.splits = _sampled_splits(self, inputs, 1)
+        return self.splits
+
     def route(self, n, d_contig, d_start, d_end, row_base=0, d_strand=None):
         """this rank's slice of unsorted rows -> the rows this shard owns:
         [gs, ge, row(, strand)] int32 device tensors (global coordinates and
         row ids), one packed all_to_all (lime_route_rows + dist.exchange)"""
         ctx, sp = self.ctx, self.space
+        if self.splits is None:
+            self.plan_splits([(n, d_contig, d_start)])
         cols = [self._i32(n) for _ in range(4 if d_strand else 3)]
         st8 = torch.empty(max(int(n), 1), dtype=torch.int8, device=self.dev) if d_strand else None
         counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=False, cap=n,
@@ -223,26 +259,42 @@ class ShardStep:
     def subtract(self, A, B, threshold=0, mode=0):
         """DistributedSubtract of this shard's own rows of A: every B row that
         overlaps one of them -- the left halo (earlier shards' rows reaching
-        in) + own B rows + the right halo -- as one sorted set.  Outputs are
-        disjoint across shards (each A row is subtracted where it is owned)
-        and carry global row ids (Subtract.scala:78-116 over the replication
-        of OverlapBasedSetTheory.scala:75-80)."""
-        my_end = -1
+        in) + own B rows + the right halo -- as one sorted set, joined on the
+        device without a sort or a read-back (lime_set_concat_sorted).
+        Outputs are disjoint across shards (each A row is subtracted where it
+        is owned) and carry global row ids (Subtract.scala:78-116 over the
+        replication of OverlapBasedSetTheory.scala:75-80).  The right halo
+        reaches to A's last start + A's widest row (no merge of A), and every
+        shard's bound and B width statistics travel in ONE all_gather."""
+        w, me = self.world, self.rank
+        cd = self.comm if self.comm is not None else self.dev
+        amin, amax, _ = A.stats()
+        bmin, bmax, bz = B.stats()
+        # [A's reach (the right halo bound), B's min width, max width, zero]
+        mine = torch.tensor([-1, bmin, bmax, int(bz)] if B.n else [-1, 1 << 32, 0, 0],
+                            dtype=torch.int64, device=self.dev)
         if A.n:
-            ma = self.ctx.merge(A)
-            my_end = _EngineRuns(ma).last_end
-            ma.close()
+            g = self._i32(1)
+            A.copy_rows_device(A.n - 1, 1, g.data_ptr(), self._i32(1).data_ptr(),
+                               self._i32(1).data_ptr())
+            self._sync()
+            mine[0] = (g[0].to(torch.int64) & 0xFFFFFFFF) + amax
+        t = torch.empty(w * 4, dtype=torch.int64, device=cd)
+        dist.all_gather_into_tensor(t, mine.to(cd), group=self.group)
+        tab = t.view(w, 4).tolist()
         left = self._left_halo(B)
-        (right,) = self._halo([B], my_end=my_end)
+        (right,) = self._halo([B], ends=[x[0] for x in tab])
         n, hl, hr = B.n, left[0].numel(), right[0].numel()
         if hl or hr:
-            gs, ge, row = self._i32(hl + n + hr), self._i32(hl + n + hr), self._i32(hl + n + hr)
-            gs[:hl], ge[:hl], row[:hl] = left
-            B.copy_rows_device(0, n, gs[hl:].data_ptr(), ge[hl:].data_ptr(), row[hl:].data_ptr())
-            gs[hl + n:hl + n + hr], ge[hl + n:hl + n + hr], row[hl + n:hl + n + hr] = right
+            # the halo rows' widths are bounded by their shards' statistics
+            src = [x for q, x in enumerate(tab) if q != me and x[2] >= x[1]]
+            wmin = min([x[1] for x in src], default=0)
+            wmax = max([x[2] for x in src], default=0)
+            zero = any(x[3] for x in src)
             self._sync()
-            Be = self.ctx.set_from_global(self.space, hl + n + hr, gs.data_ptr(), ge.data_ptr(),
-                                          row.data_ptr())
+            Be = self.ctx.set_concat_sorted((hl, *(c.data_ptr() for c in left)), B,
+                                            (hr, *(c.data_ptr() for c in right)),
+                                            min(wmin, 0xFFFFFFFF), wmax, zero)
         else:
             Be = B
         res = self.ctx.subtract(A, Be, threshold, mode)
@@ -379,10 +431,13 @@ class ShardedBitset:
         self.ctx, self.space, self.group = ctx, space, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.splits = splits or ld.coord_splits(space.span, self.world)
-        self.lo, self.hi = self.splits[self.rank], self.splits[self.rank + 1]
         self.dev = torch.device("cuda", ctx.device)
         self.comm = comm_device
+        # splits None: count-balanced, sampled from the first run's inputs and
+        # aligned to the bitset bin (at world 1 the whole genome)
+        self.splits = splits if splits or self.world > 1 else ld.coord_splits(space.span, 1)
+        self.lo, self.hi = (self.splits[self.rank], self.splits[self.rank + 1]) if self.splits \
+            else (None, None)
         # the engine shares torch's current stream (bench): stream order
         # covers the collectives; otherwise drain around them
         self.shared = shared_stream
@@ -392,6 +447,14 @@ class ShardedBitset:
         if not self.shared:
             self.ctx.synchronize()
             torch.cuda.current_stream(self.dev).synchronize()
+
+    def plan_splits(self, inputs):
+        """count-balanced shard windows from this rank's inputs [(n, d_contig,
+        d_start, d_end)] (ShardStep.plan_splits), bounds aligned to the bitset
+        bin (dist.bitset_align)"""
+        self.splits = _sampled_splits(self, inputs, ld.bitset_align(self.space.span, self.world))
+        self.lo, self.hi = self.splits[self.rank], self.splits[self.rank + 1]
+        return self.splits
 
     def shard_rows(self, n, d_contig, d_start, d_end):
         """this rank's slice of one set's rows -> the rows of this shard's
@@ -453,6 +516,8 @@ class ShardedBitset:
         coordinates), the carry (drop_first, new_last_end), the total run
         count of the unsharded result and, with gather=True, every run as an
         int64 [m, 2] tensor (global start, end) in order."""
+        if self.splits is None:
+            self.plan_splits(inputs)
         if op == "and":
             bits = [self.and_bitset(inputs)]
             res = self.ctx.bitset_runs(0, bits[0])

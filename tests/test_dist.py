@@ -403,3 +403,74 @@ def test_exchange_sets(world):
             want = [1000 * p + 100 * i + 10 * me + j for p in range(world)
                     for j in range((p + 2 * i + me) % 3)]
             assert a == want and b == [-x for x in want] and m == len(want)
+
+
+# ---------------- count-balanced splitters (dist.splits_from_weighted_samples)
+def _skewed(rank, world, n):
+    """this rank's slice of two row sets over a 1e6-base span: set A puts 85 %
+    of its rows in the first 5 % of the span (a pile-up region), set B is
+    uniform; ranks hold unequal slices (rank r: (r + 1) parts)"""
+    rng = np.random.default_rng(77)
+    span = 1_000_000
+    hot = rng.random(n) < 0.85
+    a = np.where(hot, rng.integers(0, span // 20, n), rng.integers(0, span, n))
+    b = rng.integers(0, span, n // 2)
+    parts = sum(range(1, world + 1))
+    lo = sum(range(1, rank + 1))
+
+    def sl(x):
+        m = len(x)
+        return x[m * lo // parts:m * (lo + rank + 1) // parts]
+    return span, sl(a), sl(b), a, b
+
+
+def _balance_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    try:
+        n, k = 60_000, 4096
+        span, a, b, _, _ = _skewed(rank, world, n)
+        rows = []
+        for x in (a, b):  # evenly spaced samples of the unsorted rows, + the count
+            t = torch.full((k + 1,), -1, dtype=torch.int64)
+            if len(x):
+                t[:k] = torch.from_numpy(x[(np.arange(k) * len(x)) // k].astype(np.int64))
+            t[k] = len(x)
+            rows.append(t)
+        q.put((rank, ld.splits_from_weighted_samples(torch.stack(rows), span, world,
+                                                     align=64)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sampled_splits_balance_rows(world):
+    """coordinate-even shards put > 2x the mean rows on one shard here (1.5x
+    at two shards, whose maximum is 2x); the sampled splitters every rank
+    computes (the same on every rank) stay within 1.2x of the mean, over both
+    sets together"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balance_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cuts = [r[1] for r in res]
+    assert all(c == cuts[0] for c in cuts), "every rank derives the same splitters"
+    splits = cuts[0]
+    assert splits[0] == 0 and all(x % 64 == 0 for x in splits[1:-1])
+    span, _, _, a, b = _skewed(0, world, 60_000)
+    allg = np.concatenate([a, b])
+    mean = len(allg) / world
+
+    def counts(s):
+        return np.histogram(allg, bins=s)[0]
+    even = counts(ld.even_splits(span, world))
+    assert even.max() > (1.5 if world == 2 else 2) * mean
+    assert counts(splits).max() <= 1.2 * mean

@@ -42,6 +42,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
     try:
         import lime_amd
+        from lime_amd import dist as ld
         from lime_amd.sharded import ShardStep
         ctx = lime_amd.Context(0)
         sp = lime_amd.Space(NAMES, LENS)
@@ -335,12 +336,15 @@ def _strand_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
     try:
         import lime_amd
+        from lime_amd import dist as ld
         from lime_amd.sharded import ShardStep
         ctx = lime_amd.Context(0)
         sp = lime_amd.Space(NAMES, LENS)
         off = sp.offsets
         A, B, sa, sb = _strand_rows()
-        step = ShardStep(ctx, sp, comm_device=torch.device("cpu"))
+        # (even splits: _strand_rows puts rows on exactly these shard bounds)
+        step = ShardStep(ctx, sp, splits=ld.even_splits(int(sp.offsets[-1]), world),
+                         comm_device=torch.device("cpu"))
 
         def dev(X, st=None):
             n = len(X[0])

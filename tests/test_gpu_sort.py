@@ -281,3 +281,76 @@ def test_digit_pass_sort_global(ctx):
     assert bool(((r64 - 7) % 3 == 0).all())
     assert bool((torch.sort(i).values == torch.arange(n, device="cuda")).all())
     assert bool((g64 == gs[i]).all()) and bool((e64 == ge[i]).all())
+
+
+# The bucketed sort's wider digit passes (9 + 9 bits, k_local_mid): a span
+# of 2^27 + 1 (sbits 28) with 2.2e8 rows averages more than 3072 rows per
+# 2^11-base bucket (9 + 8 bits), so the passes take 18 key bits and the
+# buckets are 2^10 bases (~1.7k rows).  Cases: u16 widths with zero-width
+# rows; widths past 2^16 (u32 ends through the 9-bit passes) as global rows
+# with the caller's row ids; piles that overflow the mid kernel (a position
+# holding 60 rows: a sub-bin past SMAX; 8,000 rows in one bucket: past its
+# 6,144-row cap; 40,000 rows: the workgroup radix over global memory).
+_W18 = 1 << 27
+
+
+@pytest.mark.parametrize("case", ["w16", "wide_global", "piles"])
+def test_bucketed_sort_nine_bit_passes(ctx, case):
+    import torch
+    sp = _space([_W18])
+    n = 220_000_000
+    hi = 70_000 if case == "wide_global" else 60
+    c, s, e = _synth(ctx, sp, n, 0x918, 0, hi)
+    if case == "piles":
+        g = torch.Generator(device="cuda")
+        g.manual_seed(18)
+        at = 0
+        for size, pos, spread in [(60, 5_000_000, 1), (8_000, 9_000_000, 1000),
+                                  (40_000, 70_000_000, 1000)]:
+            idx = torch.randperm(n, device="cuda", generator=g)[:size]
+            s[idx] = pos + torch.randint(0, spread, (size,), device="cuda", generator=g,
+                                         dtype=torch.int32)
+            w = torch.randint(0, 300, (size,), device="cuda", generator=g, dtype=torch.int32)
+            w[torch.rand(size, device="cuda", generator=g) < 0.1] = 0
+            e[idx] = s[idx] + w
+            at += size
+        torch.cuda.synchronize()
+    if case != "wide_global":
+        _check_device_order(ctx, sp, n, c, s, e)
+        return
+    # global rows with caller row ids: ties keep INPUT order
+    rows = torch.arange(n, device="cuda", dtype=torch.int64) * 5 + 3
+    r32 = torch.where(rows >= 2**31, rows - 2**32, rows).to(torch.int32)
+    torch.cuda.synchronize()
+    S = ctx.set_from_global(sp, n, s.data_ptr(), e.data_ptr(), r32.data_ptr())
+    og, oe, orow = (torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3))
+    S.copy_rows_device(0, n, og.data_ptr(), oe.data_ptr(), orow.data_ptr())
+    torch.cuda.synchronize()
+    S.close()
+    g64, e64, r64 = (x.to(torch.int64) & 0xFFFFFFFF for x in (og, oe, orow))
+    key = g64 * 2 + (e64 > g64).to(torch.int64)
+    assert bool((key[1:] >= key[:-1]).all())
+    tie = key[1:] == key[:-1]
+    assert bool((r64[1:][tie] > r64[:-1][tie]).all())
+    i = (r64 - 3) // 5
+    assert bool(((r64 - 3) % 5 == 0).all())
+    assert bool((torch.sort(i).values == torch.arange(n, device="cuda")).all())
+    assert bool((g64 == s.to(torch.int64)[i]).all()) and bool((e64 == e.to(torch.int64)[i]).all())
+    assert int((e64 - g64).max()) >= 65_536
+
+
+def test_digit_pass_pileups_ident_to16(ctx):
+    # pile-up keys through the digit passes' first pass exactly as round 4's
+    # unrecorded fault had them: caller rows (ROWS_IDENT: row = position)
+    # turned into u16 widths (EW_TO16), then EW_16 / EW_FROM16.  1.2e6 rows
+    # in 5,000 centres over hg38 average ~25 rows per 2^16-base bucket, below
+    # the bucketed sort's LMIN (32), so the four digit passes run; piles of
+    # ~240 rows per centre, zero-width rows among them
+    import torch
+    sp = _hg38()
+    n = 1_200_000
+    c, s, e = _synth(ctx, sp, n, 0x7E, 150, 600, pile=(5_000, 150))
+    z = torch.rand(n, device="cuda") < 0.02
+    e[z] = s[z]
+    torch.cuda.synchronize()
+    _check_device_order(ctx, sp, n, c, s, e)

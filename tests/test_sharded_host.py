@@ -102,7 +102,8 @@ class FakeCtx:
         def arr(p):
             return np.ctypeslib.as_array((ctypes.c_uint32 * n).from_address(p)).astype(np.int64)
         g, e, r = arr(d_gs), arr(d_ge), arr(d_row)
-        assert n == 0 or g[0] >= S.gs[-1], "halo rows start past the shard's rows"
+        # (own rows start below the shard's upper split, halo rows at or past it)
+        assert n == 0 or S.n == 0 or g[0] > S.gs[-1], "halo rows start past the shard's rows"
         w = e - g
         assert n == 0 or (w.max() <= max_w and w.min() >= min_w and (zero or not (w == 0).any()))
         return FakeSet(np.concatenate([S.gs, g]), np.concatenate([S.ge, e]),

@@ -134,7 +134,10 @@ __device__ __forceinline__ void flush_hist(uint32_t (*hist)[BINS], uint32_t *cou
 // LC: the contig table (<= PCMAX contigs) is staged in LDS, so the per-row
 // off / len gathers are LDS reads rather than dependent cache round trips
 constexpr int PCMAX = 1024;
-template <bool GLOBAL, bool WRITE = true, bool LC = false, int DB = 8>
+// W16 (caller rows, WRITE): ge receives the u16 width ge - gs, not the end
+// (the bucketed sort's first pass then reads 6 B per row; a set with a width
+// past 2^16 discards it and reads the caller's rows instead)
+template <bool GLOBAL, bool WRITE = true, bool LC = false, int DB = 8, bool W16 = false>
 __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              const uint32_t *__restrict__ start,
                                              const uint32_t *__restrict__ end,
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                                              uint32_t *__restrict__ counts, uint32_t ntiles,
                                              int hshift) {
     constexpr int BINS = 1 << DB;
+    static_assert(!(GLOBAL && W16), "u16 widths from caller rows only");
     __shared__ uint32_t hist[RWAVES][BINS];
     __shared__ SetStats ws[RWAVES];
     __shared__ uint32_t s_off[LC ? PCMAX : 1], s_len[LC ? PCMAX : 1];
@@ -278,7 +282,12 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
                     uns = 1;
                 p0 = a0[j], p1 = a1[j], pok = ok[j];
             }
-            if (WRITE) {
+            if (WRITE && W16) {
+                g4[q] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
+                reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(ge) + base)[q] =
+                    make_uint2(((a1[0] - a0[0]) & 0xffffu) | (a1[1] - a0[1]) << 16,
+                               ((a1[2] - a0[2]) & 0xffffu) | (a1[3] - a0[3]) << 16);
+            } else if (WRITE) {
                 g4[q] = make_uint4(a0[0], a0[1], a0[2], a0[3]);
                 h4[q] = make_uint4(a1[0], a1[1], a1[2], a1[3]);
             }
@@ -307,7 +316,10 @@ __global__ __launch_bounds__(RB) void k_prep(const int32_t *__restrict__ contig,
             }
             if (WRITE) {
                 gs[i] = g0;
-                ge[i] = g1;
+                if (W16)
+                    reinterpret_cast<uint16_t *>(ge)[i] = (uint16_t)(g1 - g0);
+                else
+                    ge[i] = g1;
             }
             if (row) row[i] = (uint32_t)i;
             mx = g0 > mx ? g0 : mx;
@@ -1063,7 +1075,7 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
                                                  const uint32_t (&rw)[ITEMS], uint32_t *T,
                                                  uint32_t *cw, uint32_t *scratch) {
     constexpr int NWD = 1 << (SBB - 1), SPW = NWD / NT;  // cursor words, per thread
-    static_assert(NWD % NT == 0 && SPW == 16, "16 cursor words per thread (padded layout)");
+    static_assert(NWD % NT == 0 && SPW >= 2 && (SPW & (SPW - 1)) == 0, "cursor words per thread");
     static_assert(NT * ITEMS <= (1 << POSB) && NT * ITEMS < 65536, "positions / ranks");
     constexpr int NW = NT / 64;
     const int w = threadIdx.x / 64, lane = dev::lane_id();
@@ -1073,11 +1085,11 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
     const int zb = a.zb;
     const int kb = a.L + zb;                 // local key bits
     const int sh = kb > SBB ? kb - SBB : 0;  // sub-bin = key >> sh
-    // cursor word i lives at i + i / 16: a thread's 16 words (its share of
-    // the scan) then start 17 words after its neighbour's -- every lane in
-    // its own bank (at 16 words apart, 16 lanes shared each bank)
-    auto pw = [](uint32_t i) { return i + (i >> 4); };
-    uint32_t *mine = cw + 17 * threadIdx.x;
+    // cursor word i lives at i + i / SPW: a thread's SPW words (its share of
+    // the scan) then start SPW + 1 words after its neighbour's -- every lane
+    // in its own bank (at 16 words apart, 16 lanes shared each bank)
+    auto pw = [](uint32_t i) { return i + i / SPW; };
+    uint32_t *mine = cw + (SPW + 1) * threadIdx.x;
 #pragma unroll
     for (int q = 0; q < SPW; ++q) mine[q] = 0u;
     __syncthreads();
@@ -1094,12 +1106,12 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
         }
     }
     __syncthreads();
-    uint32_t cv[SPW], csum = 0, cmax = 0;
-#pragma unroll
-    for (int q = 0; q < SPW; ++q) cv[q] = mine[q];
+    // (the thread's words are read twice, sum then starts, rather than held:
+    // 16 more registers spilled the wide shape)
+    uint32_t csum = 0, cmax = 0;
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
-        const uint32_t lo = cv[q] & 0xffffu, hi = cv[q] >> 16;
+        const uint32_t v = mine[q], lo = v & 0xffffu, hi = v >> 16;
         csum += lo + hi;
         cmax = max(cmax, max(lo, hi));
     }
@@ -1109,12 +1121,10 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
     if (lane == 0) scratch[NW + 1 + w] = mx;  // (past the scan's NW + 1 words)
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
-        const uint32_t lo = cv[q] & 0xffffu, hi = cv[q] >> 16;
-        cv[q] = st | (st + lo) << 16;
+        const uint32_t v = mine[q], lo = v & 0xffffu, hi = v >> 16;
+        mine[q] = st | (st + lo) << 16;
         st += lo + hi;
     }
-#pragma unroll
-    for (int q = 0; q < SPW; ++q) mine[q] = cv[q];
     __syncthreads();
     uint32_t big = 0;
 #pragma unroll
@@ -1134,9 +1144,10 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
         }
     }
     __syncthreads();
-    // rows sharing a sub-bin: their rank among its entries (after the claims
-    // each cursor is its sub-bin's end)
-    uint32_t dup = 0;
+    // rows sharing a sub-bin (equal starts): their rank among its entries,
+    // one item at a time (few rows share one; every item scanning to the
+    // wave's largest shared sub-bin in one loop took C3's local sort 3.8 ->
+    // 4.9 ms).  After the claims each cursor is its sub-bin's end.
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
         if (u[it] == 0xffffffffu) continue;
@@ -1167,34 +1178,38 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
     return true;
 }
 
-// Persistent, MID_WGS workgroups per CU (the others overlap one bucket's
-// loads with another's sort): buckets of up to LCAP_M rows; larger ones, or
-// with a sub-bin past SMAX rows, are listed for k_local_big.
-#ifndef LIME_MID_SBB
-#define LIME_MID_SBB 14
-#endif
-#ifndef LIME_MID_WGS
-#define LIME_MID_WGS 2
-#endif
-constexpr int LNT_M = 512, LPOS_M = 13, LCAP_M = 6144, LSBB_M = LIME_MID_SBB;  // 12 items / thread
-constexpr int MID_WGS = LIME_MID_WGS;
-using MidRegs = BucketRegs<LNT_M, LCAP_M / LNT_M, LCAP_M>;
-__global__ __launch_bounds__(LNT_M) __attribute__((amdgpu_waves_per_eu(2 * MID_WGS, 8)))
-void k_local_mid(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) {
-    __shared__ uint32_t T[LCAP_M];
-    __shared__ uint32_t cw[(1 << (LSBB_M - 1)) + (1 << (LSBB_M - 5))];  // (padded: 1 per 16)
-    __shared__ uint32_t scratch[2 * (LNT_M / 64) + 1];
+// Persistent, WGS workgroups of NT threads per CU (the others overlap one
+// bucket's loads with another's sort), buckets of up to NT * ITEMS rows;
+// larger ones, or with a sub-bin past SMAX rows, are listed for
+// k_local_big.  Two shapes:
+//   mid: 512 threads x 12 rows, two per CU (~59 KiB LDS): buckets averaging
+//        up to LAVG_M rows;
+//   wide: 1024 threads x 16 rows, one per CU (~132 KiB LDS: 2^15 sub-bins
+//        for 2^16-base buckets): buckets averaging up to LAVG_W rows (C3's
+//        5e8 pile-up rows, ~10.6k per 2^16-base bucket, under two 8-bit
+//        passes -- the 9-bit passes run at ~3 ms per 5e8 rows against ~2.4).
+template <int NT, int ITEMS, int POSB, int SBB, int WGS>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WGS * NT / 256, 8)))
+void k_local_keys(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) {
+    constexpr int CAP = NT * ITEMS;
+    __shared__ uint32_t T[CAP];
+    // (padded: one word per thread's share of the scan)
+    __shared__ uint32_t cw[(1 << (SBB - 1)) + NT];
+    __shared__ uint32_t scratch[2 * (NT / 64) + 1];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        MidRegs cur;
+        BucketRegs<NT, ITEMS, CAP> cur;
         cur.load(a, b, nb, start);
-        bool listed = cur.m > (uint32_t)LCAP_M;
+        bool listed = cur.m > (uint32_t)CAP;
         if (!listed && cur.m > 0)
-            listed = !bucket_sort_keys<LNT_M, LCAP_M / LNT_M, LPOS_M, LSBB_M>(
-                a, cur.s0, cur.m, cur.g, cur.e, cur.r, T, cw, scratch);
+            listed = !bucket_sort_keys<NT, ITEMS, POSB, SBB>(a, cur.s0, cur.m, cur.g, cur.e,
+                                                             cur.r, T, cw, scratch);
         if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
     }
 }
+constexpr int LCAP_M = 6144, LCAP_W = 16384;
+#define LIME_LOCAL_MID k_local_keys<512, 12, 13, 14, 2>
+#define LIME_LOCAL_WIDE k_local_keys<1024, 16, 14, 15, 1>
 
 // A bucket past LCAP_B rows: LSD over its key (gs mod 2^L, non-zero width) in
 // 6-bit digits by the whole workgroup, NT rows per step in order (wave ballot
@@ -1340,7 +1355,11 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
 #ifndef LIME_SORT_TBMAX
 #define LIME_SORT_TBMAX 18
 #endif
-constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4, LAVG_M = LCAP_M / 2;
+constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4, LAVG_M = LCAP_M / 2, LAVG_W = 11500;
+// the local kernel of a bucket geometry: 0 small, 1 mid, 2 wide
+static int local_shape(int tb, int64_t avg) {
+    return tb == 16 && avg <= LAVG ? 0 : avg <= LAVG_M ? 1 : 2;
+}
 
 // the (validate-only) prep of the bucketed sort, histogramming a DB-bit digit
 template <int DB>
@@ -1361,18 +1380,45 @@ void launch_prep_nowrite(lime_ctx *ctx, lime_set *set, bool global, const int32_
                            set->n_contigs, n, nullptr, nullptr, nullptr, part, mat, ntiles, hshift);
 }
 
+// the prep of the bucketed sort over caller rows when their widths may fit
+// u16: validation, statistics, the DB-bit histogram, and (gs, u16 width)
+// written for the first pass (6 B per row: it then reads those instead of
+// the caller's 12, with half the registers of the RAW pass, whose 48 loads
+// in flight spilled and waited mid-stream)
+template <int DB>
+void launch_prep_w16(lime_ctx *ctx, lime_set *set, const int32_t *d_contig,
+                     const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_len,
+                     int64_t n, uint32_t *gs, uint32_t *w16, SetStats *part, uint32_t *mat,
+                     uint32_t ntiles, int hshift) {
+    if (set->n_contigs <= PCMAX)
+        hipLaunchKernelGGL((k_prep<false, true, true, DB, true>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                           d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                           set->n_contigs, n, gs, w16, nullptr, part, mat, ntiles, hshift);
+    else
+        hipLaunchKernelGGL((k_prep<false, true, false, DB, true>), dim3(ntiles), dim3(RB), 0,
+                           S(ctx), d_contig, d_start, d_end, (const uint32_t *)set->d_off, d_len,
+                           set->n_contigs, n, gs, w16, nullptr, part, mat, ntiles, hshift);
+}
+
 // the bucketed sort's two digit passes: pass 1 (DB1 bits at L) from the
 // caller's rows (histogrammed by the prep), pass 2 (DB2 bits at L + DB1);
-// with u16 widths (every width < 2^16) pass 1 writes widths, pass 2 ends
+// with u16 widths (every width < 2^16) pass 1 writes widths, pass 2 ends.
+// pk / pw (caller rows with u16 widths): the prep's (gs, width), read by
+// pass 1 instead of the caller's rows
 template <int DB1, int DB2>
 int bucket_passes(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
                   const uint32_t *d_start, const uint32_t *d_end, int64_t n, int L, bool w16,
-                  uint32_t *mat, uint32_t ntiles, uint32_t *const (&a)[3], uint32_t *const (&o)[3]) {
+                  uint32_t *mat, uint32_t ntiles, uint32_t *const (&a)[3], uint32_t *const (&o)[3],
+                  const uint32_t *pk = nullptr, const uint32_t *pw = nullptr) {
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, ((int64_t)1 << DB1) * ntiles, nullptr));
     const uint32_t *kc = reinterpret_cast<const uint32_t *>(d_contig);
     const int8_t *nost = nullptr;
     const uint32_t *cm = mat;
-    if (global && w16)
+    if (pk && w16)
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_IDENT, false, EW_16, DB1>), dim3(ntiles),
+                           dim3(RB), 0, S(ctx), pk, pw, (const uint32_t *)nullptr, n, L, nost, cm,
+                           ntiles, a[0], a[1], a[2]);
+    else if (global && w16)
         hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_TO16, DB1>), dim3(ntiles), dim3(RB),
                            0, S(ctx), kc, d_start, d_end, n, L, nost, cm, ntiles, a[0], a[1], a[2]);
     else if (global)
@@ -1427,7 +1473,7 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         for (int tb = 16; tb <= LIME_SORT_TBMAX && sbits - tb >= 1; ++tb) {
             const int64_t nbs = (span >> (sbits - tb)) + 1;
             if (n < LMIN * nbs) break;  // (sparser still at more digit bits)
-            if (n <= (tb == 16 ? LAVG : LAVG_M) * nbs) {
+            if (n <= LAVG_W * nbs) {
                 TB = tb;
                 break;
             }
@@ -1440,7 +1486,18 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
     const int hshift = bucket_cand ? sbits - TB : set->min_shift;
     SetStats h = {0u, 0u, 0xffffffffu, 0u, 0u, 0u, {0, 0}};
     if (n > 0) {
-        if (bucket_cand) {  // validate + statistics + histogram only
+        if (bucket_cand && !global && LIME_SORT_W16) {
+            // validate + statistics + histogram, and (gs, u16 width) for the
+            // first pass (unused if a width reaches 2^16)
+            LIME_TRY(alloc(ctx, &k0, (size_t)n));
+            LIME_TRY(alloc(ctx, &e0, (size_t)(n + 1) / 2));
+            if (DB1 == 9)
+                launch_prep_w16<9>(ctx, set, d_contig, d_start, d_end, d_len, n, k0, e0, part, mat,
+                                   ntiles, hshift);
+            else
+                launch_prep_w16<8>(ctx, set, d_contig, d_start, d_end, d_len, n, k0, e0, part, mat,
+                                   ntiles, hshift);
+        } else if (bucket_cand) {  // validate + statistics + histogram only
             if (DB1 == 9)
                 launch_prep_nowrite<9>(ctx, set, global, d_contig, d_start, d_end, d_len, n, part,
                                        mat, ntiles, hshift);
@@ -1494,7 +1551,8 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
         // way the digit passes start from
         const int L = sbits - TB;
         const uint32_t nb = (h.max_gs >> L) + 1;
-        if (need && n / (int64_t)nb <= (TB == 16 ? LAVG : LAVG_M)) {
+        const int shape = local_shape(TB, n / (int64_t)nb);
+        if (need && n / (int64_t)nb <= LAVG_W) {
             uint32_t *a[3], *o[3];
             for (int q = 0; q < 3; ++q) {
                 LIME_TRY(alloc(ctx, &a[q], (size_t)n));
@@ -1503,13 +1561,15 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             const bool w16 = LIME_SORT_W16 && h.max_width < 65536u;
             if (TB == 16)
                 LIME_TRY((bucket_passes<8, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, ntiles, a, o)));
+                                              mat, ntiles, a, o, k0, e0)));
             else if (TB == 17)
                 LIME_TRY((bucket_passes<9, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, ntiles, a, o)));
+                                              mat, ntiles, a, o, k0, e0)));
             else
                 LIME_TRY((bucket_passes<9, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, ntiles, a, o)));
+                                              mat, ntiles, a, o, k0, e0)));
+            release(ctx, k0);
+            release(ctx, e0);
             release(ctx, mat);
             // every bucket sorted locally: (o) -> (a)
             uint32_t *start, *over;
@@ -1535,12 +1595,15 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (cus <= 0) cus = 256;
-            if (TB == 16)
+            if (shape == 0)
                 hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)),
                                    dim3(LNT_S), 0, S(ctx), la, nb, (const uint32_t *)start);
+            else if (shape == 1)
+                hipLaunchKernelGGL(LIME_LOCAL_MID, dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)),
+                                   dim3(512), 0, S(ctx), la, nb, (const uint32_t *)start);
             else
-                hipLaunchKernelGGL(k_local_mid, dim3(std::min<uint32_t>(nb, (uint32_t)MID_WGS * (uint32_t)cus)),
-                                   dim3(LNT_M), 0, S(ctx), la, nb, (const uint32_t *)start);
+                hipLaunchKernelGGL(LIME_LOCAL_WIDE, dim3(std::min<uint32_t>(nb, (uint32_t)cus)),
+                                   dim3(1024), 0, S(ctx), la, nb, (const uint32_t *)start);
             hipLaunchKernelGGL(k_local_big, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B), 0,
                                S(ctx), la);
             LIME_HIP(hipGetLastError());
@@ -1555,6 +1618,8 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             return LIME_OK;
         }
         // (in order, or dense buckets) the digit-pass layout from the caller's rows
+        release(ctx, k0);  // (the speculative (gs, u16 width) of the prep)
+        release(ctx, e0);
         LIME_TRY(alloc(ctx, &k0, (size_t)n));
         LIME_TRY(alloc(ctx, &e0, (size_t)n));
         LIME_TRY(alloc(ctx, &r0, (size_t)n));

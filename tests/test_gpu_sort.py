@@ -2,11 +2,12 @@
 repartitionAndSort, cli/Intersection.scala:42-43) against a numpy stable
 sort, on inputs that take every path of lime_amd/csrc/sort.hip:
 
-  - the bucketed sort (two 8-bit digit passes on bits [L, L + 16) of the
-    global start, then every 2^L-base bucket sorted in LDS): buckets of a few
-    rows, buckets of ~2-4k rows (512-thread kernel), of 4k-16k rows
-    (1024-thread kernel) and past 16k rows (the workgroup-wide radix over
-    global memory);
+  - the bucketed sort (two digit passes of 8 + 8, 9 + 8 or 9 + 9 bits on
+    bits [L, 32) of the global start, then every 2^L-base bucket sorted in
+    LDS): buckets of a few rows, of ~2k rows (k_local_small), ~2.7k
+    (k_local_keys mid), ~6-11k (k_local_keys wide), with sub-bins past SMAX
+    and buckets past 16k rows (k_local_big: ranked passes, the workgroup-wide
+    radix over global memory);
   - the digit passes (spans within 16 bits, sets of few rows per bucket,
     sets past LAVG rows per bucket: both sides of that switch at full size
     over hg38, C3-shaped pile-ups, giant piles, global rows);
@@ -205,16 +206,15 @@ def _synth(ctx, sp, n, seed, lo, hi, pile=None):
 
 
 # hg38: sbits 32, 47,125 buckets of 65,536 bases.  LAVG (2304) rows per
-# bucket switch a set from the bucketed sort to the four digit passes
-# (sort.hip); both sides of the switch are exercised at full size.
+# bucket switch a set from k_local_small to the keys kernels (sort.hip); both
+# sides of the switch are exercised at full size.
 _BUCKETS_HG38 = 47_125
 
 
 @pytest.mark.parametrize("n", [2304 * _BUCKETS_HG38 - 1_000_000, 2304 * _BUCKETS_HG38 + 1_000_000])
 def test_bucketed_sort_switch_point(ctx, n):
     # uniform rows over hg38, len U[0, 60] (zero-width rows included): below
-    # the switch two 8-bit passes and k_local_small, above it the zero-width
-    # pass and four digit passes
+    # the switch two 8-bit passes and k_local_small, above it k_local_keys
     sp = _hg38()
     c, s, e = _synth(ctx, sp, n, 0x5A, 0, 60)
     _check_device_order(ctx, sp, n, c, s, e)
@@ -222,8 +222,8 @@ def test_bucketed_sort_switch_point(ctx, n):
 
 def test_bucketed_sort_dense_buckets(ctx):
     # C3's shape at 2e8 rows: pile-ups (8e5 centres over hg38, N(0,150), len
-    # U[150,600]) averaging ~4.2k rows per 65536-base bucket: denser than the
-    # bucketed sort takes, so the four digit passes
+    # U[150,600]) averaging ~4.2k rows per 65536-base bucket: the wide keys
+    # kernel (C3 itself: ~10.6k)
     sp = _hg38()
     n = 200_000_000
     c, s, e = _synth(ctx, sp, n, 0x3C, 150, 600, pile=(800_000, 150))
@@ -231,9 +231,11 @@ def test_bucketed_sort_dense_buckets(ctx):
 
 
 def test_digit_pass_sort_giant_piles(ctx):
-    # the digit passes (1.2e8 rows over hg38: past the bucketed sort's
-    # density) with piles of 2.5k, 9k, 40k and 150k rows at single positions,
-    # zero-width rows and duplicates among them: stable at every pile
+    # 1.2e8 rows over hg38 (~2.5k per 2^16-base bucket: the mid keys kernel)
+    # with piles of 2.5k, 9k, 40k and 150k rows at single positions,
+    # zero-width rows and duplicates among them: sub-bins past SMAX and
+    # buckets past the caps (k_local_big's ranked passes and its radix over
+    # global memory), stable at every pile
     import torch
     sp = _hg38()
     n = 120_000_000
@@ -254,9 +256,9 @@ def test_digit_pass_sort_giant_piles(ctx):
 
 
 def test_digit_pass_sort_global(ctx):
-    # global-coordinate rows with the caller's row ids through the digit
-    # passes (1.15e8 rows over hg38): ties keep INPUT order, rows carried
-    # through
+    # global-coordinate rows with the caller's row ids (1.15e8 rows over hg38:
+    # the bucketed passes from the caller's (gs, ge, row), ROWS_LOAD): ties
+    # keep INPUT order, rows carried through
     import torch
     sp = _hg38()
     n = 115_000_000
@@ -283,28 +285,33 @@ def test_digit_pass_sort_global(ctx):
     assert bool((g64 == gs[i]).all()) and bool((e64 == ge[i]).all())
 
 
-# The bucketed sort's wider digit passes (9 + 9 bits, k_local_mid): a span
-# of 2^27 + 1 (sbits 28) with 2.2e8 rows averages more than 3072 rows per
-# 2^11-base bucket (9 + 8 bits), so the passes take 18 key bits and the
-# buckets are 2^10 bases (~1.7k rows).  Cases: u16 widths with zero-width
-# rows; widths past 2^16 (u32 ends through the 9-bit passes) as global rows
-# with the caller's row ids; piles that overflow the mid kernel (a position
-# holding 60 rows: a sub-bin past SMAX; 8,000 rows in one bucket: past its
-# 6,144-row cap; 40,000 rows: the workgroup radix over global memory).
+# The bucketed sort's local kernels and wider digit passes over a span of
+# 2^27 + 1 (sbits 28):
+#   mid:   9e7 rows, ~2.7k per 2^12-base bucket under two 8-bit passes
+#          (k_local_keys 512 x 12);
+#   wide:  2.2e8 rows, ~6.7k per bucket (k_local_keys 1024 x 16);
+#   nine:  4e8 rows average past LAVG_W per 2^12-base bucket, so the passes
+#          take 17 bits (9 + 8) and the buckets are 2^11 bases (~6.1k rows),
+#          with widths past 2^16 (u32 ends through the 9-bit pass) as global
+#          rows with the caller's row ids;
+#   piles: the wide shape with piles that overflow it (a position holding 60
+#          rows: a sub-bin past SMAX; 40,000 rows in one bucket: past its
+#          16,384-row cap, the workgroup radix over global memory) and 8,000
+#          rows in one bucket.
 _W18 = 1 << 27
 
 
-@pytest.mark.parametrize("case", ["w16", "wide_global", "piles"])
-def test_bucketed_sort_nine_bit_passes(ctx, case):
+@pytest.mark.parametrize("case", ["mid", "wide", "nine_global", "piles"])
+def test_bucketed_sort_local_shapes(ctx, case):
     import torch
     sp = _space([_W18])
-    n = 220_000_000
-    hi = 70_000 if case == "wide_global" else 60
+    n = {"mid": 90_000_000, "wide": 220_000_000, "nine_global": 400_000_000,
+         "piles": 220_000_000}[case]
+    hi = 70_000 if case == "nine_global" else 60
     c, s, e = _synth(ctx, sp, n, 0x918, 0, hi)
     if case == "piles":
         g = torch.Generator(device="cuda")
         g.manual_seed(18)
-        at = 0
         for size, pos, spread in [(60, 5_000_000, 1), (8_000, 9_000_000, 1000),
                                   (40_000, 70_000_000, 1000)]:
             idx = torch.randperm(n, device="cuda", generator=g)[:size]
@@ -313,25 +320,28 @@ def test_bucketed_sort_nine_bit_passes(ctx, case):
             w = torch.randint(0, 300, (size,), device="cuda", generator=g, dtype=torch.int32)
             w[torch.rand(size, device="cuda", generator=g) < 0.1] = 0
             e[idx] = s[idx] + w
-            at += size
         torch.cuda.synchronize()
-    if case != "wide_global":
+    if case != "nine_global":
         _check_device_order(ctx, sp, n, c, s, e)
         return
     # global rows with caller row ids: ties keep INPUT order
     rows = torch.arange(n, device="cuda", dtype=torch.int64) * 5 + 3
     r32 = torch.where(rows >= 2**31, rows - 2**32, rows).to(torch.int32)
+    del rows
     torch.cuda.synchronize()
     S = ctx.set_from_global(sp, n, s.data_ptr(), e.data_ptr(), r32.data_ptr())
+    del r32
     og, oe, orow = (torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3))
     S.copy_rows_device(0, n, og.data_ptr(), oe.data_ptr(), orow.data_ptr())
     torch.cuda.synchronize()
     S.close()
     g64, e64, r64 = (x.to(torch.int64) & 0xFFFFFFFF for x in (og, oe, orow))
+    del og, oe, orow
     key = g64 * 2 + (e64 > g64).to(torch.int64)
     assert bool((key[1:] >= key[:-1]).all())
     tie = key[1:] == key[:-1]
     assert bool((r64[1:][tie] > r64[:-1][tie]).all())
+    del key, tie
     i = (r64 - 3) // 5
     assert bool(((r64 - 3) % 5 == 0).all())
     assert bool((torch.sort(i).values == torch.arange(n, device="cuda")).all())

@@ -406,6 +406,27 @@ __device__ __forceinline__ int64_t upper_bound(const T *a, int64_t lo, int64_t h
     return lo;
 }
 
+// lower bounds of N keys each among w[0, n) (w sorted ascending, in LDS) by
+// binary lifting in lockstep, branch-free: a step's N reads are all issued
+// (the index clamped into the window) before any is compared, so they
+// overlap; past the window (b + step > n) the read is w[n - 1], and a key
+// above it lifts b to n, its lower bound, where it stays.  (The guarded form, `b + step <= n && w[b + step - 1] < key`,
+// compiles to a branch per read, each with its own LDS wait: 8 serial waits
+// per step in k_sub_fused, 31 % of its wave time at 1e9 rows.)
+template <int N, typename K>
+__device__ __forceinline__ void lds_lower_bounds(const uint32_t *w, int n, const K (&key)[N],
+                                                 int (&b)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) b[k] = 0;
+    for (int step = n > 0 ? (1 << (31 - __clz(n))) : 0; step > 0; step >>= 1) {
+        uint32_t v[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = w[min(b[k] + step, n) - 1];
+#pragma unroll
+        for (int k = 0; k < N; ++k) b[k] = min(b[k] + ((K)v[k] < key[k] ? step : 0), n);
+    }
+}
+
 // 65-ary search by one wave: every step probes 64 evenly spaced rows at once
 // and keeps the gap the key falls in, so a lower_bound over 1e8 rows takes
 // 5 dependent memory round trips instead of 27.  Wave-uniform result.

@@ -272,21 +272,18 @@ __global__ __launch_bounds__(IB) void k_count(StreamArgs sa, int64_t tp, int64_t
 #pragma unroll
     for (int k = 0; k < OPT; ++k) owner_keys(ogv[k], oev[k], sa.lo_off, tp, lkv[k], hkv[k]);
     if (in_lds) {
-        int bl[OPT], bh[OPT];
-#pragma unroll
-        for (int k = 0; k < OPT; ++k) bl[k] = bh[k] = 0;
-        const int wl = (int)wlen;
-        for (int step = wl > 0 ? (1 << (31 - __clz(wl))) : 0; step > 0; step >>= 1) {
-#pragma unroll
-            for (int k = 0; k < OPT; ++k) {
-                if (bl[k] + step <= wl && (int64_t)wgs[bl[k] + step - 1] < lkv[k]) bl[k] += step;
-                if (bh[k] + step <= wl && (int64_t)wgs[bh[k] + step - 1] < hkv[k]) bh[k] += step;
-            }
-        }
+        int64_t key[2 * OPT];
+        int b[2 * OPT];
 #pragma unroll
         for (int k = 0; k < OPT; ++k) {
-            lov[k] = wlo + bl[k];
-            hiv[k] = hkv[k] > lkv[k] ? wlo + bh[k] : lov[k];
+            key[k] = lkv[k];
+            key[OPT + k] = hkv[k];
+        }
+        dev::lds_lower_bounds(wgs, (int)wlen, key, b);
+#pragma unroll
+        for (int k = 0; k < OPT; ++k) {
+            lov[k] = wlo + b[k];
+            hiv[k] = hkv[k] > lkv[k] ? wlo + b[OPT + k] : lov[k];
         }
     } else {
 #pragma unroll

@@ -25,6 +25,8 @@
 // continue the fold one by one (work proportional to the hits).
 // One thread per left row, two passes (count, write); the write pass stages
 // a block's records in LDS and stores them lane-consecutively.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace lime {
@@ -174,9 +176,11 @@ __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__
                                                     const uint32_t *__restrict__ bgs, int64_t nb,
                                                     uint32_t maxw, int64_t nblk, int stride,
                                                     uint32_t *__restrict__ wstart, uint32_t maxwa,
-                                                    uint32_t *__restrict__ wend) {
-    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b >= nblk) return;
+                                                    uint32_t *__restrict__ wend,
+                                                    unsigned int *__restrict__ wmax) {
+    const int64_t b0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool ok = b0 < nblk;  // (no early exit: the wave reduces wmax below)
+    const int64_t b = ok ? b0 : nblk - 1;
     const int64_t key = (int64_t)ags[b * SUB_B * stride] - maxw;
     const int64_t hkey =
         wend ? (int64_t)ags[min((b + 1) * SUB_B * stride, na) - 1] + maxwa : (int64_t)0;
@@ -186,8 +190,14 @@ __global__ __launch_bounds__(256) void k_sub_window(const uint32_t *__restrict__
         if (r + step <= nb && (int64_t)bgs[r + step - 1] < key) r += step;
         if (wend && h + step <= nb && (int64_t)bgs[h + step - 1] < hkey) h += step;
     }
-    wstart[b] = (uint32_t)r;
-    if (wend) wend[b] = (uint32_t)h;
+    if (ok) {
+        wstart[b] = (uint32_t)r;
+        if (wend) wend[b] = (uint32_t)h;
+    }
+    if (wmax) {  // the longest window (wend + 1 - wstart), one atomic per wave
+        const uint32_t len = dev::wave_reduce_max((uint32_t)min(h + 1 - r, (int64_t)0xffffffff));
+        if (dev::lane_id() == 0) atomicMax(wmax, len);
+    }
 }
 
 // RUNS (threshold <= 0): the inside hits are not walked one by one.  A new
@@ -708,13 +718,19 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
     // not searched: a spanning block starts before a.s, so its start never
     // yields a record and the count needs only its existence and end.)
     int bl[RPL], bh[RPL];
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = 0;
-    for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
+    {
+        uint32_t key[2 * RPL];
+        int b[2 * RPL];
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
-            if (bl[k] + step <= nst && w_gs[bl[k] + step - 1] < as[k]) bl[k] += step;
-            if (bh[k] + step <= nst && w_gs[bh[k] + step - 1] < ae[k]) bh[k] += step;
+            key[k] = as[k];
+            key[RPL + k] = ae[k];
+        }
+        dev::lds_lower_bounds(w_gs, nst, key, b);
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            bl[k] = b[k];
+            bh[k] = b[RPL + k];
         }
     }
     uint64_t tot = 0;
@@ -831,6 +847,12 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
 #ifndef LIME_SUB_FWIN
 #define LIME_SUB_FWIN 1536
 #endif
+#ifndef LIME_SUB_LS
+#define LIME_SUB_LS 1
+#endif
+#ifndef LIME_SUB_KEEP
+#define LIME_SUB_KEEP 1
+#endif
 #ifndef LIME_SUB_WEND
 #define LIME_SUB_WEND 1
 #endif
@@ -846,9 +868,47 @@ struct FusedArgs {
     int64_t ntiles;
 };
 
+#ifndef LIME_SUB_PHASES
+#define LIME_SUB_PHASES 0
+#endif
+#if LIME_SUB_PHASES
+// (measurement build only) wave-cycles per phase of k_sub_fused, summed over
+// the waves of every 32nd workgroup and printed by k_sub_phases after each
+// launch (wall clock, 100 MHz)
+__device__ unsigned long long g_sub_phase[8];
+__global__ void k_sub_phases() {
+    printf("sub phases:");
+    for (int i = 0; i < 8; ++i) {
+        printf(" %llu", g_sub_phase[i]);
+        g_sub_phase[i] = 0;
+    }
+    printf("\n");
+}
+#define SUB_PH(i)                 \
+    do {                          \
+        const uint64_t t_ = wall_clock64(); \
+        ph_d[i] = t_ - ph_t;      \
+        ph_t = t_;                \
+    } while (0)
+#else
+#define SUB_PH(i) \
+    do {          \
+    } while (0)
+#endif
+
 // wstart / wend: sa's per-tile window bounds again, as restrict arguments,
 // read at the wave-uniform tile index by scalar loads: the window's staging
 // loads issue right behind the rows' loads instead of after them
+// LS (local scan): B has no zero-width rows and every tile's window fits in
+// FWIN (k_sub_window's wmax): the window's prefix max and run ids come from
+// its own starts and ends by two block scans instead of from B's merge scan
+// (4 B per row of run ids and 4 B of prefix max written and read again per
+// call: 1.6 ms of a 1e9-row subtract).  Rows before the window end before
+// the tile's first start, so the window-local prefix max equals B's wherever
+// the fold compares it (> a row's start) and a local run start (prefix max
+// before it <= its start, merge.hip) equals B's from any row's lo1 on; every
+// row's fold is the window-local one.
+template <bool LS>
 __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
                                                       const uint32_t *__restrict__ wstart,
                                                       const uint32_t *__restrict__ wend) {
@@ -857,8 +917,17 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
     __shared__ uint64_t s_wtot[FW];
     __shared__ uint64_t s_base;
     __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_scan[2 * FW];
+#if LIME_SUB_PHASES
+    uint64_t ph_t = wall_clock64(), ph_d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+#if LIME_SUB_BLOCKID  // (measurement only: dispatch order is not guaranteed)
+    if (threadIdx.x == 0) s_tile = blockIdx.x;
+#else
     if (threadIdx.x == 0) s_tile = atomicAdd(fa.ticket, 1u);
+#endif
     __syncthreads();
+    SUB_PH(0);
     // (uniform values held in scalar registers: every VGPR here costs
     // occupancy, 78 -> 84 VGPRs was 6 -> 5 waves per SIMD and +13 %)
     const int64_t tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile);
@@ -885,55 +954,149 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
         (int)min(min((int64_t)FWIN, sa.nb - wlo),
                  LIME_SUB_WEND ? (int64_t)wend[tile] + 1 - wlo : (int64_t)FWIN));
     for (int k = threadIdx.x; k < nst; k += FW * 64) {
-        w_pm[k] = sa.bpmax[wlo + k];
-        w_gs[k] = sa.bgs[wlo + k];
-        w_run[k] = sa.brun[wlo + k];
+        if constexpr (LS) {
+            w_pm[k] = sa.bge[wlo + k];  // (ends: scanned below)
+            w_gs[k] = sa.bgs[wlo + k];
+        } else {
+            w_pm[k] = sa.bpmax[wlo + k];
+            w_gs[k] = sa.bgs[wlo + k];
+            w_run[k] = sa.brun[wlo + k];
+        }
     }
     __syncthreads();
+    if constexpr (LS) {  // thread t scans window rows [PER t, PER t + PER)
+        constexpr int PER = FWIN / (FW * 64);
+        static_assert(FWIN % (FW * 64) == 0, "whole rows per thread");
+        const int r0 = threadIdx.x * PER;
+        uint32_t pv[PER], m = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            m = max(m, r0 + i < nst ? w_pm[r0 + i] : 0u);
+            pv[i] = m;
+        }
+        const uint32_t inc = dev::wave_inclusive_max(m);
+        if (lane == 63) s_scan[wv] = inc;
+        __syncthreads();
+        uint32_t c = dev::wave_shr1(inc, 0u);  // the prefix max before row r0
+        for (int w = 0; w < wv; ++w) c = max(c, s_scan[w]);
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {  // run starts: prefix max before the row <= its start
+            const uint32_t pm = max(c, pv[i]);
+            if (r0 + i < nst) {
+                cnt += (r0 + i > 0 && c <= w_gs[r0 + i]) ? 1u : 0u;
+                w_pm[r0 + i] = pm;
+            }
+            pv[i] = cnt;
+            c = pm;
+        }
+        const uint32_t sinc = dev::wave_inclusive_sum(cnt);
+        if (lane == 63) s_scan[FW + wv] = sinc;
+        __syncthreads();
+        uint32_t sb = sinc - cnt;
+        for (int w = 0; w < wv; ++w) sb += s_scan[FW + w];
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+            if (r0 + i < nst) w_run[r0 + i] = sb + pv[i];
+        __syncthreads();
+    }
+    SUB_PH(1);
     const int64_t whi = wlo + nst;
     auto in = [&](int64_t j) { return j >= wlo && j < whi; };
     auto PM = [&](int64_t j) { return in(j) ? w_pm[j - wlo] : sa.bpmax[j]; };
     auto GS = [&](int64_t j) { return in(j) ? w_gs[j - wlo] : sa.bgs[j]; };
     auto RUN = [&](int64_t j) { return in(j) ? w_run[j - wlo] : sa.brun[j]; };
-    auto NX = [&](int64_t j, int64_t hi1) -> int64_t {  // end of j's run, cut at hi1
-        const uint32_t r = RUN(j);
-        if (RUN(hi1 - 1) == r) return hi1;
-        int64_t l = j + 1, h = hi1 - 1;
-        while (l < h) {
-            const int64_t m = (l + h) >> 1;
-            if (RUN(m) > r)
-                h = m;
-            else
-                l = m + 1;
-        }
-        return l;
-    };
     const bool lime_mode = sa.mode == LIME_SUBTRACT_LIME;
     // lockstep bounds of a.s and a.e (the first spanning row, needed by the
     // writing fold only, is searched there: fewer registers, more waves)
     int bl[RPL], bh[RPL];
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) bl[k] = bh[k] = 0;
-    for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
+    {
+        uint32_t key[2 * RPL];
+        int b[2 * RPL];
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
-            if (bl[k] + step <= nst && w_gs[bl[k] + step - 1] < as[k]) bl[k] += step;
-            if (bh[k] + step <= nst && w_gs[bh[k] + step - 1] < ae[k]) bh[k] += step;
+            key[k] = as[k];
+            key[RPL + k] = ae[k];
+        }
+        dev::lds_lower_bounds(w_gs, nst, key, b);
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            bl[k] = b[k];
+            bh[k] = b[RPL + k];
         }
     }
+    SUB_PH(2);
     // a row's fold (k_subtract<_, true>'s, over this window): counts its
     // records, or with `wr` emits them into [pos, end) -- tile-local
-    // positions in the LDS stage when `staged`, else global ones
-    auto fold = [&](uint32_t a_s, uint32_t a_e, int blk, int bhk, bool wr, uint64_t pos,
-                    uint64_t end, uint32_t ar, bool staged) -> uint64_t {
-        int64_t lo1 = blk < nst ? wlo + blk : dev::lower_bound(sa.bgs, whi, sa.nb, (int64_t)a_s);
-        int64_t hi1 = lo1;
-        if (a_e > a_s)
-            hi1 = bhk < nst ? wlo + bhk
-                              : dev::lower_bound(sa.bgs, max(lo1, whi), sa.nb, (int64_t)a_e);
-        if (sa.zw) {
-            while (lo1 < sa.nb && GS(lo1) == a_s && sa.bge[lo1] == a_s) ++lo1;
-            if (hi1 < lo1) hi1 = lo1;
+    // positions in the LDS stage when `staged`, else global ones.  Two forms
+    // of one body: window-local (LOC: u32 indices relative to wlo, every
+    // read but the heads' from LDS, no bounds checks) for a row whose bounds
+    // both fall inside the window -- rows before it end before the tile's
+    // first start (k_sub_window), so its fold reads nothing else -- and B
+    // without zero-width rows; the general form (global indices, each read
+    // from the window or else global memory) for the rest.  (The kernel is
+    // VALU-issue bound: ~2000 VALU instructions per wave at 1e9 rows, the
+    // general form's 64-bit index arithmetic and window checks a large part)
+    // a long same-start group's head from the tie index; tn < 0: the index
+    // is not built (LS defers it to the first call that meets such a group):
+    // flagged, and the caller builds it and runs the pass again
+    auto tie = [&](uint32_t bs, uint32_t thr, uint32_t &hr, uint32_t &he) {
+        if (sa.tn < 0)
+            atomicOr(sa.err, 4u);
+        else
+            tie_head(sa, bs, thr, hr, he);
+    };
+    auto fold = [&](auto L, uint32_t a_s, uint32_t a_e, int blk, int bhk, bool wr, uint64_t pos,
+                    uint64_t end, uint32_t ar, bool staged) -> uint32_t {
+        constexpr bool LOC = decltype(L)::value;
+        using I = std::conditional_t<LOC, int, int64_t>;
+        auto pmf = [&](I j) -> uint32_t {
+            if constexpr (LOC) return w_pm[j];
+            else return PM(j);
+        };
+        auto gsf = [&](I j) -> uint32_t {
+            if constexpr (LOC) return w_gs[j];
+            else return GS(j);
+        };
+        auto runf = [&](I j) -> uint32_t {
+            if constexpr (LOC) return w_run[j];
+            else return RUN(j);
+        };
+        auto gef = [&](I j) -> uint32_t {
+            if constexpr (LOC) return sa.bge[wlo + j];
+            else return sa.bge[j];
+        };
+        auto rowf = [&](I j) -> uint32_t {
+            if constexpr (LOC) return sa.brow[wlo + j];
+            else return sa.brow[j];
+        };
+        auto nxf = [&](I j, I hi1) -> I {  // end of j's run, cut at hi1
+            const uint32_t r = runf(j);
+            if (runf(hi1 - 1) == r) return hi1;
+            I l = j + 1, h = hi1 - 1;
+            while (l < h) {
+                const I m = (l + h) >> 1;
+                if (runf(m) > r)
+                    h = m;
+                else
+                    l = m + 1;
+            }
+            return l;
+        };
+        I lo1, hi1;
+        if constexpr (LOC) {
+            lo1 = blk;
+            hi1 = a_e > a_s ? bhk : blk;
+        } else {
+            lo1 = blk < nst ? wlo + blk : dev::lower_bound(sa.bgs, whi, sa.nb, (int64_t)a_s);
+            hi1 = lo1;
+            if (a_e > a_s)
+                hi1 = bhk < nst ? wlo + bhk
+                                : dev::lower_bound(sa.bgs, max(lo1, whi), sa.nb, (int64_t)a_e);
+            if (sa.zw) {
+                while (lo1 < sa.nb && GS(lo1) == a_s && sa.bge[lo1] == a_s) ++lo1;
+                if (hi1 < lo1) hi1 = lo1;
+            }
         }
         const uint32_t thr = a_s;  // threshold <= 0
         auto emit = [&](uint32_t s, uint32_t e, uint32_t br, uint64_t at) {
@@ -952,7 +1115,7 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
         };
         bool any = false;
         uint32_t bs = 0, be = 0, hr = 0, he = 0, setpos = a_s;  // block, head row and end
-        uint64_t cum = 0;
+        uint32_t cum = 0;  // (a row's records: at most 2 per B run, < 2^32)
         auto close_block = [&]() {
             if (lime_mode) {
                 const uint32_t r = (bs > a_s) + (a_e > be);
@@ -971,8 +1134,10 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
             }
         };
         // the spanning block: first j in [wlo, lo1) with pmax > thr; its head
-        // the min (end, row) among its same-start rows
-        const uint32_t pm_last = lo1 > 0 ? PM(lo1 - 1) : 0u;
+        // the min (end, row) among its same-start rows.  (Rows before the
+        // window end before the tile's first start: pmax[wlo - 1] <= thr, so
+        // lo1 == wlo has no spanning block and j0 >= wlo.)
+        const uint32_t pm_last = lo1 > 0 ? pmf(lo1 - 1) : 0u;
         if (lo1 > 0 && pm_last > thr) {
             any = true;
             bs = 0;  // (counting: the spanning block starts before a.s)
@@ -980,8 +1145,18 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
             if (wr) {
                 // first j with pmax > thr: in the window when some staged
                 // pmax exceeds thr (pmax ascends)
-                int64_t j0;
-                if (nst > 0 && w_pm[nst - 1] > thr) {
+                I j0;
+                if constexpr (LOC) {
+                    int l = 0, h = lo1 - 1;
+                    while (l < h) {
+                        const int m = (l + h) >> 1;
+                        if (w_pm[m] > thr)
+                            h = m;
+                        else
+                            l = m + 1;
+                    }
+                    j0 = l;
+                } else if (nst > 0 && w_pm[nst - 1] > thr) {
                     int l = 0, h = nst - 1;
                     while (l < h) {
                         const int m = (l + h) >> 1;
@@ -994,38 +1169,39 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
                 } else {
                     j0 = first_spanning(sa.bpmax, lo1, thr);
                 }
-                bs = GS(j0);
-                hr = sa.brow[j0];
-                he = sa.bge[j0];
-                int64_t j = j0 + 1;
-                for (; j < lo1 && j <= j0 + TIE_G && GS(j) == bs; ++j) {
-                    const uint32_t g2 = sa.bge[j], r2 = sa.brow[j];
+                bs = gsf(j0);
+                hr = rowf(j0);
+                he = gef(j0);
+                I j = j0 + 1;
+                for (; j < lo1 && j <= j0 + TIE_G && gsf(j) == bs; ++j) {
+                    const uint32_t g2 = gef(j), r2 = rowf(j);
                     if (g2 > thr && (g2 < he || (g2 == he && r2 < hr))) {
                         hr = r2;
                         he = g2;
                     }
                 }
-                if (j < lo1 && GS(j) == bs) tie_head(sa, bs, thr, hr, he);  // a long group
+                if (j < lo1 && gsf(j) == bs) tie(bs, thr, hr, he);  // a long group
             }
         }
-        int64_t j = lo1;
+        I j = lo1;
         // the spanning block goes on through the inside rows of its run
-        if (any && j < hi1 && RUN(j) == RUN(lo1 - 1)) {
-            const int64_t nx = NX(j, hi1);
-            be = max(be, PM(nx - 1));
+        if (any && j < hi1 && runf(j) == runf(lo1 - 1)) {
+            const I nx = nxf(j, hi1);
+            be = max(be, pmf(nx - 1));
             j = nx;
         }
         while (j < hi1) {
-            const int64_t nx = NX(j, hi1);
-            const uint32_t gs = GS(j);
+            const I nx = nxf(j, hi1);
+            const uint32_t gs = gsf(j);
             if (!any) {  // foldLeft(List(head)): the head is folded against itself
                 any = true;
-                const uint32_t ge = sa.bge[j];
-                if (ge == gs) {  // a zero-width head closes a duplicate of itself
+                // a zero-width head closes a duplicate of itself (B without
+                // zero-width rows has none: no head load in the counting fold)
+                if (!LOC && sa.zw && gef(j) == gs) {
                     bs = be = gs;
                     if (wr) {
-                        hr = sa.brow[j];
-                        he = ge;
+                        hr = rowf(j);
+                        he = gs;
                     }
                     close_block();
                 }
@@ -1033,20 +1209,20 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
                 close_block();
             }
             bs = gs;
-            be = PM(nx - 1);  // (the inclusive prefix max: >= the head's end)
+            be = pmf(nx - 1);  // (the inclusive prefix max: >= the head's end)
             if (wr) {  // the head among the run's same-start non-empty hits: min (end, row)
-                hr = sa.brow[j];
-                he = sa.bge[j];
+                hr = rowf(j);
+                he = gef(j);
                 if (he > bs) {
-                    int64_t q = j + 1;
-                    for (; q < nx && q <= j + TIE_G && GS(q) == bs; ++q) {
-                        const uint32_t e2 = sa.bge[q], r2 = sa.brow[q];
+                    I q = j + 1;
+                    for (; q < nx && q <= j + TIE_G && gsf(q) == bs; ++q) {
+                        const uint32_t e2 = gef(q), r2 = rowf(q);
                         if (e2 < he || (e2 == he && r2 < hr)) {
                             hr = r2;
                             he = e2;
                         }
                     }
-                    if (q < nx && GS(q) == bs) tie_head(sa, bs, bs, hr, he);  // a long group
+                    if (q < nx && gsf(q) == bs) tie(bs, bs, hr, he);  // a long group
                 }
             }
             j = nx;
@@ -1062,6 +1238,20 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
         if (wr) emit(a_s, a_e, 0xffffffffu, pos);  // no hit: (L, None)
         return 1;
     };
+    // whether a row's fold may take the window-local form
+    const bool tail = whi == sa.nb;  // (bounds at nst are exact: the window reaches B's end)
+    auto local = [&](uint32_t a_s, uint32_t a_e, int blk, int bhk) {
+        return !sa.zw && (blk < nst || tail) && (a_e <= a_s || bhk < nst || tail);
+    };
+    auto fold_sel = [&](uint32_t a_s, uint32_t a_e, int blk, int bhk, bool wr, uint64_t pos,
+                        uint64_t end, uint32_t ar, bool staged) -> uint32_t {
+        if constexpr (LS)  // (every row's bounds inside the window)
+            return fold(std::true_type{}, a_s, a_e, blk, bhk, wr, pos, end, ar, staged);
+        else
+            return local(a_s, a_e, blk, bhk)
+                       ? fold(std::true_type{}, a_s, a_e, blk, bhk, wr, pos, end, ar, staged)
+                       : fold(std::false_type{}, a_s, a_e, blk, bhk, wr, pos, end, ar, staged);
+    };
     // counts, then each row's place: rows in order (k, lane) within a wave,
     // waves in order within the tile
     // (u32: a tile's records past 2^32 would need 4M records per row)
@@ -1069,12 +1259,13 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
         cnt[k] = base + k * 64 + lane < sa.na
-                     ? (uint32_t)fold(as[k], ae[k], bl[k], bh[k], false, 0, 0, 0, false)
+                     ? fold_sel(as[k], ae[k], bl[k], bh[k], false, 0, 0, 0, false)
                      : 0u;
         const uint32_t inc = dev::wave_inclusive_sum(cnt[k]);
         ex[k] = run + inc - cnt[k];
         run += dev::lane63(inc);
     }
+    SUB_PH(3);
     if (lane == 0) s_wtot[wv] = run;
     __syncthreads();
     uint64_t wpre = 0, T = 0;
@@ -1101,6 +1292,7 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
     };
     if (wv == 0 && lane == 0)
         dev::st_publish(fa.st + tile, (tile == 0 ? dev::ST_INC : dev::ST_AGG) | T);
+    SUB_PH(4);
     if (!staged) place();
     const uint64_t tb = staged ? 0 : s_base;
     // the writing folds over the wave's rows WITH records only, compacted
@@ -1141,30 +1333,56 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
             }
         }
         src &= 63;
-        uint32_t r_cnt = 0, r_ex = 0;
+        uint32_t r_cnt = 0, r_ex = 0, r_s = 0, r_e = 0, r_b = 0;
+        // (LS: the row's start, end and bounds from the counting lane's
+        // registers, no reload and no second search; the merge-scan form
+        // has no registers to spare: 78 -> 89 VGPRs, 6 -> 5 waves)
+        constexpr bool KEEP = LS && LIME_SUB_KEEP;
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
             const uint32_t v_cnt = __shfl(cnt[k], src), v_ex = __shfl(ex[k], src);
+            uint32_t v_s = 0, v_e = 0, v_b = 0;
+            if constexpr (KEEP) {
+                v_s = __shfl(as[k], src);
+                v_e = __shfl(ae[k], src);
+                v_b = __shfl((uint32_t)bl[k] | (uint32_t)bh[k] << 16, src);
+            }
             if (kk == k) {
                 r_cnt = v_cnt;
                 r_ex = v_ex;
+                r_s = v_s;
+                r_e = v_e;
+                r_b = v_b;
             }
         }
         if (e < cum[RPL]) {
             const int64_t i = base + kk * 64 + src;
-            const uint32_t a_s = sa.ags[i], a_e = sa.age[i];
-            int lb = 0, hb = 0;  // the lockstep bounds, again
-            for (int step = nst > 0 ? (1 << (31 - __clz(nst))) : 0; step > 0; step >>= 1) {
-                if (lb + step <= nst && w_gs[lb + step - 1] < a_s) lb += step;
-                if (hb + step <= nst && w_gs[hb + step - 1] < a_e) hb += step;
+            uint32_t a_s, a_e;
+            int lb, hb;
+            if constexpr (KEEP) {
+                static_assert(FWIN < (1 << 16), "bounds packed in 16 bits");
+                a_s = r_s;
+                a_e = r_e;
+                lb = r_b & 0xffff;
+                hb = r_b >> 16;
+            } else {
+                a_s = sa.ags[i];
+                a_e = sa.age[i];
+                const uint32_t key[2] = {a_s, a_e};
+                int b[2];  // the lockstep bounds, again
+                dev::lds_lower_bounds(w_gs, nst, key, b);
+                lb = b[0];
+                hb = b[1];
             }
             const uint64_t pos = tb + wpre + r_ex;
-            if (fold(a_s, a_e, lb, hb, true, pos, pos + r_cnt, sa.arow[i], staged) != r_cnt)
+            if (fold_sel(a_s, a_e, lb, hb, true, pos, pos + r_cnt, sa.arow[i], staged) != r_cnt)
                 atomicOr(sa.err, 1u);  // (the two folds disagree: flagged, not written past)
         }
     }
+    SUB_PH(5);
     if (staged) {  // the tile's records, lane-consecutive
         place();  // (its barrier also orders the staged records)
+        SUB_PH(6);
         const uint64_t gb = s_base;
         for (int q = threadIdx.x; q < (int)T; q += FW * 64) {
             const uint64_t at = gb + q;
@@ -1175,6 +1393,11 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
             sa.obr[at] = f_br[q];
         }
     }
+    SUB_PH(7);
+#if LIME_SUB_PHASES  // (the sums' atomics after the last phase: none waits on them)
+    if ((threadIdx.x & 63) == 0 && (blockIdx.x & 31) == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_sub_phase[i], (unsigned long long)ph_d[i]);
+#endif
 }
 
 // whether any same-start group has more than TIE_G rows: gs[j] == gs[j +
@@ -1343,9 +1566,36 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     PoolGuard<uint32_t> g1{ctx, mb.run_of_sorted};
     PoolGuard<uint32_t> g2{ctx, mb.gs};
     PoolGuard<uint32_t> g3{ctx, mb.ge};
+    // LS (k_sub_fused<true>): B without zero-width rows and every fused
+    // tile's window within FWIN (one read-back) -- no merge scan of B
+    uint32_t *wstart = nullptr, *wend = nullptr;
+    PoolGuard<uint32_t> gw{ctx, wstart};
+    PoolGuard<uint32_t> gwe{ctx, wend};
+    bool ls = false;
+    // (LIME_SUB_NO_LS set: the merge-scan paths, as tests force them)
+    if (runs && !B->has_zero_width && LIME_SUB_LS && !getenv("LIME_SUB_NO_LS")) {
+        const int64_t nt = blocks_for(na, FROWS);
+        unsigned int *wm;
+        LIME_TRY(alloc(ctx, &wm, 1));
+        PoolGuard<unsigned int> gm{ctx, wm};
+        LIME_TRY(alloc(ctx, &wstart, (size_t)nt));
+        LIME_TRY(alloc(ctx, &wend, (size_t)nt));
+        LIME_HIP(hipMemsetAsync(wm, 0, 4, S(ctx)));
+        hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx), A->gs,
+                           na, B->gs, B->n, B->max_width, nt, FW, wstart, A->max_width, wend, wm);
+        LIME_HIP(hipGetLastError());
+        unsigned int h_wm = 0;
+        LIME_TRY(read_back(ctx, &h_wm, wm, sizeof(h_wm)));
+        ls = h_wm <= (unsigned)FWIN;
+        if (!ls) {
+            release(ctx, wstart);
+            release(ctx, wend);
+            wstart = wend = nullptr;
+        }
+    }
     // (the same scan tells whether B has a same-start group past TIE_G)
     int tie_big = -1;
-    if (runs) LIME_TRY(merge_runs_with_pmax(ctx, B, &mb, &tie_big));
+    if (runs && !ls) LIME_TRY(merge_runs_with_pmax(ctx, B, &mb, &tie_big));
     // runs, one pass (k_sub_fused) when records are plentiful (they come
     // from A rows crossing the ends of B's runs: the sparse 1e9-row subtract,
     // 9.2e6 runs of B, 7.4e7 records for 5e8 rows); B merging into fewer runs
@@ -1353,22 +1603,23 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     // rows) leaves most tiles without a record, and there the count pass + a
     // write pass that skips them wins (1.0 vs 1.4 ms on C2's inputs: no
     // tickets, no look-back)
-    const bool fused = runs && mb.n * 64 >= na;
+    // (LS: fused always -- without the merge scan the two-pass path's one
+    // advantage, no look-back, does not pay for the scan it needs)
+    const bool fused = ls || (runs && mb.n * 64 >= na);
     // window starts: per block; per count workgroup (CNT_WAVES blocks) or
     // fused tile (FW blocks) with inline ranges
     const int stride = fused ? FW : inl ? CNT_WAVES : 1;
     const int64_t nws = (nblk + stride - 1) / stride;
-    uint32_t *wstart, *wend = nullptr;
-    LIME_TRY(alloc(ctx, &wstart, (size_t)nws));
-    PoolGuard<uint32_t> gw{ctx, wstart};
-    if (fused) LIME_TRY(alloc(ctx, &wend, (size_t)nws));
-    PoolGuard<uint32_t> gwe{ctx, wend};
-    if (B->n > 0)
-        hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nws, 256)), dim3(256), 0, S(ctx), A->gs,
-                           na, B->gs, B->n, B->max_width, nws, stride, wstart, A->max_width,
-                           wend);
-    else
-        LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nws, S(ctx)));
+    if (!ls) {
+        LIME_TRY(alloc(ctx, &wstart, (size_t)nws));
+        if (fused) LIME_TRY(alloc(ctx, &wend, (size_t)nws));
+        if (B->n > 0)
+            hipLaunchKernelGGL(k_sub_window, dim3(blocks_for(nws, 256)), dim3(256), 0, S(ctx),
+                               A->gs, na, B->gs, B->n, B->max_width, nws, stride, wstart,
+                               A->max_width, wend, (unsigned int *)nullptr);
+        else
+            LIME_HIP(hipMemsetAsync(wstart, 0, 4 * (size_t)nws, S(ctx)));
+    }
     uint32_t *bwlo = nullptr;  // runs: per-block window starts (count -> write pass)
     if (inl) LIME_TRY(alloc(ctx, &bwlo, (size_t)nblk));
     PoolGuard<uint32_t> gb{ctx, bwlo};
@@ -1397,12 +1648,27 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     sa.rcnt = rcnt;
     sa.off = off;
     sa.err = err;
-    // the tie index of B (long same-start groups), built once per set
-    if (B->n > 0) LIME_TRY(build_tie_index(ctx, B, tie_big));
-    sa.tgs = B->tie_gs;
-    sa.tge = B->tie_ge;
-    sa.trow = B->tie_row;
-    sa.tn = B->tie_n > 0 ? B->tie_n : 0;
+    // the tie index of B (long same-start groups), built once per set; LS
+    // (no merge scan to test for such groups) builds it only when its pass
+    // meets one (err bit 4) and then runs again
+    int64_t tn_now;
+    {
+        std::lock_guard<std::mutex> lock(B->ctx->mu);
+        tn_now = B->tie_n;
+    }
+    auto tie_args = [&]() {
+        sa.tgs = B->tie_gs;
+        sa.tge = B->tie_ge;
+        sa.trow = B->tie_row;
+        sa.tn = B->tie_n > 0 ? B->tie_n : 0;
+    };
+    if (ls && tn_now < 0) {
+        sa.tgs = sa.tge = sa.trow = nullptr;
+        sa.tn = -1;
+    } else {
+        if (B->n > 0) LIME_TRY(build_tie_index(ctx, B, tie_big));
+        tie_args();
+    }
     sa.ogs = sa.oge = sa.oar = sa.obr = nullptr;
     sa.brun = nullptr;
     sa.zw = B->has_zero_width ? 1 : 0;
@@ -1423,7 +1689,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         // records rarely pass one per left row; past the guess the pass runs
         // again at the exact total
         uint64_t cap = (uint64_t)na + 4096, total = 0;
-        for (int attempt = 0; attempt < 2; ++attempt) {
+        for (int attempt = 0, tie_runs = 0; attempt < 2; ++attempt) {
             LIME_TRY(alloc(ctx, &res->gs, (size_t)cap));
             LIME_TRY(alloc(ctx, &res->ge, (size_t)cap));
             LIME_TRY(alloc(ctx, &res->a_row, (size_t)cap));
@@ -1434,10 +1700,35 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
             sa.obr = res->b_row;
             fa.cap = cap;
             LIME_HIP(hipMemsetAsync(st, 0, 8 * ((size_t)ntiles + 2), S(ctx)));
-            hipLaunchKernelGGL(k_sub_fused, dim3((unsigned)ntiles), dim3(FW * 64), 0, S(ctx), sa,
-                               fa, (const uint32_t *)wstart, (const uint32_t *)wend);
+            if (ls)
+                hipLaunchKernelGGL(k_sub_fused<true>, dim3((unsigned)ntiles), dim3(FW * 64), 0,
+                                   S(ctx), sa, fa, (const uint32_t *)wstart,
+                                   (const uint32_t *)wend);
+            else
+                hipLaunchKernelGGL(k_sub_fused<false>, dim3((unsigned)ntiles), dim3(FW * 64), 0,
+                                   S(ctx), sa, fa, (const uint32_t *)wstart,
+                                   (const uint32_t *)wend);
             LIME_HIP(hipGetLastError());
+#if LIME_SUB_PHASES
+            hipLaunchKernelGGL(k_sub_phases, dim3(1), dim3(1), 0, S(ctx));
+#endif
             LIME_TRY(read_back(ctx, &total, fa.total, sizeof(total)));
+            if (sa.tn < 0) {  // (LS, B's tie index not yet built)
+                unsigned int e = 0;
+                LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
+                if (e & 4u) {  // a long same-start group: build the index, run again
+                    if (tie_runs++) return fail(LIME_ERR_DEVICE, "subtract: tie index missing");
+                    LIME_TRY(build_tie_index(ctx, B, 1));
+                    tie_args();
+                    LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
+                    release(ctx, res->gs);
+                    release(ctx, res->ge);
+                    release(ctx, res->a_row);
+                    release(ctx, res->b_row);
+                    --attempt;
+                    continue;
+                }
+            }
             if (total <= cap) break;
             release(ctx, res->gs);
             release(ctx, res->ge);

@@ -919,6 +919,41 @@ def test_subtract_runs_path(ctx, mode, t):
 
 
 @pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
+@pytest.mark.parametrize("t", [0, -3])
+def test_subtract_local_scan(ctx, mode, t, monkeypatch):
+    # B without zero-width rows and every 1024-row tile's window within 1536
+    # of B's rows takes k_sub_fused<true>: the window's prefix max and run ids
+    # by two block scans, no merge scan of B.  Book-ended rows (run breaks),
+    # duplicates, a 30-row same-start group (tie index), left rows before B
+    # and past its end, B from a tenth to 1.4x A's density and rows up to
+    # 4000 long; each against the oracle and the merge-scan path
+    # (LIME_SUB_NO_LS), which must agree record for record
+    for seed, na, nb, max_len in [(1, 9000, 900, 400), (2, 9000, 9000, 40),
+                                  (3, 9000, 12600, 60), (4, 3000, 2000, 4000),
+                                  (5, 20000, 15000, 200)]:
+        rng = np.random.default_rng(5100 + seed)
+        L = 60 * na
+        A, B = random_sets(rng, na, nb, n_contigs=3, contig_len=L, max_len=max_len,
+                           dup_frac=0.05, book_frac=0.2)
+        keep = B[2] > B[1]  # (no zero-width rows in B)
+        B = [x[keep] for x in B]
+        B[0][:30], B[1][:30] = B[0][40], B[1][40]
+        B[2][:30] = B[1][40] + rng.integers(1, 30, 30)
+        A[1][:5], A[2][:5] = 0, 3  # before B
+        A[0][5:10], A[1][5:10], A[2][5:10] = 2, L - 5, L  # past B's end
+        sp = space_for(3, L)
+        exp = oracle.subtract(A, B, t, mode)
+        res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t,
+                           mode).to_host()
+        _sub_equal(res, exp)
+        monkeypatch.setenv("LIME_SUB_NO_LS", "1")
+        ref = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), t,
+                           mode).to_host()
+        monkeypatch.delenv("LIME_SUB_NO_LS")
+        _sub_equal(ref, exp)
+
+
+@pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
 @pytest.mark.parametrize("deep", [False, True])
 def test_subtract_one_pass_and_two_pass(ctx, mode, deep):
     # threshold 0 over B's runs takes one of two launches: the one-pass
@@ -952,7 +987,7 @@ def test_subtract_one_pass_and_two_pass(ctx, mode, deep):
 
 
 @pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
-def test_subtract_sweeping_write_pass(ctx, mode):
+def test_subtract_sweeping_write_pass(ctx, mode, monkeypatch):
     # records under one per 16 blocks of 256 left rows (B covering A, C2's
     # shape) take the sweeping write pass (k_subtract<true, true, true>):
     # each workgroup tests 256 blocks and folds only those with records.
@@ -972,6 +1007,9 @@ def test_subtract_sweeping_write_pass(ctx, mode):
     B = [np.zeros(4, np.int32), np.array([0, 5, 500_001, 1_200_001], np.uint32),
          np.array([500_000, 400_000, 1_200_000, 1_500_000], np.uint32)]
     sp = space_for(1, L)
+    # (B has no zero-width rows: without LIME_SUB_NO_LS this takes the local
+    # scan's one pass)
+    monkeypatch.setenv("LIME_SUB_NO_LS", "1")
     res = ctx.subtract(ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B), 0, mode).to_host()
     exp = oracle.subtract(A, B, 0, mode)
     assert 0 < len(exp["start"]) * 16 < (n + 255) // 256

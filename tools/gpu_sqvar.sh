@@ -5,7 +5,7 @@ set -o pipefail
 T=$1; W=$2; K=$3; shift 3
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS"
+C=${SQC:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS"}
 for lib in "$@"; do
   unset LIME_AMD_LIB_VARIANT
   [ "$lib" != new ] && export LIME_AMD_LIB_VARIANT=$PWD/$lib

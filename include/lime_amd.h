@@ -45,7 +45,7 @@ extern "C" {
 
 /* 2: lime_set_lower_bound / _first_reaching return -(LIME_ERR_*) on error
  *    (was -1); lime_pairs_checksum_device and the sharded-path helpers added */
-#define LIME_ABI_VERSION 4
+#define LIME_ABI_VERSION 5
 
 /* status codes */
 #define LIME_OK 0
@@ -86,8 +86,13 @@ int lime_ctx_destroy(lime_ctx *ctx);
  * stream); NULL restores the context's own stream. */
 int lime_ctx_set_stream(lime_ctx *ctx, void *hip_stream);
 int lime_ctx_synchronize(lime_ctx *ctx);
-/* bytes currently held by the context's device pool */
+/* bytes currently held by the context's device pool (live blocks and the
+ * cached free ones) */
 int64_t lime_ctx_pool_bytes(const lime_ctx *ctx);
+/* bytes of the pool's LIVE blocks (what the context's objects and any call
+ * in flight hold); *peak (may be NULL) = their high-water mark since the
+ * last reset, reset to the live bytes when reset_peak != 0 */
+int64_t lime_ctx_pool_live_bytes(lime_ctx *ctx, int32_t reset_peak, int64_t *peak);
 
 /* ------------------------------------------------------------------- space */
 /* Contig ids are 0..n-1 in the caller's order, which must be Java String
@@ -329,9 +334,18 @@ int lime_result_format_bed(const lime_result *res, const char *const *names, cha
 /* ----------------------------------------------------- bit-per-base path */
 /* The bit-per-base set straight from UNSORTED device rows (u32 contig-local
  * coordinates, as lime_set_create_device): rows are only grouped by 2^22-base
- * bin and then by 2^19-base paint tile (two counting scatters) and painted
- * tile by tile -- no sort and no merge.  Same bits as lime_bitset_from_set
- * on the sorted set. */
+ * bin and then by 2^19-base paint tile (two counting scatters) -- no sort and
+ * no merge.  Same bits as lime_bitset_from_set on the sorted set.
+ * Memory (this and every *_from_device / *_from_global entry point below):
+ * the bitset KEEPS its input rows in binned form for its lifetime, so that
+ * an op's runs come straight from the bins (one paint per tile, no stored
+ * words): 4 B per row (packed start / length, paint-tile order) + 16 B per
+ * cross piece (a row crossing a paint tile, ~len / 2^19 of rows) + ~16 B per
+ * 2^19-base paint tile, per input set.  The words (window bits / 8 B, 386 MB
+ * over hg38) are painted on first need (popcount, an op whose other operand
+ * is not binned, an AND past 16 sets) and are then held as well.  C5's
+ * 8 x 1.25e8 rows: 4.0 GB of bins (against 386 MB of words);
+ * lime_bitset_drop_bins trades them for the words. */
 int lime_bitset_from_device(lime_ctx *ctx, const lime_space *space, int64_t n,
                             const int32_t *d_contig, const uint32_t *d_start,
                             const uint32_t *d_end, lime_bitset **out);
@@ -371,6 +385,10 @@ int lime_bitset_runs(lime_ctx *ctx, int op, const lime_bitset *a, const lime_bit
 int lime_bitset_and_runs(lime_ctx *ctx, int k, const lime_bitset *const *sets, lime_result **out,
                          int64_t *n_runs);
 int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
+/* Paint the words (if not yet painted) and free the binned rows a bitset
+ * built from rows keeps: it then holds window bits / 8 bytes, and every op
+ * reads its words (same bits, same runs).  No-op for a bitset without bins. */
+int lime_bitset_drop_bins(lime_ctx *ctx, lime_bitset *bs);
 int lime_bitset_destroy(lime_bitset *bs);
 
 /* ------------------------------------------------------ range sharding */

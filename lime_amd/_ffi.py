@@ -25,7 +25,7 @@ ERRORS = {
 }
 # the C-ABI contract this binding is written against (include/lime_amd.h
 # LIME_ABI_VERSION): checked at load, so a stale library fails loudly
-ABI_VERSION = 4
+ABI_VERSION = 5
 SUBTRACT_LIME = 0
 SUBTRACT_SET = 1
 
@@ -57,6 +57,7 @@ SIGNATURES = {
     "lime_ctx_set_stream": (C.c_int, [vp, vp]),
     "lime_ctx_synchronize": (C.c_int, [vp]),
     "lime_ctx_pool_bytes": (i64, [vp]),
+    "lime_ctx_pool_live_bytes": (i64, [vp, C.c_int32, P(i64)]),
     "lime_space_create": (C.c_int, [i32, P(i64), pp]),
     "lime_space_destroy": (C.c_int, [vp]),
     "lime_space_contigs": (i32, [vp]),
@@ -121,6 +122,7 @@ SIGNATURES = {
     "lime_bitset_runs": (C.c_int, [vp, C.c_int, vp, vp, pp, P(i64)]),
     "lime_bitset_and_runs": (C.c_int, [vp, C.c_int, P(vp), pp, P(i64)]),
     "lime_bitset_popcount": (i64, [vp, vp]),
+    "lime_bitset_drop_bins": (C.c_int, [vp, vp]),
     "lime_bitset_destroy": (C.c_int, [vp]),
     "lime_synth_uniform": (C.c_int, [vp, vp, i64, u64, u32, u32, vp, vp, vp]),
     "lime_synth_pileup": (C.c_int, [vp, vp, i64, u64, i64, u32, u32, u32, vp, vp, vp]),

@@ -1597,6 +1597,20 @@ int bitset_paint(lime_ctx *ctx, const lime_bitset *cbs) {
     return LIME_OK;
 }
 
+// the words painted (if not yet) and the binned rows released: the bitset
+// then holds span / 8 bytes, and every op reads its words
+int bitset_drop_bins(lime_ctx *ctx, lime_bitset *bs) {
+    LIME_TRY(bitset_paint(ctx, bs));
+    for (auto &b : bs->bins) {
+        release(ctx, b.slab2);
+        if (b.own_tstart) release(ctx, b.tstart);
+        release(ctx, b.xl);
+        release(ctx, b.xb);
+    }
+    bs->bins.clear();
+    return LIME_OK;
+}
+
 // the AND of k row sets' bits over window [lo, hi), straight from their
 // unsorted rows: every set binned (bin_rows) and kept, so the bitset is
 // their AND in binned form -- its runs come from one k_paint_ev over all the

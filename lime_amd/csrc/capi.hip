@@ -32,6 +32,8 @@ void *Pool::get(size_t bytes) {
         if (b.ev) spare_events.push_back(b.ev);
         free_blocks.erase(it);
         live[p] = bytes;
+        in_use += (int64_t)bytes;
+        peak = std::max(peak, in_use);
         return p;
     }
     void *p = nullptr;
@@ -51,6 +53,8 @@ void *Pool::get(size_t bytes) {
     }
     held += (int64_t)bytes;
     live[p] = bytes;
+    in_use += (int64_t)bytes;
+    peak = std::max(peak, in_use);
     return p;
 }
 void Pool::put(void *p) {
@@ -70,6 +74,7 @@ void Pool::put(void *p) {
         if (!b.ev) hipStreamSynchronize(stream ? *stream : nullptr);  // ...and drain instead
     }
     free_blocks.emplace(it->second, b);
+    in_use -= (int64_t)it->second;
     live.erase(it);
 }
 void Pool::release_all() {
@@ -82,7 +87,7 @@ void Pool::release_all() {
     free_blocks.clear();
     live.clear();
     spare_events.clear();
-    held = 0;
+    held = in_use = 0;
 }
 
 int read_back(lime_ctx *c, void *host, const void *dev, size_t bytes) {
@@ -145,6 +150,7 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
 void bitset_free(lime_bitset *bs);
+int bitset_drop_bins(lime_ctx *ctx, lime_bitset *bs);
 int synth(lime_ctx *ctx, const lime_space *sp, int kind, int64_t first, int64_t n, uint64_t seed,
           uint32_t lo, uint32_t hi, int64_t n_centres, uint32_t sigma, int32_t *d_contig,
           uint32_t *d_start, uint32_t *d_end);
@@ -425,6 +431,12 @@ int lime_ctx_synchronize(lime_ctx *ctx) {
 }
 
 int64_t lime_ctx_pool_bytes(const lime_ctx *ctx) { return ctx ? ctx->pool.held : 0; }
+int64_t lime_ctx_pool_live_bytes(lime_ctx *ctx, int32_t reset_peak, int64_t *peak) {
+    if (!ctx) return 0;
+    if (peak) *peak = ctx->pool.peak;
+    if (reset_peak) ctx->pool.peak = ctx->pool.in_use;
+    return ctx->pool.in_use;
+}
 
 // ------------------------------------------------------------------- space
 int lime_space_create(int32_t n, const int64_t *lengths, lime_space **out) {
@@ -1541,6 +1553,12 @@ int64_t lime_bitset_popcount(lime_ctx *ctx, const lime_bitset *a) {
     if (!ctx || !a || a->ctx != ctx) return -1;
     hipSetDevice(ctx->device);
     return bitset_popcount(ctx, a);
+}
+
+int lime_bitset_drop_bins(lime_ctx *ctx, lime_bitset *bs) {
+    if (!ctx || !bs || bs->ctx != ctx) return fail(LIME_ERR_ARG, "bad bitset");
+    hipSetDevice(ctx->device);
+    return bitset_drop_bins(ctx, bs);
 }
 
 int lime_bitset_destroy(lime_bitset *bs) {

@@ -56,6 +56,7 @@ struct Pool {
     const hipStream_t *stream = nullptr;  // the owning context's current stream
     bool multi_stream = false;
     int64_t held = 0;
+    int64_t in_use = 0, peak = 0;  // bytes of live blocks; their high-water mark
     void *get(size_t bytes);
     void put(void *p);
     void release_all();

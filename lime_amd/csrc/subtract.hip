@@ -841,11 +841,14 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
 // CU the sparse 1e9-row subtract took the same time)
 // (20 KiB of LDS -- a 1152-row window, 384 staged records -- for 8 waves per
 // SIMD cost 12 VGPR spills and the sparse 1e9-row subtract 11.8 -> 13.3 ms)
+#ifndef LIME_SUB_FW
+#define LIME_SUB_FW 8
+#endif
 #ifndef LIME_SUB_FCAP
-#define LIME_SUB_FCAP 448
+#define LIME_SUB_FCAP (112 * LIME_SUB_FW)
 #endif
 #ifndef LIME_SUB_FWIN
-#define LIME_SUB_FWIN 1536
+#define LIME_SUB_FWIN (384 * LIME_SUB_FW)
 #endif
 #ifndef LIME_SUB_LS
 #define LIME_SUB_LS 1
@@ -859,7 +862,7 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
 constexpr int FCAP = LIME_SUB_FCAP;
 // 1024 left rows per tile, the count pass's window (2048-row tiles with a
 // 3072-row window: the sparse 1e9-row subtract's pass 9.6 -> 10.2 ms)
-constexpr int FW = 4, FROWS = FW * SUB_B, FWIN = LIME_SUB_FWIN;
+constexpr int FW = LIME_SUB_FW, FROWS = FW * SUB_B, FWIN = LIME_SUB_FWIN;
 struct FusedArgs {
     uint64_t *st;          // per-tile status words (zeroed)
     unsigned int *ticket;  // tile ticket (zeroed)

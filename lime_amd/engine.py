@@ -307,6 +307,12 @@ class Bitset:
     def popcount(self):
         return int(_lib().lime_bitset_popcount(self.ctx.handle, self._h))
 
+    def drop_bins(self):
+        """paint the words and free the binned rows a bitset from rows keeps
+        (4 B per row per input set): same bits, window bits / 8 bytes held"""
+        check(_lib().lime_bitset_drop_bins(self.ctx.handle, self._h))
+        return self
+
     def window(self):
         """(lo, n_words): the global bits this bitset covers start at lo"""
         lo, nw = i64(), i64()
@@ -347,6 +353,12 @@ class Context:
 
     def pool_bytes(self):
         return int(_lib().lime_ctx_pool_bytes(self._h))
+
+    def pool_live_bytes(self, reset_peak=False):
+        """(live bytes, their peak since the last reset) of the device pool"""
+        peak = i64()
+        live = _lib().lime_ctx_pool_live_bytes(self._h, int(bool(reset_peak)), C.byref(peak))
+        return int(live), int(peak.value)
 
     # ------------------------------------------------------------ sets
     def set_from_host(self, space, contig, start, end):

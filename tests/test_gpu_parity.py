@@ -651,6 +651,35 @@ def test_bitset_and_fused(ctx, k, max_len):
         assert got[key].tolist() == exp[key].tolist()
 
 
+def test_bitset_drop_bins(ctx):
+    # lime_bitset_drop_bins: a bitset from rows (and the fused AND of 3 row
+    # sets) paints its words and frees its binned rows; every op's runs and
+    # the popcount are unchanged, and a second call is a no-op
+    rng = np.random.default_rng(91)
+    sets = [random_sets(rng, 20000, 1, n_contigs=3, contig_len=3_000_000, max_len=3000,
+                        zero_frac=0.05, dup_frac=0.02)[0] for _ in range(3)]
+    sp = space_for(3, 3_000_000)
+    dev = [_dev_rows(A) for A in sets]
+    rows = [(len(A[0]), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr())
+            for A, t in zip(sets, dev)]
+    a, b = (ctx.bitset_from_device(sp, *r) for r in rows[:2])
+    fused = ctx.bitset_and_from_device(sp, rows)
+
+    def runs(op, x, y=None):
+        h = ctx.bitset_runs(op, x, y).to_host()
+        return [h[k].tolist() for k in ("contig", "start", "end")]
+
+    before = [runs(0, fused), runs(1, a), runs(2, a, b), runs(3, a, b),
+              a.popcount(), fused.popcount()]
+    for x in (a, b, fused):
+        x.drop_bins()
+    fused.drop_bins()
+    after = [runs(0, fused), runs(1, a), runs(2, a, b), runs(3, a, b),
+             a.popcount(), fused.popcount()]
+    assert len(before[0][0]) > 0 and before[4] > 0
+    assert after == before
+
+
 def test_bitset_binned_runs_tile_edges(ctx):
     # bitsets from rows stay binned; an op's runs come straight from the bins
     # (k_paint_ev: per 2^19-base paint tile, events with the bit before the

@@ -1682,16 +1682,19 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     if (fused) {  // one pass: counts, places (look-back) and records
         const int64_t ntiles = blocks_for(na, FROWS);
         uint64_t *st;
-        LIME_TRY(alloc(ctx, &st, (size_t)ntiles + 2));  // + ticket, total
+        LIME_TRY(alloc(ctx, &st, (size_t)ntiles + 3));  // + ticket, total, error flags
         PoolGuard<uint64_t> gs_{ctx, st};
         FusedArgs fa;
         fa.st = st;
         fa.ticket = reinterpret_cast<unsigned int *>(st + ntiles);
         fa.total = st + ntiles + 1;
         fa.ntiles = ntiles;
+        // (the error flags beside the total: one read-back brings both)
+        sa.err = reinterpret_cast<unsigned int *>(st + ntiles + 2);
         // records rarely pass one per left row; past the guess the pass runs
         // again at the exact total
         uint64_t cap = (uint64_t)na + 4096, total = 0;
+        unsigned int fe = 0;
         for (int attempt = 0, tie_runs = 0; attempt < 2; ++attempt) {
             LIME_TRY(alloc(ctx, &res->gs, (size_t)cap));
             LIME_TRY(alloc(ctx, &res->ge, (size_t)cap));
@@ -1702,7 +1705,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
             sa.oar = res->a_row;
             sa.obr = res->b_row;
             fa.cap = cap;
-            LIME_HIP(hipMemsetAsync(st, 0, 8 * ((size_t)ntiles + 2), S(ctx)));
+            LIME_HIP(hipMemsetAsync(st, 0, 8 * ((size_t)ntiles + 3), S(ctx)));
             if (ls)
                 hipLaunchKernelGGL(k_sub_fused<true>, dim3((unsigned)ntiles), dim3(FW * 64), 0,
                                    S(ctx), sa, fa, (const uint32_t *)wstart,
@@ -1715,15 +1718,15 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
 #if LIME_SUB_PHASES
             hipLaunchKernelGGL(k_sub_phases, dim3(1), dim3(1), 0, S(ctx));
 #endif
-            LIME_TRY(read_back(ctx, &total, fa.total, sizeof(total)));
+            uint64_t te[2];  // total, error flags
+            LIME_TRY(read_back(ctx, te, fa.total, sizeof(te)));
+            total = te[0];
+            fe = (unsigned int)te[1];
             if (sa.tn < 0) {  // (LS, B's tie index not yet built)
-                unsigned int e = 0;
-                LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
-                if (e & 4u) {  // a long same-start group: build the index, run again
+                if (fe & 4u) {  // a long same-start group: build the index, run again
                     if (tie_runs++) return fail(LIME_ERR_DEVICE, "subtract: tie index missing");
                     LIME_TRY(build_tie_index(ctx, B, 1));
                     tie_args();
-                    LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
                     release(ctx, res->gs);
                     release(ctx, res->ge);
                     release(ctx, res->a_row);
@@ -1742,9 +1745,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
         // (the second attempt ran at the first one's exact total: a larger
         // total now means the passes disagree, and the arrays hold only cap)
         if (total > cap) return fail(LIME_ERR_DEVICE, "subtract: record total changed between passes");
-        unsigned int e = 0;
-        LIME_TRY(read_back(ctx, &e, err, sizeof(e)));
-        if (e) return fail(LIME_ERR_DEVICE, "subtract: the writing fold differs from the count");
+        if (fe) return fail(LIME_ERR_DEVICE, "subtract: the writing fold differs from the count");
         res->n = (int64_t)total;
         return LIME_OK;
     }

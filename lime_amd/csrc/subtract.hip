@@ -956,14 +956,32 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
     const int nst = __builtin_amdgcn_readfirstlane(
         (int)min(min((int64_t)FWIN, sa.nb - wlo),
                  LIME_SUB_WEND ? (int64_t)wend[tile] + 1 - wlo : (int64_t)FWIN));
-    for (int k = threadIdx.x; k < nst; k += FW * 64) {
-        if constexpr (LS) {
-            w_pm[k] = sa.bge[wlo + k];  // (ends: scanned below)
-            w_gs[k] = sa.bgs[wlo + k];
-        } else {
-            w_pm[k] = sa.bpmax[wlo + k];
-            w_gs[k] = sa.bgs[wlo + k];
-            w_run[k] = sa.brun[wlo + k];
+    {
+        // every staging load issued before any is stored: SPT rows per
+        // thread, the index clamped into B (a loop bounded by nst waited for
+        // its loads every one or two rows: 3-4 serial round trips per tile)
+        constexpr int SPT = (FWIN + FW * 64 - 1) / (FW * 64);
+        uint32_t v0[SPT], v1[SPT], v2[SPT];
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int64_t j = min(wlo + threadIdx.x + i * FW * 64, sa.nb - 1);
+            if constexpr (LS) {
+                v0[i] = sa.bge[j];  // (ends: scanned below)
+                v1[i] = sa.bgs[j];
+            } else {
+                v0[i] = sa.bpmax[j];
+                v1[i] = sa.bgs[j];
+                v2[i] = sa.brun[j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int k = threadIdx.x + i * FW * 64;
+            if (k < nst) {
+                w_pm[k] = v0[i];
+                w_gs[k] = v1[i];
+                if constexpr (!LS) w_run[k] = v2[i];
+            }
         }
     }
     __syncthreads();

@@ -1482,14 +1482,11 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             }
         }
     const bool bucket_cand = TB != 0;
-#ifndef LIME_SORT_DB9LAST
-#define LIME_SORT_DB9LAST 1
-#endif
     // 8 + 8, 8 + 9, 9 + 9 bits: at TB = 17 the 9-bit digit goes second,
     // where its runs of ~16 rows per digit and tile carry u32 ends (64-B
     // pieces) instead of u16 widths (32 B), and the first pass reads the
     // prep's rows with 256 digits: 1e9-row sort 22.34 -> 22.03 ms, same box
-    const int DB1 = LIME_SORT_DB9LAST ? TB / 2 : TB - TB / 2, DB2 = TB - DB1;
+    const int DB1 = TB / 2, DB2 = TB - DB1;
     // (the digit-count matrix serves both bucket passes: sized for the wider)
     const int mat_bits = bucket_cand ? std::max(DB1, DB2) : 8;
     LIME_TRY(alloc(ctx, &mat, ((size_t)1 << mat_bits) * (ntiles ? ntiles : 1)));
@@ -1574,11 +1571,8 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             if (TB == 16)
                 LIME_TRY((bucket_passes<8, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
                                               mat, mat_bits, ntiles, a, o, k0, e0)));
-            else if (TB == 17 && DB1 == 8)
-                LIME_TRY((bucket_passes<8, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, mat_bits, ntiles, a, o, k0, e0)));
             else if (TB == 17)
-                LIME_TRY((bucket_passes<9, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
+                LIME_TRY((bucket_passes<8, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
                                               mat, mat_bits, ntiles, a, o, k0, e0)));
             else
                 LIME_TRY((bucket_passes<9, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,

@@ -850,15 +850,6 @@ __global__ __launch_bounds__(CNT_WAVES * 64) void k_sub_count_runs(SubArgs sa, i
 #ifndef LIME_SUB_FWIN
 #define LIME_SUB_FWIN (384 * LIME_SUB_FW)
 #endif
-#ifndef LIME_SUB_LS
-#define LIME_SUB_LS 1
-#endif
-#ifndef LIME_SUB_KEEP
-#define LIME_SUB_KEEP 1
-#endif
-#ifndef LIME_SUB_WEND
-#define LIME_SUB_WEND 1
-#endif
 constexpr int FCAP = LIME_SUB_FCAP;
 // 1024 left rows per tile, the count pass's window (2048-row tiles with a
 // 3072-row window: the sparse 1e9-row subtract's pass 9.6 -> 10.2 ms)
@@ -924,11 +915,7 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
 #if LIME_SUB_PHASES
     uint64_t ph_t = wall_clock64(), ph_d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-#if LIME_SUB_BLOCKID  // (measurement only: dispatch order is not guaranteed)
-    if (threadIdx.x == 0) s_tile = blockIdx.x;
-#else
     if (threadIdx.x == 0) s_tile = atomicAdd(fa.ticket, 1u);
-#endif
     __syncthreads();
     SUB_PH(0);
     // (uniform values held in scalar registers: every VGPR here costs
@@ -955,7 +942,7 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
     // of the 1536 rows a fixed window staged)
     const int nst = __builtin_amdgcn_readfirstlane(
         (int)min(min((int64_t)FWIN, sa.nb - wlo),
-                 LIME_SUB_WEND ? (int64_t)wend[tile] + 1 - wlo : (int64_t)FWIN));
+                 (int64_t)wend[tile] + 1 - wlo));
     {
         // every staging load issued before any is stored: SPT rows per
         // thread, the index clamped into B (a loop bounded by nst waited for
@@ -1358,7 +1345,7 @@ __global__ __launch_bounds__(FW * 64) void k_sub_fused(SubArgs sa, FusedArgs fa,
         // (LS: the row's start, end and bounds from the counting lane's
         // registers, no reload and no second search; the merge-scan form
         // has no registers to spare: 78 -> 89 VGPRs, 6 -> 5 waves)
-        constexpr bool KEEP = LS && LIME_SUB_KEEP;
+        constexpr bool KEEP = LS;
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
             const uint32_t v_cnt = __shfl(cnt[k], src), v_ex = __shfl(ex[k], src);
@@ -1594,7 +1581,7 @@ int subtract_run(lime_ctx *ctx, const lime_set *A, const lime_set *B, int64_t th
     PoolGuard<uint32_t> gwe{ctx, wend};
     bool ls = false;
     // (LIME_SUB_NO_LS set: the merge-scan paths, as tests force them)
-    if (runs && !B->has_zero_width && LIME_SUB_LS && !getenv("LIME_SUB_NO_LS")) {
+    if (runs && !B->has_zero_width && !getenv("LIME_SUB_NO_LS")) {
         const int64_t nt = blocks_for(na, FROWS);
         unsigned int *wm;
         LIME_TRY(alloc(ctx, &wm, 1));

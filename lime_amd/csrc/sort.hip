@@ -1160,11 +1160,6 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
             rk[it] = r;
         }
     }
-#ifdef LIME_MID_EXP_IDENT
-#pragma unroll
-    for (int it = 0; it < ITEMS; ++it)  // (timing experiment: identity output order)
-        if (rk[it] != 0xffffffffu) rk[it] = u[it] & ((1u << POSB) - 1u);
-#endif
 #pragma unroll
     for (int round = 0; round < 3; ++round) {
         __syncthreads();  // (T free: ranks taken / the previous round stored)

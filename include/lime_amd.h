@@ -271,6 +271,13 @@ int lime_closest_count_chained(lime_ctx *ctx, const lime_set *a, const lime_set 
 
 /* ------------------------------------------------------------ merge et al. */
 int lime_merge(lime_ctx *ctx, const lime_set *a, lime_result **out, int64_t *n_runs);
+/* DistributedSubtract of b from a (Subtract.scala:78-116), mode
+ * LIME_SUBTRACT_LIME or LIME_SUBTRACT_SET.  At threshold <= 0 the blocks are
+ * b's merge runs; when b has no zero-width rows and every 2048-row tile of a
+ * sees at most 3072 rows of b, one pass derives them from b's rows in its
+ * window (no merge scan of b); else b's merge scan runs first.  The
+ * environment variable LIME_SUB_NO_LS (any value) forces the latter (tests
+ * compare the two). */
 int lime_subtract(lime_ctx *ctx, const lime_set *a, const lime_set *b, int64_t threshold,
                   int mode, lime_result **out, int64_t *n_regions);
 int lime_complement(lime_ctx *ctx, const lime_space *genome_space, const lime_set *a,

@@ -1008,6 +1008,7 @@ __global__ __launch_bounds__(BB) void k_popcount(const uint64_t *__restrict__ w,
 #endif
 constexpr int EV_NT = LIME_EV_NT, EV_W = LIME_EV_W, EV_TW = EV_NT * EV_W;
 constexpr int EVCAP = LIME_EVCAP;  // events of a tile staged in LDS
+constexpr int EVSLOT_MAX = 2 * TWORDS;  // k_paint_ev's largest slot (staged in its image)
 
 }  // namespace
 
@@ -1302,7 +1303,7 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a, AndArgs s) {
     __shared__ unsigned long long img[img_words(TWORDS)];
     __shared__ uint32_t scratch[PAINTB / 64 + 1];
     __shared__ uint32_t s_last;
-    static_assert(16384 * 4 <= sizeof(img), "the event slot (<= 16384) staged in img");
+    static_assert(EVSLOT_MAX * 4 <= sizeof(img), "the event slot (<= EVSLOT_MAX) staged in img");
     const int t = blockIdx.x;
     uint64_t acc[AWPT];
 #pragma unroll
@@ -1724,7 +1725,7 @@ struct EvPlan {
         for (int i = 0; i < nin && bound >= 0; ++i)
             bound = sets[i]->runs_bound < 0 ? -1 : bound + sets[i]->runs_bound;
         cap = bound < 0 ? 16384 : 2 * (2 * bound / std::max<int64_t>(nt, 1)) + 2048;
-        cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), 16384);
+        cap = std::min<int64_t>(std::max<int64_t>((cap + 255) / 256 * 256, 4096), EVSLOT_MAX);
         pa.cap = (uint32_t)cap;
         LIME_TRY(bag.get(&pa.tev, (size_t)nt * (size_t)cap));
         LIME_TRY(bag.get(&pa.tcnt, (size_t)nt));

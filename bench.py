@@ -556,10 +556,18 @@ def bench_c3(args, ctx, space, dev, world, rank, comm_dev, ev, brief=False):
         else:
             S = ctx.set_from_device(space, m, *(c.data_ptr() for c in cols))
             mg = ctx.merge(S)
-            gaps = ctx.complement(space, S)
+            # the complement from the merge's runs (as the sharded path:
+            # one merge scan per step, Complement.scala's gaps of its runs)
+            k = mg.n
+            rgs = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+            rge = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+            if k:
+                mg.copy_rows_device(0, k, rgs.data_ptr(), rge.data_ptr())
+            gaps = ctx.complement_runs(space, k, rgs.data_ptr(), rge.data_ptr())
             runs, ng = mg.n, gaps.n
             for h in (gaps, mg, S):
                 h.close()
+            del rgs, rge
         if last_step:
             state["t"] = (t0, ev())
         state["runs"], state["gaps"] = runs, ng

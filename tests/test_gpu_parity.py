@@ -385,6 +385,33 @@ def test_complement_parity(ctx, seed, zero):
         assert list(res[k]) == list(exp[k]), k
 
 
+@pytest.mark.parametrize("seed,zero", [(33, 0.0), (34, 0.1), (35, None)])
+def test_complement_of_merge_runs(ctx, seed, zero):
+    # bench.py's C3 step: the complement from the merge's runs
+    # (lime_complement_runs over [0, span)) equals lime_complement of the set
+    import torch
+    rng = np.random.default_rng(seed)
+    if zero is None:  # no rows at all: every contig one gap
+        A = (np.zeros(0, np.int32), np.zeros(0, np.int64), np.zeros(0, np.int64))
+    else:
+        A, _ = random_sets(rng, 5000, 1, n_contigs=3, contig_len=50000, max_len=400,
+                           zero_frac=zero, book_frac=0.1)
+    lens = [50000, 50000, 50000, 777]
+    sp = Space(NAMES, lens)
+    S = ctx.set_from_host(sp, *A)
+    mg = ctx.merge(S)
+    k = mg.n
+    dev = torch.device("cuda", 0)
+    gs = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+    ge = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+    if k:
+        mg.copy_rows_device(0, k, gs.data_ptr(), ge.data_ptr())
+    got = ctx.complement_runs(sp, k, gs.data_ptr(), ge.data_ptr()).to_host()
+    exp = oracle.complement(A, lens)
+    for key in ("contig", "start", "end"):
+        assert list(got[key]) == list(exp[key]), key
+
+
 def test_sorted_set_order(ctx):
     rng = np.random.default_rng(41)
     A, _ = random_sets(rng, 50000, 1, n_contigs=4, contig_len=100000, zero_frac=0.1,

@@ -362,10 +362,12 @@ struct ScanGeom {
     static constexpr int RW = RQ * 256;        // rows per wave
     static constexpr int TILE = NW * RW;       // rows per tile
 };
-// 512 threads x 32 rows: 16384-row tiles (as k_merge_scan: as few
-// look-backs), two workgroups per CU (<= 128 VGPRs)
+// 1024 threads x 32 rows: 32768-row tiles, one workgroup per CU (<= 128
+// VGPRs): half the look-backs of 16384-row tiles at two per CU, C3's merge
+// 1.355 -> 1.313 ms; 8192-row tiles at four per CU: 1.55 ms
+// (profiles/round5/merge_scan2_tiles_ab.txt)
 #ifndef LIME_MS2_NT
-#define LIME_MS2_NT 512
+#define LIME_MS2_NT 1024
 #endif
 #ifndef LIME_MS2_Q
 #define LIME_MS2_Q 8

@@ -205,17 +205,106 @@ def c5_cpu_baseline(scale, per_full, k=8, reps=3):
                       "by contig; every merge sorts its input inside the timed region"}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, script=None, argv=None):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes
+    of this script, one rank per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, rendezvous on 127.0.0.1), before this process has touched
+    the GPU (torch is not even imported here).  Rank 0's stdout is relayed
+    line by line; its JSON line must report n_gpus == N.  If any child fails,
+    the others are terminated and its exit status is returned."""
+    import subprocess
+    import threading
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)]
+                                      + list(sys.argv[1:] if argv is None else argv),
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None,
+                                      text=True))
+    lines = []
+
+    def stop_children(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        sys.exit(128 + signum)
+    import signal
+    signal.signal(signal.SIGTERM, stop_children)
+    signal.signal(signal.SIGINT, stop_children)
+
+    def relay():
+        for ln in procs[0].stdout:
+            lines.append(ln)
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    if rc:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        print(f"bench.py: a rank exited with status {rc}; the others were stopped",
+              file=sys.stderr)
+        return rc if rc > 0 else 1
+    th.join(timeout=30)
+    rec = None
+    for ln in lines:
+        try:
+            rec = json.loads(ln)
+        except ValueError:
+            continue
+    if rec is None or rec.get("n_gpus") != n:
+        print(f"bench.py: rank 0 did not report n_gpus == {n}", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}")
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and ndev < world:
+        sys.exit(f"bench.py: RCCL needs one GPU per rank ({world} ranks, {ndev} GPUs); "
+                 "--dist-backend gloo rehearses the sharded path with ranks sharing a GPU")
     # one rank per GPU; --dist-backend gloo lets several ranks share one GPU
     # (rehearsal of the multi-GPU path on a 1-GPU box, rows staged on the host)
-    gpu = local % max(torch.cuda.device_count(), 1)
+    gpu = local % max(ndev, 1)
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     comm_dev = None  # RCCL: device buffers
@@ -277,6 +366,10 @@ def main():
             ops[name] = fi(measure(st, args.ops_steps, 1))
             fi.release()
         line["operators"] = ops
+    line.setdefault("config", {}).update(
+        {"world_size": world, "dist_backend": args.dist_backend if world > 1 else None,
+         "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+         else ("bench.py --gpus N (own ranks)" if world > 1 else None)})
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -127,6 +127,11 @@ class ShardStep:
     def _i32(self, n):
         return torch.empty(max(int(n), 1), dtype=torch.int32, device=self.dev)
 
+    def _need_splits(self, what):
+        if self.splits is None:
+            raise RuntimeError(f"ShardStep.{what}: no shard bounds yet -- call "
+                               "plan_splits(inputs) with every input set first (or load())")
+
     # ----------------------------------------------------------- routing
     def plan_splits(self, inputs):
         """count-balanced shard bounds from this rank's inputs [(n, d_contig,
@@ -139,7 +144,10 @@ class ShardStep:
     def route(self, n, d_contig, d_start, d_end, row_base=0, d_strand=None):
         """this rank's slice of unsorted rows -> the rows this shard owns:
         [gs, ge, row(, strand)] int32 device tensors (global coordinates and
-        row ids), one packed all_to_all (lime_route_rows + dist.exchange)"""
+        row ids), one packed all_to_all (lime_route_rows + dist.exchange).
+        Without planned bounds only the first routed set is sampled: callers
+        with several inputs (run(A, B), subtract) should call plan_splits with
+        all of them first, as bench.py does, so that skew in any is balanced."""
         ctx, sp = self.ctx, self.space
         if self.splits is None:
             self.plan_splits([(n, d_contig, d_start)])
@@ -238,6 +246,7 @@ class ShardStep:
         end passes split[r] (a superset of the rows overlapping r's range;
         extra rows overlap nothing there).  Device rows, in order."""
         w, me = self.world, self.rank
+        self._need_splits("subtract")
         later = list(range(me + 1, w))
         got = dict(zip(later, S.first_reachings([min(self.splits[r], 0xFFFFFFFF)
                                                  for r in later])))
@@ -274,10 +283,13 @@ class ShardStep:
         mine = torch.tensor([-1, bmin, bmax, int(bz)] if B.n else [-1, 1 << 32, 0, 0],
                             dtype=torch.int64, device=self.dev)
         if A.n:
-            g = self._i32(1)
-            A.copy_rows_device(A.n - 1, 1, g.data_ptr(), self._i32(1).data_ptr(),
-                               self._i32(1).data_ptr())
+            # (the unused end / row destinations stay referenced until the
+            # sync: the engine's copy lands in them asynchronously)
+            g, ge_scratch, row_scratch = self._i32(1), self._i32(1), self._i32(1)
+            A.copy_rows_device(A.n - 1, 1, g.data_ptr(), ge_scratch.data_ptr(),
+                               row_scratch.data_ptr())
             self._sync()
+            del ge_scratch, row_scratch
             mine[0] = (g[0].to(torch.int64) & 0xFFFFFFFF) + amax
         t = torch.empty(w * 4, dtype=torch.int64, device=cd)
         dist.all_gather_into_tensor(t, mine.to(cd), group=self.group)
@@ -336,6 +348,7 @@ class ShardStep:
         data, :39-45, fall to the shard holding their start).  The shards'
         gaps concatenate to the unsharded result.  `m`: this shard's merge()
         of S when the caller has it (kept open), else merged here."""
+        self._need_splits("complement")
         own = m is None
         if own:
             m = self.merge(S)
@@ -456,9 +469,16 @@ class ShardedBitset:
         self.lo, self.hi = self.splits[self.rank], self.splits[self.rank + 1]
         return self.splits
 
+    def _ensure_splits(self, inputs):
+        """the shard windows, sampled from `inputs` when none were given
+        (collective: every rank calls the same entry point)"""
+        if self.splits is None:
+            self.plan_splits(inputs)
+
     def shard_rows(self, n, d_contig, d_start, d_end):
         """this rank's slice of one set's rows -> the rows of this shard's
         window from every rank (global coordinates, clipped): (m, gs, ge)"""
+        self._ensure_splits([(n, d_contig, d_start, d_end)])
         gs, ge, counts = self._route_clipped(n, d_contig, d_start, d_end)
         self._sync()
         (rgs, rge), rc = ld.exchange([gs, ge], counts, self.group, self.comm, packed=True)
@@ -471,6 +491,7 @@ class ShardedBitset:
         ctx, sp = self.ctx, self.space
         if self.world == 1:
             return ctx.bitset_from_device(sp, n, d_contig, d_start, d_end)
+        self._ensure_splits([(n, d_contig, d_start, d_end)])
         m, rgs, rge = self.shard_rows(n, d_contig, d_start, d_end)
         return ctx.bitset_from_global(sp, self.lo, self.hi, m, rgs.data_ptr(), rge.data_ptr())
 
@@ -498,6 +519,7 @@ class ShardedBitset:
         ctx, sp = self.ctx, self.space
         if self.world == 1:
             return ctx.bitset_and_from_device(sp, inputs)
+        self._ensure_splits(inputs)
         routed = [self._route_clipped(*x) for x in inputs]
         self._sync()
         got = ld.exchange_sets([[g, e] for g, e, _ in routed], [c for _, _, c in routed],
@@ -516,8 +538,7 @@ class ShardedBitset:
         coordinates), the carry (drop_first, new_last_end), the total run
         count of the unsharded result and, with gather=True, every run as an
         int64 [m, 2] tensor (global start, end) in order."""
-        if self.splits is None:
-            self.plan_splits(inputs)
+        self._ensure_splits(inputs)
         if op == "and":
             bits = [self.and_bitset(inputs)]
             res = self.ctx.bitset_runs(0, bits[0])

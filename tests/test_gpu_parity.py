@@ -1009,6 +1009,27 @@ def test_subtract_local_scan(ctx, mode, t, monkeypatch):
         _sub_equal(ref, exp)
 
 
+@pytest.mark.gpu
+def test_subtract_total_disagreement_fails(ctx, monkeypatch):
+    # the fused subtract reruns at the first pass's exact total when its guess
+    # overflows; a second pass that reports more than that must fail loudly
+    # (LIME_TEST_SUB_SKEW=1 makes both passes report one past their capacity)
+    # rather than return a result whose arrays were freed; the same call then
+    # succeeds without the hook
+    rng = np.random.default_rng(5200)
+    A, B = random_sets(rng, 4000, 3000, n_contigs=2, contig_len=240000, max_len=300)
+    keep = B[2] > B[1]
+    B = [x[keep] for x in B]
+    sp = space_for(2, 240000)
+    a, b = ctx.set_from_host(sp, *A), ctx.set_from_host(sp, *B)
+    monkeypatch.setenv("LIME_TEST_SUB_SKEW", "1")
+    with pytest.raises(Exception, match="record total changed"):
+        ctx.subtract(a, b, 0, SUBTRACT_LIME)
+    monkeypatch.delenv("LIME_TEST_SUB_SKEW")
+    _sub_equal(ctx.subtract(a, b, 0, SUBTRACT_LIME).to_host(),
+               oracle.subtract(A, B, 0, SUBTRACT_LIME))
+
+
 @pytest.mark.parametrize("mode", [SUBTRACT_LIME, SUBTRACT_SET])
 @pytest.mark.parametrize("deep", [False, True])
 def test_subtract_one_pass_and_two_pass(ctx, mode, deep):

@@ -305,21 +305,22 @@ def test_sharded_subtract_and_c4_ops(world):
 
 
 # ------------------- sharded complement, global run ids, stranded sets
-def _strand_rows():
-    """A (with strands 1 / 2, zero-width rows, rows on the 2- and 3-way shard
-    bounds) and B, contig-local"""
+def _strand_rows(bounds=None):
+    """A (with strands 1 / 2, zero-width rows, rows on the shard bounds:
+    `bounds`, by default the 2- and 3-way even splits) and B, contig-local"""
     from lime_amd import Space, synth
     from lime_amd import dist as ld
     A = [np.asarray(x) for x in synth.uniform(LENS, 12000, 0x33, 0, 4000)]
     B = [np.asarray(x) for x in synth.uniform(LENS, 9000, 0x44, 10, 5000)]
     sp_off = np.concatenate([[0], np.cumsum(np.array(LENS) + 1)])
+    if bounds is None:
+        bounds = [b for w in (2, 3) for b in ld.even_splits(int(sp_off[-1]), w)[1:-1]]
     extra = []
-    for w in (2, 3):
-        for b in ld.even_splits(int(sp_off[-1]), w)[1:-1]:
-            c = int(np.searchsorted(sp_off, b, side="right") - 1)
-            s = int(b - sp_off[c])
-            if 60 < s < LENS[c] - 60:
-                extra += [(c, s, s), (c, s - 50, s), (c, s, s + 40), (c, s - 5, s + 5)]
+    for b in bounds:
+        c = int(np.searchsorted(sp_off, b, side="right") - 1)
+        s = int(b - sp_off[c])
+        if 60 < s < LENS[c] - 60:
+            extra += [(c, s, s), (c, s - 50, s), (c, s, s + 40), (c, s - 5, s + 5)]
     for i, col in enumerate(zip(*extra)):
         A[i] = np.concatenate([A[i], np.array(col, A[i].dtype)])
     rng = np.random.default_rng(5)
@@ -328,7 +329,7 @@ def _strand_rows():
     return A, B, sa, sb
 
 
-def _strand_worker(rank, world, port, q):
+def _strand_worker(rank, world, port, q, mode="even"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
@@ -341,10 +342,7 @@ def _strand_worker(rank, world, port, q):
         ctx = lime_amd.Context(0)
         sp = lime_amd.Space(NAMES, LENS)
         off = sp.offsets
-        A, B, sa, sb = _strand_rows()
-        # (even splits: _strand_rows puts rows on exactly these shard bounds)
-        step = ShardStep(ctx, sp, splits=ld.even_splits(int(sp.offsets[-1]), world),
-                         comm_device=torch.device("cpu"))
+        out = {}
 
         def dev(X, st=None):
             n = len(X[0])
@@ -355,7 +353,22 @@ def _strand_worker(rank, world, port, q):
                 else None
             torch.cuda.synchronize()
             return l - f, t, s8, f
-        out = {}
+        if mode == "even":
+            # (_strand_rows puts rows on exactly these shard bounds)
+            A, B, sa, sb = _strand_rows()
+            splits = ld.even_splits(int(sp.offsets[-1]), world)
+        else:
+            # count-balanced bounds sampled from both inputs (plan_splits),
+            # then rows placed exactly on those bounds
+            A0, B0, _, _ = _strand_rows([])
+            (na, ta, _, _), (nb, tb, _, _) = dev(A0), dev(B0)
+            planner = ShardStep(ctx, sp, comm_device=torch.device("cpu"))
+            splits = planner.plan_splits([(na, ta[0].data_ptr(), ta[1].data_ptr()),
+                                          (nb, tb[0].data_ptr(), tb[1].data_ptr())])
+            assert splits != ld.even_splits(int(sp.offsets[-1]), world)
+            A, B, sa, sb = _strand_rows(splits[1:-1])
+        out["splits"] = list(splits)
+        step = ShardStep(ctx, sp, splits=splits, comm_device=torch.device("cpu"))
         # plain: merge run ids + the shard's complement gaps
         n, t, _, f = dev(A)
         S = step.load(n, *(x.data_ptr() for x in t), row_base=f)
@@ -408,8 +421,8 @@ def _strand_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_complement_run_ids_strands(world):
+@pytest.mark.parametrize("world,mode", [(2, "even"), (3, "even"), (3, "sampled")])
+def test_sharded_complement_run_ids_strands(world, mode):
     # SURVEY.md 8(e) on the device: the shards' complement gaps, the global
     # run id of every row (plain and stranded merge) and stranded pairs equal
     # the single-shard oracle (Complement.scala:39-45,67-73,112-122;
@@ -418,7 +431,8 @@ def test_sharded_complement_run_ids_strands(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_strand_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_strand_worker, args=(r, world, port, q, mode))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
@@ -426,7 +440,7 @@ def test_sharded_complement_run_ids_strands(world):
         p.join(timeout=60)
     errs = [r[1]["error"] for r in res if "error" in r[1]]
     assert not errs, errs[0]
-    A, B, sa, sb = _strand_rows()
+    A, B, sa, sb = _strand_rows(None if mode == "even" else res[0][1]["splits"][1:-1])
     m = oracle.merge(A)
     ids = dict(sum((r[1]["ids"] for r in res), []))
     assert [ids[i] for i in range(len(A[0]))] == m["run_of_row"].tolist()

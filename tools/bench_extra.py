@@ -129,11 +129,19 @@ def main():
             t1 = ev()
             m = ctx.merge(S)
             t2 = ev()
-            c = ctx.complement(space, S)
+            # the complement from the merge's runs (one merge scan per step,
+            # as bench.py's C3 line): Complement.scala's gaps of merge(A)
+            k = m.n
+            rgs = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+            rge = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+            if k:
+                m.copy_rows_device(0, k, rgs.data_ptr(), rge.data_ptr())
+            c = ctx.complement_runs(space, k, rgs.data_ptr(), rge.data_ptr())
             t3 = ev()
             rec.append((t0, t1, t2, t3, m.n, c.n))
             for h in (c, m, S):
                 h.close()
+            del rgs, rge
         units, unit = n, "intervals/s"
         desc = f"1B merge side: sort + merge (run ids) + complement of {n} pile-up intervals " \
                "(4e6 centres, N(0,150), len U[150,600])"

@@ -464,6 +464,107 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
     flush_hist(hist, counts, ntiles, tile);
 }
 
+// The bucketed sort's second histogram (DB2 bits at L + DB1, over pass 1's
+// output, whose rows are ordered by the first digit d1 = bits [L, L + DB1))
+// and the partials that place every bucket without reading its keys again:
+// the rows of first digit D form one region of pass 1's output; for every D
+// whose region starts inside this tile (D in (d1 of the row before the
+// tile, d1 of the tile's last row]), part[D][d2] = the tile's rows with
+// second digit d2 and d1 < D.  Bucket (d2, D) then starts at the scanned
+// count of (d2, the tile) + part[D][d2] (k_bucket_starts_part).  Most tiles
+// lie inside one region and only histogram.
+template <int DB1, int DB2>
+__global__ __launch_bounds__(RB) void k_hist_part(const uint32_t *__restrict__ key, int64_t n,
+                                                  int L, uint32_t *__restrict__ counts,
+                                                  uint32_t ntiles, uint32_t *__restrict__ part) {
+    constexpr int B1 = 1 << DB1, B2 = 1 << DB2, PC = 16;  // first digits per partial round
+    __shared__ uint32_t hist[RWAVES][B2];
+    __shared__ uint32_t ph[PC + 1][B2];  // [0]: rows below the round's first D
+    for (int i = threadIdx.x; i < RWAVES * B2; i += RB) (&hist[0][0])[i] = 0;
+    const int w = threadIdx.x / 64, lane = dev::lane_id();
+    const uint32_t tile = xcd_swizzle(blockIdx.x, ntiles);
+    const int64_t tile0 = (int64_t)tile * RTILE, base = tile0 + w * WITEMS;
+    const int s2 = L + DB1;
+    uint32_t vk[RITEMS];
+    bool valid[RITEMS];
+    if (base + WITEMS <= n) {
+        const uint4 *k4 = reinterpret_cast<const uint4 *>(key + base);
+#pragma unroll
+        for (int k = 0; k < RITEMS / 4; ++k) {
+            const uint4 v = k4[k * 64 + lane];
+            vk[4 * k] = v.x, vk[4 * k + 1] = v.y, vk[4 * k + 2] = v.z, vk[4 * k + 3] = v.w;
+        }
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) valid[k] = true;
+    } else {
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) {
+            const int64_t i = base + k * 64 + lane;
+            valid[k] = i < n;
+            vk[k] = valid[k] ? key[i] : 0u;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (valid[k]) atomicAdd(&hist[w][(vk[k] >> s2) & (B2 - 1)], 1u);
+    __syncthreads();
+    flush_hist(hist, counts, ntiles, tile);
+    // (uniform: every thread reads the same two keys)
+    const int64_t tend = tile0 + RTILE < n ? tile0 + RTILE : n;
+    const int prev = tile0 > 0 ? (int)((key[tile0 - 1] >> L) & (B1 - 1)) : -1;
+    const int last = (int)((key[tend - 1] >> L) & (B1 - 1));
+    for (int c0 = prev + 1; c0 <= last; c0 += PC) {
+        __syncthreads();  // (ph reused by the previous round)
+        for (int i = threadIdx.x; i < (PC + 1) * B2; i += RB) (&ph[0][0])[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k) {
+            const int d1 = (int)((vk[k] >> L) & (B1 - 1));
+            if (valid[k] && d1 < c0 + PC)
+                atomicAdd(&ph[d1 < c0 ? 0 : 1 + d1 - c0][(vk[k] >> s2) & (B2 - 1)], 1u);
+        }
+        __syncthreads();
+        for (int d2 = threadIdx.x; d2 < B2; d2 += RB) {
+            uint32_t run = ph[0][d2];
+            for (int j = 0; j < PC && c0 + j <= last; ++j) {
+                part[(int64_t)(c0 + j) * B2 + d2] = run;
+                run += ph[1 + j][d2];
+            }
+        }
+    }
+}
+
+// bucket b = (d2 << DB1) | D (= gs >> L) starts at pass 2's scanned count of
+// (d2, the tile where D's region starts) + part[D][d2]; a D without rows
+// (its region starts at n) puts every (d2, D) at the end of d2's rows.
+// start[nb] = n.  dstart1[D]: pass 1's scanned count of (D, tile 0).
+__global__ __launch_bounds__(256) void k_bucket_starts_part(
+    const uint32_t *__restrict__ dstart1, const uint32_t *__restrict__ mat2,
+    const uint32_t *__restrict__ part, int64_t n, uint32_t ntiles, uint32_t nb, int DB1, int DB2,
+    uint32_t *__restrict__ start) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b > nb) return;
+    if (b == nb) {
+        start[b] = (uint32_t)n;
+        return;
+    }
+    const uint32_t D = (uint32_t)b & ((1u << DB1) - 1u), d2 = (uint32_t)(b >> DB1);
+    const uint32_t ds = dstart1[D];
+    if ((int64_t)ds >= n)
+        start[b] = d2 + 1 < (1u << DB2) ? mat2[(int64_t)(d2 + 1) * ntiles] : (uint32_t)n;
+    else
+        start[b] = mat2[(int64_t)d2 * ntiles + ds / RTILE] + part[((int64_t)D << DB2) + d2];
+}
+
+// column 0 of a digit-major count matrix: the scanned start of every digit
+__global__ __launch_bounds__(256) void k_take_col0(const uint32_t *__restrict__ mat,
+                                                   uint32_t ntiles, int nd,
+                                                   uint32_t *__restrict__ out) {
+    const int d = blockIdx.x * 256 + threadIdx.x;
+    if (d < nd) out[d] = mat[(int64_t)d * ntiles];
+}
+
 // RAW (first pass over caller rows only): key_in / ge_in / row_in are the
 // caller's contig / start / end, and (gs, ge) = off[contig] + (start, end)
 // EW (GS passes of sets narrower than 2^16 bases): how the ends travel.
@@ -476,7 +577,11 @@ __global__ __launch_bounds__(RB) void k_hist(const uint32_t *__restrict__ key,
 // sets: 512 digits, runs of ~16 rows per digit and tile) keep their per-wave
 // digit counters as u16 and the RAW contig table aliased onto the staging
 // array, so two workgroups still fit a CU (~76 KiB LDS each)
-enum { EW_32 = 0, EW_TO16 = 1, EW_16 = 2, EW_FROM16 = 3 };
+// EW_PACK (the bucketed sort's last digit pass): reads u16 widths like
+// EW_FROM16 and writes ONE word per row, (gs mod 2^L) << 16 | width (the
+// bucket id gs >> L is implied by the position: k_bucket_starts_part), so the
+// pass writes 8 B per row and the local sort reads 8 instead of 12
+enum { EW_32 = 0, EW_TO16 = 1, EW_16 = 2, EW_FROM16 = 3, EW_PACK = 4 };
 template <int M, int ROWS, bool RAW = false, int EW = EW_32, int DB = 8>
 // 2 workgroups per CU (4 waves per SIMD): <= 128 VGPRs, ~70 KiB LDS each
 __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ key_in,
@@ -488,7 +593,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
                                                 uint32_t *__restrict__ ge_out,
                                                 uint32_t *__restrict__ row_out,
                                                 const uint32_t *__restrict__ off = nullptr,
-                                                int32_t nc = 0) {
+                                                int32_t nc = 0, int lbits = 0) {
     constexpr int BINS = M == M_GS ? 1 << DB : RBINS;
     static_assert(M == M_GS || DB == 8, "wider digits: GS passes only");
     using CT = typename std::conditional<(DB > 8), uint16_t, uint32_t>::type;
@@ -499,6 +604,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
     constexpr bool ALL3 = M != M_GS;  // digit not recomputable from the key alone
     static_assert(EW == EW_32 || M == M_GS, "u16 widths: GS passes only");
     static_assert(!RAW || EW == EW_32 || EW == EW_TO16, "a RAW pass reads the caller's ends");
+    static_assert(EW != EW_PACK || ROWS == ROWS_LOAD, "the packed pass keeps loaded rows");
     __shared__ uint32_t sk[RTILE], se[RTILE], sr[ALL3 ? RTILE : 1];
     // RAW: the contig table staged in LDS (<= PCMAX contigs), so the per-row
     // off[contig] gather is an LDS read, not a dependent cache round trip.
@@ -537,7 +643,7 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
             vr[k] = valid ? kin[o] : 0u;
             vk[k] = valid ? ein[o] : 0u;
             ve[k] = valid ? rin[o] : 0u;
-        } else if (EW == EW_16 || EW == EW_FROM16) {
+        } else if (EW == EW_16 || EW == EW_FROM16 || EW == EW_PACK) {
             vk[k] = valid ? kin[o] : 0u;
             ve[k] = valid ? (uint32_t)reinterpret_cast<const uint16_t *>(ge_in)[base + o] : 0u;
         } else {
@@ -622,6 +728,31 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
             key_out[g] = k;
             ge_out[g] = e;
             row_out[g] = sr[j];
+        }
+        return;
+    }
+    if (EW == EW_PACK) {  // keys and widths staged together, one packed store each
+        const uint32_t lmask = (1u << lbits) - 1u;
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k)
+            if (lp[k] != 0xffffffffu) {
+                sk[lp[k]] = vk[k];
+                se[lp[k]] = ve[k];
+            }
+        __syncthreads();
+        for (int j = threadIdx.x; j < count; j += RB) {
+            const uint32_t k = sk[j];
+            const uint32_t d = digit_of<M, DB>(k, 0u, 0u, shift, st);
+            key_out[gbase[d] + (uint32_t)j - dstart[d]] = (k & lmask) << 16 | se[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < RITEMS; ++k)
+            if (lp[k] != 0xffffffffu) se[lp[k]] = vr[k];
+        __syncthreads();
+        for (int j = threadIdx.x; j < count; j += RB) {
+            const uint32_t d = digit_of<M, DB>(sk[j], 0u, 0u, shift, st);
+            row_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
         }
         return;
     }
@@ -761,7 +892,9 @@ constexpr int LNT_B = 1024, LPOS_B = 14, LCAP_B = 1 << LPOS_B;  // 16 items / th
 constexpr int LDMAX = 9;  // local digit bits (key L + 1 <= 18 bits in two passes)
 
 struct LocalArgs {
-    const uint32_t *k0, *e0, *r0;  // rows grouped by gs >> L
+    // rows grouped by gs >> L; packed (PK) sets: k0 holds (gs mod 2^L) << 16 |
+    // width (EW_PACK) and e0 is unused scratch of n words
+    const uint32_t *k0, *e0, *r0;
     const uint32_t *start;         // nb + 1 bucket starts
     int L;
     int zb;                        // k_local_mid: 1 if the set has zero-width rows
@@ -836,12 +969,28 @@ __device__ __forceinline__ void lds_digit_pass(const uint32_t (&v)[ITEMS], int n
     __syncthreads();
 }
 
+// a row's local key parts from its loaded words: (gs mod 2^L, non-zero
+// width); PK: g is the packed word, e unused
+template <bool PK>
+__device__ __forceinline__ uint32_t lk_low(uint32_t g, uint32_t lmask) {
+    return PK ? g >> 16 : g & lmask;
+}
+template <bool PK>
+__device__ __forceinline__ bool lk_nz(uint32_t g, uint32_t e) {
+    return PK ? (g & 0xffffu) != 0u : e > g;
+}
+// what a row stages for its end: the end, or (PK) the width
+template <bool PK>
+__device__ __forceinline__ uint32_t lk_endw(uint32_t g, uint32_t e) {
+    return PK ? g & 0xffffu : e;
+}
+
 // bucket b = rows [s0, s0 + m), m <= NT * ITEMS, sorted in LDS from its
 // rows in registers (g, e, r: item it * 64 + lane of wave w at position
 // w c + it 64 + lane, c = nit 64; past m: padding).  STAGE: ge and row are
 // staged in LDS (else gathered from global memory, where the bucket's lines
 // are L2-resident after the load).
-template <int NT, int ITEMS, int POSB, bool STAGE, typename CT>
+template <int NT, int ITEMS, int POSB, bool STAGE, typename CT, bool PK = false>
 __device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b, uint32_t s0,
                                                  uint32_t m, const uint32_t (&g)[ITEMS],
                                                  const uint32_t (&e)[ITEMS],
@@ -858,10 +1007,11 @@ __device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b,
     for (int it = 0; it < ITEMS; ++it) {
         const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
         // padding sorts last (after every row: it follows them)
-        v[it] = pos < m ? ((((g[it] & lmask) << 1) | (e[it] > g[it] ? 1u : 0u)) << POSB) | pos
+        v[it] = pos < m ? (((lk_low<PK>(g[it], lmask) << 1) | (lk_nz<PK>(g[it], e[it]) ? 1u : 0u))
+                           << POSB) | pos
                         : 0xffffffffu;
         if (STAGE && it < nit && pos < m) {
-            s_e[pos] = e[it];
+            s_e[pos] = lk_endw<PK>(g[it], e[it]);
             s_r[pos] = r[it];
         }
     }
@@ -877,8 +1027,10 @@ __device__ __forceinline__ void bucket_sort_regs(const LocalArgs &a, uint32_t b,
     const uint32_t base = b << a.L, pm = (1u << POSB) - 1u;
     for (uint32_t q = threadIdx.x; q < m; q += NT) {
         const uint32_t x = A[q], j = x & pm;
-        a.k1[s0 + q] = base | ((x >> (POSB + 1)) & lmask);
-        a.e1[s0 + q] = STAGE ? s_e[j] : a.e0[s0 + j];
+        const uint32_t gq = base | ((x >> (POSB + 1)) & lmask);
+        const uint32_t ew = STAGE ? s_e[j] : PK ? a.k0[s0 + j] & 0xffffu : a.e0[s0 + j];
+        a.k1[s0 + q] = gq;
+        a.e1[s0 + q] = PK ? gq + ew : ew;
         a.r1[s0 + q] = STAGE ? s_r[j] : a.r0[s0 + j];
     }
 }
@@ -902,7 +1054,7 @@ constexpr int SMAX = 48;
 // counter type (u32: LDS atomics); STAGE: e / r staged in LDS by
 // position (else gathered from global memory at the end, where the
 // bucket's lines are L2-resident after its load)
-template <int NT, int ITEMS, int POSB, int SBB, bool STAGE, typename CT>
+template <int NT, int ITEMS, int POSB, int SBB, bool STAGE, typename CT, bool PK = false>
 __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b, uint32_t s0,
                                                   uint32_t m, const uint32_t (&g)[ITEMS],
                                                   const uint32_t (&e)[ITEMS],
@@ -927,11 +1079,11 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
         const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
         u[it] = 0xffffffffu;
         if (it < nit && pos < m) {
-            const uint32_t k = ((g[it] & lmask) << 1) | (e[it] > g[it] ? 1u : 0u);
+            const uint32_t k = (lk_low<PK>(g[it], lmask) << 1) | (lk_nz<PK>(g[it], e[it]) ? 1u : 0u);
             u[it] = (k << POSB) | pos;
             atomicAdd(&scur[k >> sh], 1u);
             if (STAGE) {
-                s_e[pos] = e[it];
+                s_e[pos] = lk_endw<PK>(g[it], e[it]);
                 s_r[pos] = r[it];
             }
         }
@@ -979,8 +1131,10 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
     const uint32_t base = b << a.L, pm = (1u << POSB) - 1u;
     for (uint32_t q = threadIdx.x; q < m; q += NT) {
         const uint32_t x = O[q], j = x & pm;
-        a.k1[s0 + q] = base | ((x >> (POSB + 1)) & lmask);
-        a.e1[s0 + q] = STAGE ? s_e[j] : a.e0[s0 + j];
+        const uint32_t gq = base | ((x >> (POSB + 1)) & lmask);
+        const uint32_t ew = STAGE ? s_e[j] : PK ? a.k0[s0 + j] & 0xffffu : a.e0[s0 + j];
+        a.k1[s0 + q] = gq;
+        a.e1[s0 + q] = PK ? gq + ew : ew;
         a.r1[s0 + q] = STAGE ? s_r[j] : a.r0[s0 + j];
     }
     return true;
@@ -989,9 +1143,17 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
 // a bucket's rows into registers, branch-free (positions past the bucket
 // clamped to its last row; a bucket too large for the shape, or empty, loads
 // row 0): every load issued before any is used
-template <int NT, int ITEMS, int CAP, bool LR = true>
+template <int NT, int ITEMS, int CAP, bool LR = true, bool PK = false>
 struct BucketRegs {
-    uint32_t g[ITEMS], e[ITEMS], r[LR ? ITEMS : 1];
+    uint32_t g[ITEMS], e[PK ? 1 : ITEMS], r[LR ? ITEMS : 1];
+    // the ends to pass on: PK rows carry their widths in g (the sorts then
+    // never read e), so g stands in and no e registers are held
+    __device__ __forceinline__ const uint32_t (&ends() const)[ITEMS] {
+        if constexpr (PK)
+            return g;
+        else
+            return e;
+    }
     uint32_t s0, m;
     // start: the bucket starts (a.start; the persistent kernel passes them as
     // a restrict argument, read at its wave-uniform bucket index by scalar
@@ -1015,7 +1177,7 @@ struct BucketRegs {
             const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
             const uint32_t q = base + (ok ? min(pos, m - 1) : 0u);
             g[it] = a.k0[q];
-            e[it] = a.e0[q];
+            if (!PK) e[it] = a.e0[q];  // (PK: the width rides in g)
             if (LR) r[it] = a.r0[q];  // (LR = false: gathered at the end)
         }
     }
@@ -1030,20 +1192,21 @@ struct BucketRegs {
 // buckets and the ranked digit passes inline took 78 KiB of LDS each: the
 // loads in flight per CU, not the bytes, bounded it at 3.75 TB/s.)
 constexpr int LNT_S = 512, LPOS_S = 12, LCAP_S = 3072;  // 6 items / thread
-using SmallRegs = BucketRegs<LNT_S, LCAP_S / LNT_S, LCAP_S>;
+template <bool PK>
 __global__ __launch_bounds__(LNT_S) __attribute__((amdgpu_waves_per_eu(6, 8)))
 void k_local_small(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) {
     __shared__ uint32_t A[LCAP_S], B[LCAP_S], s_e[LCAP_S], s_r[LCAP_S];
     __shared__ uint32_t sstart[LNT_S], scur[LNT_S];
     __shared__ uint32_t scratch[2 * (LNT_S / 64) + 1];
-    SmallRegs cur, nxt;
+    BucketRegs<LNT_S, LCAP_S / LNT_S, LCAP_S, true, PK> cur, nxt;
     cur.load(a, blockIdx.x, nb, start);
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         nxt.load(a, b + gridDim.x, nb, start);
         bool listed = cur.m > (uint32_t)LCAP_S;
         if (!listed && cur.m > 0)
-            listed = !bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S, 9, true, uint32_t>(
-                a, b, cur.s0, cur.m, cur.g, cur.e, cur.r, A, B, sstart, scur, scratch, s_e, s_r);
+            listed = !bucket_sort_claim<LNT_S, LCAP_S / LNT_S, LPOS_S, 9, true, uint32_t, PK>(
+                a, b, cur.s0, cur.m, cur.g, cur.ends(), cur.r, A, B, sstart, scur, scratch, s_e,
+                s_r);
         if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
         cur = nxt;
@@ -1064,12 +1227,14 @@ void k_local_small(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start)
 //   5. rows sharing a sub-bin (equal starts, or sh > 0) count the entries
 //      below their unique u = k << POSB | position (the stable order);
 //   6. the outputs leave in three rounds through T (gs, ge, row written at
-//      their ranks, stored coalesced).
+//      their ranks, stored coalesced); PK: two (the packed word gives gs
+//      and ge, then the row).
 // Every row's rank stays in a register: no per-slot pass, no rank table.
 // A sub-bin past SMAX rows (a pile of identical starts) sends the bucket to
 // k_local_big.
-template <int NT, int ITEMS, int POSB, int SBB>
-__device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0, uint32_t m,
+template <int NT, int ITEMS, int POSB, int SBB, bool PK = false>
+__device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t b, uint32_t s0,
+                                                 uint32_t m,
                                                  const uint32_t (&g)[ITEMS],
                                                  const uint32_t (&e)[ITEMS],
                                                  const uint32_t (&rw)[ITEMS], uint32_t *T,
@@ -1099,7 +1264,8 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
         const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
         u[it] = 0xffffffffu;
         if (it < nit && pos < m) {
-            const uint32_t k = ((g[it] & lmask) << zb) | (e[it] > g[it] ? (uint32_t)zb : 0u);
+            const uint32_t k = (lk_low<PK>(g[it], lmask) << zb) |
+                               (lk_nz<PK>(g[it], e[it]) ? (uint32_t)zb : 0u);
             u[it] = (k << POSB) | pos;
             const uint32_t sb = k >> sh;
             atomicAdd(&cw[pw(sb >> 1)], 1u << ((sb & 1u) << 4));
@@ -1160,6 +1326,28 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
             rk[it] = r;
         }
     }
+    if (PK) {  // packed word -> (gs, ge), then rows
+        const uint32_t base = b << a.L;
+#pragma unroll
+        for (int round = 0; round < 2; ++round) {
+            __syncthreads();  // (T free: ranks taken / the previous round stored)
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it)
+                if (rk[it] != 0xffffffffu) T[rk[it]] = round == 0 ? g[it] : rw[it];
+            __syncthreads();
+            for (uint32_t q = threadIdx.x; q < m; q += NT) {
+                const uint32_t x = T[q];
+                if (round == 0) {
+                    const uint32_t gq = base | (x >> 16);
+                    a.k1[s0 + q] = gq;
+                    a.e1[s0 + q] = gq + (x & 0xffffu);
+                } else {
+                    a.r1[s0 + q] = x;
+                }
+            }
+        }
+        return true;
+    }
 #pragma unroll
     for (int round = 0; round < 3; ++round) {
         __syncthreads();  // (T free: ranks taken / the previous round stored)
@@ -1183,7 +1371,7 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t s0
 //        for 2^16-base buckets): buckets averaging up to LAVG_W rows (C3's
 //        5e8 pile-up rows, ~10.6k per 2^16-base bucket, under two 8-bit
 //        passes -- the 9-bit passes run at ~3 ms per 5e8 rows against ~2.4).
-template <int NT, int ITEMS, int POSB, int SBB, int WGS>
+template <int NT, int ITEMS, int POSB, int SBB, int WGS, bool PK>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WGS * NT / 256, 8)))
 void k_local_keys(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) {
     constexpr int CAP = NT * ITEMS;
@@ -1192,34 +1380,52 @@ void k_local_keys(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) 
     __shared__ uint32_t cw[(1 << (SBB - 1)) + NT];
     __shared__ uint32_t scratch[2 * (NT / 64) + 1];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        BucketRegs<NT, ITEMS, CAP> cur;
+        BucketRegs<NT, ITEMS, CAP, true, PK> cur;
         cur.load(a, b, nb, start);
         bool listed = cur.m > (uint32_t)CAP;
         if (!listed && cur.m > 0)
-            listed = !bucket_sort_keys<NT, ITEMS, POSB, SBB>(a, cur.s0, cur.m, cur.g, cur.e,
-                                                             cur.r, T, cw, scratch);
+            listed = !bucket_sort_keys<NT, ITEMS, POSB, SBB, PK>(a, b, cur.s0, cur.m, cur.g,
+                                                                 cur.ends(), cur.r, T, cw, scratch);
         if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
     }
 }
 constexpr int LCAP_M = 6144, LCAP_W = 16384;
-#define LIME_LOCAL_MID k_local_keys<512, 12, 13, 14, 2>
-#define LIME_LOCAL_WIDE k_local_keys<1024, 16, 14, 15, 1>
+#define LIME_LOCAL_MID(PK) k_local_keys<512, 12, 13, 14, 2, PK>
+#define LIME_LOCAL_WIDE(PK) k_local_keys<1024, 16, 14, 15, 1, PK>
 
 // A bucket past LCAP_B rows: LSD over its key (gs mod 2^L, non-zero width) in
 // 6-bit digits by the whole workgroup, NT rows per step in order (wave ballot
 // ranks, per-wave digit counts, running digit offsets): stable.  Passes
-// alternate (k0, e0, r0) -> (k1, e1, r1) -> ...; an even number of passes
-// ends with a copy into (k1, e1, r1).
-template <int NT>
-__device__ void bucket_sort_global(const LocalArgs &a, uint32_t s0, uint32_t m, uint32_t *lds) {
+// alternate (k0, e0, r0) -> (k1, e1, r1) -> ...; the result is copied into
+// (k1, e1, r1) when it ends on the other side.  PK: the packed rows are
+// first unpacked into (k1, e1, r1), and the passes start from there.
+template <int NT, bool PK = false>
+__device__ void bucket_sort_global(const LocalArgs &a, uint32_t b, uint32_t s0, uint32_t m,
+                                   uint32_t *lds) {
     constexpr int NW = NT / 64, GD = 6, GB = 1 << GD;
     uint32_t *hist = lds, *run = lds + GB, *wc = lds + 2 * GB;  // wc[NW][GB]
     const int w = threadIdx.x / 64, lane = dev::lane_id();
     const uint32_t lmask = (1u << a.L) - 1u;
     const int kb = a.L + 1, np = (kb + GD - 1) / GD;
-    const uint32_t *src[3] = {a.k0 + s0, a.e0 + s0, a.r0 + s0};
-    uint32_t *dst[3] = {a.k1 + s0, a.e1 + s0, a.r1 + s0};
+    uint32_t *const fin[3] = {a.k1 + s0, a.e1 + s0, a.r1 + s0};
+    uint32_t *const inp[3] = {const_cast<uint32_t *>(a.k0) + s0, const_cast<uint32_t *>(a.e0) + s0,
+                              const_cast<uint32_t *>(a.r0) + s0};
+    const uint32_t *src[3] = {inp[0], inp[1], inp[2]};
+    uint32_t *dst[3] = {fin[0], fin[1], fin[2]};
+    if (PK) {  // (each thread rereads only the rows it wrote, in pass 0)
+        const uint32_t base = b << a.L;
+        for (uint32_t i = threadIdx.x; i < m; i += NT) {
+            const uint32_t x = inp[0][i], g = base | (x >> 16);
+            fin[0][i] = g;
+            fin[1][i] = g + (x & 0xffffu);
+            fin[2][i] = inp[2][i];
+        }
+        for (int q = 0; q < 3; ++q) {
+            src[q] = fin[q];
+            dst[q] = inp[q];
+        }
+    }
     for (int p = 0; p < np; ++p) {
         const int shift = p * GD;
         auto digit = [&](uint32_t g, uint32_t e) {
@@ -1279,11 +1485,11 @@ __device__ void bucket_sort_global(const LocalArgs &a, uint32_t s0, uint32_t m, 
             dst[q] = const_cast<uint32_t *>(t);
         }
     }
-    if (np % 2 == 0)  // the result is in (k0, e0, r0): copy it over
+    if (src[0] != fin[0])  // the result ended on the input side: copy it over
         for (uint32_t i = threadIdx.x; i < m; i += NT) {
-            a.k1[s0 + i] = a.k0[s0 + i];
-            a.e1[s0 + i] = a.e0[s0 + i];
-            a.r1[s0 + i] = a.r0[s0 + i];
+            fin[0][i] = src[0][i];
+            fin[1][i] = src[1][i];
+            fin[2][i] = src[2][i];
         }
 }
 
@@ -1291,6 +1497,7 @@ __device__ void bucket_sort_global(const LocalArgs &a, uint32_t s0, uint32_t m, 
 // workgroup per CU until the list is done
 // (the claim sort with 2048 sub-bins first, the ranked digit passes when a
 // pile-up puts more than SMAX rows in one of them)
+template <bool PK>
 __global__ __launch_bounds__(LNT_B) void k_local_big(LocalArgs a) {
     __shared__ uint32_t A[LCAP_B], B[LCAP_B];
     // the ranked passes' digit counters and the claim sort's sub-bin starts /
@@ -1310,14 +1517,15 @@ __global__ __launch_bounds__(LNT_B) void k_local_big(LocalArgs a) {
         const uint32_t b = a.over[i];
         const uint32_t s0 = a.start[b], m = a.start[b + 1] - s0;
         if (m <= (uint32_t)LCAP_B) {
-            BucketRegs<LNT_B, LCAP_B / LNT_B, LCAP_B> R;
+            BucketRegs<LNT_B, LCAP_B / LNT_B, LCAP_B, true, PK> R;
             R.load(a, b, b + 1, a.start);
-            if (!bucket_sort_claim<LNT_B, LCAP_B / LNT_B, LPOS_B, 11, false, uint32_t>(
-                    a, b, s0, m, R.g, R.e, R.r, A, B, sstart, scur, scratch, nullptr, nullptr))
-                bucket_sort_regs<LNT_B, LCAP_B / LNT_B, LPOS_B, false, uint16_t>(
-                    a, b, s0, m, R.g, R.e, R.r, A, B, cnt, scratch, nullptr, nullptr);
+            if (!bucket_sort_claim<LNT_B, LCAP_B / LNT_B, LPOS_B, 11, false, uint32_t, PK>(
+                    a, b, s0, m, R.g, R.ends(), R.r, A, B, sstart, scur, scratch, nullptr,
+                    nullptr))
+                bucket_sort_regs<LNT_B, LCAP_B / LNT_B, LPOS_B, false, uint16_t, PK>(
+                    a, b, s0, m, R.g, R.ends(), R.r, A, B, cnt, scratch, nullptr, nullptr);
         } else
-            bucket_sort_global<LNT_B>(a, s0, m, A);
+            bucket_sort_global<LNT_B, PK>(a, b, s0, m, A);
         __syncthreads();
     }
 }
@@ -1349,6 +1557,9 @@ int sort_set_global(lime_ctx *ctx, lime_set *set, const uint32_t *d_gs, const ui
 #endif
 #ifndef LIME_SORT_TBMAX
 #define LIME_SORT_TBMAX 18
+#endif
+#ifndef LIME_SORT_PACK
+#define LIME_SORT_PACK 1
 #endif
 constexpr int64_t LMIN = 32, LAVG = 3 * LCAP_S / 4, LAVG_M = LCAP_M / 2, LAVG_W = 11500;
 // the local kernel of a bucket geometry: 0 small, 1 mid, 2 wide
@@ -1399,13 +1610,18 @@ void launch_prep_w16(lime_ctx *ctx, lime_set *set, const int32_t *d_contig,
 // caller's rows (histogrammed by the prep), pass 2 (DB2 bits at L + DB1);
 // with u16 widths (every width < 2^16) pass 1 writes widths, pass 2 ends.
 // pk / pw (caller rows with u16 widths): the prep's (gs, width), read by
-// pass 1 instead of the caller's rows
+// pass 1 instead of the caller's rows.  pack (u16 widths, L <= 16): pass 2
+// writes the packed word (EW_PACK) and its histogram leaves the bucket-start
+// partials (k_hist_part: part, with pass 1's digit starts in dstart1)
 template <int DB1, int DB2>
 int bucket_passes(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_contig,
                   const uint32_t *d_start, const uint32_t *d_end, int64_t n, int L, bool w16,
                   uint32_t *mat, int mat_bits, uint32_t ntiles, uint32_t *const (&a)[3],
                   uint32_t *const (&o)[3], const uint32_t *pk = nullptr,
-                  const uint32_t *pw = nullptr) {
+                  const uint32_t *pw = nullptr, bool pack = false, uint32_t *dstart1 = nullptr,
+                  uint32_t *part = nullptr) {
+    if (pack && (!w16 || L > 16 || !dstart1 || !part))
+        return fail(LIME_ERR_ARG, "sort: packed pass without u16 widths");
     // (mat: 2^mat_bits counts per tile, the histograms of both passes)
     if (DB1 > mat_bits || DB2 > mat_bits) return fail(LIME_ERR_ARG, "sort: digit matrix too small");
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, ((int64_t)1 << DB1) * ntiles, nullptr));
@@ -1431,10 +1647,22 @@ int bucket_passes(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
                            dim3(RB), 0, S(ctx), kc, d_start, d_end, n, L, nost, cm, ntiles, a[0],
                            a[1], a[2], (const uint32_t *)set->d_off, set->n_contigs);
     LIME_HIP(hipGetLastError());
-    hipLaunchKernelGGL((k_hist<M_GS, DB2>), dim3(ntiles), dim3(RB), 0, S(ctx), a[0], a[1], a[2], n,
-                       L + DB1, nost, mat, ntiles, (int)ROWS_LOAD);
+    if (pack) {
+        // (pass 1's digit starts, before the second histogram reuses mat)
+        hipLaunchKernelGGL(k_take_col0, dim3(blocks_for((int64_t)1 << DB1, 256)), dim3(256), 0,
+                           S(ctx), (const uint32_t *)mat, ntiles, 1 << DB1, dstart1);
+        hipLaunchKernelGGL((k_hist_part<DB1, DB2>), dim3(ntiles), dim3(RB), 0, S(ctx),
+                           (const uint32_t *)a[0], n, L, mat, ntiles, part);
+    } else {
+        hipLaunchKernelGGL((k_hist<M_GS, DB2>), dim3(ntiles), dim3(RB), 0, S(ctx), a[0], a[1],
+                           a[2], n, L + DB1, nost, mat, ntiles, (int)ROWS_LOAD);
+    }
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, ((int64_t)1 << DB2) * ntiles, nullptr));
-    if (w16)
+    if (pack)
+        hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_PACK, DB2>), dim3(ntiles),
+                           dim3(RB), 0, S(ctx), a[0], a[1], a[2], n, L + DB1, nost, cm, ntiles,
+                           o[0], o[1], o[2], (const uint32_t *)nullptr, 0, L);
+    else if (w16)
         hipLaunchKernelGGL((k_scatter<M_GS, ROWS_LOAD, false, EW_FROM16, DB2>), dim3(ntiles),
                            dim3(RB), 0, S(ctx), a[0], a[1], a[2], n, L + DB1, nost, cm, ntiles,
                            o[0], o[1], o[2]);
@@ -1563,18 +1791,29 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
                 LIME_TRY(alloc(ctx, &o[q], (size_t)n));
             }
             const bool w16 = LIME_SORT_W16 && h.max_width < 65536u;
+            // the packed second pass: (gs mod 2^L, width) in one word, the
+            // buckets placed from the histogram partials (no key search)
+            const bool pack = LIME_SORT_PACK && w16 && L <= 16;
+            uint32_t *dstart1 = nullptr, *part = nullptr;
+            if (pack) {
+                LIME_TRY(alloc(ctx, &dstart1, (size_t)1 << DB1));
+                LIME_TRY(alloc(ctx, &part, (size_t)1 << TB));
+            }
+            PoolGuard<uint32_t> gd{ctx, dstart1}, gpart{ctx, part};
             if (TB == 16)
                 LIME_TRY((bucket_passes<8, 8>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, mat_bits, ntiles, a, o, k0, e0)));
+                                              mat, mat_bits, ntiles, a, o, k0, e0, pack, dstart1,
+                                              part)));
             else if (TB == 17)
                 LIME_TRY((bucket_passes<8, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, mat_bits, ntiles, a, o, k0, e0)));
+                                              mat, mat_bits, ntiles, a, o, k0, e0, pack, dstart1,
+                                              part)));
             else
                 LIME_TRY((bucket_passes<9, 9>(ctx, set, global, d_contig, d_start, d_end, n, L, w16,
-                                              mat, mat_bits, ntiles, a, o, k0, e0)));
+                                              mat, mat_bits, ntiles, a, o, k0, e0, pack, dstart1,
+                                              part)));
             release(ctx, k0);
             release(ctx, e0);
-            release(ctx, mat);
             // every bucket sorted locally: (o) -> (a)
             uint32_t *start, *over;
             unsigned int *nover;
@@ -1585,8 +1824,15 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             LIME_TRY(alloc(ctx, &nover, 2));
             PoolGuard<unsigned int> g2{ctx, nover};
             LIME_HIP(hipMemsetAsync(nover, 0, 8, S(ctx)));
-            hipLaunchKernelGGL(k_bucket_starts, dim3(blocks_for((int64_t)nb + 1, 256)), dim3(256),
-                               0, S(ctx), (const uint32_t *)o[0], n, nb, L, start);
+            if (pack)
+                hipLaunchKernelGGL(k_bucket_starts_part, dim3(blocks_for((int64_t)nb + 1, 256)),
+                                   dim3(256), 0, S(ctx), (const uint32_t *)dstart1,
+                                   (const uint32_t *)mat, (const uint32_t *)part, n, ntiles, nb,
+                                   DB1, DB2, start);
+            else
+                hipLaunchKernelGGL(k_bucket_starts, dim3(blocks_for((int64_t)nb + 1, 256)),
+                                   dim3(256), 0, S(ctx), (const uint32_t *)o[0], n, nb, L, start);
+            release(ctx, mat);
             LocalArgs la;
             la.k0 = o[0], la.e0 = o[1], la.r0 = o[2];
             la.start = start;
@@ -1599,17 +1845,26 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (cus <= 0) cus = 256;
-            if (shape == 0)
-                hipLaunchKernelGGL(k_local_small, dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)),
-                                   dim3(LNT_S), 0, S(ctx), la, nb, (const uint32_t *)start);
-            else if (shape == 1)
-                hipLaunchKernelGGL(LIME_LOCAL_MID, dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)),
-                                   dim3(512), 0, S(ctx), la, nb, (const uint32_t *)start);
+#define LIME_LOCAL_LAUNCH(PK)                                                                     \
+    do {                                                                                          \
+        if (shape == 0)                                                                           \
+            hipLaunchKernelGGL(k_local_small<PK>,                                                 \
+                               dim3(std::min<uint32_t>(nb, 3u * (uint32_t)cus)), dim3(LNT_S), 0,  \
+                               S(ctx), la, nb, (const uint32_t *)start);                          \
+        else if (shape == 1)                                                                      \
+            hipLaunchKernelGGL(LIME_LOCAL_MID(PK), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), \
+                               dim3(512), 0, S(ctx), la, nb, (const uint32_t *)start);            \
+        else                                                                                      \
+            hipLaunchKernelGGL(LIME_LOCAL_WIDE(PK), dim3(std::min<uint32_t>(nb, (uint32_t)cus)),  \
+                               dim3(1024), 0, S(ctx), la, nb, (const uint32_t *)start);           \
+        hipLaunchKernelGGL(k_local_big<PK>, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B),  \
+                           0, S(ctx), la);                                                        \
+    } while (0)
+            if (pack)
+                LIME_LOCAL_LAUNCH(true);
             else
-                hipLaunchKernelGGL(LIME_LOCAL_WIDE, dim3(std::min<uint32_t>(nb, (uint32_t)cus)),
-                                   dim3(1024), 0, S(ctx), la, nb, (const uint32_t *)start);
-            hipLaunchKernelGGL(k_local_big, dim3((unsigned)(cus > 0 ? cus : 256)), dim3(LNT_B), 0,
-                               S(ctx), la);
+                LIME_LOCAL_LAUNCH(false);
+#undef LIME_LOCAL_LAUNCH
             LIME_HIP(hipGetLastError());
             for (int q = 0; q < 3; ++q) release(ctx, o[q]);
             set->gs = a[0];

@@ -731,53 +731,33 @@ __global__ __launch_bounds__(RB, 4) void k_scatter(const uint32_t *__restrict__ 
         }
         return;
     }
-    if (EW == EW_PACK) {  // keys and widths staged together, one packed store each
+    // keys and ends staged together (sk, se) and stored by one loop, then
+    // the rows through se: 64 KiB of staging, two workgroups per CU, two
+    // store rounds (keys, ends, rows in three rounds: C3's first pass
+    // 2.21 ms against 2.05 for the packed second pass's two)
+#pragma unroll
+    for (int k = 0; k < RITEMS; ++k)
+        if (lp[k] != 0xffffffffu) {
+            sk[lp[k]] = vk[k];
+            se[lp[k]] = ve[k];
+        }
+    __syncthreads();
+    {
         const uint32_t lmask = (1u << lbits) - 1u;
-#pragma unroll
-        for (int k = 0; k < RITEMS; ++k)
-            if (lp[k] != 0xffffffffu) {
-                sk[lp[k]] = vk[k];
-                se[lp[k]] = ve[k];
-            }
-        __syncthreads();
         for (int j = threadIdx.x; j < count; j += RB) {
-            const uint32_t k = sk[j];
+            const uint32_t k = sk[j], e = se[j];
             const uint32_t d = digit_of<M, DB>(k, 0u, 0u, shift, st);
-            key_out[gbase[d] + (uint32_t)j - dstart[d]] = (k & lmask) << 16 | se[j];
+            const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
+            if (EW == EW_PACK) {
+                key_out[g] = (k & lmask) << 16 | e;  // (gs mod 2^L, width)
+            } else {
+                key_out[g] = k;
+                if (EW == EW_TO16 || EW == EW_16)
+                    reinterpret_cast<uint16_t *>(ge_out)[g] = (uint16_t)e;
+                else
+                    ge_out[g] = EW == EW_FROM16 ? k + e : e;
+            }
         }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < RITEMS; ++k)
-            if (lp[k] != 0xffffffffu) se[lp[k]] = vr[k];
-        __syncthreads();
-        for (int j = threadIdx.x; j < count; j += RB) {
-            const uint32_t d = digit_of<M, DB>(sk[j], 0u, 0u, shift, st);
-            row_out[gbase[d] + (uint32_t)j - dstart[d]] = se[j];
-        }
-        return;
-    }
-    // keys first (they carry the digit), then ends, then rows through one
-    // shared buffer: 64 KiB of staging instead of 96, two workgroups per CU
-#pragma unroll
-    for (int k = 0; k < RITEMS; ++k)
-        if (lp[k] != 0xffffffffu) sk[lp[k]] = vk[k];
-    __syncthreads();
-    for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t k = sk[j];
-        const uint32_t d = digit_of<M, DB>(k, 0u, 0u, shift, st);
-        key_out[gbase[d] + (uint32_t)j - dstart[d]] = k;
-    }
-#pragma unroll
-    for (int k = 0; k < RITEMS; ++k)
-        if (lp[k] != 0xffffffffu) se[lp[k]] = ve[k];
-    __syncthreads();
-    for (int j = threadIdx.x; j < count; j += RB) {
-        const uint32_t d = digit_of<M, DB>(sk[j], 0u, 0u, shift, st);
-        const uint32_t g = gbase[d] + (uint32_t)j - dstart[d];
-        if (EW == EW_TO16 || EW == EW_16)
-            reinterpret_cast<uint16_t *>(ge_out)[g] = (uint16_t)se[j];
-        else
-            ge_out[g] = EW == EW_FROM16 ? sk[j] + se[j] : se[j];
     }
     if (ROWS == ROWS_NONE) return;
     __syncthreads();
@@ -1143,7 +1123,9 @@ __device__ __forceinline__ bool bucket_sort_claim(const LocalArgs &a, uint32_t b
 // a bucket's rows into registers, branch-free (positions past the bucket
 // clamped to its last row; a bucket too large for the shape, or empty, loads
 // row 0): every load issued before any is used
-template <int NT, int ITEMS, int CAP, bool LR = true, bool PK = false>
+// SKIP: items past the wave's share of the bucket are not loaded (a
+// wave-uniform branch per item; else they reload the bucket's last row)
+template <int NT, int ITEMS, int CAP, bool LR = true, bool PK = false, bool SKIP = false>
 struct BucketRegs {
     uint32_t g[ITEMS], e[PK ? 1 : ITEMS], r[LR ? ITEMS : 1];
     // the ends to pass on: PK rows carry their widths in g (the sorts then
@@ -1174,6 +1156,7 @@ struct BucketRegs {
         const int c = ok ? (int)((m + NW * 64 - 1) / (NW * 64)) * 64 : 0;
 #pragma unroll
         for (int it = 0; it < ITEMS; ++it) {
+            if (SKIP && it * 64 >= c) continue;
             const uint32_t pos = (uint32_t)(w * c + it * 64 + lane);
             const uint32_t q = base + (ok ? min(pos, m - 1) : 0u);
             g[it] = a.k0[q];
@@ -1379,8 +1362,11 @@ void k_local_keys(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) 
     // (padded: one word per thread's share of the scan)
     __shared__ uint32_t cw[(1 << (SBB - 1)) + NT];
     __shared__ uint32_t scratch[2 * (NT / 64) + 1];
+    // (the next bucket's keys prefetched into a second register set during
+    // this one's sort, rows loaded at its start: no faster, same box --
+    // the kernel waits on LDS and barriers, not loads; not kept)
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        BucketRegs<NT, ITEMS, CAP, true, PK> cur;
+        BucketRegs<NT, ITEMS, CAP, true, PK, true> cur;
         cur.load(a, b, nb, start);
         bool listed = cur.m > (uint32_t)CAP;
         if (!listed && cur.m > 0)

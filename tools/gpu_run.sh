@@ -48,7 +48,7 @@ for S in "$@"; do
     prof)
       run prof_$a 400 rocprofv3 --kernel-trace --stats --output-format csv \
         -d gpurun_out/${T}_${a}_stats -o run -- python $(prog $a)
-      python3 tools/kstats.py gpurun_out/${T}_${a}_stats | head -16 ;;
+      python3 tools/kstats.py gpurun_out/${T}_${a}_stats > gpurun_out/${T}_${a}_kstats.txt; head -16 gpurun_out/${T}_${a}_kstats.txt ;;
     extra) run extra_$a 300 python tools/bench_extra.py --workload $a ;;
     pmc)
       for C in FETCH_SIZE WRITE_SIZE; do

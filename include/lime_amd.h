@@ -44,8 +44,10 @@ extern "C" {
 #endif
 
 /* 2: lime_set_lower_bound / _first_reaching return -(LIME_ERR_*) on error
- *    (was -1); lime_pairs_checksum_device and the sharded-path helpers added */
-#define LIME_ABI_VERSION 5
+ *    (was -1); lime_pairs_checksum_device and the sharded-path helpers added
+ * 6: lime_route_rows_interleaved, lime_deinterleave_u32 (the routed
+ *    exchange without per-column repacking) */
+#define LIME_ABI_VERSION 6
 
 /* status codes */
 #define LIME_OK 0
@@ -418,6 +420,22 @@ int lime_route_rows(lime_ctx *ctx, const lime_space *space, int64_t n, const int
                     int32_t n_shards, const uint32_t *splits, int clip, int64_t cap,
                     uint32_t *d_gs, uint32_t *d_ge, uint32_t *d_row, int64_t *counts,
                     const int8_t *d_strand_in, int8_t *d_strand_out);
+/* The same routing with the pieces written INTERLEAVED into one device
+ * array: piece p occupies d_rows[p * k .. p * k + k) = global start, global
+ * end and (k = 3) row id row_base + input index -- the send buffer of ONE
+ * all_to_all as it stands (no per-column repacking before the exchange).
+ * k = 2 (clipped rows for bit-per-base shards) or 3.  No strand codes.
+ * Errors, counts and cap as lime_route_rows.  ABI 6. */
+int lime_route_rows_interleaved(lime_ctx *ctx, const lime_space *space, int64_t n,
+                                const int32_t *d_contig, const uint32_t *d_start,
+                                const uint32_t *d_end, uint32_t row_base, int32_t n_shards,
+                                const uint32_t *splits, int clip, int64_t cap, int32_t k,
+                                uint32_t *d_rows, int64_t *counts);
+/* Interleaved rows (n rows of k = 2 or 3 u32 words, as exchanged) into k
+ * device column arrays (d_dst2 unused for k = 2): one pass, stream-ordered,
+ * no sync -- the receiving side of the routed exchange.  ABI 6. */
+int lime_deinterleave_u32(lime_ctx *ctx, int64_t n, int32_t k, const uint32_t *d_src,
+                          uint32_t *d_dst0, uint32_t *d_dst1, uint32_t *d_dst2);
 /* k evenly spaced rows' global starts (rows i * n / k, i < k) into the
  * device array d_out, for count-balanced splitters (lime_amd.dist
  * sample_splits: the sampled range partitioner behind ADAM

@@ -25,7 +25,7 @@ ERRORS = {
 }
 # the C-ABI contract this binding is written against (include/lime_amd.h
 # LIME_ABI_VERSION): checked at load, so a stale library fails loudly
-ABI_VERSION = 5
+ABI_VERSION = 6
 SUBTRACT_LIME = 0
 SUBTRACT_SET = 1
 
@@ -119,6 +119,9 @@ SIGNATURES = {
     "lime_bitset_window": (C.c_int, [vp, P(i64), P(i64)]),
     "lime_route_rows": (C.c_int, [vp, vp, i64, vp, vp, vp, u32, i32, P(u32), C.c_int, i64, vp,
                                   vp, vp, P(i64), vp, vp]),
+    "lime_route_rows_interleaved": (C.c_int, [vp, vp, i64, vp, vp, vp, u32, i32, P(u32), C.c_int,
+                                              i64, i32, vp, P(i64)]),
+    "lime_deinterleave_u32": (C.c_int, [vp, i64, i32, vp, vp, vp, vp]),
     "lime_bitset_runs": (C.c_int, [vp, C.c_int, vp, vp, pp, P(i64)]),
     "lime_bitset_and_runs": (C.c_int, [vp, C.c_int, P(vp), pp, P(i64)]),
     "lime_bitset_popcount": (i64, [vp, vp]),

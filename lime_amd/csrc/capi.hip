@@ -146,7 +146,9 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
                const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
                uint32_t *d_row, int64_t *counts, const int8_t *d_strand_in,
-               int8_t *d_strand_out);
+               int8_t *d_strand_out, uint32_t *d_iv = nullptr, int32_t ik = 0);
+int deinterleave_u32(lime_ctx *ctx, int64_t n, int32_t k, const uint32_t *src, uint32_t *d0,
+                     uint32_t *d1, uint32_t *d2);
 int bitset_runs(lime_ctx *ctx, int op, int k, const lime_bitset *const *sets, lime_result *res);
 int64_t bitset_popcount(lime_ctx *ctx, const lime_bitset *a);
 void bitset_free(lime_bitset *bs);
@@ -1487,6 +1489,28 @@ int lime_route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_
     hipSetDevice(ctx->device);
     return route_rows(ctx, sp, n, d_contig, d_start, d_end, row_base, n_shards, splits, clip, cap,
                       d_gs, d_ge, d_row, counts, d_strand_in, d_strand_out);
+}
+
+int lime_route_rows_interleaved(lime_ctx *ctx, const lime_space *sp, int64_t n,
+                                const int32_t *d_contig, const uint32_t *d_start,
+                                const uint32_t *d_end, uint32_t row_base, int32_t n_shards,
+                                const uint32_t *splits, int clip, int64_t cap, int32_t k,
+                                uint32_t *d_rows, int64_t *counts) {
+    if (!ctx || !sp || !splits || !counts || n < 0 || (n > 0 && (!d_start || !d_end)) ||
+        (k != 2 && k != 3) || (cap > 0 && !d_rows))
+        return fail(LIME_ERR_ARG, "bad route arguments");
+    if (n > 0xffffffffLL) return fail(LIME_ERR_RANGE, "more than 2^32 rows in one call");
+    hipSetDevice(ctx->device);
+    uint32_t dummy = 0;  // (the column pointers are unused in interleaved mode)
+    return route_rows(ctx, sp, n, d_contig, d_start, d_end, row_base, n_shards, splits, clip, cap,
+                      &dummy, &dummy, nullptr, counts, nullptr, nullptr, d_rows, k);
+}
+
+int lime_deinterleave_u32(lime_ctx *ctx, int64_t n, int32_t k, const uint32_t *d_src,
+                          uint32_t *d_dst0, uint32_t *d_dst1, uint32_t *d_dst2) {
+    if (!ctx) return fail(LIME_ERR_ARG, "bad deinterleave arguments");
+    hipSetDevice(ctx->device);
+    return deinterleave_u32(ctx, n, k, d_src, d_dst0, d_dst1, d_dst2);
 }
 
 int lime_sample_starts(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,

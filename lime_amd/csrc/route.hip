@@ -41,6 +41,10 @@ struct RouteArgs {
     uint32_t *mat;  // nsh * nblk + 1
     uint32_t nblk;
     uint32_t *gs, *ge, *row;
+    // interleaved output (iv != null): piece p at iv[p * ik ...] = gs, ge
+    // (, row when ik = 3) -- the send buffer of one all_to_all, no repacking
+    uint32_t *iv;
+    int ik;
     const int8_t *strand_in;  // may be null
     int8_t *strand_out;
     unsigned int *err;  // bit0 contig, bit1 end < start, bit2 end > length / span
@@ -142,9 +146,19 @@ __global__ __launch_bounds__(RT) void k_route_write(RouteArgs a) {
         for (int k = 0; k < RPT; ++k) {
             if (d < d0[k] || d > d1[k]) continue;
             const uint32_t lo = sp[d], hi = sp[d + 1];
-            a.gs[pos] = a.clip ? max(g0[k], lo) : g0[k];
-            a.ge[pos] = a.clip && g1[k] > g0[k] ? min(g1[k], hi) : g1[k];
+            const uint32_t gs = a.clip ? max(g0[k], lo) : g0[k];
+            const uint32_t ge = a.clip && g1[k] > g0[k] ? min(g1[k], hi) : g1[k];
             const int64_t i = (int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k;
+            if (a.iv) {
+                uint32_t *o = a.iv + (int64_t)pos * a.ik;
+                o[0] = gs;
+                o[1] = ge;
+                if (a.ik == 3) o[2] = a.row_base + (uint32_t)i;
+                ++pos;
+                continue;
+            }
+            a.gs[pos] = gs;
+            a.ge[pos] = ge;
             if (a.row) a.row[pos] = a.row_base + (uint32_t)i;
             if (a.strand_out) a.strand_out[pos] = a.strand_in ? a.strand_in[i] : (int8_t)0;
             ++pos;
@@ -152,10 +166,42 @@ __global__ __launch_bounds__(RT) void k_route_write(RouteArgs a) {
     }
 }
 
+// the destination starts (and the total) + the error flags in out[nsh + 1]:
+// one read-back
 __global__ void k_route_totals(const uint32_t *__restrict__ mat, uint32_t nblk, int nsh,
-                               int64_t *__restrict__ out) {
+                               const unsigned int *__restrict__ err, int64_t *__restrict__ out) {
     const int d = threadIdx.x;
     if (d <= nsh) out[d] = mat[(int64_t)d * nblk];
+    if (d == nsh + 1) out[d] = *err;
+}
+
+// interleaved rows (k words per row) -> k column arrays; 4 rows per thread,
+// 16-B loads and stores when every pointer is 16-B aligned
+template <int K, bool VEC>
+__global__ __launch_bounds__(256) void k_deinterleave(const uint32_t *__restrict__ src, int64_t n,
+                                                      uint32_t *__restrict__ d0,
+                                                      uint32_t *__restrict__ d1,
+                                                      uint32_t *__restrict__ d2) {
+    const int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (r0 >= n) return;
+    uint32_t *dst[3] = {d0, d1, d2};
+    if (VEC && r0 + 4 <= n) {
+        uint32_t w[4 * K];
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src + r0 * K);
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint4 v = s4[q];
+            w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+            *reinterpret_cast<uint4 *>(dst[c] + r0) =
+                make_uint4(w[c], w[K + c], w[2 * K + c], w[3 * K + c]);
+        return;
+    }
+    for (int64_t r = r0; r < n && r < r0 + 4; ++r)
+#pragma unroll
+        for (int c = 0; c < K; ++c) dst[c][r] = src[r * K + c];
 }
 
 // k evenly spaced rows' global starts (row i * n / k), for count-balanced
@@ -188,11 +234,27 @@ int sample_starts(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t 
     return LIME_OK;
 }
 
+int deinterleave_u32(lime_ctx *ctx, int64_t n, int32_t k, const uint32_t *src, uint32_t *d0,
+                     uint32_t *d1, uint32_t *d2) {
+    if (n < 0 || (k != 2 && k != 3) || !src || !d0 || !d1 || (k == 3 && !d2))
+        return fail(LIME_ERR_ARG, "deinterleave: k = 2 or 3 columns, every pointer set");
+    if (n == 0) return LIME_OK;
+    const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d0) |
+                       reinterpret_cast<uintptr_t>(d1) | reinterpret_cast<uintptr_t>(d2)) & 15u) == 0;
+    const dim3 g(blocks_for((n + 3) / 4, 256)), b(256);
+    if (k == 3 && vec) hipLaunchKernelGGL((k_deinterleave<3, true>), g, b, 0, S(ctx), src, n, d0, d1, d2);
+    else if (k == 3) hipLaunchKernelGGL((k_deinterleave<3, false>), g, b, 0, S(ctx), src, n, d0, d1, d2);
+    else if (vec) hipLaunchKernelGGL((k_deinterleave<2, true>), g, b, 0, S(ctx), src, n, d0, d1, d2);
+    else hipLaunchKernelGGL((k_deinterleave<2, false>), g, b, 0, S(ctx), src, n, d0, d1, d2);
+    LIME_HIP(hipGetLastError());
+    return LIME_OK;
+}
+
 int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
                const uint32_t *d_start, const uint32_t *d_end, uint32_t row_base, int32_t nsh,
                const uint32_t *splits, int clip, int64_t cap, uint32_t *d_gs, uint32_t *d_ge,
                uint32_t *d_row, int64_t *counts, const int8_t *d_strand_in,
-               int8_t *d_strand_out) {
+               int8_t *d_strand_out, uint32_t *d_iv, int32_t ik) {
     if (nsh < 1 || nsh > MAXSH) return fail(LIME_ERR_ARG, "1 to 64 shards");
     if (splits[0] != 0 || (int64_t)splits[nsh] != sp->span)
         return fail(LIME_ERR_ARG, "splits must start at 0 and end at the span");
@@ -211,7 +273,7 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
     LIME_TRY(space_device(ctx, sp->off, &d_off, &d_len));
     LIME_TRY(alloc(ctx, &err, 1));
     PoolGuard<unsigned int> g4{ctx, err};
-    LIME_TRY(alloc(ctx, &tot, (size_t)nsh + 1));
+    LIME_TRY(alloc(ctx, &tot, (size_t)nsh + 2));
     PoolGuard<int64_t> g5{ctx, tot};
     LIME_HIP(hipMemcpyAsync(d_split, splits, 4 * ((size_t)nsh + 1), hipMemcpyHostToDevice, S(ctx)));
     LIME_HIP(hipMemsetAsync(err, 0, 4, S(ctx)));
@@ -234,19 +296,20 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
     a.gs = d_gs;
     a.ge = d_ge;
     a.row = d_row;
+    a.iv = d_iv;
+    a.ik = ik;
     a.strand_in = d_strand_in;
     a.strand_out = d_strand_out;
     a.err = err;
     if (n > 0) hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(RT), 0, S(ctx), a);
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
-    hipLaunchKernelGGL(k_route_totals, dim3(1), dim3(MAXSH + 1), 0, S(ctx), (const uint32_t *)mat,
-                       nblk, nsh, tot);
+    hipLaunchKernelGGL(k_route_totals, dim3(1), dim3(MAXSH + 2), 0, S(ctx), (const uint32_t *)mat,
+                       nblk, nsh, (const unsigned int *)err, tot);
     LIME_HIP(hipGetLastError());
     // the destination starts (and the total) + the error flags: one read-back
-    std::vector<int64_t> h((size_t)nsh + 1);
-    LIME_TRY(read_back(ctx, h.data(), tot, 8 * ((size_t)nsh + 1)));
-    unsigned int herr = 0;
-    LIME_TRY(read_back(ctx, &herr, err, 4));
+    std::vector<int64_t> h((size_t)nsh + 2);
+    LIME_TRY(read_back(ctx, h.data(), tot, 8 * ((size_t)nsh + 2)));
+    const unsigned int herr = (unsigned int)h[nsh + 1];
     if (herr & 1u) return fail(LIME_ERR_CONTIG, "interval contig id outside the space");
     if (herr & 2u) return fail(LIME_ERR_RANGE, "interval end < start");
     if (herr & 4u) return fail(LIME_ERR_RANGE, "interval end beyond its contig / the span");

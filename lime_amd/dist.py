@@ -409,6 +409,67 @@ def exchange(tensors, counts, group=None, comm_device=None, packed=False):
     return out, rcounts
 
 
+def exchange_rows(buf, counts, group=None, comm_device=None):
+    """Variable all_to_all of the rows of ONE [rows, k] tensor grouped by
+    destination (counts[q] rows to rank q) -- lime_route_rows_interleaved's
+    output as it stands: no stacking of columns before the collective.
+    Returns (the received [sum, k] tensor on buf's device, received counts).
+    Bytes per routed row: the route's write + the exchange, where the
+    column form (exchange(packed=True)) added a torch.stack copy on the way
+    out and a .contiguous() per column on the way in."""
+    w, _ = _ws(group)
+    dev = buf.device
+    cd = comm_device if comm_device is not None else dev
+    sc = torch.tensor(counts, dtype=torch.int64, device=cd)
+    rc = torch.empty(w, dtype=torch.int64, device=cd)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcounts = rc.tolist()
+    src = buf[:sum(counts)].to(cd)
+    r = torch.empty((sum(rcounts), buf.shape[1]), dtype=buf.dtype, device=cd)
+    dist.all_to_all_single(r, src, output_split_sizes=rcounts, input_split_sizes=list(counts),
+                           group=group)
+    return r.to(dev), rcounts
+
+
+def exchange_sets_rows(bufs, counts, group=None, comm_device=None):
+    """exchange_sets for interleaved row buffers: bufs[i] = set i's [rows, k]
+    tensor grouped by destination, counts[i][q] rows for rank q.  ONE
+    all_to_all of the count matrix and ONE of the rows (the send buffer is
+    the (rank, set)-ordered concatenation of the sets' slices: one copy).
+    Returns, per set, [(the received [m, k] slices from each rank in rank
+    order), m, rows from other ranks]."""
+    w, me = _ws(group)
+    k = len(bufs)
+    dev = bufs[0].device
+    cd = comm_device if comm_device is not None else dev
+    ncol = bufs[0].shape[1]
+    starts = [[0] * (w + 1) for _ in range(k)]
+    for i in range(k):
+        for q in range(w):
+            starts[i][q + 1] = starts[i][q] + counts[i][q]
+    sc = torch.tensor([[counts[i][q] for i in range(k)] for q in range(w)], dtype=torch.int64,
+                      device=cd)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcm = rc.tolist()  # rcm[p][i]: rows of set i from rank p
+    parts = [bufs[i][starts[i][q]:starts[i][q + 1]] for q in range(w) for i in range(k)]
+    src = torch.cat(parts).to(cd) if parts else torch.empty((0, ncol), dtype=torch.int32,
+                                                            device=cd)
+    send_n = [sum(counts[i][q] for i in range(k)) for q in range(w)]
+    recv_n = [sum(rcm[p]) for p in range(w)]
+    r = torch.empty((sum(recv_n), ncol), dtype=src.dtype, device=cd)
+    dist.all_to_all_single(r, src, output_split_sizes=recv_n, input_split_sizes=send_n,
+                           group=group)
+    r = r.to(dev)
+    out, at = [[] for _ in range(k)], 0
+    for p in range(w):
+        for i in range(k):
+            out[i].append(r[at:at + rcm[p][i]])
+            at += rcm[p][i]
+    return [(out[i], sum(rcm[p][i] for p in range(w)),
+             sum(rcm[p][i] for p in range(w)) - rcm[me][i]) for i in range(k)]
+
+
 def exchange_sets(sets, counts, group=None, comm_device=None):
     """The rows of k sets moved by ONE packed all_to_all (plus one all_to_all
     of the k x w count matrix): sets[i] = [column tensors] with their rows

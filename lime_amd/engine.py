@@ -567,6 +567,28 @@ class Context:
                                      vp(d_strand), vp(d_strand_out)))
         return list(counts)
 
+    def route_rows_interleaved(self, space, n, d_contig, d_start, d_end, splits, k, d_rows,
+                               clip=False, cap=-1, row_base=0):
+        """lime_route_rows_interleaved: the per-shard counts; when their total
+        <= cap the pieces are written to d_rows as k (2: gs, ge; 3: + row id)
+        consecutive u32 words each, grouped by shard -- the all_to_all send
+        buffer as it stands"""
+        nsh = len(splits) - 1
+        sp = (C.c_uint32 * (nsh + 1))(*[int(x) for x in splits])
+        counts = (i64 * nsh)()
+        check(_lib().lime_route_rows_interleaved(self._h, space.handle, int(n), vp(d_contig),
+                                                 vp(d_start), vp(d_end),
+                                                 int(row_base) & 0xFFFFFFFF, nsh, sp,
+                                                 int(bool(clip)), int(cap), int(k), vp(d_rows),
+                                                 counts))
+        return list(counts)
+
+    def deinterleave(self, n, k, d_src, d_dst0, d_dst1, d_dst2=None):
+        """n interleaved rows of k u32 words -> k device columns (one pass,
+        stream-ordered)"""
+        check(_lib().lime_deinterleave_u32(self._h, int(n), int(k), vp(d_src), vp(d_dst0),
+                                           vp(d_dst1), vp(d_dst2)))
+
     def bitset_runs(self, op, a, b=None):
         h, n = vp(), i64()
         check(_lib().lime_bitset_runs(self._h, int(op), a._h, b._h if b is not None else None,

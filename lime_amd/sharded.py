@@ -151,6 +151,27 @@ class ShardStep:
         ctx, sp = self.ctx, self.space
         if self.splits is None:
             self.plan_splits([(n, d_contig, d_start)])
+        if not d_strand:
+            # interleaved: the route writes the all_to_all send buffer itself
+            # and one device pass splits the received rows into columns (the
+            # column form stacked them before the collective, 24 B per routed
+            # row, and copied each column out after it, ~48 B)
+            buf = torch.empty((max(int(n), 1), 3), dtype=torch.int32, device=self.dev)
+            counts = ctx.route_rows_interleaved(sp, n, d_contig, d_start, d_end, self.splits, 3,
+                                                buf.data_ptr(), clip=False, cap=n,
+                                                row_base=row_base)
+            self._sync()  # engine output -> the collective
+            recv, rc = ld.exchange_rows(buf, counts, self.group, self.comm)
+            del buf
+            m = recv.shape[0]
+            cols = [self._i32(m) for _ in range(3)]
+            self._sync()  # the collective's output -> the engine
+            if m:
+                ctx.deinterleave(m, 3, recv.data_ptr(), *(c.data_ptr() for c in cols))
+            self._sync()
+            del recv
+            self.routed += sum(rc) - rc[self.rank]
+            return [c[:m] for c in cols]
         cols = [self._i32(n) for _ in range(4 if d_strand else 3)]
         st8 = torch.empty(max(int(n), 1), dtype=torch.int8, device=self.dev) if d_strand else None
         counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=False, cap=n,
@@ -479,12 +500,18 @@ class ShardedBitset:
         """this rank's slice of one set's rows -> the rows of this shard's
         window from every rank (global coordinates, clipped): (m, gs, ge)"""
         self._ensure_splits([(n, d_contig, d_start, d_end)])
-        gs, ge, counts = self._route_clipped(n, d_contig, d_start, d_end)
+        buf, counts = self._route_clipped(n, d_contig, d_start, d_end)
         self._sync()
-        (rgs, rge), rc = ld.exchange([gs, ge], counts, self.group, self.comm, packed=True)
+        recv, rc = ld.exchange_rows(buf, counts, self.group, self.comm)
+        del buf
+        m = recv.shape[0]
+        gs, ge = self._i32(m), self._i32(m)
+        self._sync()
+        if m:
+            self.ctx.deinterleave(m, 2, recv.data_ptr(), gs.data_ptr(), ge.data_ptr())
         self._sync()
         self.moved += sum(rc) - rc[self.rank]
-        return sum(rc), rgs, rge
+        return m, gs, ge
 
     def bitset(self, n, d_contig, d_start, d_end):
         """this shard's bitset of one set, from this rank's slice of its rows"""
@@ -497,20 +524,19 @@ class ShardedBitset:
 
     def _route_clipped(self, n, d_contig, d_start, d_end):
         """one set's rows, clipped to the shards they overlap and grouped by
-        shard: (gs, ge) int32 device tensors and the per-shard counts"""
+        shard: an interleaved [pieces, 2] (gs, ge) int32 device tensor (the
+        all_to_all send buffer as it stands) and the per-shard counts"""
         ctx, sp = self.ctx, self.space
         cap = n + 4096
-        gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
-                                cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
+        buf = torch.empty((cap, 2), dtype=torch.int32, device=self.dev)
+        counts = ctx.route_rows_interleaved(sp, n, d_contig, d_start, d_end, self.splits, 2,
+                                            buf.data_ptr(), clip=True, cap=cap)
         if sum(counts) > cap:  # many rows cross shard bounds: exact size
             cap = sum(counts)
-            gs = torch.empty(cap, dtype=torch.int32, device=self.dev)
-            ge = torch.empty(cap, dtype=torch.int32, device=self.dev)
-            counts = ctx.route_rows(sp, n, d_contig, d_start, d_end, self.splits, clip=True,
-                                    cap=cap, d_gs=gs.data_ptr(), d_ge=ge.data_ptr())
-        return gs, ge, counts
+            buf = torch.empty((cap, 2), dtype=torch.int32, device=self.dev)
+            counts = ctx.route_rows_interleaved(sp, n, d_contig, d_start, d_end, self.splits, 2,
+                                                buf.data_ptr(), clip=True, cap=cap)
+        return buf, counts
 
     def and_bitset(self, inputs):
         """this shard's AND of k sets in one fused paint per 16
@@ -522,13 +548,28 @@ class ShardedBitset:
         self._ensure_splits(inputs)
         routed = [self._route_clipped(*x) for x in inputs]
         self._sync()
-        got = ld.exchange_sets([[g, e] for g, e, _ in routed], [c for _, _, c in routed],
-                               self.group, self.comm)
+        got = ld.exchange_sets_rows([b for b, _ in routed], [c for _, c in routed], self.group,
+                                    self.comm)
+        del routed
         self._sync()
         self.moved += sum(x for _, _, x in got)
-        return ctx.bitset_and_from_global(sp, self.lo, self.hi,
-                                          [(m, cols[0].data_ptr(), cols[1].data_ptr())
-                                           for cols, m, _ in got])
+        # each rank's slice of each set straight into the set's columns (one
+        # device pass per slice, no concatenation)
+        cols = []
+        for slices, m, _ in got:
+            gs, ge = self._i32(m), self._i32(m)
+            at = 0
+            for t in slices:
+                k = t.shape[0]
+                if k:
+                    ctx.deinterleave(k, 2, t.data_ptr(), gs[at:].data_ptr(), ge[at:].data_ptr())
+                at += k
+            cols.append((m, gs, ge))
+        res = ctx.bitset_and_from_global(sp, self.lo, self.hi,
+                                         [(m, gs.data_ptr(), ge.data_ptr()) for m, gs, ge in cols])
+        self._sync()  # (the received slices stay referenced until the engine read them)
+        del got
+        return res
 
     def run(self, inputs, gather=False, op="and"):
         """inputs: [(n, d_contig, d_start, d_end)] per set (this rank's rows,

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing
     assert set(syms) == set(_ffi.SIGNATURES), set(syms) ^ set(_ffi.SIGNATURES)
-    assert lib.lime_abi_version() == _ffi.ABI_VERSION == 5
+    assert lib.lime_abi_version() == _ffi.ABI_VERSION == 6
 
 
 def test_no_device_fails_loudly():

@@ -379,7 +379,18 @@ def _xsets_worker(rank, world, port, q):
             sets.append([t, -t])
             counts.append(c)
         got = ld.exchange_sets(sets, counts)
-        q.put((rank, [(cols[0][:m].tolist(), cols[1][:m].tolist(), m) for cols, m, _ in got]))
+        out = [(cols[0][:m].tolist(), cols[1][:m].tolist(), m) for cols, m, _ in got]
+        # the interleaved form (lime_route_rows_interleaved's [rows, 2]
+        # buffers, received as per-rank slices): the same rows, same order
+        gotr = ld.exchange_sets_rows([torch.stack(c, dim=1) for c in sets], counts)
+        outr = []
+        for slices, m, moved in gotr:
+            t = torch.cat(slices) if slices else torch.empty((0, 2), dtype=torch.int32)
+            outr.append((t[:, 0].tolist(), t[:, 1].tolist(), m))
+        # one set through exchange_rows: the single-buffer exchange
+        r1, rc = ld.exchange_rows(torch.stack(sets[1], dim=1), counts[1])
+        one = (r1[:, 0].tolist(), r1[:, 1].tolist(), sum(rc))
+        q.put((rank, out, outr, one))
     finally:
         dist.destroy_process_group()
 
@@ -398,11 +409,13 @@ def test_exchange_sets(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for me, got in res:
-        for i, (a, b, m) in enumerate(got):
+    for me, got, gotr, one in res:
+        for i, ((a, b, m), r) in enumerate(zip(got, gotr)):
             want = [1000 * p + 100 * i + 10 * me + j for p in range(world)
                     for j in range((p + 2 * i + me) % 3)]
             assert a == want and b == [-x for x in want] and m == len(want)
+            assert r == (a, b, m)
+        assert one == got[1]
 
 
 # ---------------- count-balanced splitters (dist.splits_from_weighted_samples)

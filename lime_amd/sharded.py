@@ -490,6 +490,9 @@ class ShardedBitset:
         self.lo, self.hi = self.splits[self.rank], self.splits[self.rank + 1]
         return self.splits
 
+    def _i32(self, n):
+        return torch.empty(max(int(n), 1), dtype=torch.int32, device=self.dev)
+
     def _ensure_splits(self, inputs):
         """the shard windows, sampled from `inputs` when none were given
         (collective: every rank calls the same entry point)"""

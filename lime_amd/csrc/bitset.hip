@@ -133,6 +133,8 @@ struct BinArgs {
     unsigned int *ncross;
     unsigned int *err;         // bit0 contig, bit1 end < start, bit2 end > length
     uint32_t *dummy;           // sink of the fixed-count store batches (see k_bin_write)
+    uint32_t *xbz;             // (may be null) 3 (nb PSUB + 1) words zeroed by k_tile_groups:
+                               // the set's cross buckets, so no memset follows the read-back
 };
 
 // global start of a row (0 for an invalid contig); every pass derives a
@@ -289,8 +291,13 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
     stage_contigs<LC>(a, coff, nullptr, BINB);
     __syncthreads();
     const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
-    // the matrix's extra last entry (it receives the total from the scan)
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.mat[(int64_t)a.nb * a.nchunks] = 0u;
+    // the matrix's extra last entry (it receives the total from the scan), and
+    // the set's flags (ncross, err: written only by the later passes)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.mat[(int64_t)a.nb * a.nchunks] = 0u;
+        *a.ncross = 0u;
+        *a.err = 0u;
+    }
     const int64_t r0 = (int64_t)ch * a.chunk_rows;
     const int64_t r1 = min(a.n, r0 + a.chunk_rows);
     for (int64_t base = r0; base < r1; base += STEP) {
@@ -321,10 +328,17 @@ __global__ __launch_bounds__(BINB) void k_bin_count(BinArgs a) {
 }
 
 // per paint tile: its rows in the chunk groups before each group (gpre) and
-// in all (ttot, scanned next into the tile starts)
+// in all (ttot, scanned next into the tile starts); also zeroes the set's
+// cross buckets (a.xbz, 3 (nt + 1) words), so no memset follows the host's
+// read-back.  (A one-workgroup form that scanned ttot in the same launch
+// made C4's step slower, 0.88 -> 0.93 ms same box: one CU's latency chain.)
 __global__ __launch_bounds__(256) void k_tile_groups(BinArgs a) {
     const int nt = a.nb * PSUB;
     const int t = blockIdx.x * 256 + threadIdx.x;
+    if (a.xbz && t <= nt) {
+        const int64_t ts = (int64_t)nt + 1;
+        a.xbz[t] = a.xbz[ts + t] = a.xbz[2 * ts + t] = 0u;
+    }
     if (t >= nt) return;
     uint32_t run = 0;
     for (int g = 0; g < a.ngroups; ++g) {
@@ -1182,8 +1196,8 @@ struct PaintEvArgs {
     uint32_t *tev;        // nt slots of `cap` events
     uint32_t cap;
     uint32_t *tcnt;       // events of each tile
-    uint32_t *edge;       // bit 0: the tile's first bit, bit 1: its last
-    unsigned int *oflow;  // a tile past `cap` events
+    uint32_t *edge;       // bit 0: the tile's first bit, bit 1: its last, bit 2: past `cap`
+    unsigned int *oflow;  // zeroed by block 0; k_ev_join raises it (no memset launch)
 };
 constexpr int PEW = TWORDS / PAINTB;  // consecutive words per thread (extraction)
 
@@ -1257,8 +1271,7 @@ __device__ __forceinline__ void tile_events(const PaintEvArgs &a, int t, WJ wj,
     const uint32_t mine = dev::block_exclusive_sum<PAINTB>(c, scratch, &tot);
     if (threadIdx.x == 0) {
         a.tcnt[t] = tot;
-        a.edge[t] = (uint32_t)(x[0] & 1ull) | s_last << 1;
-        if (tot > a.cap) atomicOr(a.oflow, 1u);
+        a.edge[t] = (uint32_t)(x[0] & 1ull) | s_last << 1 | (tot > a.cap ? 4u : 0u);
     }
     if (tot <= a.cap) {  // (block-uniform)
         // events staged in LDS, then stored lane-consecutively
@@ -1305,6 +1318,7 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a, AndArgs s) {
     __shared__ uint32_t s_last;
     static_assert(EVSLOT_MAX * 4 <= sizeof(img), "the event slot (<= EVSLOT_MAX) staged in img");
     const int t = blockIdx.x;
+    if (t == 0 && threadIdx.x == 0) *a.oflow = 0u;  // (raised by k_ev_join, a later launch)
     uint64_t acc[AWPT];
 #pragma unroll
     for (int j = 0; j < AWPT; ++j) acc[j] = ~0ull;
@@ -1321,10 +1335,12 @@ __global__ __launch_bounds__(PAINTB) void k_paint_ev(PaintEvArgs a, AndArgs s) {
 __global__ __launch_bounds__(256) void k_ev_join(const uint32_t *__restrict__ tcnt,
                                                  const uint32_t *__restrict__ edge, int64_t nt,
                                                  uint32_t *__restrict__ cnt2,
-                                                 uint32_t *__restrict__ skip1) {
+                                                 uint32_t *__restrict__ skip1,
+                                                 unsigned int *__restrict__ oflow) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= nt) return;
     const uint32_t e = edge[t];
+    if (e & 4u) *oflow = 1u;  // a tile past its slot (plain store: idempotent)
     const uint32_t jp = t > 0 && (edge[t - 1] & 2u) && (e & 1u);
     const uint32_t jn = t + 1 < nt && (e & 2u) && (edge[t + 1] & 1u);
     cnt2[t] = tcnt[t] - jp - jn;
@@ -1388,7 +1404,7 @@ int n_bins(int64_t width) {
 int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
              const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
              const uint32_t *d_len, int64_t lo, int64_t hi, uint32_t *slab2, uint32_t *ttot,
-             uint64_t *cross, unsigned int *flags) {
+             uint64_t *cross, unsigned int *flags, uint32_t *xbz = nullptr) {
     const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
     // chunk: 1..16 count steps; as many chunks as whole rounds of the write
@@ -1421,6 +1437,8 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     if (n == 0) {
         LIME_HIP(hipMemsetAsync(mat, 0, 4 * (size_t)mlen, S(ctx)));
         LIME_HIP(hipMemsetAsync(ttot, 0, 4 * ((size_t)nt + 1), S(ctx)));
+        LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
+        if (xbz) LIME_HIP(hipMemsetAsync(xbz, 0, 4 * 3 * ((size_t)nt + 1), S(ctx)));
         return LIME_OK;
     }
     BinArgs a;
@@ -1448,13 +1466,14 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     a.ncross = flags;
     a.err = flags + 1;
     a.dummy = dummy;
+    a.xbz = xbz;
     const bool lc = d_contig != nullptr && sp->n <= CMAX;
     LIME_HIP(hipMemsetAsync(gsum, 0, 4 * (size_t)ng * (size_t)nt, S(ctx)));
     if (lc)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);
     else
         hipLaunchKernelGGL(k_bin_count<false>, dim3(nch), dim3(BINB), 0, S(ctx), a);
-    hipLaunchKernelGGL(k_tile_groups, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx), a);
+    hipLaunchKernelGGL(k_tile_groups, dim3(blocks_for(nt + 1, 256)), dim3(256), 0, S(ctx), a);
     // (the extra last entries receive the totals)
     LIME_TRY(scan_exclusive_u32(ctx, mat, mat, mlen, nullptr));
     LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
@@ -1483,9 +1502,11 @@ namespace {
 // starts | difference-array scan (tiles wholly covered) | fill claims], each
 // tstride long (zeroed here), xl = the 2 nx piece slots
 int bucket_cross(lime_ctx *ctx, int64_t tstride, const uint64_t *cross,
-                 const unsigned int *d_ncross, unsigned int nx, uint32_t *xb, uint2 *xl) {
+                 const unsigned int *d_ncross, unsigned int nx, uint32_t *xb, uint2 *xl,
+                 bool zeroed = false) {
     uint32_t *xcnt = xb, *diff = xb + tstride, *xfill = xb + 2 * tstride;
-    LIME_HIP(hipMemsetAsync(xb, 0, 4 * 3 * (size_t)tstride, S(ctx)));
+    // (zeroed: by the set's k_tile_groups, before the host's read-back)
+    if (!zeroed) LIME_HIP(hipMemsetAsync(xb, 0, 4 * 3 * (size_t)tstride, S(ctx)));
     const unsigned g = std::min<unsigned>(blocks_for(nx, BB), 2048u);
     hipLaunchKernelGGL(k_xcount, dim3(g), dim3(BB), 0, S(ctx), cross, d_ncross, xcnt, diff);
     LIME_TRY(scan_exclusive_u32_pair(ctx, xcnt, xcnt, tstride, diff, diff, tstride));
@@ -1523,19 +1544,22 @@ int bin_set(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_con
     LIME_TRY(alloc(ctx, &b.slab2, (size_t)std::max<int64_t>(n, 1)));
     PoolBag bag{ctx, {}};
     uint64_t *cross;
-    unsigned int *flags;  // [0] ncross, [1] err
+    unsigned int *flags;  // [0] ncross, [1] err (zeroed by k_bin_count)
     LIME_TRY(bag.get(&cross, (size_t)std::max<int64_t>(2 * n, 1)));
     LIME_TRY(bag.get(&flags, 2));
-    LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));
+    // the cross buckets allocated (and zeroed on the device) before the
+    // read-back: after it only the bucketing launches remain
+    LIME_TRY(alloc(ctx, &b.xb, 3 * ((size_t)nt + 1)));
     LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, b.slab2,
-                      b.tstart, cross, flags));
+                      b.tstart, cross, flags, b.xb));
     unsigned int h[2] = {0, 0};
     LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
     LIME_TRY(rows_error(h[1]));
     if (h[0]) {
-        LIME_TRY(alloc(ctx, &b.xb, 3 * ((size_t)nt + 1)));
         LIME_TRY(alloc(ctx, &b.xl, 2 * (size_t)h[0]));
-        LIME_TRY(bucket_cross(ctx, nt + 1, cross, flags, h[0], b.xb, b.xl));
+        LIME_TRY(bucket_cross(ctx, nt + 1, cross, flags, h[0], b.xb, b.xl, true));
+    } else {
+        release(ctx, b.xb);  // (stream-ordered; the ops take xb only with xl)
     }
     return LIME_OK;
 }
@@ -1640,8 +1664,7 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     unsigned int *flags;
     LIME_TRY(keep.get(&cross[0], (size_t)std::max<int64_t>(2 * nmax, 1)));
     LIME_TRY(keep.get(&cross[1], (size_t)std::max<int64_t>(2 * nmax, 1)));
-    LIME_TRY(keep.get(&flags, 2 * (size_t)k));
-    LIME_HIP(hipMemsetAsync(flags, 0, 8 * (size_t)k, S(ctx)));
+    LIME_TRY(keep.get(&flags, 2 * (size_t)k));  // (zeroed per set by its k_bin_count)
     // set q's (ncross, err) land in the upper half of the pinned scratch
     // (read_back uses the lower half)
     unsigned int *hflags = reinterpret_cast<unsigned int *>(static_cast<char *>(ctx->pinned) + 2048);
@@ -1666,20 +1689,23 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
         LIME_HIP(hipEventSynchronize(ev.e[q % 2]));
         const unsigned int nx = hflags[2 * (q % 2)], err = hflags[2 * (q % 2) + 1];
         LIME_TRY(rows_error(err));
-        if (nx == 0) return LIME_OK;
         lime_bitset::Bins &b = bs->bins[q];
-        LIME_TRY(alloc(ctx, &b.xb, 3 * tstride));
+        if (nx == 0) {
+            release(ctx, b.xb);
+            return LIME_OK;
+        }
         LIME_TRY(alloc(ctx, &b.xl, 2 * (size_t)nx));
         return bucket_cross(ctx, (int64_t)tstride, cross[q % 2],
-                            (const unsigned int *)(flags + 2 * q), nx, b.xb, b.xl);
+                            (const unsigned int *)(flags + 2 * q), nx, b.xb, b.xl, true);
     };
     for (int q = 0; q < k; ++q) {
         lime_bitset::Bins &b = bs->bins[q];
         b.tstart = ttot_all + tstride * (size_t)q;
         LIME_TRY(alloc(ctx, &b.slab2, (size_t)std::max<int64_t>(n[q], 1)));
+        LIME_TRY(alloc(ctx, &b.xb, 3 * tstride));
         // (cross[q % 2] was last used by set q - 2, bucketed before this)
         LIME_TRY(bin_rows(ctx, sp, n[q], d_contig[q], d_start[q], d_end[q], d_off, d_len, lo, hi,
-                          b.slab2, b.tstart, cross[q % 2], flags + 2 * q));
+                          b.slab2, b.tstart, cross[q % 2], flags + 2 * q, b.xb));
         LIME_HIP(hipMemcpyAsync(hflags + 2 * (q % 2), flags + 2 * q, 8, hipMemcpyDeviceToHost,
                                 S(ctx)));
         LIME_HIP(hipEventRecord(ev.e[q % 2], S(ctx)));
@@ -1733,8 +1759,7 @@ struct EvPlan {
         LIME_TRY(bag.get(&cnt2, (size_t)nt));
         LIME_TRY(bag.get(&skip1, (size_t)nt));
         LIME_TRY(bag.get(&toff, (size_t)nt));
-        LIME_TRY(bag.get(&hdr, 2));
-        LIME_HIP(hipMemsetAsync(hdr, 0, 8, S(ctx)));
+        LIME_TRY(bag.get(&hdr, 2));  // [0] zeroed by k_paint_ev, [1] the scan's total
         pa.oflow = hdr;
         return LIME_OK;
     }
@@ -1743,7 +1768,8 @@ struct EvPlan {
     // can be sized from the bound)
     int queue(lime_result *res) {
         hipLaunchKernelGGL(k_ev_join, dim3(blocks_for(nt, 256)), dim3(256), 0, S(ctx),
-                           (const uint32_t *)pa.tcnt, (const uint32_t *)pa.edge, nt, cnt2, skip1);
+                           (const uint32_t *)pa.tcnt, (const uint32_t *)pa.edge, nt, cnt2, skip1,
+                           pa.oflow);
         LIME_HIP(hipGetLastError());
         LIME_TRY(scan_exclusive_u32(ctx, cnt2, toff, nt, hdr + 1));
         rcap = bound < 0 ? -1 : std::min<int64_t>(bound, nt * (cap / 2));

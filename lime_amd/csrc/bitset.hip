@@ -135,7 +135,13 @@ struct BinArgs {
     uint32_t *dummy;           // sink of the fixed-count store batches (see k_bin_write)
     uint32_t *xbz;             // (may be null) 3 (nb PSUB + 1) words zeroed by k_tile_groups:
                                // the set's cross buckets, so no memset follows the read-back
+    uint32_t rcap;             // optimistic binning (no count pass): rows of (bin b, chunk
+                               // c) at slab[(b nchunks + c) rcap ...), the rest SLAB_PAD
 };
+// an unused slot of an optimistic slab region (no packed row has offset
+// 2^BSH - 1 with length LMAX: its length is clamped to 1 there)
+constexpr uint32_t SLAB_PAD = 0xffffffffu;
+constexpr unsigned int ERR_REGION = 256u;  // an optimistic region overflowed
 
 // global start of a row (0 for an invalid contig); every pass derives a
 // row's bin and tile from it alone, so they always agree.  u32 arithmetic
@@ -356,7 +362,14 @@ __global__ __launch_bounds__(256) void k_tile_groups(BinArgs a) {
 #endif
 // LC: the contig table in LDS; HC: rows carry contig ids (else global
 // coordinates)
-template <bool LC, bool HC>
+// OPT (optimistic, no count pass): the chunk's rows of bin t go to its
+// region slab[(t nchunks + ch) rcap, + rcap) (sized from the window's
+// uniform density; rows past a region go to the sink and raise ERR_REGION,
+// and the host bins the set again through the counted path); the unused
+// rest of each region is filled with SLAB_PAD, and the rows per paint tile
+// (LDS, u16 pairs) are added into the chunk group's totals (gsum), which
+// k_bin_count made otherwise
+template <bool LC, bool HC, bool OPT = false>
 __global__ __launch_bounds__(WRB)
 __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bin_write(BinArgs a) {
     __shared__ uint32_t stage[WSTEP];
@@ -364,14 +377,20 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
     __shared__ uint32_t hist[NBMAX], soff[NBMAX], cur[NBMAX];
     __shared__ uint32_t scratch[WRB / 64 + 1];
     __shared__ uint32_t coff[LC ? CMAX : 1], clen[LC ? CMAX : 1];
+    __shared__ uint32_t th[OPT ? NTMAX / 2 : 1];  // rows per paint tile, two u16 per word
     const uint32_t *off = LC ? coff : a.off, *len = LC ? clen : a.len;
     stage_contigs<LC>(a, coff, clen, WRB);
     const uint32_t ch = xcd_chunk(blockIdx.x, a.nchunks);
     for (int t = threadIdx.x; t < NBMAX; t += WRB) {
-        cur[t] = t < a.nb ? a.mat[(int64_t)t * a.nchunks + ch] : 0u;
+        cur[t] = t < a.nb ? (OPT ? (uint32_t)(((uint64_t)t * a.nchunks + ch) * a.rcap)
+                                 : a.mat[(int64_t)t * a.nchunks + ch])
+                          : 0u;
         hist[t] = 0;
     }
+    if (OPT)
+        for (int i = threadIdx.x; i < NTMAX / 2; i += WRB) th[i] = 0u;
     __syncthreads();
+    uint32_t ovf = 0;  // (OPT) a row past its region
     const int64_t r0 = (int64_t)ch * a.chunk_rows;
     const int64_t r1 = min(a.n, r0 + a.chunk_rows);
     uint32_t err = 0;
@@ -417,6 +436,10 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
             pk[k] = (o << LENB) | l;
             if ((valid & (1u << k)) && g1 > g0 + l)
                 a.cross[atomicAdd(a.ncross, 1u)] = ((uint64_t)(g0 + l) << 32) | g1;
+            if (OPT && (valid & (1u << k))) {  // (the split's tile of the row: bin piece start)
+                const uint32_t tile = (uint32_t)t * PSUB + min(o >> PSH, (uint32_t)PSUB - 1);
+                atomicAdd(&th[tile >> 1], 1u << ((tile & 1u) << 4));
+            }
         }
         next();
         // rank per bin (16 independent LDS atomics), then bin offsets in the
@@ -463,7 +486,13 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
         for (int k = 0; k < SROWS; ++k) {
             const int j = threadIdx.x + k * WRB;
             const uint32_t t = sbin[j];
-            uint32_t *dst = j < cnt ? a.slab + (cur[t] + (uint32_t)j - soff[t]) : a.dummy;
+            const uint32_t pos = cur[t] + (uint32_t)j - soff[t];
+            bool in = j < cnt;
+            if (OPT && in && pos >= (uint32_t)(((uint64_t)t * a.nchunks + ch + 1) * a.rcap)) {
+                in = false;
+                ovf = 1;
+            }
+            uint32_t *dst = in ? a.slab + pos : a.dummy;
             *dst = stage[j];
         }
         __syncthreads();
@@ -506,6 +535,28 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
         load_step<true, WRB>(a, tail, r1, c, s, e, valid);
         step(tail, valid, [] {});
     }
+    if (OPT) {
+        __syncthreads();  // (cur final, th complete)
+        // the regions' unused slots: SLAB_PAD, lane-consecutive per wave
+        const int wv = threadIdx.x / 64, lane = dev::lane_id();
+        for (int t = wv; t < a.nb; t += WRB / 64) {
+            const uint32_t rend = (uint32_t)(((uint64_t)t * a.nchunks + ch + 1) * a.rcap);
+            for (uint32_t p = cur[t] + lane; p < rend; p += 64) a.slab[p] = SLAB_PAD;
+        }
+        // this chunk's rows per paint tile into its chunk group's totals
+        uint32_t g = (uint32_t)(((uint64_t)ch * a.ngroups + a.ngroups - 1) / a.nchunks);
+        while (g > 0 && (int64_t)(g * (uint64_t)a.nchunks / a.ngroups) > ch) --g;
+        while (g + 1 < (uint32_t)a.ngroups &&
+               (int64_t)((g + 1) * (uint64_t)a.nchunks / a.ngroups) <= ch)
+            ++g;
+        const int nt = a.nb * PSUB;
+        for (int i = threadIdx.x; i < (nt + 1) / 2; i += WRB) {
+            const uint32_t w = th[i];
+            if (w & 0xffffu) atomicAdd(&a.gsum[(int64_t)g * nt + 2 * i], w & 0xffffu);
+            if ((w >> 16) && 2 * i + 1 < nt) atomicAdd(&a.gsum[(int64_t)g * nt + 2 * i + 1], w >> 16);
+        }
+        if (ovf) err |= ERR_REGION;
+    }
     err = dev::wave_reduce_or(err);
     if (err && dev::lane_id() == 0) atomicOr(a.err, err);
 }
@@ -522,6 +573,9 @@ constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
 #ifndef LIME_SPLIT_BLOCKS
 #define LIME_SPLIT_BLOCKS 3072
 #endif
+// OPT: the bin's rows of chunks [c0, c1) are their regions, SLAB_PAD slots
+// skipped
+template <bool OPT = false>
 __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
     constexpr int NWV = SPB / 64, PV = 8;
     __shared__ uint32_t wc[NWV][PSUB], wbase[NWV][PSUB], cur[PSUB];
@@ -536,8 +590,10 @@ __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
     if (threadIdx.x < NWV * PSUB) (&wc[0][0])[threadIdx.x] = 0u;
     const int64_t c0 = (int64_t)g * a.nchunks / a.ngroups,
                   c1 = (int64_t)(g + 1) * a.nchunks / a.ngroups;
-    const uint32_t r0 = a.mat[(int64_t)b * a.nchunks + c0],
-                   r1 = a.mat[(int64_t)b * a.nchunks + c1];
+    const uint32_t r0 = OPT ? (uint32_t)(((uint64_t)b * a.nchunks + c0) * a.rcap)
+                            : a.mat[(int64_t)b * a.nchunks + c0],
+                   r1 = OPT ? (uint32_t)(((uint64_t)b * a.nchunks + c1) * a.rcap)
+                            : a.mat[(int64_t)b * a.nchunks + c1];
     __syncthreads();
     const uint64_t bin0 = (uint64_t)b << BSH;
     constexpr uint32_t CH = SPB * PV;  // rows per chunk
@@ -550,7 +606,7 @@ __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
         uint32_t q[PV], val[PV], rk[PV];
 #pragma unroll
         for (int k = 0; k < PV; ++k) {
-            const bool v = c0 + mine + k * 64 < r1;
+            const bool v = c0 + mine + k * 64 < r1 && (!OPT || pv[k] != SLAB_PAD);
             const uint32_t o = pv[k] >> LENB, l = pv[k] & LMAX;
             q[k] = v ? min(o >> PSH, (uint32_t)PSUB - 1) : PSUB;  // PSUB: no row
             const uint32_t qend = (q[k] + 1) << PSH;
@@ -1404,7 +1460,8 @@ int n_bins(int64_t width) {
 int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_contig,
              const uint32_t *d_start, const uint32_t *d_end, const uint32_t *d_off,
              const uint32_t *d_len, int64_t lo, int64_t hi, uint32_t *slab2, uint32_t *ttot,
-             uint64_t *cross, unsigned int *flags, uint32_t *xbz = nullptr) {
+             uint64_t *cross, unsigned int *flags, uint32_t *xbz = nullptr,
+             bool allow_opt = true) {
     const int nb = n_bins(hi - lo);
     const int nt = nb * PSUB;
     // chunk: 1..16 count steps; as many chunks as whole rounds of the write
@@ -1427,10 +1484,35 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     // the split at 42 serial 4096-row rounds per workgroup on C5's sets)
     const int ng = (int)std::min<int64_t>(std::max<int64_t>((LIME_SPLIT_BLOCKS + nb - 1) / nb, 1),
                                           std::min<int64_t>(nch, 16));
+    // optimistic binning (no count pass; opt-in: LIME_BIN_OPTIMISTIC=1) when
+    // the rows per (bin, chunk) are many enough that regions of mean + 6
+    // sigma under the window's uniform density pad the slab by at most ~1.6x
+    // (C5's sets: ~166 rows, 251 slots); rows clustered by input order
+    // (sorted BED) overflow a region and the set is binned again through the
+    // counted path (the caller sees ERR_REGION in its flags read-back),
+    // which then stays the first choice for this context's next builds
+    // (bin_pessimism).  Measured on C5, same box: the count pass's 223 us
+    // per set went, but the write pass took 636 -> 804 us (a tile count per
+    // row, the padding filled, the group totals added) and the split 267 ->
+    // 331 us (padding read): 1126 vs 1135 us per set, so it is not the
+    // default (profiles/round6/c5_optimistic_binning_*)
+    const double E = (double)R * (double)(1ll << BSH) / (double)std::max<int64_t>(hi - lo, 1);
+    uint32_t rcap = 0;
+    const char *ov = getenv("LIME_BIN_OPTIMISTIC");  // (per call: tests set it at run time)
+    const bool opt_on = ov && ov[0] == '1';
+    if (allow_opt && opt_on && ctx->bin_pessimism == 0 && nb >= 8 && E >= 128.0) {
+        const double c = std::ceil(E + 6.0 * std::sqrt(E)) + 8.0;
+        const uint64_t cap = ((uint64_t)c + 3) / 4 * 4;
+        if ((uint64_t)nb * nch * cap < 0xffff0000ull) rcap = (uint32_t)cap;
+    }
+    if (!rcap && ctx->bin_pessimism > 0) --ctx->bin_pessimism;
+    if (getenv("LIME_TRACE_BINNING"))  // (read per call: tests set it at run time)
+        fprintf(stderr, "lime: bin_rows n=%lld %s (rows per region %.0f, slots %u)\n",
+                (long long)n, rcap ? "optimistic" : "counted", E, rcap);
     PoolBag bag{ctx, {}};
     uint32_t *mat, *slab, *dummy, *gsum, *gpre;
-    LIME_TRY(bag.get(&mat, (size_t)mlen));
-    LIME_TRY(bag.get(&slab, (size_t)std::max<int64_t>(n, 1)));
+    LIME_TRY(bag.get(&mat, rcap ? 1 : (size_t)mlen));
+    LIME_TRY(bag.get(&slab, rcap ? (size_t)nb * nch * rcap : (size_t)std::max<int64_t>(n, 1)));
     LIME_TRY(bag.get(&dummy, 64));
     LIME_TRY(bag.get(&gsum, (size_t)ng * (size_t)nt));
     LIME_TRY(bag.get(&gpre, (size_t)nt * (size_t)ng));
@@ -1467,8 +1549,25 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     a.err = flags + 1;
     a.dummy = dummy;
     a.xbz = xbz;
+    a.rcap = rcap;
     const bool lc = d_contig != nullptr && sp->n <= CMAX;
     LIME_HIP(hipMemsetAsync(gsum, 0, 4 * (size_t)ng * (size_t)nt, S(ctx)));
+    if (rcap) {
+        // write (tile totals counted on the way) -> tile groups -> split
+        LIME_HIP(hipMemsetAsync(flags, 0, 8, S(ctx)));  // (k_bin_count zeroes them otherwise)
+        if (lc)
+            hipLaunchKernelGGL((k_bin_write<true, true, true>), dim3(nch), dim3(WRB), 0, S(ctx), a);
+        else if (d_contig)
+            hipLaunchKernelGGL((k_bin_write<false, true, true>), dim3(nch), dim3(WRB), 0, S(ctx), a);
+        else
+            hipLaunchKernelGGL((k_bin_write<false, false, true>), dim3(nch), dim3(WRB), 0, S(ctx), a);
+        hipLaunchKernelGGL(k_tile_groups, dim3(blocks_for(nt + 1, 256)), dim3(256), 0, S(ctx), a);
+        LIME_TRY(scan_exclusive_u32(ctx, ttot, ttot, (int64_t)nt + 1, nullptr));
+        hipLaunchKernelGGL(k_bin_split_atomic<true>, dim3((unsigned)(nb * ng)), dim3(SPB), 0,
+                           S(ctx), a);
+        LIME_HIP(hipGetLastError());
+        return LIME_OK;
+    }
     if (lc)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(nch), dim3(BINB), 0, S(ctx), a);
     else
@@ -1484,7 +1583,8 @@ int bin_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_co
     else
         hipLaunchKernelGGL((k_bin_write<false, false>), dim3(nch), dim3(WRB), 0, S(ctx), a);
     // the atomic-claim split (C5 12.05 -> 11.73 ms against a ballot-ranked one)
-    hipLaunchKernelGGL(k_bin_split_atomic, dim3((unsigned)(nb * ng)), dim3(SPB), 0, S(ctx), a);
+    hipLaunchKernelGGL(k_bin_split_atomic<false>, dim3((unsigned)(nb * ng)), dim3(SPB), 0, S(ctx),
+                       a);
     LIME_HIP(hipGetLastError());
     return LIME_OK;
 }
@@ -1555,6 +1655,14 @@ int bin_set(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_con
     unsigned int h[2] = {0, 0};
     LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
     LIME_TRY(rows_error(h[1]));
+    if (h[1] & ERR_REGION) {  // an optimistic region overflowed: the counted path
+        if (getenv("LIME_TRACE_BINNING")) fprintf(stderr, "lime: region overflow, counted again\n");
+        ctx->bin_pessimism = 32;
+        LIME_TRY(bin_rows(ctx, sp, n, d_contig, d_start, d_end, d_off, d_len, lo, hi, b.slab2,
+                          b.tstart, cross, flags, b.xb, false));
+        LIME_TRY(read_back(ctx, h, flags, sizeof(h)));
+        LIME_TRY(rows_error(h[1]));
+    }
     if (h[0]) {
         LIME_TRY(alloc(ctx, &b.xl, 2 * (size_t)h[0]));
         LIME_TRY(bucket_cross(ctx, nt + 1, cross, flags, h[0], b.xb, b.xl, true));
@@ -1687,8 +1795,20 @@ int bitset_and_rows(lime_ctx *ctx, const lime_space *sp, int k, const int64_t *n
     // behind its binning; wait for that copy only)
     auto bucket = [&](int q) -> int {
         LIME_HIP(hipEventSynchronize(ev.e[q % 2]));
-        const unsigned int nx = hflags[2 * (q % 2)], err = hflags[2 * (q % 2) + 1];
+        unsigned int nx = hflags[2 * (q % 2)], err = hflags[2 * (q % 2) + 1];
         LIME_TRY(rows_error(err));
+        if (err & ERR_REGION) {  // set q again through the counted path
+            if (getenv("LIME_TRACE_BINNING"))
+                fprintf(stderr, "lime: region overflow, counted again\n");
+            ctx->bin_pessimism = 32;
+            lime_bitset::Bins &b = bs->bins[q];
+            LIME_TRY(bin_rows(ctx, sp, n[q], d_contig[q], d_start[q], d_end[q], d_off, d_len, lo,
+                              hi, b.slab2, b.tstart, cross[q % 2], flags + 2 * q, b.xb, false));
+            unsigned int h[2] = {0, 0};
+            LIME_TRY(read_back(ctx, h, flags + 2 * q, sizeof(h)));
+            LIME_TRY(rows_error(h[1]));
+            nx = h[0];
+        }
         lime_bitset::Bins &b = bs->bins[q];
         if (nx == 0) {
             release(ctx, b.xb);

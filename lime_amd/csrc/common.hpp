@@ -88,6 +88,9 @@ struct lime_ctx {
     std::map<std::vector<uint32_t>, std::shared_ptr<lime::SpaceDev>> spaces;
     static constexpr size_t SPACE_CACHE = 8;
     hipEvent_t ev = nullptr;
+    // bit-per-base builds: after an optimistic (uncounted) binning overflowed
+    // its regions, this many later builds take the counted path first
+    int bin_pessimism = 0;
 };
 
 struct lime_space {

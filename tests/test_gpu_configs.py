@@ -313,6 +313,68 @@ def test_c5_eight_way_and_density(ctx):
     assert 0.01 < cov / sum(sp.lengths) < 0.05  # 8-way ~2.7% of the genome
 
 
+@pytest.mark.timeout(600)
+def test_c5_optimistic_binning_and_sorted_fallback(monkeypatch, capfd):
+    # With LIME_BIN_OPTIMISTIC=1 bit-per-base builds bin rows without a count
+    # pass when the window's uniform density fills each (bin, chunk) region
+    # (mean + 6 sigma slots): C5's shape, here on hg38/8 with 3 x 1.5625e7
+    # rows.  (Opt-in: on C5 it measured no faster than the counted path.)  The same rows in
+    # SORTED order (a sorted BED file) put each chunk's rows in one or two
+    # bins: the regions overflow, the set is binned again through the counted
+    # path, and the results are unchanged -- through the k-way AND (pipelined
+    # sets) and the one-set build, against the oracle fold (A.4).  A fresh
+    # context: after an overflow the context prefers the counted path for its
+    # next builds (lime_ctx.bin_pessimism), which must not leak into other tests
+    import torch
+
+    import lime_amd
+    monkeypatch.setenv("LIME_TRACE_BINNING", "1")
+    monkeypatch.setenv("LIME_BIN_OPTIMISTIC", "1")
+    c = lime_amd.Context(0)
+    try:
+        sp = hg38(8)
+        per = 125_000_000 // 8
+        devs, merged = [], []
+        for i in range(3):
+            dev, X = device_rows(c, sp, per, 0x70 + i, 10, 40)
+            devs.append(dev)
+            merged.append(oracle.merge_mt(len(sp.names), X))
+        exp = fold_and(len(sp.names), merged)
+        want = coalesce(exp["contig"], exp["start"], exp["end"])
+
+        def and_runs(ds):
+            b = c.bitset_and_from_device(
+                sp, [(d[0].numel(), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr()) for d in ds])
+            r = c.bitset_runs(0, b).to_host()
+            b.close()
+            return coalesce(r["contig"], r["start"], r["end"])
+        capfd.readouterr()
+        assert_runs_equal(and_runs(devs), want)
+        log = capfd.readouterr().err
+        assert log.count("optimistic") == 3 and "overflow" not in log, log
+        # the same rows sorted by (contig, start)
+        sdevs = []
+        for d in devs:
+            key = d[0].to(torch.int64) * (1 << 32) + d[1].to(torch.int64)
+            o = torch.argsort(key)
+            sdevs.append(tuple(x[o].contiguous() for x in d))
+        torch.cuda.synchronize()
+        assert_runs_equal(and_runs(sdevs), want)
+        log = capfd.readouterr().err
+        assert "overflow" in log and "counted" in log, log
+        # one set through the single-set build (bin_set), sorted: counted first
+        # now, then (pessimism spent) optimistic again, overflowing again
+        one = merged[0]
+        w1 = coalesce(one["contig"], one["start"], one["end"])
+        for _ in range(2):
+            b = dbits(c, sp, sdevs[0])
+            r = c.bitset_runs(0, b).to_host()
+            b.close()
+            assert_runs_equal(coalesce(r["contig"], r["start"], r["end"]), w1)
+    finally:
+        c.close()
+
+
 @pytest.mark.timeout(900)
 def test_c2_subtract_full_size(ctx):
     # DistributedSubtract (Subtract.scala:91-116) on C2's inputs at full size,

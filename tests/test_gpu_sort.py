@@ -11,6 +11,9 @@ sort, on inputs that take every path of lime_amd/csrc/sort.hip:
   - the digit passes (spans within 16 bits, sets of few rows per bucket,
     sets past LAVG rows per bucket: both sides of that switch at full size
     over hg38, C3-shaped pile-ups, giant piles, global rows);
+  - the packed second bucket pass (one word per row, gs mod 2^L and the
+    width) with the bucket starts from its histogram's partial counts,
+    first-digit regions crowded into a few tiles, widths at the u16 limit;
   - host, device and global-coordinate inputs, zero-width rows, exact
     duplicates, rows already in order.
 
@@ -218,6 +221,31 @@ def test_bucketed_sort_switch_point(ctx, n):
     sp = _hg38()
     c, s, e = _synth(ctx, sp, n, 0x5A, 0, 60)
     _check_device_order(ctx, sp, n, c, s, e)
+
+
+def test_bucketed_sort_packed_partials(ctx):
+    # the packed second pass places every bucket from k_hist_part's partial
+    # counts.  Here 2.05e6 rows over hg38: 2e6 of them in one pile at one
+    # start (one first digit, one bucket through k_local_big's workgroup
+    # radix), the rest spread thin, so the first-digit regions of those few
+    # rows crowd into a handful of pass-1 tiles: a tile sees many regions
+    # start (the partial rounds of 16 first digits each), and most (d2, D)
+    # buckets are empty (their starts from the scanned counts alone).
+    # Widths up to 65,535 (the packed word's limit) and zero-width rows.
+    rng = np.random.default_rng(61)
+    sp = _hg38()
+    lens = np.array(sp.lengths)
+    n_pile, n_thin = 2_000_000, 50_000
+    c = np.concatenate([np.full(n_pile, 2, np.int32),
+                        rng.integers(0, len(lens), n_thin).astype(np.int32)])
+    s = np.concatenate([np.full(n_pile, 1_234_567, np.int64),
+                        (rng.random(n_thin) * (lens[c[n_pile:]] - 70_000)).astype(np.int64)])
+    w = rng.integers(0, 600, len(c))
+    w[rng.integers(0, len(c), 500)] = 65_535
+    w[rng.integers(0, len(c), 20_000)] = 0
+    e = s + w
+    perm = rng.permutation(len(c))
+    _check_host_set(ctx, sp, c[perm], s[perm], e[perm])
 
 
 def test_bucketed_sort_dense_buckets(ctx):

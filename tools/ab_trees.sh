@@ -17,5 +17,6 @@ done; done
 for tr in "$@"; do
   tag=$(echo $tr | tr '/.' '__')
   (cd $tr && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $top/gpurun_out/${T}_${tag}_kt -o run -- python tools/bench_extra.py --workload $W $XARGS > $top/gpurun_out/${T}_${tag}_kt.log 2>&1) || { tail -20 $top/gpurun_out/${T}_${tag}_kt.log; exit 1; }
-  echo "== $tr"; python3 tools/kstats.py gpurun_out/${T}_${tag}_kt | head -14
+  python3 tools/kstats.py gpurun_out/${T}_${tag}_kt > gpurun_out/${T}_${tag}_kstats.txt
+  echo "== $tr"; head -14 gpurun_out/${T}_${tag}_kstats.txt
 done

@@ -1378,7 +1378,10 @@ void k_local_keys(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) 
 }
 constexpr int LCAP_M = 6144, LCAP_W = 16384;
 #define LIME_LOCAL_MID(PK) k_local_keys<512, 12, 13, 14, 2, PK>
-#define LIME_LOCAL_WIDE(PK) k_local_keys<1024, 16, 14, 15, 1, PK>
+#ifndef LIME_WIDE_SBB
+#define LIME_WIDE_SBB 15
+#endif
+#define LIME_LOCAL_WIDE(PK) k_local_keys<1024, 16, 14, LIME_WIDE_SBB, 1, PK>
 
 // A bucket past LCAP_B rows: LSD over its key (gs mod 2^L, non-zero width) in
 // 6-bit digits by the whole workgroup, NT rows per step in order (wave ballot

@@ -61,6 +61,10 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-scale", type=int, default=100,
                    help="CPU sample: C2 density on hg38/scale with n/scale rows")
+    p.add_argument("--sharded", action="store_true",
+                   help="c2 at N = 1 through the sharded step (a one-rank process group): "
+                        "the route / exchange / carry overheads the N > 1 runs pay, measured "
+                        "on one GPU (a diagnostic, not the metric's N = 1 line)")
     return p.parse_args()
 
 
@@ -308,7 +312,13 @@ def main():
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     comm_dev = None  # RCCL: device buffers
-    if world > 1:
+    args.sharded_step = world > 1 or (args.sharded and args.workload == "c2")
+    if args.sharded_step and world == 1:  # a one-rank group (--sharded)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if args.sharded_step:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -367,13 +377,14 @@ def main():
             fi.release()
         line["operators"] = ops
     line.setdefault("config", {}).update(
-        {"world_size": world, "dist_backend": args.dist_backend if world > 1 else None,
+        {"world_size": world, "dist_backend": args.dist_backend if args.sharded_step else None,
+         "sharded_step": bool(args.sharded_step),
          "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
          else ("bench.py --gpus N (own ranks)" if world > 1 else None)})
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
+    if args.sharded_step:
         dist.destroy_process_group()
 
 
@@ -407,7 +418,7 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
             fills.append((e0, ev(), k, plan.n))
 
     shard = None
-    if world > 1:
+    if args.sharded_step:
         from lime_amd.sharded import ShardStep
         shard = ShardStep(ctx, space, comm_device=comm_dev, shared_stream=True)
         # count-balanced shard bounds from samples of both inputs, once
@@ -462,7 +473,7 @@ def bench_c2(args, ctx, space, dev, world, rank, comm_dev, ev):
         avg_b = sum(fill_bytes) / max(len(fill_bytes), 1)
         achieved = avg_b / (avg_ms * 1e-3) / 1e9 if avg_ms else 0.0
         p = state["phases"]
-        if world > 1:
+        if shard is not None:
             breakdown = {"route_sort_ms": p[0].elapsed_time(p[1]),
                          "merge_halo_count_fill_carry_ms": p[1].elapsed_time(p[2]),
                          "fill_ms": sum(fill_ms[-max(1, -(-state["npairs"] // chunk)):]),

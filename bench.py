@@ -291,6 +291,9 @@ def spawn_ranks(n, script=None, argv=None):
 
 def main():
     args = parse()
+    if os.environ.get("LIME_BENCH_WATCHDOG"):  # debugging: every thread's stack, then exit
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["LIME_BENCH_WATCHDOG"]), exit=True)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))

@@ -22,9 +22,21 @@ all interval compute stays in the engine (lime_amd.engine) on each GPU.
 
 The functions work on int64 torch tensors on any device, so the same code
 runs over RCCL (backend "nccl") on MI355X and over gloo on the CPU in tests.
+
+Every variable-size exchange goes through _a2a_counts + _a2a_payload: no
+collective at world size 1 (the exchange is the identity there), and at most
+A2A_MAX_BYTES per rank pair per collective -- larger messages go in rounds.
+RCCL 2.26 (this image) completes only part of a point-to-point message of
+about 1 GiB or more: one rank's all_to_all_single of 1.2e9 B moved its first
+600 MB and 2.4e9 B its first 1.2 GB, while 720 MB moved whole
+(tools/rccl_probe.py --big).
 """
+import os
+
 import torch
 import torch.distributed as dist
+
+A2A_MAX_BYTES = 512 << 20
 
 
 def _ws(group):
@@ -110,17 +122,72 @@ def splits_from_samples(s, span, world, group=None, align=1):
     return cuts
 
 
+def _a2a_max_bytes():
+    # read per call: tests shrink it to force several rounds
+    return int(os.environ.get("LIME_A2A_MAX_BYTES", A2A_MAX_BYTES))
+
+
+def _a2a_counts(rows, group, cd):
+    """rows[q]: the list of row counts this rank sends to rank q (one per set).
+    ONE all_to_all of them, each message carrying this rank's largest
+    per-destination total too.  Returns (recv[p]: the list rank p sends
+    here, the largest per-pair row total of any rank -- every rank gets the
+    same, so they agree on the payload's rounds).  World size 1: no
+    collective."""
+    w, _ = _ws(group)
+    mx = max((sum(r) for r in rows), default=0)
+    if w == 1:
+        return [list(r) for r in rows], mx
+    k = len(rows[0])
+    sc = torch.tensor([list(r) + [mx] for r in rows], dtype=torch.int64, device=cd)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    m = rc.tolist()
+    return [x[:k] for x in m], max(x[k] for x in m)
+
+
+def _a2a_payload(src, send_n, recv_n, pair_max, group):
+    """Variable all_to_all of src's rows (grouped by destination, send_n[q] to
+    rank q; recv_n[p] from rank p) on src's device.  World size 1: src itself.
+    Messages over A2A_MAX_BYTES per pair (pair_max rows, from _a2a_counts)
+    move in rounds of at most that many bytes per pair."""
+    w, _ = _ws(group)
+    if w == 1:
+        return src
+    tail = tuple(src.shape[1:])
+    row_b = src.element_size()
+    for d in tail:
+        row_b *= d
+    cap = max(1, _a2a_max_bytes() // max(row_b, 1))
+    out = torch.empty((sum(recv_n),) + tail, dtype=src.dtype, device=src.device)
+    rounds = max(1, -(-pair_max // cap))
+    if rounds == 1:
+        dist.all_to_all_single(out, src, output_split_sizes=list(recv_n),
+                               input_split_sizes=list(send_n), group=group)
+        return out
+    so, ro = [0], [0]
+    for q in range(w):
+        so.append(so[-1] + send_n[q])
+        ro.append(ro[-1] + recv_n[q])
+    for j in range(rounds):
+        lo = j * cap
+        s_n = [max(0, min(cap, n - lo)) for n in send_n]
+        r_n = [max(0, min(cap, n - lo)) for n in recv_n]
+        s = torch.cat([src[so[q] + lo:so[q] + lo + s_n[q]] for q in range(w)])
+        r = torch.empty((sum(r_n),) + tail, dtype=src.dtype, device=src.device)
+        dist.all_to_all_single(r, s, output_split_sizes=r_n, input_split_sizes=s_n, group=group)
+        at = 0
+        for p in range(w):
+            out[ro[p] + lo:ro[p] + lo + r_n[p]] = r[at:at + r_n[p]]
+            at += r_n[p]
+    return out
+
+
 def _alltoallv(send, counts, group):
     """Variable all_to_all of a 2-D int64 tensor [rows, k]; counts[q] rows to q."""
-    w, _ = _ws(group)
-    dev = send.device
-    sc = torch.tensor(counts, dtype=torch.int64, device=dev)
-    rc = torch.empty(w, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(rc, sc, group=group)
-    rcounts = rc.tolist()
-    recv = torch.empty((sum(rcounts), send.shape[1]), dtype=send.dtype, device=dev)
-    dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
-                           input_split_sizes=list(counts), group=group)
+    rcm, mx = _a2a_counts([[c] for c in counts], group, send.device)
+    rcounts = [x[0] for x in rcm]
+    recv = _a2a_payload(send.contiguous(), list(counts), rcounts, mx, group)
     return recv, rcounts
 
 
@@ -384,28 +451,19 @@ def exchange(tensors, counts, group=None, comm_device=None, packed=False):
     xGMI's point-to-point links).  The counts cost one all_to_all and one
     host read: all_to_all_single takes its split sizes on the host.
     Returns (received tensors on the input device, received counts)."""
-    w, _ = _ws(group)
     dev = tensors[0].device
     cd = comm_device if comm_device is not None else dev
-    sc = torch.tensor(counts, dtype=torch.int64, device=cd)
-    rc = torch.empty(w, dtype=torch.int64, device=cd)
-    dist.all_to_all_single(rc, sc, group=group)
-    rcounts = rc.tolist()
+    rcm, mx = _a2a_counts([[c] for c in counts], group, cd)
+    rcounts = [x[0] for x in rcm]
     if packed and len(tensors) > 1:
         t = sum(counts)
         src = torch.stack([x[:t] for x in tensors], dim=1).to(cd)
-        r = torch.empty((sum(rcounts), len(tensors)), dtype=src.dtype, device=cd)
-        dist.all_to_all_single(r, src, output_split_sizes=rcounts,
-                               input_split_sizes=list(counts), group=group)
-        r = r.to(dev)
+        r = _a2a_payload(src, list(counts), rcounts, mx, group).to(dev)
         return [r[:, j].contiguous() for j in range(len(tensors))], rcounts
     out = []
     for t in tensors:
         src = t[:sum(counts)].to(cd)
-        r = torch.empty(sum(rcounts), dtype=t.dtype, device=cd)
-        dist.all_to_all_single(r, src, output_split_sizes=rcounts,
-                               input_split_sizes=list(counts), group=group)
-        out.append(r.to(dev))
+        out.append(_a2a_payload(src, list(counts), rcounts, mx, group).to(dev))
     return out, rcounts
 
 
@@ -417,18 +475,12 @@ def exchange_rows(buf, counts, group=None, comm_device=None):
     Bytes per routed row: the route's write + the exchange, where the
     column form (exchange(packed=True)) added a torch.stack copy on the way
     out and a .contiguous() per column on the way in."""
-    w, _ = _ws(group)
     dev = buf.device
     cd = comm_device if comm_device is not None else dev
-    sc = torch.tensor(counts, dtype=torch.int64, device=cd)
-    rc = torch.empty(w, dtype=torch.int64, device=cd)
-    dist.all_to_all_single(rc, sc, group=group)
-    rcounts = rc.tolist()
+    rcm, mx = _a2a_counts([[c] for c in counts], group, cd)
+    rcounts = [x[0] for x in rcm]
     src = buf[:sum(counts)].to(cd)
-    r = torch.empty((sum(rcounts), buf.shape[1]), dtype=buf.dtype, device=cd)
-    dist.all_to_all_single(r, src, output_split_sizes=rcounts, input_split_sizes=list(counts),
-                           group=group)
-    return r.to(dev), rcounts
+    return _a2a_payload(src, list(counts), rcounts, mx, group).to(dev), rcounts
 
 
 def exchange_sets_rows(bufs, counts, group=None, comm_device=None):
@@ -447,20 +499,14 @@ def exchange_sets_rows(bufs, counts, group=None, comm_device=None):
     for i in range(k):
         for q in range(w):
             starts[i][q + 1] = starts[i][q] + counts[i][q]
-    sc = torch.tensor([[counts[i][q] for i in range(k)] for q in range(w)], dtype=torch.int64,
-                      device=cd)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    rcm = rc.tolist()  # rcm[p][i]: rows of set i from rank p
+    # rcm[p][i]: rows of set i from rank p
+    rcm, mx = _a2a_counts([[counts[i][q] for i in range(k)] for q in range(w)], group, cd)
     parts = [bufs[i][starts[i][q]:starts[i][q + 1]] for q in range(w) for i in range(k)]
     src = torch.cat(parts).to(cd) if parts else torch.empty((0, ncol), dtype=torch.int32,
                                                             device=cd)
     send_n = [sum(counts[i][q] for i in range(k)) for q in range(w)]
     recv_n = [sum(rcm[p]) for p in range(w)]
-    r = torch.empty((sum(recv_n), ncol), dtype=src.dtype, device=cd)
-    dist.all_to_all_single(r, src, output_split_sizes=recv_n, input_split_sizes=send_n,
-                           group=group)
-    r = r.to(dev)
+    r = _a2a_payload(src, send_n, recv_n, mx, group).to(dev)
     out, at = [[] for _ in range(k)], 0
     for p in range(w):
         for i in range(k):
@@ -487,20 +533,14 @@ def exchange_sets(sets, counts, group=None, comm_device=None):
         for q in range(w):
             starts[i][q + 1] = starts[i][q] + counts[i][q]
     # counts: to rank q the k numbers counts[.][q]
-    sc = torch.tensor([[counts[i][q] for i in range(k)] for q in range(w)], dtype=torch.int64,
-                      device=cd)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    rcm = rc.tolist()  # rcm[p][i]: rows of set i from rank p
+    # rcm[p][i]: rows of set i from rank p
+    rcm, mx = _a2a_counts([[counts[i][q] for i in range(k)] for q in range(w)], group, cd)
     parts = [torch.stack([c[starts[i][q]:starts[i][q + 1]] for c in sets[i]], dim=1)
              for q in range(w) for i in range(k)]
     src = torch.cat(parts).to(cd) if parts else torch.empty((0, ncol), device=cd)
     send_n = [sum(counts[i][q] for i in range(k)) for q in range(w)]
     recv_n = [sum(rcm[p]) for p in range(w)]
-    r = torch.empty((sum(recv_n), ncol), dtype=src.dtype, device=cd)
-    dist.all_to_all_single(r, src, output_split_sizes=recv_n, input_split_sizes=send_n,
-                           group=group)
-    r = r.to(dev)
+    r = _a2a_payload(src, send_n, recv_n, mx, group).to(dev)
     out, at = [[] for _ in range(k)], 0
     for p in range(w):
         for i in range(k):

@@ -361,7 +361,9 @@ def test_sharded_merge_run_ids_complement_strands(world):
     assert got == want
 
 
-def _xsets_worker(rank, world, port, q):
+def _xsets_worker(rank, world, port, q, cap=None):
+    if cap:  # rounds of at most `cap` bytes per rank pair (dist._a2a_payload)
+        os.environ["LIME_A2A_MAX_BYTES"] = str(cap)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     from datetime import timedelta
@@ -395,14 +397,16 @@ def _xsets_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_exchange_sets(world):
+@pytest.mark.parametrize("world,cap", [(1, None), (2, None), (3, None), (2, 8), (3, 12)])
+def test_exchange_sets(world, cap):
     # C5's batched exchange: every (source, set) segment lands in its set, in
-    # rank order, both columns aligned
+    # rank order, both columns aligned; cap: payloads cut into rounds of a
+    # few bytes per rank pair (the guard against RCCL's ~1 GiB message limit)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_xsets_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_xsets_worker, args=(r, world, port, q, cap))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in range(world))

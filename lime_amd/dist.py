@@ -127,6 +127,12 @@ def _a2a_max_bytes():
     return int(os.environ.get("LIME_A2A_MAX_BYTES", A2A_MAX_BYTES))
 
 
+def _identity_at_one(w):
+    # LIME_A2A_FORCE=1 (tests): a one-rank group still issues the
+    # collectives, so the rounds run over RCCL on a one-GPU box
+    return w == 1 and os.environ.get("LIME_A2A_FORCE") != "1"
+
+
 def _a2a_counts(rows, group, cd):
     """rows[q]: the list of row counts this rank sends to rank q (one per set).
     ONE all_to_all of them, each message carrying this rank's largest
@@ -136,7 +142,7 @@ def _a2a_counts(rows, group, cd):
     collective."""
     w, _ = _ws(group)
     mx = max((sum(r) for r in rows), default=0)
-    if w == 1:
+    if _identity_at_one(w):
         return [list(r) for r in rows], mx
     k = len(rows[0])
     sc = torch.tensor([list(r) + [mx] for r in rows], dtype=torch.int64, device=cd)
@@ -152,7 +158,7 @@ def _a2a_payload(src, send_n, recv_n, pair_max, group):
     Messages over A2A_MAX_BYTES per pair (pair_max rows, from _a2a_counts)
     move in rounds of at most that many bytes per pair."""
     w, _ = _ws(group)
-    if w == 1:
+    if _identity_at_one(w):
         return src
     tail = tuple(src.shape[1:])
     row_b = src.element_size()

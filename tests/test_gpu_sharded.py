@@ -464,3 +464,42 @@ def test_sharded_complement_run_ids_strands(world, mode):
                      for X, st, i in ((A, sa, p[0][0]), (B, sb, p[0][1]))]) for p in extra + missing]
         raise AssertionError(f"{len(got)} vs {len(want)} pairs; extra {extra}; missing {missing}; "
                              f"rows {info}")
+
+
+def _rccl_rounds_worker(port, q):
+    # a one-rank RCCL group with the collectives forced on (no world-1
+    # shortcut) and 64 MiB rounds: 1.2 GB of rows in 18 rounds, every row
+    # back in place -- one all_to_all_single of 1.2 GB moves only its first
+    # 600 MB on this image's RCCL (tools/rccl_probe.py --big)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                      WORLD_SIZE="1", LIME_A2A_FORCE="1", LIME_A2A_MAX_BYTES=str(64 << 20))
+    import torch
+    import torch.distributed as dist
+    from lime_amd import dist as ld
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    try:
+        n = 100_000_000
+        buf = torch.randint(0, 1 << 30, (n, 3), dtype=torch.int32, device=dev)
+        r, rc = ld.exchange_rows(buf, [n])
+        ok_rows = rc == [n] and torch.equal(r, buf)
+        del r
+        small = [buf[:1000, :2].contiguous(), buf[1000:1500, :2].contiguous()]
+        got = ld.exchange_sets_rows(small, [[1000], [500]])
+        ok_sets = all(torch.equal(torch.cat(sl), x) and m == x.shape[0] and moved == 0
+                      for (sl, m, moved), x in zip(got, small))
+        q.put((bool(ok_rows), bool(ok_sets)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_rounds_one_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_rounds_worker, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=150)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert res == (True, True)

@@ -653,15 +653,13 @@ __device__ __forceinline__ void paint_lds(unsigned long long *img, uint32_t s0, 
         }
         return;
     }
-    for (uint32_t w = wa; w <= wb; ++w) {
-        const uint32_t lo = w == wa ? (s0 & 63) : 0;
-        const uint32_t hi = w == wb ? ((e0 - 1) & 63) : 63;
-        const uint64_t mk = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo);
-        if (mk == ~0ull)
-            img[w] = mk;  // whole word: a plain store is idempotent with the ORs
-        else
-            atomicOr(&img[w], (unsigned long long)mk);
-    }
+    // head and tail words by ORs, the whole words between by plain stores
+    // (idempotent with the ORs): one store per interior word, no per-word
+    // mask arithmetic (C4's rows span ~5 words)
+    const uint64_t head = ~0ull << (s0 & 63), tail = ~0ull >> (63 - ((e0 - 1) & 63));
+    atomicOr(&img[wa], (unsigned long long)head);
+    atomicOr(&img[wb], (unsigned long long)tail);
+    for (uint32_t w = wa + 1; w < wb; ++w) img[w] = ~0ull;
 }
 
 // ---------------------------------------- k-way AND straight from rows

@@ -641,16 +641,28 @@ __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
 
 // bits [s0, e0) of a tile image (LDS); rows within two words (C4/C5's
 // lengths) take a branch-free path: two masked ORs
+#ifndef LIME_PAINT2
+#define LIME_PAINT2 1
+#endif
 __device__ __forceinline__ void paint_lds(unsigned long long *img, uint32_t s0, uint32_t e0) {
     const uint32_t wa = s0 >> 6, wb = (e0 - 1) >> 6;
     if (wb - wa <= 1) {
         const uint64_t head = ~0ull << (s0 & 63), tail = ~0ull >> (63 - ((e0 - 1) & 63));
+#if LIME_PAINT2
+        // branch-free: two ORs always (the same word twice when the row is
+        // inside one), where a lane-divergent one-or-two made a wave of
+        // mixed rows issue three (C5's rows span one or two words)
+        const bool one = wa == wb;
+        atomicOr(&img[wa], (unsigned long long)(one ? head & tail : head));
+        atomicOr(&img[wb], (unsigned long long)(one ? head & tail : tail));
+#else
         if (wa == wb) {
             atomicOr(&img[wa], (unsigned long long)(head & tail));
         } else {
             atomicOr(&img[wa], (unsigned long long)head);
             atomicOr(&img[wb], (unsigned long long)tail);
         }
+#endif
         return;
     }
     // head and tail words by ORs, the whole words between by plain stores
@@ -885,10 +897,12 @@ __device__ __forceinline__ uint64_t op_raw(const OpArgs &a, int64_t w) {
     }
 }
 
-__device__ __forceinline__ void events_of(uint64_t x, uint64_t prev, uint64_t &st, uint64_t &en) {
-    const uint64_t sh = (x << 1) | (prev >> 63);
-    st = x & ~sh;
-    en = ~x & sh;
+// the events of word x after `prev` (whose top bit precedes x's bit 0): bit
+// i where x_i != x_(i-1) -- a run start where x_i is set, an end where it is
+// clear; starts and ends alternate, so their order tells them apart and one
+// mask (one xor, one popcount) serves both)
+__device__ __forceinline__ uint64_t event_bits(uint64_t x, uint64_t prev) {
+    return x ^ ((x << 1) | (prev >> 63));
 }
 
 // NOT within contigs: clear the pad bits and every bit past the window
@@ -998,9 +1012,7 @@ __global__ __launch_bounds__(BB) void k_ev_count(OpArgs a, uint32_t *__restrict_
     stage_tile(a, w0, img, s_pad, &s_npad);
     uint32_t c = 0;
     for (int i = threadIdx.x; i < BT; i += BB) {
-        uint64_t st, en;
-        events_of(img[ipad(i + 1)], img[ipad(i)], st, en);
-        c += __popcll(st) + __popcll(en);
+        c += __popcll(event_bits(img[ipad(i + 1)], img[ipad(i)]));
     }
     c = dev::wave_reduce_sum(c);
     if (dev::lane_id() == 0) ws[threadIdx.x / 64] = c;
@@ -1026,17 +1038,13 @@ __global__ __launch_bounds__(BB) void k_ev_write(OpArgs a, const uint32_t *__res
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
-        uint64_t st, en;
-        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
-        c += __popcll(st) + __popcll(en);
+        c += __popcll(event_bits(img[ipad(q0 + k + 1)], img[ipad(q0 + k)]));
     }
     uint32_t tot;
     uint32_t ev = toff[blockIdx.x] + dev::block_exclusive_sum<BB>(c, scratch, &tot);
 #pragma unroll
     for (int k = 0; k < BW; ++k) {
-        uint64_t st, en;
-        events_of(img[ipad(q0 + k + 1)], img[ipad(q0 + k)], st, en);
-        uint64_t all = st | en;
+        uint64_t all = event_bits(img[ipad(q0 + k + 1)], img[ipad(q0 + k)]);
         const uint32_t base = (uint32_t)((a.word0 + w0 + q0 + k) * 64);
         while (all) {
             const int b = __builtin_ctzll(all);
@@ -1164,9 +1172,7 @@ __global__ __launch_bounds__(EV_NT) void k_ev_local(OpArgs a, uint32_t *__restri
         uint64_t p = prev;
 #pragma unroll
         for (int k = 0; k < EV_W; ++k) {
-            uint64_t st, en;
-            events_of(x[k], p, st, en);
-            c += __popcll(st) + __popcll(en);
+            c += __popcll(event_bits(x[k], p));
             p = x[k];
         }
     }
@@ -1182,10 +1188,8 @@ __global__ __launch_bounds__(EV_NT) void k_ev_local(OpArgs a, uint32_t *__restri
         uint64_t p = prev;
 #pragma unroll
         for (int k = 0; k < EV_W; ++k) {
-            uint64_t st, en;
-            events_of(x[k], p, st, en);
+            uint64_t all = event_bits(x[k], p);
             p = x[k];
-            uint64_t all = st | en;
             const uint32_t base = (uint32_t)((a.word0 + q0 + k) * 64);
             while (all) {
                 const int b = __builtin_ctzll(all);
@@ -1267,15 +1271,21 @@ __device__ __forceinline__ void tile_events(const PaintEvArgs &a, int t, WJ wj,
     const int64_t nw = a.n_words;
     const int64_t w0 = (int64_t)t * TWORDS;
     const int64_t plo = (a.word0 + w0) * 64, phi = plo + (int64_t)TWORDS * 64;
+    // (only a tile reaching past the window's last word or bit tests its
+    // words: a tile-uniform branch)
+    const bool edge = w0 + TWORDS > nw || (a.notmask && (a.word0 + w0 + TWORDS) * 64 > a.hi_bit);
 #pragma unroll
     for (int j = 0; j < AWPT; ++j) {
         const int q = threadIdx.x + j * PAINTB;
-        uint64_t x = w0 + q < nw ? wj(j) : 0ull;
-        if (a.notmask) {  // nothing past the window
-            const int64_t b0 = (a.word0 + w0 + q) * 64;
-            if (b0 + 64 > a.hi_bit) {
-                const int64_t keep = a.hi_bit - b0;
-                x &= keep <= 0 ? 0ull : ((1ull << keep) - 1);
+        uint64_t x = wj(j);
+        if (edge) {
+            if (w0 + q >= nw) x = 0ull;
+            if (a.notmask) {  // nothing past the window
+                const int64_t b0 = (a.word0 + w0 + q) * 64;
+                if (b0 + 64 > a.hi_bit) {
+                    const int64_t keep = a.hi_bit - b0;
+                    x &= keep <= 0 ? 0ull : ((1ull << keep) - 1);
+                }
             }
         }
         img[ipad(q)] = x;
@@ -1310,9 +1320,7 @@ __device__ __forceinline__ void tile_events(const PaintEvArgs &a, int t, WJ wj,
         uint64_t p = prev;
 #pragma unroll
         for (int k = 0; k < PEW; ++k) {
-            uint64_t st, en;
-            events_of(x[k], p, st, en);
-            c += __popcll(st) + __popcll(en);
+            c += __popcll(event_bits(x[k], p));
             p = x[k];
         }
     }
@@ -1335,10 +1343,8 @@ __device__ __forceinline__ void tile_events(const PaintEvArgs &a, int t, WJ wj,
         uint64_t p = prev;
 #pragma unroll
         for (int k = 0; k < PEW; ++k) {
-            uint64_t st, en;
-            events_of(x[k], p, st, en);
+            uint64_t all = event_bits(x[k], p);
             p = x[k];
-            uint64_t all = st | en;
             while (all) {
                 const int b = __builtin_ctzll(all);
                 all &= all - 1;

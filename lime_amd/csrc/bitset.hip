@@ -569,7 +569,13 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 // stored there (a wave's rows of one tile are consecutive slots).  Claims
 // inside a group come back in any order: a tile's rows are ORed in any order.
 static_assert(NBMAX % WRB == 0 || WRB % NBMAX == 0, "write-pass bin scan: whole bins per thread");
-constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
+#ifndef LIME_SPB
+#define LIME_SPB 512
+#endif
+#ifndef LIME_SPLIT_PV
+#define LIME_SPLIT_PV 8
+#endif
+constexpr int SPB = LIME_SPB;  // split block: 3 blocks (24 waves) per CU
 #ifndef LIME_SPLIT_BLOCKS
 #define LIME_SPLIT_BLOCKS 3072
 #endif
@@ -577,7 +583,7 @@ constexpr int SPB = 512;  // split block: 3 blocks (24 waves) per CU
 // skipped
 template <bool OPT = false>
 __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
-    constexpr int NWV = SPB / 64, PV = 8;
+    constexpr int NWV = SPB / 64, PV = LIME_SPLIT_PV;
     __shared__ uint32_t wc[NWV][PSUB], wbase[NWV][PSUB], cur[PSUB];
     // workgroup (bin b, chunk group g): the bin's rows of chunks [c0, c1),
     // consecutive in the bin-ordered slab; each tile's cursor starts past

@@ -342,7 +342,7 @@ int lime_result_format_bed(const lime_result *res, const char *const *names, cha
 
 /* ----------------------------------------------------- bit-per-base path */
 /* The bit-per-base set straight from UNSORTED device rows (u32 contig-local
- * coordinates, as lime_set_create_device): rows are only grouped by 2^22-base
+ * coordinates, as lime_set_create_device): rows are only grouped by 2^23-base
  * bin and then by 2^19-base paint tile (two counting scatters) -- no sort and
  * no merge.  Same bits as lime_bitset_from_set on the sorted set.
  * Memory (this and every *_from_device / *_from_global entry point below):

@@ -81,13 +81,19 @@ __global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
 //                runs' events extracted in place (no words stored)
 // Why two levels: a one-level scatter to 5,900 paint tiles (hg38) keeps
 // (destinations x resident blocks) lines open per XCD, far beyond its 4 MiB
-// L2, and wrote 3.9x its bytes (profiles/round2_c5_pmc_onelevel.txt); 737
+// L2, and wrote 3.9x its bytes (profiles/round2_c5_pmc_onelevel.txt); 369
 // bins x one block per CU fit.  Staging the step in LDS (runs per bin) beat
 // direct per-row stores 0.90 vs 1.38 ms per 1.25e8 rows.
 // HBM per row: 8 B (count) + 12 B + 4 B (write) + 4 B + 4 B (split) + 4 B
 // (paint), + G/8 bits.
+// 2^23-base bins (369 for hg38): the write pass's runs per bin and step are
+// twice as long as at 2^22 (737 bins), so its partial lines halve -- C5's
+// write pass 661 -> 597 us per set, C4's 59 -> 51, same box; the split then
+// fills 16 tiles per bin and takes 16 rows per lane per chunk
+// (profiles/round6/c4_c5_bins_2e23_ab.txt).  Lengths in a bin slab: 9 bits
+// (rows past 511 bases leave their remainder to the cross list)
 #ifndef LIME_BSH
-#define LIME_BSH 22
+#define LIME_BSH 23
 #endif
 #ifndef LIME_PSH
 #define LIME_PSH 19
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(BB) void k_paint(const uint32_t *__restrict__ rgs,
 #ifndef LIME_PAINTB
 #define LIME_PAINTB 512
 #endif
-constexpr int BSH = LIME_BSH;            // bin = 2^22 bases
+constexpr int BSH = LIME_BSH;            // bin = 2^23 bases
 constexpr int PSH = LIME_PSH;            // paint tile = 2^19 bases = 8192 words (64 KiB)
 constexpr int PSUB = 1 << (BSH - PSH);   // paint tiles per bin
 constexpr int TWORDS = 1 << (PSH - 6);
@@ -562,8 +568,8 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 }
 
 // one block per bin: its rows -> its PSUB paint tiles.  The bin's rows go
-// in chunks of SPB * 8: every row claims a slot on its WAVE's counter for its
-// tile (one returning LDS atomic; 64 lanes over 8 counters, where a counter
+// in chunks of SPB * PV: every row claims a slot on its WAVE's counter for its
+// tile (one returning LDS atomic; 64 lanes over 16 counters, where a counter
 // per block took 512), a scan over the 8 waves per tile places the waves'
 // slot groups one after the other at the tile's cursor, and the rows are
 // stored there (a wave's rows of one tile are consecutive slots).  Claims
@@ -573,9 +579,9 @@ static_assert(NBMAX % WRB == 0 || WRB % NBMAX == 0, "write-pass bin scan: whole 
 #define LIME_SPB 512
 #endif
 #ifndef LIME_SPLIT_PV
-#define LIME_SPLIT_PV 8
+#define LIME_SPLIT_PV 16
 #endif
-constexpr int SPB = LIME_SPB;  // split block: 3 blocks (24 waves) per CU
+constexpr int SPB = LIME_SPB;  // split block (16 rows per lane: 2 blocks per CU)
 #ifndef LIME_SPLIT_BLOCKS
 #define LIME_SPLIT_BLOCKS 3072
 #endif

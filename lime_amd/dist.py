@@ -426,9 +426,9 @@ def complement_frame(table, rank):
 
 # ------------------------------------------------------ device exchanges
 def bitset_align(span, world):
-    """the bitset build's 2^22-base bin, or a smaller power of two (>= 64, the
+    """the bitset build's 2^23-base bin, or a smaller power of two (>= 64, the
     bitset's word) for small spans, so that no shard is rounded away"""
-    align = 1 << 22
+    align = 1 << 23
     while align > 64 and align * 4 * world > span:
         align >>= 1
     return align

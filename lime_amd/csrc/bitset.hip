@@ -587,10 +587,18 @@ constexpr int SPB = LIME_SPB;  // split block (16 rows per lane: 2 blocks per CU
 #endif
 // OPT: the bin's rows of chunks [c0, c1) are their regions, SLAB_PAD slots
 // skipped
+// STAGE: the chunk's rows are staged in LDS tile by tile and stored as one
+// contiguous run per tile (~CH / PSUB rows), where each wave's store had
+// scattered its 64 lanes over the bin's 16 tiles
+#ifndef LIME_SPLIT_STAGE
+#define LIME_SPLIT_STAGE 1
+#endif
 template <bool OPT = false>
 __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
     constexpr int NWV = SPB / 64, PV = LIME_SPLIT_PV;
+    constexpr bool STG = LIME_SPLIT_STAGE != 0;
     __shared__ uint32_t wc[NWV][PSUB], wbase[NWV][PSUB], cur[PSUB];
+    __shared__ uint32_t stg[STG ? SPB * PV : 1], sst[PSUB + 1], sgs[PSUB];
     // workgroup (bin b, chunk group g): the bin's rows of chunks [c0, c1),
     // consecutive in the bin-ordered slab; each tile's cursor starts past
     // its rows of the earlier groups (gpre), so the groups split in parallel
@@ -632,6 +640,48 @@ __global__ __launch_bounds__(SPB) void k_bin_split_atomic(BinArgs a) {
 #pragma unroll
             for (int k = 0; k < PV; ++k) pv[k] = a.slab[min(c0 + CH + mine + k * 64, r1 - 1)];
         __syncthreads();
+        if (STG) {
+            if (threadIdx.x < 64) {  // wave 0: tile d = lane (PSUB <= 64)
+                static_assert(PSUB <= 64, "one tile per lane of wave 0");
+                const int d = lane;
+                uint32_t run = 0;
+                if (d < PSUB)
+#pragma unroll
+                    for (int w = 0; w < NWV; ++w) {
+                        const uint32_t c = wc[w][d];
+                        wbase[w][d] = run;  // (relative to the tile's staging start)
+                        wc[w][d] = 0u;
+                        run += c;
+                    }
+                // the tiles' staging starts: an exclusive scan over the lanes
+                const uint32_t inc = dev::wave_inclusive_sum(run);
+                if (d < PSUB) {
+                    const uint32_t st0 = inc - run;
+                    sst[d] = st0;
+                    sgs[d] = cur[d];
+                    cur[d] += run;
+#pragma unroll
+                    for (int w = 0; w < NWV; ++w) wbase[w][d] += st0;
+                }
+                if (d == PSUB - 1) sst[PSUB] = inc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PV; ++k)
+                if (q[k] < PSUB) stg[wbase[wv][q[k]] + rk[k]] = val[k];
+            __syncthreads();
+            // one contiguous run per tile: slot j is tile t's (j - sst[t])-th
+            const uint32_t cnt = sst[PSUB];
+            for (uint32_t j = threadIdx.x; j < cnt; j += SPB) {
+                int t = 0;
+#pragma unroll
+                for (int h = PSUB / 2; h >= 1; h >>= 1)
+                    if (sst[t + h] <= j) t += h;
+                a.slab2[sgs[t] + (j - sst[t])] = stg[j];
+            }
+            __syncthreads();  // (stg and the tables are rewritten by the next chunk)
+            continue;
+        }
         if (threadIdx.x < PSUB) {  // the waves' groups, one after the other per tile
             const int d = threadIdx.x;
             uint32_t run = cur[d];

@@ -50,22 +50,43 @@ struct RouteArgs {
     unsigned int *err;  // bit0 contig, bit1 end < start, bit2 end > length / span
 };
 
-// global [g0, g1) of row i (validated; invalid rows become [0, 0) and raise err)
-__device__ __forceinline__ void route_row(const RouteArgs &a, int64_t i, uint32_t &g0, uint32_t &g1,
-                                          uint32_t &err) {
+// global [g0, g1) of a row from its loaded (contig, start, end) (validated;
+// invalid rows become [0, 0) and raise err)
+__device__ __forceinline__ void route_vals(const RouteArgs &a, int32_t c, uint32_t s, uint32_t e,
+                                           uint32_t &g0, uint32_t &g1, uint32_t &err,
+                                           const uint32_t *off, const uint32_t *len) {
     g0 = g1 = 0;
-    const uint32_t s = a.start[i], e = a.end[i];
     if (!a.contig) {
         if (e < s) err |= 2u;
         else if (e > a.span) err |= 4u;
         else g0 = s, g1 = e;
         return;
     }
-    const int32_t c = a.contig[i];
     if (c < 0 || c >= a.nc) err |= 1u;
     else if (e < s) err |= 2u;
-    else if (e > a.len[c]) err |= 4u;
-    else g0 = a.off[c] + s, g1 = a.off[c] + e;
+    else if (e > len[c]) err |= 4u;
+    else g0 = off[c] + s, g1 = off[c] + e;
+}
+// the same for row i
+__device__ __forceinline__ void route_row(const RouteArgs &a, int64_t i, uint32_t &g0, uint32_t &g1,
+                                          uint32_t &err, const uint32_t *off, const uint32_t *len) {
+    route_vals(a, a.contig ? a.contig[i] : 0, a.start[i], a.end[i], g0, g1, err, off, len);
+}
+// the contig table in LDS when it fits (the per-row off / len gathers are
+// then LDS reads, not dependent cache round trips behind the contig load)
+constexpr int RCMAX = 1024;
+__device__ __forceinline__ void route_tables(const RouteArgs &a, uint32_t *s_off, uint32_t *s_len,
+                                             const uint32_t *&off, const uint32_t *&len) {
+    off = a.off;
+    len = a.len;
+    if (a.contig && a.nc <= RCMAX) {
+        for (int i = threadIdx.x; i < a.nc; i += blockDim.x) {
+            s_off[i] = a.off[i];
+            s_len[i] = a.len[i];
+        }
+        off = s_off;
+        len = s_len;
+    }
 }
 
 // largest r with split[r] <= g (split in LDS, nsh <= 64)
@@ -91,19 +112,35 @@ __device__ __forceinline__ void dests(const RouteArgs &a, const uint32_t *sp, ui
 __global__ __launch_bounds__(RT) void k_route_count(RouteArgs a) {
     __shared__ uint32_t sp[MAXSH + 1];
     __shared__ uint32_t cnt[MAXSH];
+    __shared__ uint32_t s_off[RCMAX], s_len[RCMAX];
+    const uint32_t *off, *len;
+    route_tables(a, s_off, s_len, off, len);
     for (int i = threadIdx.x; i <= a.nsh; i += RT) sp[i] = a.split[i];
     for (int i = threadIdx.x; i < a.nsh; i += RT) cnt[i] = 0;
     __syncthreads();
     uint32_t err = 0;
+    // the wave's pieces per destination: one LDS add per (wave, destination)
+    // over the wave's destination range (a per-row atomic sent all 64 lanes
+    // of a wave to ONE counter at one shard)
+    int d0[RPT], d1[RPT], dmin = MAXSH, dmax = -1;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
         const int64_t i = (int64_t)blockIdx.x * RBLK + k * RT + threadIdx.x;
+        d0[k] = 0, d1[k] = -1;
         if (i >= a.n) continue;
         uint32_t g0, g1;
-        route_row(a, i, g0, g1, err);
-        int d0, d1;
-        dests(a, sp, g0, g1, d0, d1);
-        for (int d = d0; d <= d1; ++d) atomicAdd(&cnt[d], 1u);
+        route_row(a, i, g0, g1, err, off, len);
+        dests(a, sp, g0, g1, d0[k], d1[k]);
+        dmin = min(dmin, d0[k]);
+        dmax = max(dmax, d1[k]);
+    }
+    const int wlo = -dev::wave_reduce_max(-dmin), whi = dev::wave_reduce_max(dmax);
+    for (int d = wlo; d <= whi; ++d) {  // (wave-uniform bounds)
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) c += (d >= d0[k] && d <= d1[k]);
+        c = dev::wave_reduce_sum(c);
+        if (c && dev::lane_id() == 0) atomicAdd(&cnt[d], c);
     }
     err = dev::wave_reduce_or(err);
     if (err && dev::lane_id() == 0) atomicOr(a.err, err);
@@ -111,57 +148,95 @@ __global__ __launch_bounds__(RT) void k_route_count(RouteArgs a) {
     for (int d = threadIdx.x; d < a.nsh; d += RT) a.mat[(int64_t)d * a.nblk + blockIdx.x] = cnt[d];
 }
 
-__global__ __launch_bounds__(RT) void k_route_write(RouteArgs a) {
+// vec: every input pointer 16-B aligned, so a whole block's thread loads its
+// RPT = 4 consecutive rows by one 16-B load per array (four 4-B loads at a
+// 16-B lane stride had each touched four times the lines)
+__global__ __launch_bounds__(RT) void k_route_write(RouteArgs a, int vec) {
     __shared__ uint32_t sp[MAXSH + 1];
-    __shared__ uint32_t scratch[RT / 64 + 1];
+    __shared__ uint64_t scratch[RT / 64 + 1];
+    __shared__ uint32_t s_off[RCMAX], s_len[RCMAX];
+    const uint32_t *off, *len;
+    route_tables(a, s_off, s_len, off, len);
     for (int i = threadIdx.x; i <= a.nsh; i += RT) sp[i] = a.split[i];
     __syncthreads();
     // rows of this thread: blocked (k * RT + t keeps loads coalesced; the
     // order within a destination is the thread-major order below)
+    static_assert(RPT == 4, "one 16-B load per array and thread");
     uint32_t g0[RPT], g1[RPT];
     int d0[RPT], d1[RPT];
     uint32_t err = 0;
     int dmin = MAXSH, dmax = -1;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-        const int64_t i = (int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k;
-        d0[k] = 0, d1[k] = -1;
-        if (i >= a.n) continue;
-        route_row(a, i, g0[k], g1[k], err);
-        dests(a, sp, g0[k], g1[k], d0[k], d1[k]);
-        dmin = min(dmin, d0[k]);
-        dmax = max(dmax, d1[k]);
-    }
-    // per destination: offset of this thread's pieces = block scan
-    for (int d = 0; d < a.nsh; ++d) {
-        uint32_t c = 0;
-        if (d >= dmin && d <= dmax)
-#pragma unroll
-            for (int k = 0; k < RPT; ++k) c += (d >= d0[k] && d <= d1[k]);
-        uint32_t tot;
-        uint32_t pos = a.mat[(int64_t)d * a.nblk + blockIdx.x] +
-                       dev::block_exclusive_sum<RT>(c, scratch, &tot);
-        if (c == 0) continue;
+    const int64_t i0 = (int64_t)blockIdx.x * RBLK + threadIdx.x * RPT;
+    if (vec && i0 + RPT <= a.n) {
+        const int4 cv = a.contig ? *reinterpret_cast<const int4 *>(a.contig + i0) : int4{0, 0, 0, 0};
+        const uint4 sv = *reinterpret_cast<const uint4 *>(a.start + i0);
+        const uint4 ev = *reinterpret_cast<const uint4 *>(a.end + i0);
+        const int32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
+        const uint32_t ss[4] = {sv.x, sv.y, sv.z, sv.w}, ee[4] = {ev.x, ev.y, ev.z, ev.w};
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
-            if (d < d0[k] || d > d1[k]) continue;
-            const uint32_t lo = sp[d], hi = sp[d + 1];
-            const uint32_t gs = a.clip ? max(g0[k], lo) : g0[k];
-            const uint32_t ge = a.clip && g1[k] > g0[k] ? min(g1[k], hi) : g1[k];
-            const int64_t i = (int64_t)blockIdx.x * RBLK + threadIdx.x * RPT + k;
-            if (a.iv) {
-                uint32_t *o = a.iv + (int64_t)pos * a.ik;
-                o[0] = gs;
-                o[1] = ge;
-                if (a.ik == 3) o[2] = a.row_base + (uint32_t)i;
+            route_vals(a, cc[k], ss[k], ee[k], g0[k], g1[k], err, off, len);
+            dests(a, sp, g0[k], g1[k], d0[k], d1[k]);
+            dmin = min(dmin, d0[k]);
+            dmax = max(dmax, d1[k]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const int64_t i = i0 + k;
+            d0[k] = 0, d1[k] = -1;
+            if (i >= a.n) continue;
+            route_row(a, i, g0[k], g1[k], err, off, len);
+            dests(a, sp, g0[k], g1[k], d0[k], d1[k]);
+            dmin = min(dmin, d0[k]);
+            dmax = max(dmax, d1[k]);
+        }
+    }
+    // per destination: offset of this thread's pieces = block scan, four
+    // destinations per scan (16-bit fields of a u64: a block holds at most
+    // RBLK pieces per destination)
+    static_assert(RBLK < 65536, "16-bit piece counts per destination");
+    for (int db = 0; db < a.nsh; db += 4) {
+        uint64_t c4 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = db + j;
+            uint32_t c = 0;
+            if (d >= dmin && d <= dmax)
+#pragma unroll
+                for (int k = 0; k < RPT; ++k) c += (d >= d0[k] && d <= d1[k]);
+            c4 |= (uint64_t)c << (16 * j);
+        }
+        uint64_t tot;
+        const uint64_t ex = dev::block_exclusive_sum<RT>(c4, scratch, &tot);
+        if (c4 == 0) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = db + j;
+            if (((c4 >> (16 * j)) & 0xffffu) == 0) continue;
+            uint32_t pos = a.mat[(int64_t)d * a.nblk + blockIdx.x] + (uint32_t)((ex >> (16 * j)) & 0xffffu);
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                if (d < d0[k] || d > d1[k]) continue;
+                const uint32_t lo = sp[d], hi = sp[d + 1];
+                const uint32_t gs = a.clip ? max(g0[k], lo) : g0[k];
+                const uint32_t ge = a.clip && g1[k] > g0[k] ? min(g1[k], hi) : g1[k];
+                const int64_t i = i0 + k;
+                if (a.iv) {  // one store per piece: 12 B (gs, ge, row) or 8 B
+                    if (a.ik == 3)
+                        *reinterpret_cast<uint3 *>(a.iv + (int64_t)pos * 3) =
+                            make_uint3(gs, ge, a.row_base + (uint32_t)i);
+                    else
+                        *reinterpret_cast<uint2 *>(a.iv + (int64_t)pos * 2) = make_uint2(gs, ge);
+                    ++pos;
+                    continue;
+                }
+                a.gs[pos] = gs;
+                a.ge[pos] = ge;
+                if (a.row) a.row[pos] = a.row_base + (uint32_t)i;
+                if (a.strand_out) a.strand_out[pos] = a.strand_in ? a.strand_in[i] : (int8_t)0;
                 ++pos;
-                continue;
             }
-            a.gs[pos] = gs;
-            a.ge[pos] = ge;
-            if (a.row) a.row[pos] = a.row_base + (uint32_t)i;
-            if (a.strand_out) a.strand_out[pos] = a.strand_in ? a.strand_in[i] : (int8_t)0;
-            ++pos;
         }
     }
 }
@@ -316,7 +391,9 @@ int route_rows(lime_ctx *ctx, const lime_space *sp, int64_t n, const int32_t *d_
     // (h[nsh] is mat's last entry: the total, the scan's exclusive sum)
     for (int d = 0; d < nsh; ++d) counts[d] = h[d + 1] - h[d];
     if (h[nsh] > cap || n == 0) return LIME_OK;  // counts only
-    hipLaunchKernelGGL(k_route_write, dim3(nblk), dim3(RT), 0, S(ctx), a);
+    const int vec = ((reinterpret_cast<uintptr_t>(d_contig) | reinterpret_cast<uintptr_t>(d_start) |
+                      reinterpret_cast<uintptr_t>(d_end)) & 15u) == 0;
+    hipLaunchKernelGGL(k_route_write, dim3(nblk), dim3(RT), 0, S(ctx), a, vec);
     LIME_HIP(hipGetLastError());
     // (the caller's rows are consumed before the return on the context's own
     // stream, as lime_amd.h states for device inputs)

@@ -503,3 +503,65 @@ def test_rccl_exchange_rounds_one_rank():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert res == (True, True)
+
+
+@pytest.mark.parametrize("nsh", [1, 5, 9, 64])
+def test_route_rows_many_shards(nsh):
+    # lime_route_rows / _interleaved against numpy on one process: every
+    # piece at its destination in input order, clipped or not, 2- and
+    # 3-word interleaved rows and the column form; misaligned inputs take
+    # the scalar-load path (the write pass's counts go four destinations to
+    # a block scan: nsh 5, 9, 64 cross those groups)
+    import torch
+    import lime_amd
+    ctx = lime_amd.Context(0)
+    sp = lime_amd.Space(NAMES, LENS)
+    off = sp.offsets
+    span = int(sp.span)
+    rng = np.random.default_rng(1000 + nsh)
+    n = 200_003
+    c = rng.integers(0, len(LENS), n).astype(np.int32)
+    L = np.array(LENS)[c]
+    s = (rng.random(n) * (L - 1)).astype(np.int64)
+    e = np.minimum(s + rng.integers(0, 40_000, n), L)
+    g0 = off[c] + s
+    g1 = off[c] + e
+    cuts = np.sort(rng.choice(np.arange(1, span), nsh - 1, replace=False)) if nsh > 1 else []
+    splits = [0] + [int(x) for x in cuts] + [span]
+    dev = torch.device("cuda", 0)
+    for shift in (0, 1):  # 1: inputs one element off 16-B alignment
+        cols = [torch.from_numpy(np.concatenate([np.zeros(shift, x.dtype), x]).astype(np.int32))
+                .to(dev)[shift:] for x in (c, s, e)]
+        torch.cuda.synchronize()
+        ptrs = [t.data_ptr() for t in cols]
+        for clip in (False, True):
+            sa = np.array(splits, np.int64)
+            d0 = np.searchsorted(sa, g0, side="right") - 1
+            wide = clip & (g1 > g0)
+            d1 = np.where(wide, np.searchsorted(sa, g1 - 1, side="right") - 1, d0)
+            per = d1 - d0 + 1
+            rows = np.repeat(np.arange(n), per)
+            dd = np.repeat(d0, per) + (np.arange(per.sum()) - np.repeat(np.cumsum(per) - per, per))
+            a, b = g0[rows], g1[rows]
+            if clip:
+                a = np.maximum(a, sa[dd])
+                b = np.where(wide[rows], np.minimum(b, sa[dd + 1]), b)
+            order = np.argsort(dd, kind="stable")  # by destination, input order kept
+            want = np.stack([a[order], b[order], 7 + rows[order]], 1).astype(np.int64)
+            exp_cnt = np.bincount(dd, minlength=nsh).tolist()
+            m = len(want)
+            for k in (2, 3):
+                buf = torch.empty((max(m, 1), k), dtype=torch.int32, device=dev)
+                cnt = ctx.route_rows_interleaved(sp, n, *ptrs, splits, k, buf.data_ptr(),
+                                                 clip=clip, cap=m, row_base=7)
+                torch.cuda.synchronize()
+                assert cnt == exp_cnt, (shift, clip, k)
+                got = buf[:m].cpu().numpy().view(np.uint32).astype(np.int64)
+                assert np.array_equal(got, want[:, :k]), (shift, clip, k)
+            outs = [torch.empty(max(m, 1), dtype=torch.int32, device=dev) for _ in range(3)]
+            cnt = ctx.route_rows(sp, n, *ptrs, splits, clip=clip, cap=m,
+                                 d_gs=outs[0].data_ptr(), d_ge=outs[1].data_ptr(),
+                                 d_row=outs[2].data_ptr(), row_base=7)
+            torch.cuda.synchronize()
+            got = np.stack([o[:m].cpu().numpy().view(np.uint32).astype(np.int64) for o in outs], 1)
+            assert cnt == exp_cnt and np.array_equal(got, want)

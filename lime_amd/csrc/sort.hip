@@ -881,7 +881,9 @@ struct LocalArgs {
     uint32_t *k1, *e1, *r1;        // the sorted set
     unsigned int *nover;           // [0] listed buckets, [1] the big kernel's ticket
     uint32_t *over;                // listed bucket ids
+    uint32_t *sink;                // LSINK words: stores past a bucket's rows
 };
+constexpr int LSINK = 1024;
 
 __global__ __launch_bounds__(256) void k_bucket_starts(const uint32_t *__restrict__ k, int64_t n,
                                                        uint32_t nb, int L,
@@ -1215,13 +1217,20 @@ void k_local_small(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start)
 // Every row's rank stays in a register: no per-slot pass, no rank table.
 // A sub-bin past SMAX rows (a pile of identical starts) sends the bucket to
 // k_local_big.
-template <int NT, int ITEMS, int POSB, int SBB, bool PK = false>
+// prefetch(): called once the ranks are known, before the output stores --
+// the persistent kernel loads its next bucket there.  Every thread then
+// issues exactly ITEMS stores per output array (slots past the bucket's rows
+// go to the sink): loads and stores share vmcnt, so with a static store
+// count the next bucket's first use of its rows waits for those loads only,
+// not for this bucket's stores (a loop bounded by the bucket's size made the
+// compiler wait for every store: the prefetch then bought nothing)
+template <int NT, int ITEMS, int POSB, int SBB, bool PK = false, class PF>
 __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t b, uint32_t s0,
                                                  uint32_t m,
                                                  const uint32_t (&g)[ITEMS],
                                                  const uint32_t (&e)[ITEMS],
                                                  const uint32_t (&rw)[ITEMS], uint32_t *T,
-                                                 uint32_t *cw, uint32_t *scratch) {
+                                                 uint32_t *cw, uint32_t *scratch, PF &&prefetch) {
     constexpr int NWD = 1 << (SBB - 1), SPW = NWD / NT;  // cursor words, per thread
     static_assert(NWD % NT == 0 && SPW >= 2 && (SPW & (SPW - 1)) == 0, "cursor words per thread");
     static_assert(NT * ITEMS <= (1 << POSB) && NT * ITEMS < 65536, "positions / ranks");
@@ -1309,6 +1318,8 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t b,
             rk[it] = r;
         }
     }
+    prefetch();
+    uint32_t *const sink = a.sink + threadIdx.x % LSINK;
     if (PK) {  // packed word -> (gs, ge), then rows
         const uint32_t base = b << a.L;
 #pragma unroll
@@ -1318,14 +1329,17 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t b,
             for (int it = 0; it < ITEMS; ++it)
                 if (rk[it] != 0xffffffffu) T[rk[it]] = round == 0 ? g[it] : rw[it];
             __syncthreads();
-            for (uint32_t q = threadIdx.x; q < m; q += NT) {
-                const uint32_t x = T[q];
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) {
+                const uint32_t q = threadIdx.x + (uint32_t)it * NT;
+                const bool in = q < m;
+                const uint32_t x = T[q];  // (q < NT ITEMS: inside T)
                 if (round == 0) {
                     const uint32_t gq = base | (x >> 16);
-                    a.k1[s0 + q] = gq;
-                    a.e1[s0 + q] = gq + (x & 0xffffu);
+                    *(in ? a.k1 + s0 + q : sink) = gq;
+                    *(in ? a.e1 + s0 + q : sink) = gq + (x & 0xffffu);
                 } else {
-                    a.r1[s0 + q] = x;
+                    *(in ? a.r1 + s0 + q : sink) = x;
                 }
             }
         }
@@ -1339,7 +1353,11 @@ __device__ __forceinline__ bool bucket_sort_keys(const LocalArgs &a, uint32_t b,
             if (rk[it] != 0xffffffffu) T[rk[it]] = round == 0 ? g[it] : round == 1 ? e[it] : rw[it];
         __syncthreads();
         uint32_t *dst = round == 0 ? a.k1 : round == 1 ? a.e1 : a.r1;
-        for (uint32_t q = threadIdx.x; q < m; q += NT) dst[s0 + q] = T[q];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const uint32_t q = threadIdx.x + (uint32_t)it * NT;
+            *(q < m ? dst + s0 + q : sink) = T[q];
+        }
     }
     return true;
 }
@@ -1365,15 +1383,36 @@ void k_local_keys(LocalArgs a, uint32_t nb, const uint32_t *__restrict__ start) 
     // (the next bucket's keys prefetched into a second register set during
     // this one's sort, rows loaded at its start: no faster, same box --
     // the kernel waits on LDS and barriers, not loads; not kept)
+    if constexpr (!PK) {  // (u32 ends: no registers to spare for a second bucket)
+        for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+            BucketRegs<NT, ITEMS, CAP, true, PK, true> cur;
+            cur.load(a, b, nb, start);
+            bool listed = cur.m > (uint32_t)CAP;
+            if (!listed && cur.m > 0)
+                listed = !bucket_sort_keys<NT, ITEMS, POSB, SBB, PK>(
+                    a, b, cur.s0, cur.m, cur.g, cur.ends(), cur.r, T, cw, scratch, [] {});
+            if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;
+            __syncthreads();  // (the next bucket overwrites the staging)
+        }
+        return;
+    }
+    // PK: the next bucket's rows are loaded behind this one's sort, before
+    // its output stores (bucket_sort_keys' prefetch)
+    BucketRegs<NT, ITEMS, CAP, true, PK, true> cur, nxt;
+    cur.load(a, blockIdx.x, nb, start);
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        BucketRegs<NT, ITEMS, CAP, true, PK, true> cur;
-        cur.load(a, b, nb, start);
-        bool listed = cur.m > (uint32_t)CAP;
+        bool listed = cur.m > (uint32_t)CAP, fetched = false;
+        auto prefetch = [&]() {
+            nxt.load(a, b + gridDim.x, nb, start);
+            fetched = true;
+        };
         if (!listed && cur.m > 0)
-            listed = !bucket_sort_keys<NT, ITEMS, POSB, SBB, PK>(a, b, cur.s0, cur.m, cur.g,
-                                                                 cur.ends(), cur.r, T, cw, scratch);
+            listed = !bucket_sort_keys<NT, ITEMS, POSB, SBB, PK>(
+                a, b, cur.s0, cur.m, cur.g, cur.ends(), cur.r, T, cw, scratch, prefetch);
+        if (!fetched) nxt.load(a, b + gridDim.x, nb, start);  // (listed or empty)
         if (listed && threadIdx.x == 0) a.over[atomicAdd(&a.nover[0], 1u)] = b;  // for the big kernel
         __syncthreads();  // (the next bucket overwrites the staging)
+        cur = nxt;
     }
 }
 constexpr int LCAP_M = 6144, LCAP_W = 16384;
@@ -1830,6 +1869,10 @@ int sort_set_impl(lime_ctx *ctx, lime_set *set, bool global, const int32_t *d_co
             la.k1 = a[0], la.e1 = a[1], la.r1 = a[2];
             la.nover = nover;
             la.over = over;
+            uint32_t *sink;
+            LIME_TRY(alloc(ctx, &sink, (size_t)LSINK));
+            PoolGuard<uint32_t> g3{ctx, sink};
+            la.sink = sink;
             int dev = 0, cus = 256;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

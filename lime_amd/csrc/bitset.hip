@@ -111,8 +111,12 @@ constexpr int PLENB = 32 - PSH;          // packed length bits (tile slab)
 constexpr int NBMAX = 1 << (32 - BSH);   // bins (span < 2^32)
 constexpr int NTMAX = NBMAX * PSUB;      // paint tiles
 constexpr int BINB = 1024;               // count / split block
+// the write pass: 1024-thread workgroups, one per CU, so a step holds
+// 12288 rows and each bin's run per step is twice as long (fewer partial
+// lines) as with two 512-thread workgroups per CU: C5's write pass 567 ->
+// 519 us per set, same box (profiles/round6/c5_write_1024_threads_ab.txt)
 #ifndef LIME_WRB
-#define LIME_WRB 512
+#define LIME_WRB 1024
 #endif
 constexpr int WRB = LIME_WRB;            // write block (<= 256 VGPRs: no spills)
 constexpr int PAINTB = LIME_PAINTB;
@@ -210,9 +214,9 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t bid, uint32_t nch) {
 // A step = SROWS rows per lane: groups of 4 consecutive rows, the groups
 // BINB * 4 rows apart, so every load is a lane-consecutive 16-B access and a
 // step keeps 6-9 loads in flight per lane.
-// 12 rows per lane and two write workgroups per CU (<= 128 VGPRs, 57 KiB
-// LDS): C5 10.8-11.1 -> 10.5-10.8 ms against 16 rows at one per CU (8 rows:
-// no gain, shorter runs per bin)
+// 12 rows per lane (<= 128 VGPRs): with two 512-thread write workgroups per
+// CU, C5 10.8-11.1 -> 10.5-10.8 ms against 16 rows at one per CU (8 rows: no
+// gain, shorter runs per bin); now one 1024-thread workgroup (LIME_WRB)
 #ifndef LIME_SROWS
 #define LIME_SROWS 12
 #endif
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(256) void k_tile_groups(BinArgs a) {
 }
 
 #ifndef LIME_WRITE_BLOCKS
-#define LIME_WRITE_BLOCKS 2
+#define LIME_WRITE_BLOCKS 1
 #endif
 #ifndef LIME_BIN_PREFETCH
 #define LIME_BIN_PREFETCH 1
@@ -406,7 +410,7 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
     // (the following step's loads: in flight across this step's barriers --
     // plain loads survive __syncthreads), then rank, stage and store
     auto step = [&](int64_t base, uint32_t valid, auto next) {
-        // tb[k]: the row's bin, then (bin << 13 | its rank among the step's
+        // tb[k]: the row's bin, then (bin << RKB | its rank among the step's
         // rows of the bin) once ranked: one register per row for both
         uint32_t tb[SROWS], pk[SROWS];
 #pragma unroll
@@ -450,10 +454,11 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
         next();
         // rank per bin (16 independent LDS atomics), then bin offsets in the
         // step (one scan over <= 1024 bins), then stage in bin order
-        static_assert(WSTEP <= (1 << 13) && NBMAX <= (1 << 19), "bin / rank packing");
+        constexpr int RKB = WSTEP <= (1 << 13) ? 13 : 14;  // rank bits
+        static_assert(WSTEP <= (1 << RKB) && NBMAX <= (1 << (32 - RKB)), "bin / rank packing");
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
-            if (valid & (1u << k)) tb[k] = (tb[k] << 13) | atomicAdd(&hist[tb[k]], 1u);
+            if (valid & (1u << k)) tb[k] = (tb[k] << RKB) | atomicAdd(&hist[tb[k]], 1u);
         __syncthreads();
         {
             // bins BPT t .. BPT t + BPT - 1 per thread (fewer bins than
@@ -476,8 +481,8 @@ __attribute__((amdgpu_waves_per_eu(LIME_WRITE_BLOCKS * WRB / 256, 8))) void k_bi
 #pragma unroll
         for (int k = 0; k < SROWS; ++k)
             if (valid & (1u << k)) {
-                const uint32_t t = tb[k] >> 13;
-                const uint32_t j = soff[t] + (tb[k] & 0x1fffu);
+                const uint32_t t = tb[k] >> RKB;
+                const uint32_t j = soff[t] + (tb[k] & ((1u << RKB) - 1u));
                 stage[j] = pk[k];
                 sbin[j] = (uint16_t)t;
             }

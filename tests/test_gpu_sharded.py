@@ -565,3 +565,28 @@ def test_route_rows_many_shards(nsh):
             torch.cuda.synchronize()
             got = np.stack([o[:m].cpu().numpy().view(np.uint32).astype(np.int64) for o in outs], 1)
             assert cnt == exp_cnt and np.array_equal(got, want)
+
+
+def test_bench_sharded_step_matches_unsharded():
+    # bench.py's C2 step through ShardStep in a one-rank RCCL group
+    # (--sharded: route, exchange, global-row sort, carry all_gather, owned
+    # pairs) reports the unsharded step's pair and run totals
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(*extra):
+        cmd = [sys.executable, "bench.py", "--no-ops", "--no-cpu-baseline", "--steps", "1",
+               "--warmup", "0", "--rows", "2000000", *extra]
+        env = dict(os.environ)
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+            env.pop(k, None)
+        out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-2000:]
+        line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+        return json.loads(line)
+    plain, sharded = run(), run("--sharded")
+    assert sharded["config"]["sharded_step"] and not plain["config"]["sharded_step"]
+    for k in ("pairs_per_step", "runs_per_step"):
+        assert sharded["config"][k] == plain["config"][k] > 0, k
